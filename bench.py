@@ -1,0 +1,276 @@
+#!/usr/bin/env python
+"""bench.py -- scored triples/s of the link-prediction sweep (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+One step = one complete filtered link-prediction evaluation of the configured workload
+(default C2: FB15K-237-ZS test set, TransE d=200, norm_flag, all 17,596 test triples in both
+head_batch and tail_batch mode = 35,192 sweeps over 14,208 entities): entity-table prep, query
+vectors, truth scores + filter correction, the fused sweep + rank epilogue, (N>1) the RCCL
+all-gather of per-rank rank-count lists, the D2H copy of the counts and the Test.h metric
+reduction. Inputs (tables, queries, filter lists) are resident in HBM before timing starts.
+N>1: launched by torch.distributed.run, one rank per GPU, relation-sharded (LPT) queries.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "multimodal-relation-extrapolation_amd")
+for p in (PKG, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "scored triples/sec + hit@10 parity, FB15K-237-ZS TransE d=200 at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD-32 x 2.4 GHz (lane-ops/s)
+
+CONFIGS = {
+    "c2": dict(dataset="FB15K-237-ZS", model="transe", dim=200, norm=True,
+               workload="C2 FB15K-237-ZS TransE d=200 p=1 norm_flag, filtered link prediction"),
+    "c3": dict(dataset="DB15K-ZS", model="complex", dim=200, norm=False,
+               workload="C3 DB15K-ZS ComplEx d=200, filtered link prediction (MFMA f32)"),
+    "c4": dict(dataset="FB15K-237-ZS", model="rotate", dim=512, norm=False,
+               workload="C4 FB15K-237-ZS RotatE d=512, filtered link prediction"),
+    "c5": dict(dataset="synthetic-1M", model="distmult", dim=256, norm=False,
+               workload="C5 synthetic |E|=1M DistMult d=256, 8,192 sweeps (MFMA f32)"),
+}
+
+
+def bytes_per_triple(model, dim):
+    """algorithmic fp32 bytes of the entity row(s) read per scored triple."""
+    return {"transe": 4 * dim, "transe_l2": 4 * dim, "distmult": 4 * dim, "complex": 8 * dim,
+            "rotate": 8 * dim}[model]
+
+
+def valu_ops_per_triple(model, dim):
+    """VALU lane-instructions per scored triple in the sweep's inner loop."""
+    return {"transe": 2 * dim, "transe_l2": 2 * dim, "rotate": 11 * dim}.get(model)
+
+
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Base.so printf()s to fd 1; keep rank 0's stdout a single JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def cpu_baseline(w, n_sample: int):
+    """The reference's CPU path on this host's cores: the OpenKE Tester loop
+    (Tester.py:70-91) = Base.so getHeadBatch -> TransE.predict on torch CPU (the op sequence of
+    TransE.py:62-76: gather, F.normalize, h + (r - t) / (h + r) - t, torch.norm p=1) ->
+    Base.so testHead/testTail. Base.so is the reference's own C++ (oracle/_ref, compiled from
+    /root/reference/OpenKE/openke/base/Base.cpp); without it the oracle's ranker is used."""
+    import torch.nn.functional as F
+    E, d = w["n_ent"], w["dim"]
+    ent, rel = w["ent"].float(), w["rel"].float()
+    ref_so = os.path.join(REPO, "oracle", "_ref", "Base.so")
+    kind = "reference" if os.path.exists(ref_so) else "port"
+    n = min(n_sample, len(w["test_h"]))
+    th, tr, tt = w["test_h"][:n], w["test_r"][:n], w["test_t"][:n]
+
+    def predict(ph, pt, pr, mode):
+        h = F.normalize(ent[ph], 2, -1)
+        r = F.normalize(rel[pr], 2, -1)
+        t = F.normalize(ent[pt], 2, -1)
+        h = h.view(-1, r.shape[0], h.shape[-1])
+        t = t.view(-1, r.shape[0], t.shape[-1])
+        r = r.view(-1, r.shape[0], r.shape[-1])
+        s = h + (r - t) if mode == "head_batch" else (h + r) - t
+        return torch.norm(s, 1, -1).flatten().cpu().data.numpy()
+
+    if kind == "reference":
+        tmp = tempfile.mkdtemp(prefix="mmre_cpu_")
+        trn = np.stack([w["filter_h"][:-len(w["test_h"])], w["filter_t"][:-len(w["test_h"])],
+                        w["filter_r"][:-len(w["test_h"])]], 1)
+        for name, arr in (("train2id.txt", trn), ("valid2id.txt", np.zeros((0, 3), np.int64)),
+                          ("test2id.txt", np.stack([th, tt, tr], 1))):
+            with open(os.path.join(tmp, name), "w") as f:
+                f.write(f"{len(arr)}\n")
+                np.savetxt(f, arr, fmt="%d")
+        for name, cnt in (("entity2id.txt", E), ("relation2id.txt", w["n_rel"])):
+            with open(os.path.join(tmp, name), "w") as f:
+                f.write(f"{cnt}\n")
+        lib = ctypes.CDLL(ref_so)
+        P, I = ctypes.c_void_p, ctypes.c_int64
+        lib.setInPath.argtypes = [ctypes.c_char_p]
+        lib.getHeadBatch.argtypes = [P, P, P]
+        lib.getTailBatch.argtypes = [P, P, P]
+        lib.testHead.argtypes = [P, I, I]
+        lib.testTail.argtypes = [P, I, I]
+        lib.test_link_prediction.argtypes = [I]
+        with stdout_to_stderr():
+            lib.setInPath((tmp + "/").encode())
+            lib.importTrainFiles()
+            lib.importTestFiles()
+            lib.initTest()
+        ph, pt, pr = (np.zeros(E, np.int64) for _ in range(3))
+        t0 = time.perf_counter()
+        with stdout_to_stderr():
+            for idx in range(n):
+                lib.getHeadBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
+                s = predict(torch.from_numpy(ph), torch.from_numpy(pt[:1]), torch.from_numpy(pr[:1]), "head_batch")
+                lib.testHead(s.ctypes.data, idx, 0)
+                lib.getTailBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
+                s = predict(torch.from_numpy(ph[:1]), torch.from_numpy(pt), torch.from_numpy(pr[:1]), "tail_batch")
+                lib.testTail(s.ctypes.data, idx, 0)
+            lib.test_link_prediction(0)
+        elapsed = time.perf_counter() - t0
+    else:
+        import oracle
+        hrt = oracle.sorted_hrt(w["filter_h"], w["filter_r"], w["filter_t"])
+        t0 = time.perf_counter()
+        for i in range(n):
+            for mode in ("head_batch", "tail_batch"):
+                if mode == "head_batch":
+                    s = predict(torch.arange(E), torch.tensor([tt[i]]), torch.tensor([tr[i]]), mode)
+                else:
+                    s = predict(torch.tensor([th[i]]), torch.arange(E), torch.tensor([tr[i]]), mode)
+                oracle.test_rank(mode, s[None, :], th[i:i + 1], tr[i:i + 1], tt[i:i + 1], hrt)
+        elapsed = time.perf_counter() - t0
+    triples = 2 * n * E
+    return {"value": triples / elapsed, "unit": "scored triples/s", "cores": torch.get_num_threads(),
+            "kind": kind,
+            "sample": f"{n} FB15K-237-ZS test triples x {{head,tail}} = {2 * n} sweeps x {E} entities through the "
+                      f"OpenKE Tester loop (torch {torch.__version__} CPU TransE.predict op sequence + "
+                      f"{'reference Base.so' if kind == 'reference' else 'oracle'} testHead/testTail), "
+                      f"{elapsed:.2f} s on {torch.get_num_threads()} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample", type=int, default=1000, help="test triples in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from mmre.link import FilterIndex, LinkSweep, ScoreSpec, link_metrics, rotate_phase_denom
+    from mmre.sharding import ShardPlan, gather_counts, lpt_partition
+    from mmre.workloads import synthetic_large, zs_workload
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    if cfg["dataset"] == "synthetic-1M":
+        w = synthetic_large()
+    else:
+        w = zs_workload(cfg["dataset"], cfg["model"], cfg["dim"])
+    model, dim = cfg["model"], cfg["dim"]
+    E = w["n_ent"]
+    n = len(w["test_h"])
+    qh = np.concatenate([w["test_h"], w["test_h"]]).astype(np.int64)
+    qr = np.concatenate([w["test_r"], w["test_r"]]).astype(np.int64)
+    qt = np.concatenate([w["test_t"], w["test_t"]]).astype(np.int64)
+    qm = np.concatenate([np.zeros(n, np.int8), np.ones(n, np.int8)])
+    masks = lpt_partition(qr, world)
+    mine = masks[rank]
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
+    off, ids = index.filters(qh[mine], qr[mine], qt[mine], qm[mine])
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    lq = [to(qh[mine]), to(qr[mine]), to(qt[mine]), to(qm[mine])]
+    filt = (to(off), to(ids))
+    pk = {"transe": 0, "distmult": 2, "complex": 2, "rotate": 3}[model]
+    spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
+                     ent_im=w.get("ent_im").to(dev) if "ent_im" in w else None,
+                     rel_im=w.get("rel_im").to(dev) if "rel_im" in w else None, norm_flag=cfg["norm"],
+                     pred_kind=pk, margin=float(w.get("margin", 0.0)),
+                     phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
+    sw = LinkSweep(spec)
+    bufs = sw.alloc_queries(int(mine.sum()))
+    plan = ShardPlan(masks, dev) if world > 1 else None
+    n_local = int(mine.sum())
+
+    def step(events=None):
+        res = sw.run(*lq, filt=filt, buffers=bufs, prepare=True, sweep_events=events)
+        counts = res["counts"]
+        full = gather_counts(counts, plan) if world > 1 else counts
+        host = full.cpu().numpy()
+        return link_metrics(host[:, :n], host[:, n:])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    metrics = None
+    for i in range(args.steps):
+        metrics = step(evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_triples = 2 * n * E
+    value = total_triples * args.steps / elapsed
+    if rank == 0:
+        bpt = bytes_per_triple(model, dim)
+        achieved = n_local * E * bpt / (sweep_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "k_sweep_valu" if model in ("transe", "rotate") else "k_sweep_mfma",
+                "kernel_ms": sweep_ms, "bytes_per_triple": bpt, "triples_per_launch": n_local * E}
+        vo = valu_ops_per_triple(model, dim)
+        if vo:
+            tps = n_local * E / (sweep_ms * 1e-3)
+            roof["valu_bound_triples_per_s"] = VALU_LANE_OPS / vo
+            roof["valu_frac"] = tps / (VALU_LANE_OPS / vo)
+        out = {"metric": METRIC if args.config == "c2" else f"scored triples/sec, {cfg['workload']}",
+               "value": value, "unit": "scored triples/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic tables (OpenKE xavier/uniform init, seed 0) over the real test triples; "
+                       "filter set = test + 272,115 synthetic train triples",
+               "config": {"workload": cfg["workload"], "n_entities": E, "dim": dim, "n_sweeps": 2 * n,
+                          "parallelism": f"relation-sharded x{world} (LPT), RCCL all-gather of rank counts"},
+               "roofline": roof,
+               "parity": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
+                          "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
+                          "mr": metrics["filter"]["mr"]}}
+        if world == 1 and not args.no_cpu_baseline and model == "transe":
+            out["cpu_baseline"] = cpu_baseline(w, args.cpu_sample)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * mmre.h -- C ABI of libmmre_hip.so, the MI355X-native hot path of
+ * luisrui/Multimodal-Relation-Extrapolation (KG scoring sweep, negative-sampling
+ * margin loss, zero-shot relation-embedding generator).
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no torch types.
+ *   - Pointers named d_* are DEVICE pointers (hipMalloc / torch CUDA tensors);
+ *     pointers named h_* are HOST pointers. Every device entry point takes an
+ *     explicit hipStream_t (passed as void*; NULL = default stream) and only
+ *     enqueues work: no allocation, no synchronisation, graph-capturable.
+ *   - Return value: 0 on success, MMRE_ERR_* (> 0) on a bad argument, or
+ *     MMRE_ERR_HIP_BASE + hipError_t for a HIP failure. Nothing aborts.
+ *   - The library is stateless: all state lives in caller-owned buffers.
+ *   - Model ids: MMRE_TRANSE_L1 / _L2 / DISTMULT / COMPLEX / ROTATE.
+ *
+ * Each entry point names the reference interface it replaces (file:line under
+ * the reference tree). INTEGRATION.md shows the ctypes binding a maintainer of
+ * the reference would add.
+ */
+#ifndef MMRE_H
+#define MMRE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  MMRE_TRANSE_L1 = 0,
+  MMRE_TRANSE_L2 = 1,
+  MMRE_DISTMULT = 2,
+  MMRE_COMPLEX = 3,
+  MMRE_ROTATE = 4
+};
+enum { MMRE_HEAD_BATCH = 0, MMRE_TAIL_BATCH = 1 };
+enum {
+  MMRE_OK = 0,
+  MMRE_ERR_ARG = 1,
+  MMRE_ERR_MODEL = 2,
+  MMRE_ERR_SHAPE = 3,
+  MMRE_ERR_WORKSPACE = 4,
+  MMRE_ERR_HIP_BASE = 1000
+};
+
+/* Library / ABI version (major*10000 + minor*100 + patch). */
+int mmre_version(void);
+
+/* ====================================================================== *
+ *  Link prediction: the all-entity score sweep with fused rank epilogue.  *
+ *  Replaces, per evaluation, the Tester loop (OpenKE/openke/config/       *
+ *  Tester.py:70-91) = getHeadBatch/getTailBatch (Test.h:36-53) +          *
+ *  model.predict (TransE.py:104-110, DistMult.py:70-72, ComplEx.py:60-62, *
+ *  RotatE.py:89-91) + testHead/testTail (Test.h:65-192, _find            *
+ *  Corrupt.h:166-177).                                                    *
+ * ====================================================================== */
+
+/* Width K of the k-major planes for a model (d, or 2d for ComplEx/RotatE),
+ * rounded up to the sweep's K step. */
+int64_t mmre_link_k(int model, int dim);
+/* Padded entity / query counts used by the k-major planes. */
+int64_t mmre_link_pad(int64_t n);
+
+/* Entity table -> k-major plane d_ent_km[K][e_pad] (F.normalize first when
+ * norm_flag, TransE.py:63-66). Tables: TransE/DistMult (E, d); ComplEx re/im
+ * (E, d) each; RotatE (E, 2d) = [re | im] (RotatE.py:48-49). */
+int mmre_link_prepare_entities(int model, int norm_flag, const float* d_ent, const float* d_ent_im,
+                               int64_t n_ent, int dim, float* d_ent_km, int64_t e_pad, void* stream);
+
+/* Query vectors for each (h, r, t, mode) -> d_q_km[K][q_pad]; d_q_true[i] = the
+ * entity the sweep must rank (h for head_batch, t for tail_batch). phase_denom:
+ * RotatE's rel_range/pi as torch evaluates it (RotatE.py:51). */
+int mmre_link_prepare_queries(int model, int norm_flag, const float* d_ent, const float* d_ent_im,
+                              const float* d_rel, const float* d_rel_im, int64_t n_ent, int64_t n_rel,
+                              int dim, float phase_denom, const int64_t* d_qh, const int64_t* d_qr,
+                              const int64_t* d_qt, const int8_t* d_qmode, int64_t n_query, float* d_q_km,
+                              int64_t q_pad, int32_t* d_q_true, void* stream);
+
+/* Per-query threshold and filter bookkeeping, enqueued before the sweep:
+ * zeroes d_counts, writes d_truth[i] = pred(true(i)) with exactly the sweep's
+ * arithmetic, then subtracts from the filtered columns every known entity j of
+ * query i (j != true) with pred(j) < pred(true) -- Test.h:85 `not _find(...)`.
+ * filter CSR: d_filt_off[n_query+1] (int64), d_filt_ids (int32): the known heads
+ *   (head_batch) / tails (tail_batch) of the query in train+valid+test
+ *   (Reader.h:201-226); NULL/NULL = no filtering.
+ * type masks: uint32 [n_rel][ceil(E/32)] bitsets of the relation's allowed heads
+ *   / tails (type_constrain.txt, Reader.h:266-317); NULL/NULL disables.
+ * d_counts: int32 [4][n_query] = raw, filt, raw_tc, filt_tc.
+ * pred_kind: 0 s, 1 m-(m-s), 2 -s, 3 -(m-s)  (DESIGN.md §3). */
+int mmre_link_truth(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
+                    int64_t e_pad, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
+                    const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
+                    const int64_t* d_filt_off, const int32_t* d_filt_ids, const uint32_t* d_type_head,
+                    const uint32_t* d_type_tail, int32_t* d_counts, float* d_truth, void* stream);
+
+/* The sweep (after mmre_link_truth on the same stream). For every query i and
+ * every entity j != true(i):  raw += pred(j) < pred(true)   (Test.h:80-86, strict
+ * <, ties favour the truth), added to the raw AND filtered columns (and the _tc
+ * columns for allowed j when type masks are given, Test.h:88-98).
+ * d_scores (nullable): (n_query, E) predicted values, for parity tests only. */
+int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
+                    int64_t e_pad, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
+                    const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
+                    const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
+                    const float* d_truth, float* d_scores, void* stream);
+
+/* Test.h:232-327 test_link_prediction + getTestLink* (Test.h:356-390), host side,
+ * with the reference's float accumulation order (P14). Counts: int32, column c of
+ * query i at counts[c*stride + i] (c = raw, filt, raw_tc, filt_tc).
+ * h_out[20] = {mrr, mr, hit10, hit3, hit1} x {filter, raw, filter_tc, raw_tc}. */
+int mmre_link_metrics(const int32_t* h_head_counts, const int32_t* h_tail_counts, int64_t n, int64_t stride,
+                      float* h_out);
+
+/* ====================================================================== *
+ *  OpenKE negative sampler (Base.cpp:78-197 sampling/getBatch,           *
+ *  Corrupt.h:7-163 corrupt_head/tail/rel, Random.h:11-29).               *
+ *  Bit-exact: each positive's LCG state is reached by affine jump-ahead  *
+ *  from its thread's seed, so the whole batch samples in parallel.       *
+ * ====================================================================== */
+/* glibc rand() stream after srand(1) (randReset's seeds, Random.h:11-15). */
+int mmre_glibc_rand(int64_t skip, int64_t n, int64_t* h_out);
+/* Advance host-side per-thread LCG states by one sampling() call. */
+int mmre_sampler_advance(uint64_t* h_seeds, int64_t work_threads, int64_t batch_size, int64_t neg_rate,
+                         int64_t neg_rel_rate, int64_t mode);
+/* One sampling() call on the GPU. Index arrays are the Reader.h:53-160 train
+ * index (int64 rows (h, r, t); head_hrt sorted (h,r,t), tail_hrt (t,r,h),
+ * rel_hrt (h,t,r); lef/rig per entity). d_left_mean/d_right_mean NULL = bern off.
+ * d_seeds: per-thread states BEFORE this call (device copy). Outputs int64/f32,
+ * length batch_size * (1 + neg_rate + neg_rel_rate), negative k at [k*B, (k+1)*B). */
+int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                        const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                        const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                        const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                        const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
+                        int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                        int64_t mode, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
+                        float* d_batch_y, void* stream);
+
+/* ====================================================================== *
+ *  Negative-sampling margin loss, fused (OpenKE strategy/NegativeSampling *
+ *  .py:23-32 + loss/MarginLoss.py:24-28 + model forward/regularization;   *
+ *  repo module/NegativeSampling.py:204-229,307-314 + module/loss.py:19-23)*
+ *  Rows: N = B*(1+k), positive b at row b, its negative j at row b+(j+1)B.*
+ *  Entity rows come from d_ent[idx], relation rows from d_rel[ridx].       *
+ * ====================================================================== */
+/* Forward. d_score[N]: model(data) (TransE.py:78-90 etc.); d_loss[0]: margin
+ * loss (+ regul_rate * regularization when regul_rate != 0). adv_temperature
+ * <= 0 disables the self-adversarial weights. d_work: >= mmre_ns_workspace(B, k) floats. */
+int64_t mmre_ns_workspace(int64_t batch, int64_t neg);
+int mmre_ns_forward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
+                    const float* d_ent_im, const float* d_rel, const float* d_rel_im, int dim, float phase_denom,
+                    const int64_t* d_h, const int64_t* d_t, const int64_t* d_r, int64_t batch, int64_t neg,
+                    float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
+                    float* d_work, void* stream);
+/* Backward of the forward above: accumulates d(loss)/d(table) * d_grad_loss[0]
+ * into the dense gradient tables (float atomics). */
+int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
+                     const float* d_ent_im, const float* d_rel, const float* d_rel_im, int dim,
+                     float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r, int64_t batch,
+                     int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
+                     const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
+                     float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
+
+/* ====================================================================== *
+ *  Zero-shot relation-embedding generator (module/model.py:674-686):     *
+ *  cat(noise, cls) -> SN-Linear -> SN-Linear -> SN-Linear ->            *
+ *  LayerNormalization (module/submodule.py:58-77). Spectral norm         *
+ *  (module/spectral_norm.py:39-89): sigma = u . (W v); in training mode  *
+ *  one power iteration first updates u, v in place.                      *
+ * ====================================================================== */
+int64_t mmre_generator_workspace(int64_t n_rows, int in0, int out0, int out1, int out2);
+int mmre_generator_forward(const float* d_noise, int noise_dim, const float* d_cls, int cls_dim,
+                           int64_t n_rows, const float* d_w0, const float* d_b0, float* d_u0, float* d_v0,
+                           int out0, const float* d_w1, const float* d_b1, float* d_u1, float* d_v1, int out1,
+                           const float* d_w2, const float* d_b2, float* d_u2, float* d_v2, int out2,
+                           const float* d_ln_a, const float* d_ln_b, float ln_eps, int power_iteration,
+                           float sn_eps, float* d_out, float* d_work, void* stream);
+
+/* ====================================================================== *
+ *  Candidate-list rankings.                                               *
+ * ====================================================================== */
+/* main.evaluate (main.py:232-250): TransE L1, no normalisation
+ * (module/NegativeSampling.py:294-302): score = |(h + r) - t|_1 for each
+ * candidate of query i (CSR, true tail first); rank = #(s<p) + #(s==p)//2 + 1. */
+int mmre_candidate_rank_transe(const float* d_ent, const float* d_rel, int dim, const int64_t* d_qh,
+                               const int64_t* d_qr, int64_t n_query, const int64_t* d_cand_off,
+                               const int64_t* d_cand_ids, float* d_scores, int32_t* d_rank, void* stream);
+/* ZSLmodule.eval (zsl_module.py:699-706): score = mean_s cos(cand, rel_vec[s]);
+ * rank = 1 + #(score > score[true]) with the true candidate first (tie-free). */
+int mmre_cosine_rank(const float* d_cand, int dim, const int64_t* d_cand_off, int64_t n_query,
+                     const float* d_rel_vecs, int n_samples, const int64_t* d_rel_of_query, float* d_scores,
+                     int32_t* d_rank, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMRE_H */

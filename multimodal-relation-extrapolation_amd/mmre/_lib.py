@@ -1,0 +1,104 @@
+"""ctypes binding of libmmre_hip.so (the C ABI declared in include/mmre.h).
+
+The library is the only compute path: if it is missing or cannot load, every op
+raises -- there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first: libmmre_hip binds to the same libamdhip64.so.7)
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmmre_hip.so")
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+F32 = ctypes.c_float
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "mmre_version": (I32, []),
+    "mmre_link_k": (I64, [I32, I32]),
+    "mmre_link_pad": (I64, [I64]),
+    "mmre_link_prepare_entities": (I32, [I32, I32, P, P, I64, I32, P, I64, P]),
+    "mmre_link_prepare_queries": (I32, [I32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, P, I64, P, I64, P, P]),
+    "mmre_link_truth": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P, P]),
+    "mmre_link_sweep": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P]),
+    "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
+    "mmre_glibc_rand": (I32, [I64, I64, P]),
+    "mmre_sampler_advance": (I32, [P, I64, I64, I64, I64, I64]),
+    "mmre_sampler_openke": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64, I64,
+                                  P, P, P, P, P]),
+    "mmre_ns_workspace": (I64, [I64, I64]),
+    "mmre_ns_forward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
+                              P]),
+    "mmre_ns_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
+                               P, P, P, P, P]),
+    "mmre_generator_workspace": (I64, [I64, I32, I32, I32, I32]),
+    "mmre_generator_forward": (I32, [P, I32, P, I32, I64, P, P, P, P, I32, P, P, P, P, I32, P, P, P, P, I32, P, P,
+                                     F32, I32, F32, P, P, P]),
+    "mmre_candidate_rank_transe": (I32, [P, P, I32, P, P, I64, P, P, P, P, P]),
+    "mmre_cosine_rank": (I32, [P, I32, P, I64, P, I32, P, P, P, P]),
+}
+
+ERRORS = {1: "bad argument", 2: "unknown model", 3: "unsupported shape", 4: "workspace too small"}
+
+_lib = None
+
+
+class MMREError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libmmre_hip.so once; raise loudly when it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MMREError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() "
+                            f"(make -C multimodal-relation-extrapolation_amd). There is no fallback path.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name, None)
+            if fn is None:
+                continue  # call() raises for a symbol this build does not export
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        if rc >= 1000:
+            raise MMREError(f"{what}: HIP error {rc - 1000}")
+        raise MMREError(f"{what}: {ERRORS.get(rc, 'error')} (code {rc})")
+
+
+def call(name: str, *args):
+    fn = getattr(lib(), name, None)
+    if fn is None:
+        raise MMREError(f"{LIB_PATH} does not export {name}: rebuild it")
+    rc = fn(*args)
+    check(rc, name)
+    return rc
+
+
+def ptr(t):
+    """Device/host pointer of a tensor (or None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise MMREError("mmre ops take device tensors (the HIP path is the only path)")

@@ -1,0 +1,42 @@
+"""Build mmre/datasets/*_test.npz from the reference's zero-shot datasets.
+
+Runs in the build container only (reads /root/reference/origin_data, which does not exist on
+the GPU box); the .npz files it writes are committed. They hold only integer ids:
+test_tasks_zsl.json triples mapped through entity2ids_zsl.json and relation2ids.json, in the
+file's relation order (as ZSLmodule / main.evaluate read them, zsl_module.py:146-151).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+SRC = "/root/reference/origin_data"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def convert(name, out):
+    d = os.path.join(SRC, name)
+    e2id = json.load(open(os.path.join(d, "entity2ids_zsl.json")))
+    r2id = json.load(open(os.path.join(d, "relation2ids.json")))
+    tasks = json.load(open(os.path.join(d, "test_tasks_zsl.json")))
+    h, r, t = [], [], []
+    missing = 0
+    for rel, triples in tasks.items():
+        for (a, b, c) in triples:
+            if a not in e2id or c not in e2id or b not in r2id:
+                missing += 1
+                continue
+            h.append(e2id[a]); r.append(r2id[b]); t.append(e2id[c])
+    np.savez_compressed(os.path.join(OUT, out), h=np.array(h, np.int32), r=np.array(r, np.int32),
+                        t=np.array(t, np.int32), n_ent=np.array(len(e2id)), n_rel=np.array(len(r2id)),
+                        missing=np.array(missing))
+    print(name, "triples", len(h), "E", len(e2id), "R", len(r2id), "unmapped", missing,
+          "relations", len(set(r)))
+
+
+if __name__ == "__main__":
+    if not os.path.isdir(SRC):
+        sys.exit("reference data not available")
+    convert("FB15K-237-ZS", "fb15k237zs_test.npz")
+    convert("DB15K-ZS", "db15kzs_test.npz")

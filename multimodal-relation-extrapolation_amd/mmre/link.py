@@ -1,0 +1,223 @@
+"""Link prediction engine: the fused all-entity sweep + rank epilogue on the GPU.
+
+One `LinkSweep.run` call replaces the whole per-query loop of the reference
+Tester (OpenKE/openke/config/Tester.py:70-91): getHeadBatch/getTailBatch
+(Test.h:36-53) -> model.predict (a D2H copy of E scores per query) ->
+testHead/testTail (Test.h:65-192). Here every head- and tail-batch query of the
+evaluation is scored against every entity in one launch sequence, and only the
+integer rank counts come back.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+
+MODEL_IDS = {"transe": 0, "transe_l2": 1, "distmult": 2, "complex": 3, "rotate": 4}
+HEAD, TAIL = 0, 1
+METRIC_NAMES = ["mrr", "mr", "hit10", "hit3", "hit1"]
+GROUPS = ["filter", "raw", "filter_tc", "raw_tc"]
+
+
+@dataclass
+class ScoreSpec:
+    """How a model scores: which kernel, which tables, and predict's transform."""
+    model: str                      # key of MODEL_IDS
+    ent: torch.Tensor               # (E, d) or RotatE (E, 2d); ComplEx: real part
+    rel: torch.Tensor               # (R, d); ComplEx: real part
+    dim: int
+    ent_im: torch.Tensor | None = None
+    rel_im: torch.Tensor | None = None
+    norm_flag: bool = False
+    pred_kind: int = 0              # 0 s, 1 m-(m-s), 2 -s, 3 -(m-s)
+    margin: float = 0.0
+    phase_denom: float = 0.0        # RotatE
+
+
+def rotate_phase_denom(margin: float, epsilon: float, dim: int) -> float:
+    """RotatE.py:51 ``r / (rel_embedding_range.item() / pi)``: torch evaluates the python-float /
+    float32-tensor quotient as ``reciprocal(pi) * range`` in float32."""
+    rng = np.float32((margin + epsilon) / dim)
+    pi = np.float32(3.14159265358979323846)
+    return float(np.float32(np.float32(np.float32(1.0) / pi) * rng))
+
+
+class FilterIndex:
+    """Known-triple index (train + valid + test, Reader.h:201-226) for filtered ranks, and the
+    per-relation type constraints (type_constrain.txt, Reader.h:266-317), as device CSR lists /
+    bitsets for the sweep's epilogue."""
+
+    def __init__(self, h, r, t, n_ent: int, n_rel: int, type_heads=None, type_tails=None):
+        a = np.unique(np.stack([np.asarray(h, np.int64), np.asarray(r, np.int64), np.asarray(t, np.int64)], 1),
+                      axis=0)
+        self.n_ent, self.n_rel = int(n_ent), int(n_rel)
+        # tail filter: (h, r) -> tails ; head filter: (r, t) -> heads
+        self._hr_key = a[:, 0] * n_rel + a[:, 1]
+        o = np.lexsort((a[:, 2], self._hr_key))
+        self._hr_key, self._hr_val = self._hr_key[o], a[o, 2]
+        self._rt_key = a[:, 1] * n_ent + a[:, 2]
+        o = np.lexsort((a[:, 0], self._rt_key))
+        self._rt_key, self._rt_val = self._rt_key[o], a[o, 0]
+        self.type_heads, self.type_tails = type_heads, type_tails
+
+    @staticmethod
+    def _gather(keys, vals, qkeys):
+        s = np.searchsorted(keys, qkeys, "left")
+        e = np.searchsorted(keys, qkeys, "right")
+        ln = e - s
+        off = np.zeros(len(qkeys) + 1, np.int64)
+        np.cumsum(ln, out=off[1:])
+        idx = np.repeat(s - off[:-1], ln) + np.arange(off[-1])
+        return off, vals[idx].astype(np.int32)
+
+    def filters(self, qh, qr, qt, qmode):
+        qh, qr, qt, qmode = (np.asarray(x, np.int64) for x in (qh, qr, qt, qmode))
+        n = len(qh)
+        off = np.zeros(n + 1, np.int64)
+        head = qmode == HEAD
+        lens = np.zeros(n, np.int64)
+        per = [None] * 2
+        if head.any():
+            per[0] = self._gather(self._rt_key, self._rt_val, qr[head] * self.n_ent + qt[head])
+            lens[head] = np.diff(per[0][0])
+        if (~head).any():
+            per[1] = self._gather(self._hr_key, self._hr_val, qh[~head] * self.n_rel + qr[~head])
+            lens[~head] = np.diff(per[1][0])
+        np.cumsum(lens, out=off[1:])
+        ids = np.empty(off[-1], np.int32)
+        # scatter each group's lists into query order
+        for g, mask in ((0, head), (1, ~head)):
+            if per[g] is None:
+                continue
+            goff, gids = per[g]
+            qi = np.nonzero(mask)[0]
+            dst = np.repeat(off[qi] - goff[:-1], np.diff(goff)) + np.arange(goff[-1])
+            ids[dst] = gids
+        return off, ids
+
+    def type_masks(self):
+        if self.type_heads is None:
+            return None
+        words = (self.n_ent + 31) // 32
+        out = []
+        for lists in (self.type_heads, self.type_tails):
+            m = np.zeros((self.n_rel, words * 32), np.uint8)
+            for r, ids in enumerate(lists):
+                ids = np.asarray(ids, np.int64)
+                ids = ids[(ids >= 0) & (ids < self.n_ent)]
+                m[r, ids] = 1
+            w = (m.reshape(self.n_rel, words, 32).astype(np.uint64) << np.arange(32, dtype=np.uint64)).sum(-1)
+            out.append(np.ascontiguousarray(w.astype(np.uint32)))
+        return out
+
+
+class LinkSweep:
+    """Device-resident link-prediction evaluator for one model snapshot."""
+
+    def __init__(self, spec: ScoreSpec):
+        self.spec = spec
+        self.model_id = MODEL_IDS[spec.model]
+        dev = spec.ent.device
+        _lib.require_cuda(spec.ent, spec.rel, spec.ent_im, spec.rel_im)
+        self.device = dev
+        self.n_ent = int(spec.ent.shape[0])
+        self.n_rel = int(spec.rel.shape[0])
+        L = _lib.lib()
+        self.K = int(L.mmre_link_k(self.model_id, spec.dim))
+        self.e_pad = int(L.mmre_link_pad(self.n_ent))
+        self._ent = spec.ent.detach().contiguous().float()
+        self._rel = spec.rel.detach().contiguous().float()
+        self._ent_im = None if spec.ent_im is None else spec.ent_im.detach().contiguous().float()
+        self._rel_im = None if spec.rel_im is None else spec.rel_im.detach().contiguous().float()
+        self.ent_km = torch.empty((self.K, self.e_pad), dtype=torch.float32, device=dev)
+        self.prepared = False
+
+    def prepare_entities(self):
+        s = self.spec
+        call("mmre_link_prepare_entities", self.model_id, int(bool(s.norm_flag)), ptr(self._ent), ptr(self._ent_im),
+             self.n_ent, s.dim, ptr(self.ent_km), self.e_pad, stream_ptr(self.device))
+        self.prepared = True
+
+    def alloc_queries(self, n_query: int):
+        q_pad = int(_lib.lib().mmre_link_pad(n_query))
+        dev = self.device
+        return dict(q_km=torch.empty((self.K, q_pad), dtype=torch.float32, device=dev),
+                    q_true=torch.empty(q_pad, dtype=torch.int32, device=dev),
+                    counts=torch.empty((4, n_query), dtype=torch.int32, device=dev),
+                    truth=torch.empty(n_query, dtype=torch.float32, device=dev), q_pad=q_pad)
+
+    def run(self, qh, qr, qt, qmode, filt=None, type_masks=None, return_scores=False, buffers=None,
+            prepare=True, sweep_events=None):
+        """qh/qr/qt int64 and qmode int8 device tensors. filt: (off int64, ids int32) device CSR.
+        sweep_events: optional (start, end) torch.cuda.Event pair recorded around the sweep kernel alone
+        (on the stream the kernels are launched on).
+        Returns dict(counts=(4, Q) int32 [raw, filt, raw_tc, filt_tc], truth=(Q,), scores=(Q, E)|None)."""
+        s = self.spec
+        n = int(qh.shape[0])
+        if prepare or not self.prepared:
+            self.prepare_entities()
+        b = buffers if buffers is not None else self.alloc_queries(n)
+        st = stream_ptr(self.device)
+        call("mmre_link_prepare_queries", self.model_id, int(bool(s.norm_flag)), ptr(self._ent), ptr(self._ent_im),
+             ptr(self._rel), ptr(self._rel_im), self.n_ent, self.n_rel, s.dim, float(s.phase_denom), ptr(qh),
+             ptr(qr), ptr(qt), ptr(qmode), n, ptr(b["q_km"]), b["q_pad"], ptr(b["q_true"]), st)
+        scores = None
+        if return_scores:
+            scores = torch.empty((n, self.n_ent), dtype=torch.float32, device=self.device)
+        off, ids = (None, None) if filt is None else filt
+        th, tt = (None, None) if type_masks is None else type_masks
+        call("mmre_link_truth", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
+             self.e_pad, ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(off),
+             ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
+        if sweep_events is not None:
+            sweep_events[0].record()
+        call("mmre_link_sweep", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
+             self.e_pad, ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(th),
+             ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(scores), st)
+        if sweep_events is not None:
+            sweep_events[1].record()
+        return dict(counts=b["counts"], truth=b["truth"], scores=scores)
+
+
+def link_metrics(head_counts: np.ndarray, tail_counts: np.ndarray):
+    """Test.h:232-327 metric reduction (host C++ in libmmre, P14 float order).
+    head_counts/tail_counts: (4, n) int32 = raw, filt, raw_tc, filt_tc."""
+    import ctypes
+    h = np.ascontiguousarray(head_counts, np.int32)
+    t = np.ascontiguousarray(tail_counts, np.int32)
+    n = h.shape[1]
+    out = np.zeros(20, np.float32)
+    call("mmre_link_metrics", h.ctypes.data_as(ctypes.c_void_p), t.ctypes.data_as(ctypes.c_void_p), n, n,
+         out.ctypes.data_as(ctypes.c_void_p))
+    return {g: {m: float(out[5 * gi + mi]) for mi, m in enumerate(METRIC_NAMES)} for gi, g in enumerate(GROUPS)}
+
+
+def evaluate_link_prediction(spec: ScoreSpec, test_h, test_r, test_t, index: FilterIndex | None = None,
+                             type_constrain: bool = False):
+    """Full OpenKE link-prediction evaluation in test order (testList sorted by (r, h, t),
+    Reader.h:227). Returns (metrics dict, per-query counts (head, tail) as numpy)."""
+    test_h, test_r, test_t = (np.asarray(x, np.int64) for x in (test_h, test_r, test_t))
+    n = len(test_h)
+    dev = spec.ent.device
+    qh = np.concatenate([test_h, test_h])
+    qr = np.concatenate([test_r, test_r])
+    qt = np.concatenate([test_t, test_t])
+    qm = np.concatenate([np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)])
+    filt = None
+    masks = None
+    if index is not None:
+        off, ids = index.filters(qh, qr, qt, qm)
+        filt = (torch.from_numpy(off).to(dev), torch.from_numpy(ids).to(dev))
+        if type_constrain:
+            tm = index.type_masks()
+            masks = tuple(torch.from_numpy(m).to(dev) for m in tm)
+    sw = LinkSweep(spec)
+    res = sw.run(*(torch.from_numpy(x).to(dev) for x in (qh, qr, qt)), torch.from_numpy(qm).to(dev), filt=filt,
+                 type_masks=masks)
+    counts = res["counts"].cpu().numpy()
+    head, tail = counts[:, :n], counts[:, n:]
+    return link_metrics(head, tail), (head, tail)

@@ -1,0 +1,201 @@
+"""GPU parity of the link-prediction sweep (libmmre_hip.so, through the C ABI) against the
+oracle (oracle/) and the reference's golden vectors (tests/golden/link_small.npz).
+
+Bar: predicted scores bit-identical to the oracle's canonical arithmetic; raw / filtered /
+type-constrained counts exact; Test.h metrics bit-identical to the reference Base.so's on the
+golden dataset; reference torch scores within 1e-4 (relative above 1).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+GOLD_CFG = {
+    "transe": dict(model="transe", norm=True, margin=None),
+    "transe_nonorm_margin": dict(model="transe", norm=False, margin=5.0),
+    "transe_l2": dict(model="transe_l2", norm=True, margin=None),
+    "distmult": dict(model="distmult", norm=False, margin=None),
+    "complex": dict(model="complex", norm=False, margin=None),
+    "rotate": dict(model="rotate", norm=False, margin=6.0),
+}
+
+
+def _spec_from(model, ent, rel, ent_im=None, rel_im=None, norm=False, margin=None, dim=None, eps=2.0):
+    from mmre.link import ScoreSpec, rotate_phase_denom
+    import oracle
+    dev = torch.device("cuda:0")
+    t = lambda a: None if a is None else torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(dev)
+    d = dim if dim is not None else rel.shape[1]
+    pk = oracle.pred_kind(model, margin is not None)
+    pd = rotate_phase_denom(margin, eps, d) if model == "rotate" else 0.0
+    return ScoreSpec(model=model, ent=t(ent), rel=t(rel), dim=d, ent_im=t(ent_im), rel_im=t(rel_im), norm_flag=norm,
+                     pred_kind=pk, margin=float(margin or 0.0), phase_denom=pd)
+
+
+def _tables(g, name):
+    if name == "complex":
+        return (g[f"{name}.ent_re_embeddings.weight"], g[f"{name}.rel_re_embeddings.weight"],
+                g[f"{name}.ent_im_embeddings.weight"], g[f"{name}.rel_im_embeddings.weight"])
+    return g[f"{name}.ent_embeddings.weight"], g[f"{name}.rel_embeddings.weight"], None, None
+
+
+def _run(spec, qh, qr, qt, qm, index=None, tc=False, scores=True):
+    from mmre.link import LinkSweep
+    dev = spec.ent.device
+    filt = masks = None
+    if index is not None:
+        off, ids = index.filters(qh, qr, qt, qm)
+        filt = (torch.from_numpy(off).to(dev), torch.from_numpy(ids).to(dev))
+        if tc:
+            masks = tuple(torch.from_numpy(m).to(dev) for m in index.type_masks())
+    res = LinkSweep(spec).run(*(torch.from_numpy(np.asarray(x, np.int64)).to(dev) for x in (qh, qr, qt)),
+                              torch.from_numpy(np.asarray(qm, np.int8)).to(dev), filt=filt, type_masks=masks,
+                              return_scores=scores)
+    torch.cuda.synchronize()
+    out = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.items()}
+    return out
+
+
+@pytest.mark.parametrize("name", list(GOLD_CFG))
+@pytest.mark.parametrize("tc", [0, 1])
+def test_golden_link_small(golden, oracle_mod, name, tc):
+    from mmre.data import OpenKEDataset
+    from mmre.link import FilterIndex, link_metrics
+    g = golden("link_small")
+    c = GOLD_CFG[name]
+    ent, rel, ent_im, rel_im = _tables(g, name)
+    dim = 16 if name == "rotate" else rel.shape[1]
+    spec = _spec_from(c["model"], ent, rel, ent_im, rel_im, norm=c["norm"], margin=c["margin"], dim=dim)
+    ds = OpenKEDataset(os.path.join(GOLDEN, "data", "small"))
+    index = FilterIndex(*ds.all_triples(), ds.n_ent, ds.n_rel, ds.type_heads, ds.type_tails)
+    qh, qr, qt = g["qh"], g["qr"], g["qt"]
+    n = len(qh)
+    QH, QR, QT = (np.concatenate([x, x]) for x in (qh, qr, qt))
+    QM = np.concatenate([np.zeros(n, np.int8), np.ones(n, np.int8)])
+    out = _run(spec, QH, QR, QT, QM, index=index, tc=bool(tc))
+    okw = dict(ent_im=ent_im, rel_im=rel_im, norm_flag=c["norm"], margin=c["margin"])
+    if c["model"] == "rotate":
+        okw["phase_denom"] = spec.phase_denom
+    trip = np.concatenate([ds.train, ds.valid, ds.test])
+    hrt = oracle_mod.sorted_hrt(trip[:, 0], trip[:, 2], trip[:, 1])
+    counts = {}
+    for side, mode, sl in (("head", "head_batch", slice(0, n)), ("tail", "tail_batch", slice(n, 2 * n))):
+        o_pred = oracle_mod.link_predict(c["model"], mode, ent, rel, qh, qr, qt, **okw)
+        # 1. scores: bit-identical to the oracle (canonical arithmetic), within 1e-4 of the reference
+        assert np.array_equal(out["scores"][sl], o_pred), np.abs(out["scores"][sl] - o_pred).max()
+        ref = g[f"{name}_pred_{side}"]
+        assert np.all(np.abs(out["scores"][sl] - ref) <= 1e-4 * np.maximum(1, np.abs(ref)))
+        # 2. counts: exact vs the oracle's Test.h restatement
+        toff = tids = None
+        if tc:
+            lists = ds.type_heads if side == "head" else ds.type_tails
+            toff = np.cumsum([0] + [len(x) for x in lists])
+            tids = np.concatenate([np.asarray(x, np.int64) for x in lists])
+        o_c = oracle_mod.test_rank(mode, o_pred, qh, qr, qt, hrt, toff, tids)
+        got = out["counts"][:, sl].T
+        cols = [0, 1, 2, 3] if tc else [0, 1]
+        assert np.array_equal(got[:, cols], o_c[:, cols])
+        counts[side] = out["counts"][:, sl]
+    # 3. metrics: Test.h float semantics; equal to the reference Base.so where no near-tie
+    m = link_metrics(counts["head"], counts["tail"])
+    grp = m["filter_tc" if tc else "filter"]
+    got = np.array([grp[k] for k in ("mrr", "mr", "hit10", "hit3", "hit1")], np.float32)
+    ref_counts_equal = (np.array_equal(counts["head"][[0, 1]].T, g[f"{name}_tc{tc}_head_counts"][:, :2]) and
+                        np.array_equal(counts["tail"][[0, 1]].T, g[f"{name}_tc{tc}_tail_counts"][:, :2]))
+    if ref_counts_equal:
+        assert np.array_equal(got, g[f"{name}_tc{tc}_metrics"])
+    # hit@{1,3,10} are count thresholds: they must match the reference exactly
+    assert np.array_equal(got[2:], g[f"{name}_tc{tc}_metrics"][2:])
+
+
+def _random_case(model, E, R, d, Q, seed, norm=False, margin=None, with_ties=False):
+    rng = np.random.default_rng(seed)
+    ent_w = 2 * d if model == "rotate" else d
+    ent = rng.uniform(-0.5, 0.5, (E, ent_w)).astype(np.float32)
+    rel = rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32)
+    ent_im = rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32) if model == "complex" else None
+    rel_im = rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32) if model == "complex" else None
+    qh = rng.integers(0, E, Q)
+    qr = rng.integers(0, R, Q)
+    qt = rng.integers(0, E, Q)
+    qm = rng.integers(0, 2, Q).astype(np.int8)
+    if with_ties:  # duplicate rows: exact ties with the truth must not count (strict <)
+        for i in range(0, Q, 7):
+            tgt = qh[i] if qm[i] == 0 else qt[i]
+            dup = (tgt + 1 + i) % E
+            ent[dup] = ent[tgt]
+            if ent_im is not None:
+                ent_im[dup] = ent_im[tgt]
+    return ent, rel, ent_im, rel_im, qh, qr, qt, qm
+
+
+@pytest.mark.parametrize("model,E,d,Q,norm,margin", [
+    ("transe", 1000, 200, 300, True, None),
+    ("transe", 333, 100, 129, False, 4.0),
+    ("transe", 129, 7, 1, True, None),
+    ("transe_l2", 700, 64, 257, True, None),
+    ("distmult", 1000, 200, 300, False, None),
+    ("distmult", 250, 13, 77, False, None),
+    ("complex", 900, 200, 200, False, None),
+    ("rotate", 600, 64, 150, False, 6.0),
+])
+def test_random_bit_exact(oracle_mod, model, E, d, Q, norm, margin):
+    from mmre.link import FilterIndex
+    ent, rel, ent_im, rel_im, qh, qr, qt, qm = _random_case(model, E, 11, d, Q, seed=E + d + Q, norm=norm,
+                                                            margin=margin, with_ties=True)
+    spec = _spec_from(model, ent, rel, ent_im, rel_im, norm=norm, margin=margin, dim=d)
+    rng = np.random.default_rng(5)
+    th, tr, tt = rng.integers(0, E, 4 * E), rng.integers(0, 11, 4 * E), rng.integers(0, E, 4 * E)
+    th = np.concatenate([th, qh]); tr = np.concatenate([tr, qr]); tt = np.concatenate([tt, qt])
+    index = FilterIndex(th, tr, tt, E, 11)
+    out = _run(spec, qh, qr, qt, qm, index=index)
+    hrt = oracle_mod.sorted_hrt(th, tr, tt)
+    okw = dict(ent_im=ent_im, rel_im=rel_im, norm_flag=norm, margin=margin,
+               phase_denom=spec.phase_denom)
+    for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+        sel = qm == mode_id
+        if not sel.any():
+            continue
+        o_pred = oracle_mod.link_predict(model, mode, ent, rel, qh[sel], qr[sel], qt[sel], **okw)
+        assert np.array_equal(out["scores"][sel], o_pred)
+        o_c = oracle_mod.test_rank(mode, o_pred, qh[sel], qr[sel], qt[sel], hrt)
+        assert np.array_equal(out["counts"][:, sel].T[:, :2], o_c[:, :2])
+        tv = out["truth"][sel]
+        truth_ids = qh[sel] if mode_id == 0 else qt[sel]
+        assert np.array_equal(tv, o_pred[np.arange(sel.sum()), truth_ids])
+
+
+def test_full_size_c2_properties(oracle_mod):
+    """BASELINE config C2 at full size (FB15K-237-ZS, E=14,208, d=200, Q=35,192 sweeps):
+    size-independent properties on every query + oracle parity on a seeded subset."""
+    from mmre.data import load_zs_test
+    from mmre.link import FilterIndex
+    z = load_zs_test("FB15K-237-ZS")
+    E, R = int(z["n_ent"]), int(z["n_rel"])
+    rng = np.random.default_rng(0)
+    bound = np.sqrt(6.0 / (E + 200))
+    ent = rng.uniform(-bound, bound, (E, 200)).astype(np.float32)
+    rel = rng.uniform(-np.sqrt(6.0 / (R + 200)), np.sqrt(6.0 / (R + 200)), (R, 200)).astype(np.float32)
+    h, r, t = z["h"].astype(np.int64), z["r"].astype(np.int64), z["t"].astype(np.int64)
+    n = len(h)
+    qh, qr, qt = np.concatenate([h, h]), np.concatenate([r, r]), np.concatenate([t, t])
+    qm = np.concatenate([np.zeros(n, np.int8), np.ones(n, np.int8)])
+    index = FilterIndex(h, r, t, E, R)
+    spec = _spec_from("transe", ent, rel, norm=True, dim=200)
+    out = _run(spec, qh, qr, qt, qm, index=index, scores=False)
+    c = out["counts"]
+    assert np.all(c[0] >= c[1]) and np.all(c[1] >= 0) and np.all(c[0] <= E - 1)
+    off, ids = index.filters(qh, qr, qt, qm)
+    assert np.all(c[0] - c[1] <= np.diff(off))
+    sub = rng.choice(2 * n, 48, replace=False)
+    hrt = oracle_mod.sorted_hrt(h, r, t)
+    for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+        s = sub[qm[sub] == mode_id]
+        o_pred = oracle_mod.link_predict("transe", mode, ent, rel, qh[s], qr[s], qt[s], norm_flag=True)
+        o_c = oracle_mod.test_rank(mode, o_pred, qh[s], qr[s], qt[s], hrt)
+        assert np.array_equal(c[:, s].T[:, :2], o_c[:, :2])
