@@ -62,20 +62,24 @@ int64_t mmre_link_k(int model, int dim);
 /* Padded entity / query counts used by the k-major planes. */
 int64_t mmre_link_pad(int64_t n);
 
-/* Entity table -> k-major plane d_ent_km[K][e_pad] (F.normalize first when
- * norm_flag, TransE.py:63-66). Tables: TransE/DistMult (E, d); ComplEx re/im
- * (E, d) each; RotatE (E, 2d) = [re | im] (RotatE.py:48-49). */
+/* Entity table -> k-major planes d_ent_km[K][e_pad] for the sweep and the same
+ * values row-major in d_ent_rows[n_ent][K] for per-entity gathers (F.normalize
+ * first when norm_flag, TransE.py:63-66). Tables: TransE/DistMult (E, d);
+ * ComplEx re/im (E, d) each; RotatE (E, 2d) = [re | im] (RotatE.py:48-49). */
 int mmre_link_prepare_entities(int model, int norm_flag, const float* d_ent, const float* d_ent_im,
-                               int64_t n_ent, int dim, float* d_ent_km, int64_t e_pad, void* stream);
+                               int64_t n_ent, int dim, float* d_ent_km, int64_t e_pad, float* d_ent_rows,
+                               void* stream);
 
-/* Query vectors for each (h, r, t, mode) -> d_q_km[K][q_pad]; d_q_true[i] = the
- * entity the sweep must rank (h for head_batch, t for tail_batch). phase_denom:
- * RotatE's rel_range/pi as torch evaluates it (RotatE.py:51). */
-int mmre_link_prepare_queries(int model, int norm_flag, const float* d_ent, const float* d_ent_im,
-                              const float* d_rel, const float* d_rel_im, int64_t n_ent, int64_t n_rel,
-                              int dim, float phase_denom, const int64_t* d_qh, const int64_t* d_qr,
-                              const int64_t* d_qt, const int8_t* d_qmode, int64_t n_query, float* d_q_km,
-                              int64_t q_pad, int32_t* d_q_true, void* stream);
+/* Query vectors for each (h, r, t, mode) -> d_q_km[K][q_pad] (element-wise from the
+ * prepared d_ent_rows); d_q_true[i] = the entity the sweep must rank (h for
+ * head_batch, t for tail_batch). d_rel_work: (n_rel, d) floats, required for
+ * TransE with norm_flag (normalised relation rows). phase_denom: RotatE's
+ * rel_range/pi as torch evaluates it (RotatE.py:51). */
+int mmre_link_prepare_queries(int model, int norm_flag, const float* d_ent_rows, const float* d_rel,
+                              const float* d_rel_im, int64_t n_ent, int64_t n_rel, int dim, float phase_denom,
+                              const int64_t* d_qh, const int64_t* d_qr, const int64_t* d_qt,
+                              const int8_t* d_qmode, int64_t n_query, float* d_q_km, int64_t q_pad,
+                              int32_t* d_q_true, float* d_rel_work, void* stream);
 
 /* Per-query threshold and filter bookkeeping, enqueued before the sweep:
  * zeroes d_counts, writes d_truth[i] = pred(true(i)) with exactly the sweep's
@@ -89,7 +93,7 @@ int mmre_link_prepare_queries(int model, int norm_flag, const float* d_ent, cons
  * d_counts: int32 [4][n_query] = raw, filt, raw_tc, filt_tc.
  * pred_kind: 0 s, 1 m-(m-s), 2 -s, 3 -(m-s)  (DESIGN.md §3). */
 int mmre_link_truth(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
-                    int64_t e_pad, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
+                    int64_t e_pad, const float* d_ent_rows, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
                     const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
                     const int64_t* d_filt_off, const int32_t* d_filt_ids, const uint32_t* d_type_head,
                     const uint32_t* d_type_tail, int32_t* d_counts, float* d_truth, void* stream);

@@ -11,7 +11,7 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime first: libmmre_hip binds to the same libamdhip64.so.7)
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libmmre_hip.so")
+LIB_PATH = os.environ.get("MMRE_LIB") or os.path.join(LIB_DIR, "libmmre_hip.so")
 
 P = ctypes.c_void_p
 I64 = ctypes.c_int64
@@ -23,9 +23,9 @@ SIGNATURES = {
     "mmre_version": (I32, []),
     "mmre_link_k": (I64, [I32, I32]),
     "mmre_link_pad": (I64, [I64]),
-    "mmre_link_prepare_entities": (I32, [I32, I32, P, P, I64, I32, P, I64, P]),
-    "mmre_link_prepare_queries": (I32, [I32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, P, I64, P, I64, P, P]),
-    "mmre_link_truth": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P, P]),
+    "mmre_link_prepare_entities": (I32, [I32, I32, P, P, I64, I32, P, I64, P, P]),
+    "mmre_link_prepare_queries": (I32, [I32, I32, P, P, P, I64, I64, I32, F32, P, P, P, P, I64, P, I64, P, P, P]),
+    "mmre_link_truth": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, P, I64, I64, I32, P, P, P, P, P, P, P]),
     "mmre_link_sweep": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P]),
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
     "mmre_glibc_rand": (I32, [I64, I64, P]),

@@ -134,12 +134,14 @@ class LinkSweep:
         self._ent_im = None if spec.ent_im is None else spec.ent_im.detach().contiguous().float()
         self._rel_im = None if spec.rel_im is None else spec.rel_im.detach().contiguous().float()
         self.ent_km = torch.empty((self.K, self.e_pad), dtype=torch.float32, device=dev)
+        self.ent_rows = torch.empty((self.n_ent, self.K), dtype=torch.float32, device=dev)
+        self.rel_work = torch.empty((self.n_rel, spec.dim), dtype=torch.float32, device=dev)
         self.prepared = False
 
     def prepare_entities(self):
         s = self.spec
         call("mmre_link_prepare_entities", self.model_id, int(bool(s.norm_flag)), ptr(self._ent), ptr(self._ent_im),
-             self.n_ent, s.dim, ptr(self.ent_km), self.e_pad, stream_ptr(self.device))
+             self.n_ent, s.dim, ptr(self.ent_km), self.e_pad, ptr(self.ent_rows), stream_ptr(self.device))
         self.prepared = True
 
     def alloc_queries(self, n_query: int):
@@ -162,16 +164,16 @@ class LinkSweep:
             self.prepare_entities()
         b = buffers if buffers is not None else self.alloc_queries(n)
         st = stream_ptr(self.device)
-        call("mmre_link_prepare_queries", self.model_id, int(bool(s.norm_flag)), ptr(self._ent), ptr(self._ent_im),
-             ptr(self._rel), ptr(self._rel_im), self.n_ent, self.n_rel, s.dim, float(s.phase_denom), ptr(qh),
-             ptr(qr), ptr(qt), ptr(qmode), n, ptr(b["q_km"]), b["q_pad"], ptr(b["q_true"]), st)
+        call("mmre_link_prepare_queries", self.model_id, int(bool(s.norm_flag)), ptr(self.ent_rows), ptr(self._rel),
+             ptr(self._rel_im), self.n_ent, self.n_rel, s.dim, float(s.phase_denom), ptr(qh), ptr(qr), ptr(qt),
+             ptr(qmode), n, ptr(b["q_km"]), b["q_pad"], ptr(b["q_true"]), ptr(self.rel_work), st)
         scores = None
         if return_scores:
             scores = torch.empty((n, self.n_ent), dtype=torch.float32, device=self.device)
         off, ids = (None, None) if filt is None else filt
         th, tt = (None, None) if type_masks is None else type_masks
         call("mmre_link_truth", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
-             self.e_pad, ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(off),
+             self.e_pad, ptr(self.ent_rows), ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(off),
              ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
         if sweep_events is not None:
             sweep_events[0].record()
