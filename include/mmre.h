@@ -124,6 +124,8 @@ int mmre_link_metrics(const int32_t* h_head_counts, const int32_t* h_tail_counts
  * ====================================================================== */
 /* glibc rand() stream after srand(1) (randReset's seeds, Random.h:11-15). */
 int mmre_glibc_rand(int64_t skip, int64_t n, int64_t* h_out);
+/* LCG draws one positive consumes in getBatch (Base.cpp:103-146). */
+int64_t mmre_sampler_draws_per_positive(int64_t neg_rate, int64_t neg_rel_rate, int64_t mode);
 /* Advance host-side per-thread LCG states by one sampling() call. */
 int mmre_sampler_advance(uint64_t* h_seeds, int64_t work_threads, int64_t batch_size, int64_t neg_rate,
                          int64_t neg_rel_rate, int64_t mode);
@@ -140,6 +142,20 @@ int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const 
                         int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
                         int64_t mode, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
                         float* d_batch_y, void* stream);
+
+/* The repo's per-edge filtered sampler (module/NegativeSampling.py:114-140,
+ * 321-375): per positive edge b (local ids d_eh/d_et, relation d_er), neg
+ * negatives split head/tail by Bernoulli(0.5); candidates uniform over the local
+ * node list [0, n_local) (NegativeSampling.py:210), rejected when their global id
+ * (d_local_to_global, NULL = identity) is a known head of (t, r) (key t*n_rel+r in
+ * the d_hf_* CSR over sorted keys) or a known tail of (h, r) (d_tf_*), distinct
+ * within the positive. Counter-based (SplitMix64) draws from `seed` replace the
+ * reference's unseeded Python `random` (P13). Output [pos | neg_1 | ... | neg_k]. */
+int mmre_sampler_repo(const int64_t* d_eh, const int64_t* d_et, const int64_t* d_er, int64_t batch, int64_t neg,
+                      int64_t n_local, const int64_t* d_local_to_global, int64_t n_rel, const int64_t* d_hf_keys,
+                      const int64_t* d_hf_off, const int64_t* d_hf_vals, int64_t hf_n, const int64_t* d_tf_keys,
+                      const int64_t* d_tf_off, const int64_t* d_tf_vals, int64_t tf_n, uint64_t seed,
+                      int filter_flag, int64_t* d_out_h, int64_t* d_out_t, int64_t* d_out_r, void* stream);
 
 /* ====================================================================== *
  *  Negative-sampling margin loss, fused (OpenKE strategy/NegativeSampling *

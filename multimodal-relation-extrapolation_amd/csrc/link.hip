@@ -283,7 +283,7 @@ __global__ __launch_bounds__(64) void k_filter_correct(
 // double-buffered steps of 8 rows (16 B per thread per plane per operand). Per-query
 // counts stay in registers until the workgroup moves to the next query tile.
 template <int OP, bool TC, bool STORE>
-__global__ __launch_bounds__(NT, 4) void k_sweep_valu(
+__global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
     int64_t q_pad, int64_t n_query, int kp, int n_et, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,

@@ -1,0 +1,262 @@
+// sampler.hip -- negative samplers on the GPU.
+//
+// 1. OpenKE's filtered sampler (Base.cpp:78-197 getBatch/sampling, Corrupt.h:7-163,
+//    Random.h:11-29), bit-exact. The reference runs `workThreads` pthreads, thread `id`
+//    filling the slice [lef, rig) of the batch sequentially from its own 64-bit LCG
+//    (next = next * 25214903917 + 11). Every positive consumes a FIXED number of draws
+//    (1 + 2*neg_rate in mode 0, 1 + neg_rate otherwise, + neg_rel_rate), so the state at
+//    the start of positive b is the thread seed advanced by (b - lef) * draws via an
+//    affine jump-ahead: one GPU thread per positive, same outputs as the pthreads.
+// 2. The repo's per-edge sampler (module/NegativeSampling.py:114-140, 321-375): per
+//    positive, Bernoulli(0.5) head/tail split of the neg_ent negatives, candidates drawn
+//    uniformly from the local node list [0, n_local) (NegativeSampling.py:210) and rejected
+//    when their global id is a known head of (t, r) / tail of (h, r) (filter_flag), distinct
+//    within a positive. The reference's draws come from the unseeded Python `random` (P13),
+//    so parity is distributional; this kernel uses a counter-based generator (SplitMix64) so
+//    a given seed is reproducible.
+#include "mmre_common.h"
+
+namespace mmre {
+
+__device__ __forceinline__ uint64_t lcg_next(uint64_t* st) {
+  *st = *st * 25214903917ULL + 11ULL;
+  return *st;
+}
+__device__ __forceinline__ int64_t rand_max(uint64_t* st, int64_t x) {
+  return (int64_t)(lcg_next(st) % (uint64_t)x);
+}
+__device__ uint64_t lcg_jump(uint64_t x, uint64_t n) {
+  uint64_t A = 1, C = 0, a = 25214903917ULL, c = 11ULL;
+  while (n) {
+    if (n & 1) { A = A * a; C = C * a + c; }
+    c = c * a + c;
+    a = a * a;
+    n >>= 1;
+  }
+  return A * x + C;
+}
+
+// corrupt_head (Corrupt.h:7-43): uniform entity not among the known TAILS of (h, r),
+// found by skipping the sorted tails of the (h, r) block of trainHead.
+__device__ int64_t corrupt_head(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_head,
+                                const int64_t* __restrict__ rig_head, int64_t n_ent, uint64_t* st, int64_t h,
+                                int64_t r) {
+  int64_t lef = lef_head[h] - 1, rig = rig_head[h], mid, ll, rr;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] >= r) rig = mid; else lef = mid; }
+  ll = rig;
+  lef = lef_head[h]; rig = rig_head[h] + 1;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] <= r) lef = mid; else rig = mid; }
+  rr = lef;
+  const int64_t tmp = rand_max(st, n_ent - (rr - ll + 1));
+  if (tmp < T[3 * ll + 2]) return tmp;
+  if (tmp > T[3 * rr + 2] - rr + ll - 1) return tmp + rr - ll + 1;
+  lef = ll; rig = rr + 1;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
+  return tmp + lef - ll + 1;
+}
+
+// corrupt_tail (Corrupt.h:45-81): uniform entity not among the known HEADS of (t, r);
+// T rows are (h, r, t) sorted by (t, r, h).
+__device__ int64_t corrupt_tail(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_tail,
+                                const int64_t* __restrict__ rig_tail, int64_t n_ent, uint64_t* st, int64_t t,
+                                int64_t r) {
+  int64_t lef = lef_tail[t] - 1, rig = rig_tail[t], mid, ll, rr;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] >= r) rig = mid; else lef = mid; }
+  ll = rig;
+  lef = lef_tail[t]; rig = rig_tail[t] + 1;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] <= r) lef = mid; else rig = mid; }
+  rr = lef;
+  const int64_t tmp = rand_max(st, n_ent - (rr - ll + 1));
+  if (tmp < T[3 * ll + 0]) return tmp;
+  if (tmp > T[3 * rr + 0] - rr + ll - 1) return tmp + rr - ll + 1;
+  lef = ll; rig = rr + 1;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 0] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
+  return tmp + lef - ll + 1;
+}
+
+// corrupt_rel with p == false (Corrupt.h:85-162); T rows (h, r, t) sorted by (h, t, r).
+__device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_rel,
+                               const int64_t* __restrict__ rig_rel, int64_t n_rel, uint64_t* st, int64_t h, int64_t t,
+                               int64_t r) {
+  (void)r;
+  int64_t lef = lef_rel[h] - 1, rig = rig_rel[h], mid, ll, rr;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] >= t) rig = mid; else lef = mid; }
+  ll = rig;
+  lef = lef_rel[h]; rig = rig_rel[h] + 1;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] <= t) lef = mid; else rig = mid; }
+  rr = lef;
+  const int64_t tmp = rand_max(st, n_rel - (rr - ll + 1));
+  if (tmp < T[3 * ll + 1]) return tmp;
+  if (tmp > T[3 * rr + 1] - rr + ll - 1) return tmp + rr - ll + 1;
+  lef = ll; rig = rr + 1;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
+  return tmp + lef - ll + 1;
+}
+
+__global__ void k_sampler_openke(const int64_t* __restrict__ train_list, int64_t train_total,
+                                 const int64_t* __restrict__ head_hrt, const int64_t* __restrict__ tail_hrt,
+                                 const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
+                                 const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail,
+                                 const int64_t* __restrict__ rig_tail, const int64_t* __restrict__ lef_rel,
+                                 const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
+                                 const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel,
+                                 const uint64_t* __restrict__ seeds, int64_t work_threads, int64_t B, int64_t neg,
+                                 int64_t neg_rel, int64_t mode, int64_t* __restrict__ bh, int64_t* __restrict__ bt,
+                                 int64_t* __restrict__ br, float* __restrict__ by) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  // slice of the reference's pthread `id` that owns position b (Base.cpp:93-100)
+  int64_t id, lef;
+  if (B % work_threads == 0) {
+    const int64_t per = B / work_threads;
+    id = b / per;
+    lef = id * per;
+  } else {
+    const int64_t per = B / work_threads + 1;
+    id = b / per;
+    lef = id * per;
+  }
+  const int64_t draws = 1 + (mode == 0 ? 2 : 1) * neg + neg_rel;
+  uint64_t st = lcg_jump(seeds[id], (uint64_t)((b - lef) * draws));
+  const int64_t i = rand_max(&st, train_total);
+  const int64_t h = train_list[3 * i], r = train_list[3 * i + 1], t = train_list[3 * i + 2];
+  bh[b] = h; bt[b] = t; br[b] = r; by[b] = 1.0f;
+  int64_t last = B;
+  for (int64_t k = 0; k < neg; ++k) {
+    bool replace_tail;
+    if (mode == 0) {
+      float prob = 500.0f;
+      if (left_mean) prob = 1000.0f * right_mean[r] / (right_mean[r] + left_mean[r]);
+      replace_tail = (float)(lcg_next(&st) % 1000ULL) < prob;
+    } else {
+      replace_tail = mode != -1;
+    }
+    if (replace_tail) {  // corrupt_head returns a replacement TAIL (Base.cpp:116)
+      bh[b + last] = h; bt[b + last] = corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r); br[b + last] = r;
+    } else {
+      bh[b + last] = corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r); bt[b + last] = t; br[b + last] = r;
+    }
+    by[b + last] = -1.0f;
+    last += B;
+  }
+  for (int64_t k = 0; k < neg_rel; ++k) {
+    bh[b + last] = h; bt[b + last] = t; br[b + last] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r);
+    by[b + last] = -1.0f;
+    last += B;
+  }
+}
+
+// ---------------------------------------------------------------- repo sampler --
+__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+// Is global entity g in the sorted value list of `key` (CSR over sorted keys)?
+__device__ bool in_filter(const int64_t* __restrict__ keys, const int64_t* __restrict__ off,
+                          const int64_t* __restrict__ vals, int64_t n_keys, int64_t key, int64_t g) {
+  int64_t lo = 0, hi = n_keys;
+  while (lo < hi) { int64_t mid = (lo + hi) >> 1; if (keys[mid] < key) lo = mid + 1; else hi = mid; }
+  if (lo >= n_keys || keys[lo] != key) return false;
+  int64_t a = off[lo], b = off[lo + 1];
+  while (a < b) { int64_t mid = (a + b) >> 1; if (vals[mid] < g) a = mid + 1; else b = mid; }
+  return a < off[lo + 1] && vals[a] == g;
+}
+
+__global__ void k_sampler_repo(const int64_t* __restrict__ eh, const int64_t* __restrict__ et,
+                               const int64_t* __restrict__ er, int64_t B, int64_t neg, int64_t n_local,
+                               const int64_t* __restrict__ local_to_global, int64_t n_rel,
+                               const int64_t* __restrict__ hf_keys, const int64_t* __restrict__ hf_off,
+                               const int64_t* __restrict__ hf_vals, int64_t hf_n,
+                               const int64_t* __restrict__ tf_keys, const int64_t* __restrict__ tf_off,
+                               const int64_t* __restrict__ tf_vals, int64_t tf_n, uint64_t seed, int filter_flag,
+                               int64_t* __restrict__ out_h, int64_t* __restrict__ out_t, int64_t* __restrict__ out_r) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int64_t h = eh[b], t = et[b], r = er[b];
+  out_h[b] = h; out_t[b] = t; out_r[b] = r;
+  uint64_t ctr = splitmix(seed ^ (uint64_t)b * 0xD1B54A32D192ED03ULL);
+  // Bernoulli(0.5) split (NegativeSampling.py:324-329): heads first, then tails
+  int64_t n_head = 0;
+  for (int64_t k = 0; k < neg; ++k) {
+    ctr = splitmix(ctr);
+    n_head += (ctr >> 11) * (1.0 / 9007199254740992.0) < 0.5;
+  }
+  const int64_t gh = local_to_global ? local_to_global[h] : h;
+  const int64_t gt = local_to_global ? local_to_global[t] : t;
+  for (int64_t k = 0; k < neg; ++k) {
+    const bool corrupt_h = k < n_head;
+    int64_t cand = 0;
+    for (int tries = 0; tries < 4096; ++tries) {
+      ctr = splitmix(ctr);
+      cand = (int64_t)(ctr % (uint64_t)n_local);
+      const int64_t g = local_to_global ? local_to_global[cand] : cand;
+      bool bad = false;
+      if (filter_flag) {
+        bad = corrupt_h ? in_filter(hf_keys, hf_off, hf_vals, hf_n, gt * n_rel + r, g)
+                        : in_filter(tf_keys, tf_off, tf_vals, tf_n, gh * n_rel + r, g);
+      }
+      for (int64_t j = 0; j < k && !bad; ++j) {  // distinct within a positive (random.sample)
+        const bool same_side = (j < n_head) == corrupt_h;
+        if (same_side) bad = (corrupt_h ? out_h[b + (j + 1) * B] : out_t[b + (j + 1) * B]) == cand;
+      }
+      if (!bad) break;
+    }
+    const int64_t row = b + (k + 1) * B;
+    out_h[row] = corrupt_h ? cand : h;
+    out_t[row] = corrupt_h ? t : cand;
+    out_r[row] = r;
+  }
+}
+
+}  // namespace mmre
+
+using namespace mmre;
+
+extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                   const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
+                                   int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                                   int64_t mode, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
+                                   float* d_batch_y, void* stream) {
+  if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
+      !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y)
+    return MMRE_ERR_ARG;
+  if (neg_rel_rate > 0 && (!d_rel_hrt || !d_lef_rel || !d_rig_rel)) return MMRE_ERR_ARG;
+  if ((d_left_mean == nullptr) != (d_right_mean == nullptr)) return MMRE_ERR_ARG;
+  if (train_total <= 0 || n_ent <= 1 || work_threads <= 0 || batch_size <= 0 || neg_rate < 0 || neg_rel_rate < 0)
+    return MMRE_ERR_ARG;
+  if (mode < -1 || mode > 1) return MMRE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int threads = 256;
+  hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((batch_size + threads - 1) / threads)), dim3(threads), 0, st,
+                     d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
+                     d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
+                     work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_batch_h, d_batch_t, d_batch_r,
+                     d_batch_y);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_sampler_repo(const int64_t* d_eh, const int64_t* d_et, const int64_t* d_er, int64_t batch,
+                                 int64_t neg, int64_t n_local, const int64_t* d_local_to_global, int64_t n_rel,
+                                 const int64_t* d_hf_keys, const int64_t* d_hf_off, const int64_t* d_hf_vals,
+                                 int64_t hf_n, const int64_t* d_tf_keys, const int64_t* d_tf_off,
+                                 const int64_t* d_tf_vals, int64_t tf_n, uint64_t seed, int filter_flag,
+                                 int64_t* d_out_h, int64_t* d_out_t, int64_t* d_out_r, void* stream) {
+  if (!d_eh || !d_et || !d_er || !d_out_h || !d_out_t || !d_out_r || batch <= 0 || neg < 0 || n_local <= 0)
+    return MMRE_ERR_ARG;
+  if (filter_flag && (!d_hf_keys || !d_hf_off || !d_hf_vals || !d_tf_keys || !d_tf_off || !d_tf_vals))
+    return MMRE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int threads = 64;
+  hipLaunchKernelGGL(k_sampler_repo, dim3((unsigned)((batch + threads - 1) / threads)), dim3(threads), 0, st, d_eh,
+                     d_et, d_er, batch, neg, n_local, d_local_to_global, n_rel, d_hf_keys, d_hf_off, d_hf_vals, hf_n,
+                     d_tf_keys, d_tf_off, d_tf_vals, tf_n, seed, filter_flag, d_out_h, d_out_t, d_out_r);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}

@@ -87,3 +87,50 @@ def load_zs_test(name: str):
     fn = {"FB15K-237-ZS": "fb15k237zs_test.npz", "DB15K-ZS": "db15kzs_test.npz"}[name]
     with np.load(os.path.join(DATASETS_DIR, fn), allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+class TrainIndex:
+    """The training-triple index of importTrainFiles (Reader.h:53-160), as arrays:
+
+    train_list  unique (h, r, t) rows in cmp_head order (h, r, t)        -- trainList
+    head_hrt    same order                                               -- trainHead
+    tail_hrt    rows sorted by (t, r, h)                                 -- trainTail
+    rel_hrt     rows sorted by (h, t, r)                                 -- trainRel
+    lef/rig_*   first / last row of each entity's block (rig = -1 when absent)
+    left_mean / right_mean   per relation, freq / #distinct heads|tails  (bern, Reader.h:142-159)
+    """
+
+    def __init__(self, h, t, r, n_ent: int, n_rel: int):
+        a = np.stack([np.asarray(h, np.int64), np.asarray(r, np.int64), np.asarray(t, np.int64)], 1)
+        a = np.unique(a, axis=0)
+        self.n_ent, self.n_rel = int(n_ent), int(n_rel)
+        self.train_list = a
+        self.head_hrt = a
+        self.tail_hrt = a[np.lexsort((a[:, 0], a[:, 1], a[:, 2]))]
+        self.rel_hrt = a[np.lexsort((a[:, 1], a[:, 2], a[:, 0]))]
+        self.lef_head, self.rig_head = self._block(self.head_hrt[:, 0])
+        self.lef_tail, self.rig_tail = self._block(self.tail_hrt[:, 2])
+        self.lef_rel, self.rig_rel = self._block(self.rel_hrt[:, 0])
+        freq = np.bincount(a[:, 1], minlength=n_rel).astype(np.float32)
+        lcount = np.bincount(np.unique(a[:, :2], axis=0)[:, 1], minlength=n_rel).astype(np.float32)
+        rcount = np.bincount(np.unique(a[:, [2, 1]], axis=0)[:, 1], minlength=n_rel).astype(np.float32)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            self.left_mean = (freq / lcount).astype(np.float32)
+            self.right_mean = (freq / rcount).astype(np.float32)
+
+    def _block(self, keys):
+        n = keys.shape[0]
+        lef = np.zeros(self.n_ent, np.int64)
+        rig = np.full(self.n_ent, -1, np.int64)
+        first = np.ones(n, bool)
+        first[1:] = keys[1:] != keys[:-1]
+        last = np.ones(n, bool)
+        last[:-1] = keys[1:] != keys[:-1]
+        idx = np.arange(n)
+        lef[keys[first]] = idx[first]
+        rig[keys[last]] = idx[last]
+        return lef, rig
+
+    @property
+    def train_total(self) -> int:
+        return int(self.train_list.shape[0])

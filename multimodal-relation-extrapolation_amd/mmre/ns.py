@@ -1,0 +1,97 @@
+"""Fused negative-sampling margin loss (csrc/ns.hip) as a torch.autograd.Function.
+
+forward  = model(data) in 'normal' mode for B*(1+k) rows -> MarginLoss (optionally
+           self-adversarial) + regul_rate * regularization, one launch + one fixed-order
+           reduction (OpenKE strategy/NegativeSampling.py:23-32, MarginLoss.py:24-28,
+           TransE.py:92-102; repo module/NegativeSampling.py:204-229).
+backward = d(loss)/d(embedding tables) scattered into dense gradient tables (float atomics).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import call, lib, ptr, require_cuda, stream_ptr
+
+MODEL_IDS = {"transe": 0, "transe_l2": 1, "distmult": 2, "complex": 3, "rotate": 4}
+
+
+class NSSpec:
+    """Static description of how rows are scored (the model's forward in 'normal' mode)."""
+
+    def __init__(self, model: str, dim: int, norm_flag: bool = False, model_margin: float | None = None,
+                 phase_denom: float = 0.0):
+        self.model = model
+        self.model_id = MODEL_IDS[model]
+        self.dim = int(dim)
+        self.norm_flag = bool(norm_flag)
+        self.use_model_margin = model_margin is not None
+        self.model_margin = float(model_margin or 0.0)
+        self.phase_denom = float(phase_denom)
+
+
+def _scalar_args(spec, batch, neg, loss_margin, adv_t, regul_rate):
+    return (spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin))
+
+
+class _FusedNS(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate):
+        dev = ent.device
+        N = batch * (1 + neg)
+        score = torch.empty(N, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        work = torch.empty(int(lib().mmre_ns_workspace(batch, neg)), dtype=torch.float32, device=dev)
+        call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
+             ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
+             batch, neg, float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(loss), ptr(work),
+             stream_ptr(dev))
+        ctx.save_for_backward(ent, rel, ent_im if ent_im is not None else ent, rel_im if rel_im is not None else rel,
+                              h, t, r, score)
+        ctx.has_im = ent_im is not None
+        ctx.cfg = (spec, batch, neg, loss_margin, adv_t, regul_rate)
+        ctx.mark_non_differentiable(score)
+        return loss[0], score
+
+    @staticmethod
+    def backward(ctx, g_loss, g_score):
+        ent, rel, ent_im, rel_im, h, t, r, score = ctx.saved_tensors
+        spec, batch, neg, loss_margin, adv_t, regul_rate = ctx.cfg
+        if not ctx.has_im:
+            ent_im = rel_im = None
+        dev = ent.device
+        gl = g_loss.reshape(1).to(torch.float32).contiguous()
+        ge = torch.zeros_like(ent)
+        gr = torch.zeros_like(rel)
+        gei = torch.zeros_like(ent_im) if ent_im is not None else None
+        gri = torch.zeros_like(rel_im) if rel_im is not None else None
+        call("mmre_ns_backward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
+             ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
+             batch, neg, float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei),
+             ptr(gr), ptr(gri), None, stream_ptr(dev))
+        return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None
+
+
+def fused_ns_loss(spec: NSSpec, ent, rel, h, t, r, batch: int, neg: int, loss_margin: float,
+                  adv_temperature: float | None = None, regul_rate: float = 0.0, ent_im=None, rel_im=None):
+    """Returns (loss scalar tensor, scores (B*(1+k),)). Differentiable w.r.t. the tables."""
+    require_cuda(ent, rel, h, t, r, ent_im, rel_im)
+    h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
+    if ent.dtype != torch.float32 or rel.dtype != torch.float32:
+        raise TypeError("fused_ns_loss: float32 tables")
+    return _FusedNS.apply(ent.contiguous(), rel.contiguous(), None if ent_im is None else ent_im.contiguous(),
+                          None if rel_im is None else rel_im.contiguous(), h, t, r, spec, int(batch), int(neg),
+                          float(loss_margin), float(adv_temperature or 0.0), float(regul_rate))
+
+
+def score_rows(spec: NSSpec, ent, rel, h, t, r, ent_im=None, rel_im=None):
+    """model(data) in 'normal' mode for arbitrary rows (no loss): one row per 'positive'."""
+    require_cuda(ent, rel, h, t, r)
+    n = int(h.shape[0])
+    dev = ent.device
+    score = torch.empty(n, dtype=torch.float32, device=dev)
+    work = torch.empty(int(lib().mmre_ns_workspace(n, 0)), dtype=torch.float32, device=dev)
+    h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
+    call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
+         ptr(ent.contiguous()), ptr(ent_im), ptr(rel.contiguous()), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h),
+         ptr(t), ptr(r), n, 0, 0.0, 0.0, 0.0, ptr(score), None, ptr(work), stream_ptr(dev))
+    return score
