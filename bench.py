@@ -165,8 +165,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    from mmre.link import FilterIndex, LinkSweep, ScoreSpec, link_metrics, rotate_phase_denom
-    from mmre.sharding import ShardPlan, gather_counts, lpt_partition
+    from mmre.link import FilterIndex, ScoreSpec, rotate_phase_denom
+    from mmre.sharding import ShardedLinkEvaluation
     from mmre.workloads import synthetic_large, zs_workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,34 +189,18 @@ def main():
     model, dim = cfg["model"], cfg["dim"]
     E = w["n_ent"]
     n = len(w["test_h"])
-    qh = np.concatenate([w["test_h"], w["test_h"]]).astype(np.int64)
-    qr = np.concatenate([w["test_r"], w["test_r"]]).astype(np.int64)
-    qt = np.concatenate([w["test_t"], w["test_t"]]).astype(np.int64)
-    qm = np.concatenate([np.zeros(n, np.int8), np.ones(n, np.int8)])
-    masks = lpt_partition(qr, world)
-    mine = masks[rank]
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
-    off, ids = index.filters(qh[mine], qr[mine], qt[mine], qm[mine])
-    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    lq = [to(qh[mine]), to(qr[mine]), to(qt[mine]), to(qm[mine])]
-    filt = (to(off), to(ids))
     pk = {"transe": 0, "distmult": 2, "complex": 2, "rotate": 3}[model]
     spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
                      ent_im=w.get("ent_im").to(dev) if "ent_im" in w else None,
                      rel_im=w.get("rel_im").to(dev) if "rel_im" in w else None, norm_flag=cfg["norm"],
                      pred_kind=pk, margin=float(w.get("margin", 0.0)),
                      phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
-    sw = LinkSweep(spec)
-    bufs = sw.alloc_queries(int(mine.sum()))
-    plan = ShardPlan(masks, dev) if world > 1 else None
-    n_local = int(mine.sum())
+    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+    n_local = int(ev.masks[rank].sum())
 
     def step(events=None):
-        res = sw.run(*lq, filt=filt, buffers=bufs, prepare=True, sweep_events=events)
-        counts = res["counts"]
-        full = gather_counts(counts, plan) if world > 1 else counts
-        host = full.cpu().numpy()
-        return link_metrics(host[:, :n], host[:, n:])
+        return ev.run(events)[0]
 
     for _ in range(args.warmup):
         step()

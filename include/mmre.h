@@ -91,7 +91,7 @@ int mmre_link_prepare_queries(int model, int norm_flag, const float* d_ent_rows,
  * type masks: uint32 [n_rel][ceil(E/32)] bitsets of the relation's allowed heads
  *   / tails (type_constrain.txt, Reader.h:266-317); NULL/NULL disables.
  * d_counts: int32 [4][n_query] = raw, filt, raw_tc, filt_tc.
- * pred_kind: 0 s, 1 m-(m-s), 2 -s, 3 -(m-s)  (DESIGN.md §3). */
+ * pred_kind: 0 s, 1 m-(m-s), 2 -s, 3 -(m-s), 4 m-s  (DESIGN.md §3). */
 int mmre_link_truth(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
                     int64_t e_pad, const float* d_ent_rows, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
                     const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
@@ -181,6 +181,15 @@ int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model
                      int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
                      const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
                      float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
+
+/* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
+ * batch = n_rows, neg = 0, d_loss = NULL. Its backward: accumulate
+ * d_grad_score[i] * d(score_i)/d(tables) into the dense gradient tables. */
+int mmre_score_rows_backward(int model, int norm_flag, float model_margin, int use_model_margin,
+                             const float* d_ent, const float* d_ent_im, const float* d_rel, const float* d_rel_im,
+                             int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r,
+                             int64_t n_rows, const float* d_grad_score, float* d_grad_ent, float* d_grad_ent_im,
+                             float* d_grad_rel, float* d_grad_rel_im, void* stream);
 
 /* ====================================================================== *
  *  Zero-shot relation-embedding generator (module/model.py:674-686):     *

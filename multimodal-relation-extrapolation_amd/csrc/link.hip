@@ -624,9 +624,10 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
                             const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, const uint32_t* th,
                             const uint32_t* tt, int64_t tw, int32_t* counts, float* scores) {
   const int n_et = (int)(e_pad / TE);
-  // 8 workgroups per resident slot: short per-workgroup ranges let the dispatcher balance CUs
-  // that run at different speeds (measured: 8192 groups 3.45 ms vs 1024 groups 4.0 ms at C2).
-  int g = 8 * resident_groups((const void*)k_sweep_valu<OP, TCV, STV>, NT);
+  // 16 workgroups per resident slot: short per-workgroup ranges let the dispatcher balance
+  // CUs that run at different speeds (C2 on MI355X: 1,024 groups 4.0 ms, 8,192 3.43 ms,
+  // 16,384 3.30 ms, 30,528 (one unit each) 3.36 ms).
+  int g = 16 * resident_groups((const void*)k_sweep_valu<OP, TCV, STV>, NT);
   // MMRE_SWEEP_GRID (experiments): "tiles" = one workgroup per (query tile, 1/8 of the
   // entity tiles); a number = that many persistent workgroups.
   static const char* gmode = getenv("MMRE_SWEEP_GRID");
@@ -726,7 +727,7 @@ static int check_link_args(int model, int pred_kind, const float* d_ent_km, int6
                            int64_t n_query, int64_t q_pad, const uint32_t* d_type_head, const uint32_t* d_type_tail,
                            const int32_t* d_counts, const float* d_truth) {
   if (!valid_model(model)) return MMRE_ERR_MODEL;
-  if (pred_kind < 0 || pred_kind > 3) return MMRE_ERR_ARG;
+  if (pred_kind < 0 || pred_kind > 4) return MMRE_ERR_ARG;
   if (!d_ent_km || !d_q_km || !d_q_true || !d_counts || !d_truth || !d_qmode || !d_qr) return MMRE_ERR_ARG;
   if (n_query <= 0 || n_ent <= 0 || e_pad < n_ent || e_pad % TE || q_pad < n_query || q_pad % TQ) return MMRE_ERR_ARG;
   if ((d_type_head == nullptr) != (d_type_tail == nullptr)) return MMRE_ERR_ARG;

@@ -31,13 +31,15 @@ __host__ __device__ inline int model_k(int model, int dim) {
 
 // Prediction transform applied to a raw score: what OpenKE's model.predict returns.
 //   0: s (TransE)   1: m - (m - s) (TransE with margin)   2: -s (DistMult/ComplEx)
-//   3: -(m - s) (RotatE)                 (TransE.py:88-94, DistMult.py:70-72, RotatE.py:86-91)
+//   3: -(m - s) (RotatE)   4: m - s (forward() of TransE with margin / RotatE)
+//                                      (TransE.py:88-110, DistMult.py:70-72, RotatE.py:86-91)
 __device__ __forceinline__ float apply_pred(int kind, float m, float s) {
   switch (kind) {
     case 0: return s;
     case 1: return m - (m - s);
     case 2: return -s;
-    default: return -(m - s);
+    case 3: return -(m - s);
+    default: return m - s;
   }
 }
 

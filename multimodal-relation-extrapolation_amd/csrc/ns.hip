@@ -301,6 +301,16 @@ __global__ __launch_bounds__(256) void k_ns_backward(NSArgs A, const float* __re
   row_backward(A, b, lane, gp, reg_ent, reg_rel, gent, gent_im, grel, grel_im);
 }
 
+// model(data) backward for arbitrary rows: dL/d(score of row i) = grad_score[i] (one wave per row).
+__global__ __launch_bounds__(256) void k_rows_backward(NSArgs A, const float* __restrict__ grad_score, float* gent,
+                                                       float* gent_im, float* grel, float* grel_im) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * NS_WAVES + (threadIdx.x >> 6);
+  if (row >= A.B) return;
+  const float g = grad_score[row];
+  if (g != 0.0f) row_backward(A, row, lane, g, 0.0f, 0.0f, gent, gent_im, grel, grel_im);
+}
+
 static int ns_args(NSArgs& A, int model, int norm_flag, float model_margin, int use_model_margin, const float* ent,
                    const float* ent_im, const float* rel, const float* rel_im, int dim, float phase_denom,
                    const int64_t* h, const int64_t* t, const int64_t* r, int64_t batch, int64_t neg,
@@ -365,6 +375,25 @@ extern "C" int mmre_ns_backward(int model, int norm_flag, float model_margin, in
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_ns_backward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
                      d_score, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_margin, int use_model_margin,
+                                        const float* d_ent, const float* d_ent_im, const float* d_rel,
+                                        const float* d_rel_im, int dim, float phase_denom, const int64_t* d_h,
+                                        const int64_t* d_t, const int64_t* d_r, int64_t n_rows,
+                                        const float* d_grad_score, float* d_grad_ent, float* d_grad_ent_im,
+                                        float* d_grad_rel, float* d_grad_rel_im, void* stream) {
+  NSArgs A;
+  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                   phase_denom, d_h, d_t, d_r, n_rows, 0, 0.0f, 0.0f, 0.0f);
+  if (rc) return rc;
+  if (!d_grad_score || !d_grad_ent || !d_grad_rel) return MMRE_ERR_ARG;
+  if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_rows_backward, dim3((unsigned)((n_rows + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
+                     d_grad_score, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }

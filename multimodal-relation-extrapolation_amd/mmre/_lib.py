@@ -30,6 +30,7 @@ SIGNATURES = {
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
     "mmre_glibc_rand": (I32, [I64, I64, P]),
     "mmre_sampler_advance": (I32, [P, I64, I64, I64, I64, I64]),
+    "mmre_sampler_draws_per_positive": (I64, [I64, I64, I64]),
     "mmre_sampler_openke": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64, I64,
                                   P, P, P, P, P]),
     "mmre_sampler_repo": (I32, [P, P, P, I64, I64, I64, P, I64, P, P, P, I64, P, P, P, I64, ctypes.c_uint64, I32,
@@ -39,6 +40,7 @@ SIGNATURES = {
                               P]),
     "mmre_ns_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
                                P, P, P, P, P]),
+    "mmre_score_rows_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, P, P, P, P, P, P]),
     "mmre_generator_workspace": (I64, [I64, I32, I32, I32, I32]),
     "mmre_generator_forward": (I32, [P, I32, P, I32, I64, P, P, P, P, I32, P, P, P, P, I32, P, P, P, P, I32, P, P,
                                      F32, I32, F32, P, P, P]),

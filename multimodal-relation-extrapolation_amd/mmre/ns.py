@@ -83,15 +83,42 @@ def fused_ns_loss(spec: NSSpec, ent, rel, h, t, r, batch: int, neg: int, loss_ma
                           float(loss_margin), float(adv_temperature or 0.0), float(regul_rate))
 
 
+class _ScoreRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec):
+        n = int(h.shape[0])
+        dev = ent.device
+        score = torch.empty(n, dtype=torch.float32, device=dev)
+        work = torch.empty(int(lib().mmre_ns_workspace(n, 0)), dtype=torch.float32, device=dev)
+        call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
+             ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r), n, 0,
+             0.0, 0.0, 0.0, ptr(score), None, ptr(work), stream_ptr(dev))
+        ctx.save_for_backward(ent, rel, ent_im if ent_im is not None else ent, rel_im if rel_im is not None else rel,
+                              h, t, r)
+        ctx.has_im = ent_im is not None
+        ctx.spec = spec
+        return score
+
+    @staticmethod
+    def backward(ctx, g_score):
+        ent, rel, ent_im, rel_im, h, t, r = ctx.saved_tensors
+        spec = ctx.spec
+        if not ctx.has_im:
+            ent_im = rel_im = None
+        g = g_score.to(torch.float32).contiguous()
+        ge, gr = torch.zeros_like(ent), torch.zeros_like(rel)
+        gei = torch.zeros_like(ent_im) if ent_im is not None else None
+        gri = torch.zeros_like(rel_im) if rel_im is not None else None
+        call("mmre_score_rows_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
+             int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom,
+             ptr(h), ptr(t), ptr(r), int(h.shape[0]), ptr(g), ptr(ge), ptr(gei), ptr(gr), ptr(gri),
+             stream_ptr(ent.device))
+        return ge, gr, gei, gri, None, None, None, None
+
+
 def score_rows(spec: NSSpec, ent, rel, h, t, r, ent_im=None, rel_im=None):
-    """model(data) in 'normal' mode for arbitrary rows (no loss): one row per 'positive'."""
-    require_cuda(ent, rel, h, t, r)
-    n = int(h.shape[0])
-    dev = ent.device
-    score = torch.empty(n, dtype=torch.float32, device=dev)
-    work = torch.empty(int(lib().mmre_ns_workspace(n, 0)), dtype=torch.float32, device=dev)
+    """model(data) in 'normal' mode for arbitrary rows (differentiable w.r.t. the tables)."""
+    require_cuda(ent, rel, h, t, r, ent_im, rel_im)
     h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
-    call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
-         ptr(ent.contiguous()), ptr(ent_im), ptr(rel.contiguous()), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h),
-         ptr(t), ptr(r), n, 0, 0.0, 0.0, 0.0, ptr(score), None, ptr(work), stream_ptr(dev))
-    return score
+    c = lambda x: None if x is None else x.contiguous()
+    return _ScoreRows.apply(c(ent), c(rel), c(ent_im), c(rel_im), h, t, r, spec)

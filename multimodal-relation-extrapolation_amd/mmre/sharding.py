@@ -56,8 +56,68 @@ def gather_counts(local_counts: torch.Tensor, plan: ShardPlan, group=None):
     import torch.distributed as dist
     buf = torch.zeros((4, plan.pad), dtype=torch.int32, device=plan.device)
     buf[:, :local_counts.shape[1]] = local_counts
-    out = torch.empty((plan.world, 4, plan.pad), dtype=torch.int32, device=plan.device)
-    dist.all_gather_into_tensor(out, buf, group=group)
+    out = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32, device=plan.device)
+    dist.all_gather_into_tensor(out, buf, group=group)  # rank-major concatenation along dim 0
+    out = out.view(plan.world, 4, plan.pad)
     full = torch.empty((4, plan.n_total), dtype=torch.int32, device=plan.device)
     full[:, plan.dst] = out.permute(1, 0, 2).reshape(4, -1)[:, plan.cols]
     return full
+
+
+class ShardedLinkEvaluation:
+    """Relation-sharded filtered link prediction for one process of a torch.distributed job
+    (one process per GPU; backend 'nccl' = RCCL over xGMI on MI355X, 'gloo' in CPU tests).
+
+    Every rank builds the same LPT partition of the evaluation's queries (test triples x
+    {head_batch, tail_batch}), sweeps only its own relations' queries, then one all-gather of
+    the int32 rank counts gives every rank the full count table; the Test.h metric reduction
+    then runs in the reference's sequential query order, so rank 0's metrics are bit-identical
+    to a single-GPU evaluation. `local_runner(qh, qr, qt, qm, filt)` -> (4, n_local) int32
+    device tensor is the per-rank sweep (defaults to mmre.link.LinkSweep)."""
+
+    def __init__(self, spec, test_h, test_r, test_t, index=None, type_constrain=False, group=None,
+                 device=None, local_runner=None):
+        import torch.distributed as dist
+        from .link import HEAD, TAIL
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        th, tr, tt = (np.asarray(x, np.int64) for x in (test_h, test_r, test_t))
+        self.n = len(th)
+        qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
+        qm = np.concatenate([np.full(self.n, HEAD, np.int8), np.full(self.n, TAIL, np.int8)])
+        self.masks = lpt_partition(qr, self.world)
+        mine = self.masks[self.rank]
+        dev = torch.device(device) if device is not None else (spec.ent.device if spec is not None else
+                                                               torch.device("cpu"))
+        self.device = dev
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.q = [to(qh[mine]), to(qr[mine]), to(qt[mine]), to(qm[mine])]
+        self.q_host = (qh[mine], qr[mine], qt[mine], qm[mine])
+        self.filt = None
+        self.masks_tc = None
+        if index is not None:
+            off, ids = index.filters(qh[mine], qr[mine], qt[mine], qm[mine])
+            self.filt = (to(off), to(ids))
+            if type_constrain:
+                self.masks_tc = tuple(to(m) for m in index.type_masks())
+        self.plan = ShardPlan(self.masks, dev) if self.world > 1 else None
+        if local_runner is None:
+            from .link import LinkSweep
+            sw = LinkSweep(spec)
+            bufs = sw.alloc_queries(int(mine.sum()))
+
+            def local_runner(qh_, qr_, qt_, qm_, filt, masks_tc, events=None):
+                return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs,
+                              sweep_events=events)["counts"]
+        self.local_runner = local_runner
+
+    def counts(self, events=None):
+        """(4, 2n) int32 counts in global query order (head block, then tail block)."""
+        local = self.local_runner(*self.q, self.filt, self.masks_tc, events)
+        return gather_counts(local, self.plan, self.group) if self.world > 1 else local
+
+    def run(self, events=None):
+        from .link import link_metrics
+        c = self.counts(events).cpu().numpy()
+        return link_metrics(c[:, :self.n], c[:, self.n:]), c

@@ -1,0 +1,3 @@
+from .BaseModule import BaseModule
+
+__all__ = ["BaseModule"]

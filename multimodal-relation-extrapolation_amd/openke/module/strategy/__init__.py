@@ -1,0 +1,4 @@
+from .NegativeSampling import NegativeSampling
+from .Strategy import Strategy
+
+__all__ = ["Strategy", "NegativeSampling"]

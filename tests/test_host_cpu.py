@@ -1,0 +1,158 @@
+"""CPU-side tests: the C ABI library loads and exports every symbol of include/mmre.h, and the
+host-side parts (metric reduction, glibc seeds, LCG bookkeeping, dataset/filter/train indices,
+relation sharding) agree with the oracle and the reference's golden vectors. No GPU needed."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO
+
+
+def _header_functions():
+    src = open(os.path.join(REPO, "include", "mmre.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mmre_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from mmre import _lib
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    names = _header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+    # every declared entry point is also bound (with argtypes) by the Python layer
+    assert not [n for n in names if n not in _lib.SIGNATURES]
+
+
+def test_product_binding_loads_without_gpu():
+    from mmre import _lib
+    L = _lib.lib()
+    assert L.mmre_version() >= 100
+    assert L.mmre_link_pad(1) == 128 and L.mmre_link_pad(129) == 256
+    assert L.mmre_link_k(0, 200) == 200 and L.mmre_link_k(3, 200) == 400 and L.mmre_link_k(4, 13) == 32
+
+
+def test_metrics_host_matches_reference(golden):
+    """mmre_link_metrics (host C++) reproduces Base.so's Test.h float accumulation bit-for-bit
+    from the reference's own per-query counts."""
+    from mmre.link import link_metrics
+    g = golden("link_small")
+    for name in ["transe", "transe_nonorm_margin", "transe_l2", "distmult", "complex", "rotate"]:
+        for tc in (0, 1):
+            h = g[f"{name}_tc{tc}_head_counts"].T.astype(np.int32)
+            t = g[f"{name}_tc{tc}_tail_counts"].T.astype(np.int32)
+            m = link_metrics(h, t)
+            grp = m["filter_tc" if tc else "filter"]
+            got = np.array([grp[k] for k in ("mrr", "mr", "hit10", "hit3", "hit1")], np.float32)
+            assert np.array_equal(got, g[f"{name}_tc{tc}_metrics"]), (name, tc)
+
+
+def test_metrics_host_matches_oracle_large():
+    """Large counts (sums past 2^24, where float accumulation order matters)."""
+    import oracle
+    from mmre.link import link_metrics
+    rng = np.random.default_rng(0)
+    n = 40000
+    h = rng.integers(0, 14000, (n, 4)).astype(np.int64)
+    t = rng.integers(0, 14000, (n, 4)).astype(np.int64)
+    o = oracle.link_metrics(h, t)
+    m = link_metrics(h.T.astype(np.int32), t.T.astype(np.int32))
+    for grp in ("filter", "raw", "filter_tc", "raw_tc"):
+        for k in ("mrr", "mr", "hit10", "hit3", "hit1"):
+            assert np.float32(m[grp][k]) == o[grp][k], (grp, k)
+
+
+def test_glibc_seeds_and_lcg_advance(golden):
+    import oracle
+    from mmre.data import OpenKEDataset, TrainIndex
+    from mmre.sampler import glibc_seeds
+    assert glibc_seeds(5).tolist() == oracle.glibc_rand(5).tolist()
+    assert glibc_seeds(3, skip=7).tolist() == oracle.glibc_rand(10)[7:].tolist()
+    # mmre_sampler_advance == the oracle's sequential per-thread draws (and the reference's)
+    g = golden("sampler_medium")
+    d = OpenKEDataset(os.path.join(GOLDEN, "data", "medium"))
+    from mmre._lib import call
+    for name in sorted({k[:-len("_cfg")] for k in g if k.endswith("_cfg")}):
+        threads, B, neg, negrel, mode, bern = g[f"{name}_cfg"].tolist()
+        seeds = g[f"{name}_seeds0"].copy()
+        for _ in range(3):
+            call("mmre_sampler_advance", seeds.ctypes.data_as(ctypes.c_void_p), threads, B, neg, negrel, mode)
+        assert np.array_equal(seeds, g[f"{name}_seeds_end"]), name
+
+
+def test_train_index_matches_oracle():
+    import oracle
+    from mmre.data import OpenKEDataset, TrainIndex
+    d = OpenKEDataset(os.path.join(GOLDEN, "data", "medium"))
+    ix = TrainIndex(d.train[:, 0], d.train[:, 1], d.train[:, 2], d.n_ent, d.n_rel)
+    o = oracle.train_index(d.train[:, 0], d.train[:, 1], d.train[:, 2], d.n_ent, d.n_rel)
+    for a, b in [("train_list", "train_list"), ("head_hrt", "head"), ("tail_hrt", "tail"), ("rel_hrt", "rel"),
+                 ("lef_head", "lef_head"), ("rig_head", "rig_head"), ("lef_tail", "lef_tail"),
+                 ("rig_tail", "rig_tail"), ("lef_rel", "lef_rel"), ("rig_rel", "rig_rel")]:
+        assert np.array_equal(getattr(ix, a), o[b]), a
+    assert np.array_equal(ix.left_mean, o["left_mean"], equal_nan=True)
+    assert np.array_equal(ix.right_mean, o["right_mean"], equal_nan=True)
+
+
+def test_filter_index_and_type_masks():
+    from mmre.data import OpenKEDataset
+    from mmre.link import FilterIndex
+    d = OpenKEDataset(os.path.join(GOLDEN, "data", "small"))
+    idx = FilterIndex(*d.all_triples(), d.n_ent, d.n_rel, d.type_heads, d.type_tails)
+    h, r, t = d.test_list()
+    n = len(h)
+    qh, qr, qt = (np.concatenate([x, x]) for x in (h, r, t))
+    qm = np.r_[np.zeros(n, np.int8), np.ones(n, np.int8)]
+    off, ids = idx.filters(qh, qr, qt, qm)
+    S = set(zip(*(x.tolist() for x in d.all_triples())))
+    for i in range(2 * n):
+        got = set(ids[off[i]:off[i + 1]].tolist())
+        if qm[i] == 0:
+            exp = {j for j in range(d.n_ent) if (j, qr[i], qt[i]) in S}
+        else:
+            exp = {j for j in range(d.n_ent) if (qh[i], qr[i], j) in S}
+        assert got == exp and off[i + 1] - off[i] == len(exp)
+    mh, mt = idx.type_masks()
+    for r_ in range(d.n_rel):
+        bits = [(mh[r_, e >> 5] >> (e & 31)) & 1 for e in range(d.n_ent)]
+        assert np.nonzero(bits)[0].tolist() == d.type_heads[r_]
+        bits = [(mt[r_, e >> 5] >> (e & 31)) & 1 for e in range(d.n_ent)]
+        assert np.nonzero(bits)[0].tolist() == d.type_tails[r_]
+
+
+def test_test_list_order_matches_reference(golden):
+    """testList sorted by (r, h, t) (Reader.h:227): the reference Base.so's query order."""
+    from mmre.data import OpenKEDataset
+    g = golden("link_small")
+    h, r, t = OpenKEDataset(os.path.join(GOLDEN, "data", "small")).test_list()
+    assert np.array_equal(h, g["qh"]) and np.array_equal(r, g["qr"]) and np.array_equal(t, g["qt"])
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_lpt_partition(world):
+    from mmre.data import load_zs_test
+    from mmre.sharding import lpt_partition
+    z = load_zs_test("FB15K-237-ZS")
+    qr = np.concatenate([z["r"], z["r"]])
+    masks = lpt_partition(qr, world)
+    assert np.array_equal(np.sum(masks, 0), np.ones(len(qr)))  # a partition
+    for m in masks:  # whole relations per rank
+        for r in np.unique(qr[m]):
+            assert m[qr == r].all()
+    loads = [m.sum() for m in masks]
+    # FB15K-237-ZS LPT ceilings 1.99 / 3.98 / 7.84 at 2 / 4 / 8 ranks
+    ceiling = len(qr) / max(loads)
+    assert ceiling >= {1: 1.0, 2: 1.98, 4: 3.9, 8: 7.5}[world]
+
+
+def test_zs_datasets_shipped():
+    from mmre.data import load_zs_test
+    z = load_zs_test("FB15K-237-ZS")
+    assert len(z["h"]) == 17596 and int(z["n_ent"]) == 14208 and int(z["n_rel"]) == 235
+    assert len(np.unique(z["r"])) == 29
+    z = load_zs_test("DB15K-ZS")
+    assert len(z["h"]) == 5653 and int(z["n_ent"]) == 12741 and int(z["n_rel"]) == 157
