@@ -59,6 +59,26 @@ def valu_ops_per_triple(model, dim):
     return {"transe": 2 * dim, "transe_l2": 2 * dim, "rotate": 11 * dim}.get(model)
 
 
+KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false>", "rotate": "k_sweep_valu<2, false, false>",
+                "distmult": "k_sweep_mfma<false, false>", "complex": "k_sweep_mfma<false, false>"}
+
+
+def pmc_traffic(config: str, model: str):
+    """HBM-side bytes per sweep launch from the committed rocprofv3 PMC passes
+    (profiles/pmc_<config>.json, made by scripts/pmc.sh + scripts/pmc_summary.py on this
+    workload at N=1): (2 x FETCH_SIZE + WRITE_SIZE) KiB -- FETCH_SIZE reads half the bytes of
+    wide coalesced loads on gfx950 (MI355X_MICROARCH.md §HBM)."""
+    path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    for name, c in d.items():
+        if KERNEL_NAMES[model] in name and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, REPO)
+    return None, None
+
+
 @contextlib.contextmanager
 def stdout_to_stderr():
     """Base.so printf()s to fd 1; keep rank 0's stdout a single JSON line."""
@@ -228,10 +248,18 @@ def main():
     if rank == 0:
         bpt = bytes_per_triple(model, dim)
         achieved = n_local * E * bpt / (sweep_ms * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "k_sweep_valu" if model in ("transe", "rotate") else "k_sweep_mfma",
-                "kernel_ms": sweep_ms, "bytes_per_triple": bpt, "triples_per_launch": n_local * E}
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
+                "traffic_source": tsrc, "kernel": KERNEL_NAMES[model], "kernel_ms": sweep_ms,
+                "bytes_per_triple": bpt, "triples_per_launch": n_local * E,
+                "note": "algorithmic bytes per SURVEY 8(d); the sweep reuses each entity row across a "
+                        "128-query LDS tile, so frac > 1 is expected -- the binding roof for TransE/RotatE "
+                        "is VALU (valu_frac), for DistMult/ComplEx f32 MFMA"}
+        if model in ("distmult", "complex"):
+            fl = 2.0 * dim * (2 if model == "complex" else 1) * n_local * E / (sweep_ms * 1e-3)
+            roof["mfma_achieved_tflops"] = fl / 1e12
+            roof["mfma_frac"] = fl / 157.3e12
         vo = valu_ops_per_triple(model, dim)
         if vo:
             tps = n_local * E / (sweep_ms * 1e-3)

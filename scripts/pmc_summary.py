@@ -1,6 +1,8 @@
-"""Summarise scripts/pmc.sh output per kernel: mean counter value per dispatch."""
+"""Summarise scripts/pmc.sh output per kernel: mean counter value per dispatch.
+usage: python scripts/pmc_summary.py <tag> [--json out.json]"""
 import csv
 import glob
+import json
 import sys
 from collections import defaultdict
 
@@ -8,9 +10,14 @@ tag = sys.argv[1]
 acc = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"gpurun_out/pmc_{tag}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        name = r.get("Kernel_Name", "")[:60]
+        name = r.get("Kernel_Name", "")
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+summary = {}
 for k, d in acc.items():
-    print(k)
-    for c, v in sorted(d.items()):
-        print(f"   {c:28s} {sum(v) / len(v):.4g}  (n={len(v)})")
+    summary[k] = {c: sum(v) / len(v) for c, v in d.items()}
+    print(k[:90])
+    for c, v in sorted(summary[k].items()):
+        print(f"   {c:28s} {v:.4g}")
+if "--json" in sys.argv:
+    out = sys.argv[sys.argv.index("--json") + 1]
+    json.dump(summary, open(out, "w"), indent=1, sort_keys=True)
