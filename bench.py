@@ -220,7 +220,7 @@ def main():
     n_local = int(ev.masks[rank].sum())
 
     def step(events=None):
-        return ev.run(events)[0]
+        return ev.run(events, copy_counts=False)[0]
 
     for _ in range(args.warmup):
         step()

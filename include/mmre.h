@@ -74,17 +74,19 @@ int mmre_link_prepare_entities(int model, int norm_flag, const float* d_ent, con
  * prepared d_ent_rows); d_q_true[i] = the entity the sweep must rank (h for
  * head_batch, t for tail_batch). d_rel_work: (n_rel, d) floats, required for
  * TransE with norm_flag (normalised relation rows). phase_denom: RotatE's
- * rel_range/pi as torch evaluates it (RotatE.py:51). */
+ * rel_range/pi as torch evaluates it (RotatE.py:51). d_q_rows (nullable): the
+ * same vectors row-major [n_query][K], for mmre_link_truth_grouped. */
 int mmre_link_prepare_queries(int model, int norm_flag, const float* d_ent_rows, const float* d_rel,
                               const float* d_rel_im, int64_t n_ent, int64_t n_rel, int dim, float phase_denom,
                               const int64_t* d_qh, const int64_t* d_qr, const int64_t* d_qt,
                               const int8_t* d_qmode, int64_t n_query, float* d_q_km, int64_t q_pad,
-                              int32_t* d_q_true, float* d_rel_work, void* stream);
+                              int32_t* d_q_true, float* d_rel_work, float* d_q_rows, void* stream);
 
 /* Per-query threshold and filter bookkeeping, enqueued before the sweep:
- * zeroes d_counts, writes d_truth[i] = pred(true(i)) with exactly the sweep's
- * arithmetic, then subtracts from the filtered columns every known entity j of
- * query i (j != true) with pred(j) < pred(true) -- Test.h:85 `not _find(...)`.
+ * writes d_truth[i] = pred(true(i)) with exactly the sweep's arithmetic and
+ * initialises d_counts[.][i] = {0, -c, 0, -c_tc}, c = the known entities j of query i
+ * (j != true) with pred(j) < pred(true) -- Test.h:85 `not _find(...)` -- so the
+ * sweep's raw additions leave the filtered columns filtered.
  * filter CSR: d_filt_off[n_query+1] (int64), d_filt_ids (int32): the known heads
  *   (head_batch) / tails (tail_batch) of the query in train+valid+test
  *   (Reader.h:201-226); NULL/NULL = no filtering.
@@ -98,7 +100,27 @@ int mmre_link_truth(int model, int pred_kind, float margin, const float* d_ent_k
                     const int64_t* d_filt_off, const int32_t* d_filt_ids, const uint32_t* d_type_head,
                     const uint32_t* d_type_tail, int32_t* d_counts, float* d_truth, void* stream);
 
-/* The sweep (after mmre_link_truth on the same stream). For every query i and
+/* mmre_link_truth for filter GROUPS: queries with the same (mode, r, anchor) -- the
+ * key of Test.h:85's _find: (r, t) for head_batch, (h, r) for tail_batch -- share one
+ * known-entity list, so each listed entity is scored once per group. Two launches:
+ * every truth and every listed entity scored as one flat set of lanes (listed entity
+ * p with the query vector of query d_entry_q[p], any member of its group), then one
+ * wave per group counts, for each member, the listed entities that beat its truth.
+ * d_q_rows: row-major query vectors [n_query][K] (mmre_link_prepare_queries).
+ * d_grp_qoff[n_groups+1] (int64) / d_grp_q (int32): a partition of 0..n_query-1
+ *   (every query in exactly one group; groups of <= 64 queries run best).
+ * d_filt_off[n_groups+1] (int64) / d_filt_ids[n_entries] (int32): each group's list.
+ * d_list_scores: float workspace [n_entries]. Writes d_truth and all of d_counts
+ * exactly as mmre_link_truth does. */
+int mmre_link_truth_grouped(int model, int pred_kind, float margin, const float* d_ent_rows, int64_t n_ent,
+                            const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr,
+                            const int8_t* d_qmode, int64_t n_query, int dim, const int64_t* d_grp_qoff,
+                            const int32_t* d_grp_q, int64_t n_groups, const int64_t* d_filt_off,
+                            const int32_t* d_filt_ids, const int32_t* d_entry_q, int64_t n_entries,
+                            const uint32_t* d_type_head, const uint32_t* d_type_tail, float* d_list_scores,
+                            int32_t* d_counts, float* d_truth, void* stream);
+
+/* The sweep (after mmre_link_truth[_grouped] on the same stream). For every query i and
  * every entity j != true(i):  raw += pred(j) < pred(true)   (Test.h:80-86, strict
  * <, ties favour the truth), added to the raw AND filtered columns (and the _tc
  * columns for allowed j when type masks are given, Test.h:88-98).

@@ -4,6 +4,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <emmintrin.h>
+
 #include <vector>
 
 #include "../../include/mmre.h"
@@ -14,34 +16,67 @@ extern "C" int mmre_version(void) { return 100; }
 // float globals exactly as testHead/testTail do (Test.h:102-112: `+= 1` on float,
 // `+= (count+1)` long->float, `+= 1.0/(count+1)` in double then stored as float),
 // then divide by testTotal (float) and average the two sides (float).
-static void side(const int32_t* c, int64_t n, int64_t stride, int col, float tot, float out[5]) {
-  float t10 = 0, t3 = 0, t1 = 0, rank = 0, reci = 0;
-  const int32_t* p = c + (int64_t)col * stride;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t s = p[i];
-    if (s < 10) t10 += 1;
-    if (s < 3) t3 += 1;
-    if (s < 1) t1 += 1;
-    rank += (float)(s + 1);
-    reci = (float)((double)reci + 1.0 / (double)(s + 1));
-  }
-  out[0] = reci / tot;
-  out[1] = rank / tot;
-  out[2] = t10 / tot;
-  out[3] = t3 / tot;
-  out[4] = t1 / tot;
-}
-
+// The 8 (side, column) accumulations are independent serial chains: they advance together
+// in one pass as the 8 lanes of SSE2 vectors. The hit@k sums are exact small integers in
+// float (< 2^24), so they are counted as integers and converted once. Counts must be
+// >= 0 and < 2^24 (true for ranks of |E| < 2^24 entities).
 extern "C" int mmre_link_metrics(const int32_t* h_head_counts, const int32_t* h_tail_counts, int64_t n,
                                  int64_t stride, float* h_out) {
   if (!h_head_counts || !h_tail_counts || !h_out || n <= 0 || stride < n) return MMRE_ERR_ARG;
+  if (n >= (int64_t)1 << 24) return MMRE_ERR_SHAPE;
   const float tot = (float)n;
+  const int32_t* p[8];
+  for (int j = 0; j < 8; ++j) p[j] = (j < 4 ? h_head_counts : h_tail_counts) + (int64_t)(j & 3) * stride;
+  // Lanes j = 0..7 of two SSE float vectors (rank, reci) and four double pairs: every lane
+  // performs exactly the scalar sequence of its own chain (IEEE add / convert per lane).
+  __m128 rank_lo = _mm_setzero_ps(), rank_hi = _mm_setzero_ps();
+  __m128 reci_lo = _mm_setzero_ps(), reci_hi = _mm_setzero_ps();
+  __m128i c10_lo = _mm_setzero_si128(), c10_hi = _mm_setzero_si128();
+  __m128i c3_lo = _mm_setzero_si128(), c3_hi = _mm_setzero_si128();
+  __m128i c1_lo = _mm_setzero_si128(), c1_hi = _mm_setzero_si128();
+  const __m128i ten = _mm_set1_epi32(10), three = _mm_set1_epi32(3), one_i = _mm_set1_epi32(1);
+  const __m128d one = _mm_set1_pd(1.0);
+  auto reci_step = [&](__m128 r, __m128i s1) {
+    // r[k] = (float)((double)r[k] + 1.0 / (double)s1[k]) for the 4 lanes
+    const __m128d lo = _mm_add_pd(_mm_cvtps_pd(r), _mm_div_pd(one, _mm_cvtepi32_pd(s1)));
+    const __m128d hi = _mm_add_pd(_mm_cvtps_pd(_mm_movehl_ps(r, r)),
+                                  _mm_div_pd(one, _mm_cvtepi32_pd(_mm_shuffle_epi32(s1, 0x4E))));
+    return _mm_movelh_ps(_mm_cvtpd_ps(lo), _mm_cvtpd_ps(hi));
+  };
+  for (int64_t i = 0; i < n; ++i) {
+    const __m128i s_lo = _mm_set_epi32(p[3][i], p[2][i], p[1][i], p[0][i]);
+    const __m128i s_hi = _mm_set_epi32(p[7][i], p[6][i], p[5][i], p[4][i]);
+    c10_lo = _mm_sub_epi32(c10_lo, _mm_cmplt_epi32(s_lo, ten));
+    c10_hi = _mm_sub_epi32(c10_hi, _mm_cmplt_epi32(s_hi, ten));
+    c3_lo = _mm_sub_epi32(c3_lo, _mm_cmplt_epi32(s_lo, three));
+    c3_hi = _mm_sub_epi32(c3_hi, _mm_cmplt_epi32(s_hi, three));
+    c1_lo = _mm_sub_epi32(c1_lo, _mm_cmplt_epi32(s_lo, one_i));
+    c1_hi = _mm_sub_epi32(c1_hi, _mm_cmplt_epi32(s_hi, one_i));
+    const __m128i s1_lo = _mm_add_epi32(s_lo, one_i), s1_hi = _mm_add_epi32(s_hi, one_i);
+    rank_lo = _mm_add_ps(rank_lo, _mm_cvtepi32_ps(s1_lo));  // (float)(s + 1): exact below 2^24
+    rank_hi = _mm_add_ps(rank_hi, _mm_cvtepi32_ps(s1_hi));
+    reci_lo = reci_step(reci_lo, s1_lo);
+    reci_hi = reci_step(reci_hi, s1_hi);
+  }
+  float rank[8], reci[8];
+  int32_t c10[8], c3[8], c1[8];
+  _mm_storeu_ps(rank, rank_lo); _mm_storeu_ps(rank + 4, rank_hi);
+  _mm_storeu_ps(reci, reci_lo); _mm_storeu_ps(reci + 4, reci_hi);
+  _mm_storeu_si128((__m128i*)c10, c10_lo); _mm_storeu_si128((__m128i*)(c10 + 4), c10_hi);
+  _mm_storeu_si128((__m128i*)c3, c3_lo); _mm_storeu_si128((__m128i*)(c3 + 4), c3_hi);
+  _mm_storeu_si128((__m128i*)c1, c1_lo); _mm_storeu_si128((__m128i*)(c1 + 4), c1_hi);
   const int cols[4] = {1, 0, 3, 2};  // filter, raw, filter_tc, raw_tc
   for (int g = 0; g < 4; ++g) {
-    float l[5], r[5];
-    side(h_head_counts, n, stride, cols[g], tot, l);
-    side(h_tail_counts, n, stride, cols[g], tot, r);
-    for (int i = 0; i < 5; ++i) h_out[5 * g + i] = (l[i] + r[i]) / 2;
+    float v[2][5];
+    for (int sd = 0; sd < 2; ++sd) {
+      const int j = sd * 4 + cols[g];
+      v[sd][0] = reci[j] / tot;
+      v[sd][1] = rank[j] / tot;
+      v[sd][2] = (float)c10[j] / tot;
+      v[sd][3] = (float)c3[j] / tot;
+      v[sd][4] = (float)c1[j] / tot;
+    }
+    for (int i = 0; i < 5; ++i) h_out[5 * g + i] = (v[0][i] + v[1][i]) / 2;
   }
   return MMRE_OK;
 }

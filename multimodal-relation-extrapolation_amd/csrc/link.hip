@@ -9,10 +9,10 @@
 // conflict-free LDS reads, no transposes inside the hot loop.
 //
 // Kernels (per evaluation, one stream):
-//   k_prep_entities   table -> k-major plane (F.normalize for TransE norm_flag)
+//   k_prep_rows       table -> k-major plane + row-major copy (F.normalize for TransE norm_flag)
 //   k_prep_queries    (h, r, t, mode) -> k-major query vectors (+ truth ids)
-//   k_truth           pred(truth) per query, same arithmetic as the sweep
-//   k_filter_correct  subtracts known (filtered) entities that beat the truth
+//   k_truth_filter    pred(truth) per query (the sweep's arithmetic) and the filtered-rank
+//                     correction, one workgroup per filter group (queries sharing a list)
 //   k_sweep_valu      TransE L1/L2, RotatE: VALU 8x8 register micro-tiles
 //   k_sweep_mfma      DistMult/ComplEx: v_mfma_f32_32x32x2_f32, ballot/popcount epilogue
 #include <stdlib.h>
@@ -32,126 +32,180 @@ __host__ __device__ inline int plane_rows(int dim) { return (int)round_up(dim, K
 __host__ __device__ inline int n_planes(int model) { return (model == MMRE_COMPLEX || model == MMRE_ROTATE) ? 2 : 1; }
 
 // ------------------------------------------------------------------ prep ----
-// Canonical sum of squares of a row: sequential in k (loads issued 8 at a time).
-__device__ __forceinline__ float seq_sumsq(const float* __restrict__ r, int dim) {
-  float ss = 0.0f;
-  int k = 0;
-  for (; k + 8 <= dim; k += 8) {
-    float v[8];
+// Both prep kernels stage a block of rows through LDS (row stride kt+1: odd, so the
+// per-row sequential reads and the column-wise k-major writes are bank-conflict free):
+// global reads are contiguous row segments, global writes are contiguous in both the
+// row-major and the k-major layout.
+
+// Rows per LDS block for a row width kt: a power of two <= 16 (so it divides the 256
+// threads; 64-B k-major write runs, ~900 workgroups at |E| = 14k) with <= 64 KB of LDS.
+__host__ inline int stage_rows(int kt) {
+  int rb = 16;
+  while (rb > 1 && (int64_t)rb * (kt + 1) * 4 > 64 * 1024) rb >>= 1;
+  return rb;
+}
+
+// Value k (< np*kp) of source row e in the plane layout [re 0..kp) [im kp..2kp).
+__device__ __forceinline__ float plane_src(int model, const float* __restrict__ src, const float* __restrict__ src_im,
+                                           int64_t e, int dim, int kp, int k) {
+  const int pl = k >= kp;
+  const int kk = k - pl * kp;
+  if (kk >= dim) return 0.0f;
+  if (model == MMRE_COMPLEX) return (pl ? src_im : src)[e * dim + kk];
+  if (model == MMRE_ROTATE) return src[e * 2 * dim + pl * dim + kk];  // RotatE rows [re | im] (RotatE.py:48-49)
+  return src[e * dim + kk];
+}
+
+// Thread layouts of the staging kernels (256 threads): row phases use 8 row slots x 32
+// lanes along k (coalesced row segments, independent loads per thread); the k-major write
+// uses rb lanes along the rows x 256/rb k slots (contiguous rb-float runs per k).
+__device__ __forceinline__ void write_k_major(const float* lds, int ls, int rb, int kt, float* __restrict__ out,
+                                              int64_t pad, int64_t r0) {
+  const int i = threadIdx.x % rb, ks = threadIdx.x / rb, kstep = 256 / rb;
+  const int64_t e = r0 + i;
+  if (e >= pad) return;
+#pragma unroll 4
+  for (int k = ks; k < kt; k += kstep) out[(int64_t)k * pad + e] = lds[i * ls + k];
+}
+
+// Table rows -> (optional) k-major planes out_km[kt][pad] and row-major rows[n][rw]
+// (rw <= kt). TransE with norm_flag: F.normalize(x, 2, -1) = x / max(||x||_2, 1e-12)
+// (TransE.py:63-66), ||x|| from the canonical sequential sum of squares.
+__global__ __launch_bounds__(256) void k_prep_rows(int model, int norm_flag, const float* __restrict__ src,
+                                                   const float* __restrict__ src_im, int64_t n, int dim, int kp,
+                                                   int rb, float* __restrict__ out_km, int64_t pad,
+                                                   float* __restrict__ rows, int rw) {
+  extern __shared__ float lds[];
+  __shared__ float s_norm[32];
+  const int kt = n_planes(model) * kp, ls = kt + 1;
+  const int lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
+  const int64_t e0 = (int64_t)blockIdx.x * rb;
+  for (int i = slot; i < rb; i += 8) {
+    const int64_t e = e0 + i;
+    float* x = lds + i * ls;
+#pragma unroll 4
+    for (int k = lane; k < kt; k += 32) x[k] = e < n ? plane_src(model, src, src_im, e, dim, kp, k) : 0.0f;
+  }
+  __syncthreads();
+  const bool transe = model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2;
+  if (transe && norm_flag) {
+    if (threadIdx.x < rb) {
+      const float* x = lds + threadIdx.x * ls;
+      float ss = 0.0f;  // canonical sequential order; LDS reads batched 16 per round
+      int k = 0;
+      for (; k + 16 <= dim; k += 16) {
+        float v[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = r[k + u];
+        for (int u = 0; u < 16; ++u) v[u] = x[k + u];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) ss = ss + v[u] * v[u];
+        for (int u = 0; u < 16; ++u) ss = ss + v[u] * v[u];
+      }
+      for (; k < dim; ++k) ss = ss + x[k] * x[k];
+      const float nr = sqrtf(ss);
+      s_norm[threadIdx.x] = nr < 1e-12f ? 1e-12f : nr;
+    }
+    __syncthreads();
+    for (int i = slot; i < rb; i += 8) {
+      float* x = lds + i * ls;
+      const float nr = s_norm[i];
+      for (int k = lane; k < kt; k += 32) x[k] = x[k] / nr;
+    }
+    __syncthreads();
   }
-  for (; k < dim; ++k) ss = ss + r[k] * r[k];
-  return ss;
+  for (int i = slot; i < rb; i += 8) {
+    const int64_t e = e0 + i;
+    if (e >= n) break;
+    const float* x = lds + i * ls;
+#pragma unroll 4
+    for (int k = lane; k < rw; k += 32) rows[e * rw + k] = x[k];
+  }
+  if (out_km) write_k_major(lds, ls, rb, kt, out_km, pad, e0);
 }
 
-__global__ void k_prep_entities(int model, int norm_flag, const float* __restrict__ ent,
-                                const float* __restrict__ ent_im, int64_t n_ent, int dim, int kp,
-                                float* __restrict__ out, int64_t e_pad, float* __restrict__ rows) {
-  // out: k-major planes [np*kp][e_pad] for the sweep; rows: the same values row-major
-  // [n_ent][np*kp] for the per-entity gathers of the truth / filter kernels.
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= e_pad) return;
+// Query vectors, one LDS block of rb queries: the anchor rows (t for head_batch, h for
+// tail_batch) are copied from the prepared entity rows, combined element-wise with the
+// relation row (rel = normalised relation rows for TransE norm_flag), written k-major.
+__global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __restrict__ ent_rows,
+                                                      const float* __restrict__ rel, const float* __restrict__ rel_im,
+                                                      int dim, int kp, int rb, float phase_denom,
+                                                      const int64_t* __restrict__ qh, const int64_t* __restrict__ qr,
+                                                      const int64_t* __restrict__ qt, const int8_t* __restrict__ qmode,
+                                                      int64_t n_query, float* __restrict__ out, int64_t q_pad,
+                                                      int32_t* __restrict__ qtrue, float* __restrict__ q_rows) {
+  extern __shared__ float lds[];
+  __shared__ int64_t s_anchor[32], s_rel[32];
+  __shared__ int s_head[32];
   const int np = n_planes(model);
-  const int kt = np * kp;
-  if (e >= n_ent) {
-    for (int k = 0; k < kt; ++k) out[(int64_t)k * e_pad + e] = 0.0f;
-    return;
+  const int kt = np * kp, ls = kt + 1;
+  const int lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
+  const int64_t q0 = (int64_t)blockIdx.x * rb;
+  if (threadIdx.x < rb) {
+    const int64_t q = q0 + threadIdx.x;
+    int64_t a = -1, r = 0;
+    int head = 0;
+    if (q < n_query) {
+      head = qmode[q] == MMRE_HEAD_BATCH;
+      a = head ? qt[q] : qh[q];
+      r = qr[q];
+      qtrue[q] = (int32_t)(head ? qh[q] : qt[q]);
+    }
+    s_anchor[threadIdx.x] = a;
+    s_rel[threadIdx.x] = r;
+    s_head[threadIdx.x] = head;
   }
-  float* row = rows + e * kt;
-  if (model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2) {
-    const float* x = ent + e * dim;
-    float n = 1.0f;
-    if (norm_flag) {  // F.normalize(x, 2, -1): x / max(||x||_2, 1e-12)   (TransE.py:63-66)
-      n = sqrtf(seq_sumsq(x, dim));
-      if (n < 1e-12f) n = 1e-12f;
-    }
-    for (int k = 0; k < kp; ++k) {
-      const float v = k < dim ? (norm_flag ? x[k] / n : x[k]) : 0.0f;
-      out[(int64_t)k * e_pad + e] = v;
-      row[k] = v;
-    }
-  } else if (model == MMRE_DISTMULT) {
-    const float* x = ent + e * dim;
-    for (int k = 0; k < kp; ++k) {
-      const float v = k < dim ? x[k] : 0.0f;
-      out[(int64_t)k * e_pad + e] = v;
-      row[k] = v;
-    }
-  } else {
-    // ComplEx: planes re | im from two tables; RotatE rows are [re | im] of width 2d (RotatE.py:48-49)
-    const float* re = model == MMRE_COMPLEX ? ent + e * dim : ent + e * 2 * dim;
-    const float* im = model == MMRE_COMPLEX ? ent_im + e * dim : ent + e * 2 * dim + dim;
-    for (int k = 0; k < kp; ++k) {
-      const float a = k < dim ? re[k] : 0.0f, b = k < dim ? im[k] : 0.0f;
-      out[(int64_t)k * e_pad + e] = a;
-      out[(int64_t)(kp + k) * e_pad + e] = b;
-      row[k] = a;
-      row[kp + k] = b;
+  __syncthreads();
+  for (int i = slot; i < rb; i += 8) {
+    const int64_t a = s_anchor[i];
+    float* x = lds + i * ls;
+    const float* src = ent_rows + (a < 0 ? 0 : a) * kt;
+#pragma unroll 4
+    for (int k = lane; k < kt; k += 32) x[k] = a < 0 ? 0.0f : src[k];
+  }
+  __syncthreads();
+  for (int i = slot; i < rb; i += 8) {
+    float* x = lds + i * ls;
+    const bool valid = s_anchor[i] >= 0;
+    const int64_t r = s_rel[i];
+    const bool head = s_head[i];
+#pragma unroll 2
+    for (int k = lane; k < kp; k += 32) {
+      if (!valid || k >= dim) {
+        x[k] = 0.0f;
+        if (np == 2) x[kp + k] = 0.0f;
+        continue;
+      }
+      if (model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2) {
+        // head_batch: score = h + (r - t) -> q = -(r - t); tail_batch: (h + r) - t -> q = h + r
+        // (TransE.py:71-74). |q - e| reproduces both element-wise bit-for-bit.
+        const float b = rel[r * dim + k];
+        x[k] = head ? -(b - x[k]) : (x[k] + b);
+      } else if (model == MMRE_DISTMULT) {  // head: h*(r*t) ; tail: (h*r)*t  (DistMult.py:37-42)
+        const float b = rel[r * dim + k];
+        x[k] = head ? b * x[k] : x[k] * b;
+      } else if (model == MMRE_COMPLEX) {  // ComplEx.py:20-27 regrouped by the candidate entity
+        const float rr = rel[r * dim + k], ri = rel_im[r * dim + k];
+        const float ar = x[k], ai = x[kp + k];  // anchor (t for head_batch, h for tail_batch)
+        if (head) { x[k] = ar * rr + ai * ri; x[kp + k] = ai * rr - ar * ri; }
+        else      { x[k] = ar * rr - ai * ri; x[kp + k] = ai * rr + ar * ri; }
+      } else {  // RotatE (RotatE.py:51-72): rotate by the relation phase, regrouped per candidate
+        float sn, cs;
+        canon_sincos(rel[r * dim + k] / phase_denom, &sn, &cs);
+        const float ar = x[k], ai = x[kp + k];
+        if (head) { x[k] = cs * ar + sn * ai; x[kp + k] = cs * ai - sn * ar; }
+        else      { x[k] = ar * cs - ai * sn; x[kp + k] = ar * sn + ai * cs; }
+      }
     }
   }
-}
-
-// F.normalize of the relation rows (TransE norm_flag), one sequential row per thread.
-__global__ void k_norm_rows(const float* __restrict__ x, int64_t n, int dim, float* __restrict__ out) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* r = x + i * dim;
-  const float ss = seq_sumsq(r, dim);
-  float nrm = sqrtf(ss);
-  if (nrm < 1e-12f) nrm = 1e-12f;
-  for (int k = 0; k < dim; ++k) out[i * dim + k] = r[k] / nrm;
-}
-
-// Query vectors, one thread per (query, k): element-wise ops on prepared rows
-// (ent_rows = the sweep's entity values; rel = normalised relation rows for TransE).
-__global__ void k_prep_queries(int model, const float* __restrict__ ent_rows, const float* __restrict__ rel,
-                               const float* __restrict__ rel_im, int dim, int kp, float phase_denom,
-                               const int64_t* __restrict__ qh, const int64_t* __restrict__ qr,
-                               const int64_t* __restrict__ qt, const int8_t* __restrict__ qmode,
-                               int64_t n_query, float* __restrict__ out, int64_t q_pad,
-                               int32_t* __restrict__ qtrue) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = blockIdx.y;  // 0 .. kp-1
-  if (q >= q_pad) return;
-  const int np = n_planes(model);
-  const int kt = np * kp;
-  if (q >= n_query || k >= dim) {
-    out[(int64_t)k * q_pad + q] = 0.0f;
-    if (np == 2) out[(int64_t)(kp + k) * q_pad + q] = 0.0f;
-    return;
-  }
-  const int64_t h = qh[q], r = qr[q], t = qt[q];
-  const bool head = qmode[q] == MMRE_HEAD_BATCH;
-  if (k == 0) qtrue[q] = (int32_t)(head ? h : t);
-  const float* hrow = ent_rows + h * kt;
-  const float* trow = ent_rows + t * kt;
-  if (model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2) {
-    // head_batch: score = h + (r - t) -> q = -(r - t); tail_batch: (h + r) - t -> q = h + r
-    // (TransE.py:71-74). |q - e| reproduces both element-wise bit-for-bit.
-    const float b = rel[r * dim + k];
-    out[(int64_t)k * q_pad + q] = head ? -(b - trow[k]) : (hrow[k] + b);
-  } else if (model == MMRE_DISTMULT) {  // head: h*(r*t) ; tail: (h*r)*t  (DistMult.py:37-42)
-    const float b = rel[r * dim + k];
-    out[(int64_t)k * q_pad + q] = head ? b * trow[k] : hrow[k] * b;
-  } else if (model == MMRE_COMPLEX) {  // ComplEx.py:20-27 regrouped by the candidate entity
-    const float rr = rel[r * dim + k], ri = rel_im[r * dim + k];
-    const float tr = trow[k], ti = trow[kp + k], hr = hrow[k], hi = hrow[kp + k];
-    float a, b;
-    if (head) { a = tr * rr + ti * ri; b = ti * rr - tr * ri; }
-    else      { a = hr * rr - hi * ri; b = hi * rr + hr * ri; }
-    out[(int64_t)k * q_pad + q] = a;
-    out[(int64_t)(kp + k) * q_pad + q] = b;
-  } else {  // RotatE (RotatE.py:51-72): rotate by the relation phase, regrouped per candidate
-    float s, c;
-    canon_sincos(rel[r * dim + k] / phase_denom, &s, &c);
-    float a, b;
-    if (head) { const float tre = trow[k], tim = trow[kp + k]; a = c * tre + s * tim; b = c * tim - s * tre; }
-    else      { const float hre = hrow[k], him = hrow[kp + k]; a = hre * c - him * s; b = hre * s + him * c; }
-    out[(int64_t)k * q_pad + q] = a;
-    out[(int64_t)(kp + k) * q_pad + q] = b;
+  __syncthreads();
+  write_k_major(lds, ls, rb, kt, out, q_pad, q0);
+  if (q_rows) {  // row-major copy for the per-group loads of k_truth_filter
+    for (int i = slot; i < rb; i += 8) {
+      const int64_t q = q0 + i;
+      if (q >= n_query) break;
+      const float* x = lds + i * ls;
+#pragma unroll 4
+      for (int k = lane; k < kt; k += 32) q_rows[q * kt + k] = x[k];
+    }
   }
 }
 
@@ -181,94 +235,307 @@ __host__ __device__ inline int op_of_model(int model) {
          : model == MMRE_DISTMULT ? 3 : 4;
 }
 
-// Score of one (query, entity) pair in the canonical k order; entity values from the
-// row-major copy (one contiguous row per entity, loaded 8 at a time), query values from
-// the k-major plane. kp is a multiple of 8 (KC).
+__device__ __forceinline__ bool type_bit(const uint32_t* __restrict__ mask, int64_t words, int64_t r, int64_t e) {
+  return (mask[r * words + (e >> 5)] >> (e & 31)) & 1u;
+}
+
+// Two scores of the query vector sq against entity rows e1 and e2 at once (two independent
+// canonical chains; their loads share the round trips): 32 floats of each row per round
+// (RotatE: 16 re + 16 im of each). kp % 8 == 0.
 template <int OP>
-__device__ float pair_score(const float* __restrict__ ent_rows, const float* __restrict__ q_km, int64_t q_pad,
-                            int kp, int64_t q, int64_t e) {
-  float acc = 0.0f;
-  const int np = (OP == 2 || OP == 4) ? 2 : 1;
-  const float* row = ent_rows + e * (int64_t)np * kp;
-  const float* qc = q_km + q;
-  if constexpr (OP == 2) {
-    for (int k0 = 0; k0 < kp; k0 += 8) {
-      float x[8], y[8], a[8], b[8];
-      *reinterpret_cast<float4*>(&x[0]) = *reinterpret_cast<const float4*>(row + k0);
-      *reinterpret_cast<float4*>(&x[4]) = *reinterpret_cast<const float4*>(row + k0 + 4);
-      *reinterpret_cast<float4*>(&y[0]) = *reinterpret_cast<const float4*>(row + kp + k0);
-      *reinterpret_cast<float4*>(&y[4]) = *reinterpret_cast<const float4*>(row + kp + k0 + 4);
+__device__ void pair_score2_lds(const float* __restrict__ ent_rows, const float* sq, int kp, int64_t e1, int64_t e2,
+                                float* s1, float* s2) {
+  constexpr int NP = (OP == 2 || OP == 4) ? 2 : 1;
+  constexpr int W = (OP == 2) ? 16 : 32;  // floats of one plane per row per round
+  const int kt = NP * kp;
+  const float* r1 = ent_rows + e1 * (int64_t)kt;
+  const float* r2 = ent_rows + e2 * (int64_t)kt;
+  float a1 = 0.0f, a2 = 0.0f;
+  const int kend = (OP == 2) ? kp : kt;  // RotatE walks k over one plane, pairing re/im
+  int k0 = 0;
+  for (; k0 + W <= kend; k0 += W) {
+    float4 x1[W / 4], x2[W / 4], y1[OP == 2 ? W / 4 : 1], y2[OP == 2 ? W / 4 : 1];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        a[i] = qc[(int64_t)(k0 + i) * q_pad];
-        b[i] = qc[(int64_t)(kp + k0 + i) * q_pad];
+    for (int i = 0; i < W / 4; ++i) {
+      x1[i] = *reinterpret_cast<const float4*>(r1 + k0 + 4 * i);
+      x2[i] = *reinterpret_cast<const float4*>(r2 + k0 + 4 * i);
+      if constexpr (OP == 2) {
+        y1[i] = *reinterpret_cast<const float4*>(r1 + kp + k0 + 4 * i);
+        y2[i] = *reinterpret_cast<const float4*>(r2 + kp + k0 + 4 * i);
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc = op_step<OP>(acc, a[i], b[i], x[i], y[i]);
     }
-  } else {
-    const int kt = np * kp;  // ComplEx: re plane then im plane, one fma chain
-    for (int k0 = 0; k0 < kt; k0 += 8) {
-      float x[8], a[8];
-      *reinterpret_cast<float4*>(&x[0]) = *reinterpret_cast<const float4*>(row + k0);
-      *reinterpret_cast<float4*>(&x[4]) = *reinterpret_cast<const float4*>(row + k0 + 4);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a[i] = qc[(int64_t)(k0 + i) * q_pad];
+    for (int i = 0; i < W / 4; ++i) {
+      const int k = k0 + 4 * i;
+      if constexpr (OP == 2) {
+        a1 = op_step<OP>(a1, sq[k + 0], sq[kp + k + 0], x1[i].x, y1[i].x);
+        a2 = op_step<OP>(a2, sq[k + 0], sq[kp + k + 0], x2[i].x, y2[i].x);
+        a1 = op_step<OP>(a1, sq[k + 1], sq[kp + k + 1], x1[i].y, y1[i].y);
+        a2 = op_step<OP>(a2, sq[k + 1], sq[kp + k + 1], x2[i].y, y2[i].y);
+        a1 = op_step<OP>(a1, sq[k + 2], sq[kp + k + 2], x1[i].z, y1[i].z);
+        a2 = op_step<OP>(a2, sq[k + 2], sq[kp + k + 2], x2[i].z, y2[i].z);
+        a1 = op_step<OP>(a1, sq[k + 3], sq[kp + k + 3], x1[i].w, y1[i].w);
+        a2 = op_step<OP>(a2, sq[k + 3], sq[kp + k + 3], x2[i].w, y2[i].w);
+      } else {
+        a1 = op_step<OP>(a1, sq[k + 0], 0.0f, x1[i].x, 0.0f);
+        a2 = op_step<OP>(a2, sq[k + 0], 0.0f, x2[i].x, 0.0f);
+        a1 = op_step<OP>(a1, sq[k + 1], 0.0f, x1[i].y, 0.0f);
+        a2 = op_step<OP>(a2, sq[k + 1], 0.0f, x2[i].y, 0.0f);
+        a1 = op_step<OP>(a1, sq[k + 2], 0.0f, x1[i].z, 0.0f);
+        a2 = op_step<OP>(a2, sq[k + 2], 0.0f, x2[i].z, 0.0f);
+        a1 = op_step<OP>(a1, sq[k + 3], 0.0f, x1[i].w, 0.0f);
+        a2 = op_step<OP>(a2, sq[k + 3], 0.0f, x2[i].w, 0.0f);
+      }
+    }
+  }
+  for (; k0 < kend; k0 += 8) {
+    float x1[8], x2[8], y1[8], y2[8];
+    *reinterpret_cast<float4*>(&x1[0]) = *reinterpret_cast<const float4*>(r1 + k0);
+    *reinterpret_cast<float4*>(&x1[4]) = *reinterpret_cast<const float4*>(r1 + k0 + 4);
+    *reinterpret_cast<float4*>(&x2[0]) = *reinterpret_cast<const float4*>(r2 + k0);
+    *reinterpret_cast<float4*>(&x2[4]) = *reinterpret_cast<const float4*>(r2 + k0 + 4);
+    if constexpr (OP == 2) {
+      *reinterpret_cast<float4*>(&y1[0]) = *reinterpret_cast<const float4*>(r1 + kp + k0);
+      *reinterpret_cast<float4*>(&y1[4]) = *reinterpret_cast<const float4*>(r1 + kp + k0 + 4);
+      *reinterpret_cast<float4*>(&y2[0]) = *reinterpret_cast<const float4*>(r2 + kp + k0);
+      *reinterpret_cast<float4*>(&y2[4]) = *reinterpret_cast<const float4*>(r2 + kp + k0 + 4);
+    }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc = op_step<OP>(acc, a[i], 0.0f, x[i], 0.0f);
+    for (int i = 0; i < 8; ++i) {
+      const float qb = (OP == 2) ? sq[kp + k0 + i] : 0.0f;
+      a1 = op_step<OP>(a1, sq[k0 + i], qb, x1[i], (OP == 2) ? y1[i] : 0.0f);
+      a2 = op_step<OP>(a2, sq[k0 + i], qb, x2[i], (OP == 2) ? y2[i] : 0.0f);
+    }
+  }
+  *s1 = op_final<OP>(a1);
+  *s2 = op_final<OP>(a2);
+}
+
+// Truth scores + filtered-rank correction, one 64-thread workgroup (one wave) per filter
+// group. A filter group is a set of queries with the same (mode, r, anchor) -- the lookup
+// key of Test.h:85's `_find` ((r, t) for head_batch, (h, r) for tail_batch) -- so its
+// members share the query vector and the known-entity list. Per pass, lane i scores listed
+// entity i of the pass and (first pass) the truth of member query i in one fused pair of
+// chains, then every member counts the listed entities that beat its own truth:
+//   thr[q]        = pred(true(q))                 (same arithmetic as the sweep)
+//   counts[.][q]  = {0, -c, 0, -cc}, c = #{listed j != true(q) : pred(j) < thr[q]}
+//                   (cc: those allowed by the type constraint); the sweep adds the raw counts.
+// Groups of more than 64 queries are walked 64 at a time (FilterIndex.groups splits them).
+// grp_qoff/grp_q == NULL: every query is its own group (off indexed by query).
+constexpr int FT = 64;  // threads per filter workgroup = listed entities per pass
+template <int OP>
+__global__ __launch_bounds__(FT) void k_truth_filter(
+    const float* __restrict__ ent_rows, int64_t n_ent, const float* __restrict__ q_km, int64_t q_pad, int kp,
+    const float* __restrict__ q_rows, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,
+    const int8_t* __restrict__ qmode, int64_t n_query, int pred_kind, float margin, const int64_t* __restrict__ grp_qoff,
+    const int32_t* __restrict__ grp_q, int64_t n_groups, const int64_t* __restrict__ off,
+    const int32_t* __restrict__ ids, const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail,
+    int64_t type_words, float* __restrict__ thr, int32_t* __restrict__ counts) {
+  extern __shared__ float sq[];  // [NP * kp] query vector of the group
+  __shared__ float s_v[FT];
+  __shared__ int32_t s_id[FT];
+  __shared__ uint8_t s_tb[FT];
+  constexpr int NP = (OP == 2 || OP == 4) ? 2 : 1;
+  const int tid = threadIdx.x;
+  for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+    const int64_t qa = grp_qoff ? grp_qoff[g] : g, qb = grp_qoff ? grp_qoff[g + 1] : g + 1;
+    const int64_t la = off ? off[g] : 0, lb = off ? off[g + 1] : 0;
+    const int64_t q0 = grp_q ? grp_q[qa] : qa;
+    __syncthreads();  // previous group done with sq / s_*
+    if (q_rows) {  // one contiguous row (the k-major column would touch one cache line per k)
+      for (int k = tid; k < NP * kp; k += FT) sq[k] = q_rows[q0 * NP * kp + k];
+    } else {
+      for (int k = tid; k < NP * kp; k += FT) sq[k] = q_km[(int64_t)k * q_pad + q0];
+    }
+    const uint32_t* tm = type_head ? (qmode[q0] == MMRE_HEAD_BATCH ? type_head : type_tail) : nullptr;
+    const int64_t r = qr[q0];
+    __syncthreads();
+    for (int64_t qc = qa; qc < qb; qc += FT) {
+      const int64_t qi = qc + tid;
+      const bool active = qi < qb;
+      const int64_t q = active ? (grp_q ? grp_q[qi] : qi) : 0;
+      const int32_t tr = active ? qtrue[q] : 0;
+      float th = 0.0f;
+      int c = 0, cc = 0;
+      int64_t lc = la;
+      bool first = true;
+      do {  // at least one pass: the truth scores ride on the first
+        const int nl = (int)((lb - lc) < FT ? (lb - lc) : FT);
+        const int64_t j = tid < nl ? (int64_t)ids[lc + tid] : -1;
+        const bool ok = j >= 0 && j < n_ent;
+        float vt, vj;
+        pair_score2_lds<OP>(ent_rows, sq, kp, tr, ok ? j : 0, &vt, &vj);
+        if (first) {
+          th = apply_pred(pred_kind, margin, vt);
+          if (active) thr[q] = th;
+        }
+        s_id[tid] = ok ? (int32_t)j : -1;
+        s_v[tid] = apply_pred(pred_kind, margin, vj);
+        s_tb[tid] = (ok && tm) ? (uint8_t)type_bit(tm, type_words, r, j) : (uint8_t)0;
+        __syncthreads();
+        if (active) {
+          for (int i = 0; i < nl; ++i) {
+            const int32_t e = s_id[i];
+            if (e >= 0 && e != tr && s_v[i] < th) {
+              c += 1;
+              cc += s_tb[i];
+            }
+          }
+        }
+        __syncthreads();  // s_* reuse
+        lc += nl;
+        first = false;
+      } while (lc < lb);
+      if (active) {
+        counts[0 * n_query + q] = 0;
+        counts[1 * n_query + q] = -c;
+        counts[2 * n_query + q] = 0;
+        counts[3 * n_query + q] = -cc;
+      }
+    }
+  }
+}
+
+// --------------------------------------------- grouped truth + filter (2 phases) ---
+// Phase 1, k_filter_scores: one lane per score task, all tasks of the evaluation in one
+// flat launch (~1.3k waves at FB15K-237-ZS, resident at once): task t < n_query is the
+// truth of query t -> thr[t]; task n_query + p is listed entity p of the filter CSR, scored
+// with the query vector of its group's representative query entry_q[p] -> list_v[p].
+// Both rows stream from global 32 floats per round (RotatE 16 re + 16 im).
+template <int OP>
+__device__ float row_score(const float* __restrict__ qv, const float* __restrict__ ev, int kp) {
+  constexpr int W = (OP == 2) ? 16 : 32;
+  const int kend = (OP == 2) ? kp : ((OP == 4) ? 2 * kp : kp);
+  float acc = 0.0f;
+  int k0 = 0;
+  for (; k0 + W <= kend; k0 += W) {
+    float4 a[W / 4], x[W / 4], b[OP == 2 ? W / 4 : 1], y[OP == 2 ? W / 4 : 1];
+#pragma unroll
+    for (int i = 0; i < W / 4; ++i) {
+      a[i] = *reinterpret_cast<const float4*>(qv + k0 + 4 * i);
+      x[i] = *reinterpret_cast<const float4*>(ev + k0 + 4 * i);
+      if constexpr (OP == 2) {
+        b[i] = *reinterpret_cast<const float4*>(qv + kp + k0 + 4 * i);
+        y[i] = *reinterpret_cast<const float4*>(ev + kp + k0 + 4 * i);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W / 4; ++i) {
+      if constexpr (OP == 2) {
+        acc = op_step<OP>(acc, a[i].x, b[i].x, x[i].x, y[i].x);
+        acc = op_step<OP>(acc, a[i].y, b[i].y, x[i].y, y[i].y);
+        acc = op_step<OP>(acc, a[i].z, b[i].z, x[i].z, y[i].z);
+        acc = op_step<OP>(acc, a[i].w, b[i].w, x[i].w, y[i].w);
+      } else {
+        acc = op_step<OP>(acc, a[i].x, 0.0f, x[i].x, 0.0f);
+        acc = op_step<OP>(acc, a[i].y, 0.0f, x[i].y, 0.0f);
+        acc = op_step<OP>(acc, a[i].z, 0.0f, x[i].z, 0.0f);
+        acc = op_step<OP>(acc, a[i].w, 0.0f, x[i].w, 0.0f);
+      }
+    }
+  }
+  for (; k0 < kend; k0 += 4) {  // kp % 8 == 0, so whole float4s remain
+    const float4 a = *reinterpret_cast<const float4*>(qv + k0);
+    const float4 x = *reinterpret_cast<const float4*>(ev + k0);
+    if constexpr (OP == 2) {
+      const float4 b = *reinterpret_cast<const float4*>(qv + kp + k0);
+      const float4 y = *reinterpret_cast<const float4*>(ev + kp + k0);
+      acc = op_step<OP>(acc, a.x, b.x, x.x, y.x);
+      acc = op_step<OP>(acc, a.y, b.y, x.y, y.y);
+      acc = op_step<OP>(acc, a.z, b.z, x.z, y.z);
+      acc = op_step<OP>(acc, a.w, b.w, x.w, y.w);
+    } else {
+      acc = op_step<OP>(acc, a.x, 0.0f, x.x, 0.0f);
+      acc = op_step<OP>(acc, a.y, 0.0f, x.y, 0.0f);
+      acc = op_step<OP>(acc, a.z, 0.0f, x.z, 0.0f);
+      acc = op_step<OP>(acc, a.w, 0.0f, x.w, 0.0f);
     }
   }
   return op_final<OP>(acc);
 }
 
 template <int OP>
-__global__ void k_truth(const float* __restrict__ ent_rows, const float* __restrict__ q_km,
-                        int64_t q_pad, int kp, const int32_t* __restrict__ qtrue, int64_t n_query,
-                        int pred_kind, float margin, float* __restrict__ thr) {
-  int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= n_query) return;
-  thr[q] = apply_pred(pred_kind, margin, pair_score<OP>(ent_rows, q_km, q_pad, kp, q, qtrue[q]));
+__global__ __launch_bounds__(256) void k_filter_scores(const float* __restrict__ ent_rows, int64_t n_ent,
+                                                       const float* __restrict__ q_rows, int kp,
+                                                       const int32_t* __restrict__ qtrue, int64_t n_query,
+                                                       int pred_kind, float margin, const int32_t* __restrict__ entry_q,
+                                                       const int32_t* __restrict__ ids, int64_t n_entries,
+                                                       float* __restrict__ thr, float* __restrict__ list_v) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_query + n_entries) return;
+  const int64_t kt = (int64_t)((OP == 2 || OP == 4) ? 2 : 1) * kp;
+  if (t < n_query) {
+    thr[t] = apply_pred(pred_kind, margin, row_score<OP>(q_rows + t * kt, ent_rows + (int64_t)qtrue[t] * kt, kp));
+    return;
+  }
+  const int64_t p = t - n_query;
+  const int64_t j = ids[p];
+  const int64_t vq = entry_q[p];
+  if (j < 0 || j >= n_ent || vq < 0 || vq >= n_query) {
+    list_v[p] = __builtin_nanf("");  // never < a threshold: an invalid id is not counted
+    return;
+  }
+  list_v[p] = apply_pred(pred_kind, margin, row_score<OP>(q_rows + vq * kt, ent_rows + j * kt, kp));
 }
 
-__device__ __forceinline__ bool type_bit(const uint32_t* __restrict__ mask, int64_t words, int64_t r, int64_t e) {
-  return (mask[r * words + (e >> 5)] >> (e & 31)) & 1u;
-}
-
-// Filtered rank correction: for each known entity j of query q (filter CSR), j != truth,
-// that beats the truth, subtract one from the filtered counts (Test.h:85 `not _find`).
-// One 64-thread workgroup per query (grid-stride), lanes over its list.
-template <int OP>
-__global__ __launch_bounds__(64) void k_filter_correct(
-    const float* __restrict__ ent_rows, int64_t n_ent, const float* __restrict__ q_km, int64_t q_pad, int kp,
-    const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
-    int64_t n_query, int pred_kind, float margin, const float* __restrict__ thr, const int64_t* __restrict__ off,
-    const int32_t* __restrict__ ids, const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail,
-    int64_t type_words, int32_t* __restrict__ counts) {
-  for (int64_t q = blockIdx.x; q < n_query; q += gridDim.x) {
-    const int64_t a = off[q], b = off[q + 1];
-    const float th = thr[q];
-    const int32_t tr = qtrue[q];
-    int c = 0, cc = 0;
-    for (int64_t p = a + threadIdx.x; p < b; p += blockDim.x) {
-      const int64_t j = ids[p];
-      if (j == tr || j < 0 || j >= n_ent) continue;
-      const float v = apply_pred(pred_kind, margin, pair_score<OP>(ent_rows, q_km, q_pad, kp, q, j));
-      if (v < th) {
-        c += 1;
-        if (type_head) {
-          const uint32_t* m = qmode[q] == MMRE_HEAD_BATCH ? type_head : type_tail;
-          cc += type_bit(m, type_words, qr[q], j);
+// Phase 2, k_filter_count: one wave per filter group (queries sharing (mode, r, anchor),
+// see mmre_link_truth_grouped); the group's listed scores are staged in LDS 64 at a time and
+// every member query (one per lane) counts those that beat its own truth:
+//   counts[.][q] = {0, -c, 0, -cc}, c = #{listed j != true(q) : pred(j) < thr[q]} (Test.h:85)
+__global__ __launch_bounds__(64) void k_filter_count(const int64_t* __restrict__ grp_qoff,
+                                                     const int32_t* __restrict__ grp_q, int64_t n_groups,
+                                                     const int64_t* __restrict__ off, const int32_t* __restrict__ ids,
+                                                     const float* __restrict__ list_v,
+                                                     const int32_t* __restrict__ qtrue, const float* __restrict__ thr,
+                                                     const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
+                                                     int64_t n_query, int64_t n_ent,
+                                                     const uint32_t* __restrict__ type_head,
+                                                     const uint32_t* __restrict__ type_tail, int64_t type_words,
+                                                     int32_t* __restrict__ counts) {
+  __shared__ float s_v[64];
+  __shared__ int32_t s_id[64];
+  __shared__ uint8_t s_tb[64];
+  const int tid = threadIdx.x;
+  for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
+    const int64_t qa = grp_qoff[g], qb = grp_qoff[g + 1];
+    const int64_t la = off[g], lb = off[g + 1];
+    const int64_t q0 = grp_q[qa];
+    const uint32_t* tm = type_head ? (qmode[q0] == MMRE_HEAD_BATCH ? type_head : type_tail) : nullptr;
+    const int64_t r = qr[q0];
+    for (int64_t qc = qa; qc < qb; qc += 64) {
+      const int64_t qi = qc + tid;
+      const bool active = qi < qb;
+      const int64_t q = active ? grp_q[qi] : 0;
+      const int32_t tr = active ? qtrue[q] : -1;
+      const float th = active ? thr[q] : 0.0f;
+      int c = 0, cc = 0;
+      for (int64_t lc = la; lc < lb; lc += 64) {
+        const int nl = (int)((lb - lc) < 64 ? (lb - lc) : 64);
+        __syncthreads();  // s_* reuse
+        if (tid < nl) {
+          const int64_t j = ids[lc + tid];
+          const bool ok = j >= 0 && j < n_ent;
+          s_id[tid] = ok ? (int32_t)j : -1;
+          s_v[tid] = list_v[lc + tid];
+          s_tb[tid] = (ok && tm) ? (uint8_t)type_bit(tm, type_words, r, j) : (uint8_t)0;
+        }
+        __syncthreads();
+        if (active) {
+          for (int i = 0; i < nl; ++i) {
+            const int32_t e = s_id[i];
+            if (e >= 0 && e != tr && s_v[i] < th) {
+              c += 1;
+              cc += s_tb[i];
+            }
+          }
         }
       }
-    }
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-      c += __shfl_xor(c, s);
-      cc += __shfl_xor(cc, s);
-    }
-    if (threadIdx.x == 0) {
-      if (c) atomicSub(&counts[1 * n_query + q], c);
-      if (cc) atomicSub(&counts[3 * n_query + q], cc);
+      if (active) {
+        counts[0 * n_query + q] = 0;
+        counts[1 * n_query + q] = -c;
+        counts[2 * n_query + q] = 0;
+        counts[3 * n_query + q] = -cc;
+      }
     }
   }
 }
@@ -667,9 +934,12 @@ extern "C" int mmre_link_prepare_entities(int model, int norm_flag, const float*
   if (!d_ent || !d_ent_km || !d_ent_rows || n_ent <= 0 || dim <= 0 || e_pad < n_ent || e_pad % TE) return MMRE_ERR_ARG;
   if (model == MMRE_COMPLEX && !d_ent_im) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const int threads = 256;
-  hipLaunchKernelGGL(k_prep_entities, dim3((unsigned)((e_pad + threads - 1) / threads)), dim3(threads), 0, st,
-                     model, norm_flag, d_ent, d_ent_im, n_ent, dim, plane_rows(dim), d_ent_km, e_pad, d_ent_rows);
+  const int kp = plane_rows(dim), kt = n_planes(model) * kp;
+  const int rb = stage_rows(kt);
+  const size_t lds = sizeof(float) * (size_t)rb * (kt + 1);
+  if (lds > 64 * 1024) return MMRE_ERR_SHAPE;
+  hipLaunchKernelGGL(k_prep_rows, dim3((unsigned)((e_pad + rb - 1) / rb)), dim3(256), lds, st, model, norm_flag, d_ent,
+                     d_ent_im, n_ent, dim, kp, rb, d_ent_km, e_pad, d_ent_rows, kt);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
@@ -679,7 +949,7 @@ extern "C" int mmre_link_prepare_queries(int model, int norm_flag, const float* 
                                          float phase_denom, const int64_t* d_qh, const int64_t* d_qr,
                                          const int64_t* d_qt, const int8_t* d_qmode, int64_t n_query,
                                          float* d_q_km, int64_t q_pad, int32_t* d_q_true, float* d_rel_work,
-                                         void* stream) {
+                                         float* d_q_rows, void* stream) {
   if (!valid_model(model)) return MMRE_ERR_MODEL;
   if (!d_ent_rows || !d_rel || !d_qh || !d_qr || !d_qt || !d_qmode || !d_q_km || !d_q_true) return MMRE_ERR_ARG;
   if (n_query <= 0 || q_pad < n_query || q_pad % TQ || dim <= 0 || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
@@ -688,37 +958,39 @@ extern "C" int mmre_link_prepare_queries(int model, int norm_flag, const float* 
   const bool transe = model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2;
   if (transe && norm_flag && !d_rel_work) return MMRE_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  const int threads = 256;
+  const int kp = plane_rows(dim), kt = n_planes(model) * kp;
   const float* rel = d_rel;
-  if (transe && norm_flag) {
-    hipLaunchKernelGGL(k_norm_rows, dim3((unsigned)((n_rel + threads - 1) / threads)), dim3(threads), 0, st, d_rel,
-                       n_rel, dim, d_rel_work);
+  if (transe && norm_flag) {  // normalised relation rows (TransE.py:63-66) into d_rel_work (n_rel, dim)
+    const int rb = stage_rows(kp);
+    hipLaunchKernelGGL(k_prep_rows, dim3((unsigned)((n_rel + rb - 1) / rb)), dim3(256),
+                       sizeof(float) * (size_t)rb * (kp + 1), st, model, 1, d_rel, (const float*)nullptr, n_rel, dim,
+                       kp, rb, (float*)nullptr, (int64_t)0, d_rel_work, dim);
     MMRE_CHECK_LAUNCH();
     rel = d_rel_work;
   }
-  const int kp = plane_rows(dim);
-  hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((q_pad + threads - 1) / threads), (unsigned)kp), dim3(threads),
-                     0, st, model, d_ent_rows, rel, d_rel_im, dim, kp, phase_denom, d_qh, d_qr, d_qt, d_qmode,
-                     n_query, d_q_km, q_pad, d_q_true);
+  const int rb = stage_rows(kt);
+  const size_t lds = sizeof(float) * (size_t)rb * (kt + 1);
+  if (lds > 64 * 1024) return MMRE_ERR_SHAPE;
+  hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((q_pad + rb - 1) / rb)), dim3(256), lds, st, model, d_ent_rows,
+                     rel, d_rel_im, dim, kp, rb, phase_denom, d_qh, d_qr, d_qt, d_qmode, n_query, d_q_km, q_pad,
+                     d_q_true, d_q_rows);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
 
 template <int OP>
-static int launch_aux(hipStream_t st, const float* ent_rows, int64_t n_ent, const float* q_km, int64_t q_pad, int kp,
-                      const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, int64_t n_query, int pk, float m,
-                      float* thr, const int64_t* off, const int32_t* ids, const uint32_t* th, const uint32_t* tt,
-                      int64_t tw, int32_t* counts) {
-  const int threads = 256;
-  hipLaunchKernelGGL((k_truth<OP>), dim3((unsigned)((n_query + threads - 1) / threads)), dim3(threads), 0, st,
-                     ent_rows, q_km, q_pad, kp, qtrue, n_query, pk, m, thr);
+static int launch_truth_filter(hipStream_t st, const float* ent_rows, int64_t n_ent, const float* q_km, int64_t q_pad,
+                               int kp, const float* q_rows, const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, int64_t n_query,
+                               int pk, float m, const int64_t* grp_qoff, const int32_t* grp_q, int64_t n_groups,
+                               const int64_t* off, const int32_t* ids, const uint32_t* th, const uint32_t* tt,
+                               int64_t tw, float* thr, int32_t* counts) {
+  constexpr int NP = (OP == 2 || OP == 4) ? 2 : 1;
+  const size_t lds = sizeof(float) * (size_t)NP * kp;
+  if (lds > 64 * 1024) return MMRE_ERR_SHAPE;
+  const unsigned blocks = (unsigned)(n_groups < (1 << 20) ? n_groups : (1 << 20));
+  hipLaunchKernelGGL((k_truth_filter<OP>), dim3(blocks), dim3(FT), lds, st, ent_rows, n_ent, q_km, q_pad, kp, q_rows,
+                     qtrue, qr, qmode, n_query, pk, m, grp_qoff, grp_q, n_groups, off, ids, th, tt, tw, thr, counts);
   MMRE_CHECK_LAUNCH();
-  if (off) {
-    const unsigned blocks = (unsigned)(n_query < 16384 ? n_query : 16384);
-    hipLaunchKernelGGL((k_filter_correct<OP>), dim3(blocks), dim3(64), 0, st, ent_rows, n_ent, q_km, q_pad, kp,
-                       qtrue, qr, qmode, n_query, pk, m, thr, off, ids, th, tt, tw, counts);
-    MMRE_CHECK_LAUNCH();
-  }
   return MMRE_OK;
 }
 
@@ -735,6 +1007,56 @@ static int check_link_args(int model, int pred_kind, const float* d_ent_km, int6
   return MMRE_OK;
 }
 
+template <int OP>
+static int launch_filter_scores(hipStream_t st, const float* ent_rows, int64_t n_ent, const float* q_rows, int kp,
+                                const int32_t* qtrue, int64_t n_query, int pk, float m, const int32_t* entry_q,
+                                const int32_t* ids, int64_t n_entries, float* thr, float* list_v) {
+  const int64_t tasks = n_query + n_entries;
+  hipLaunchKernelGGL((k_filter_scores<OP>), dim3((unsigned)((tasks + 255) / 256)), dim3(256), 0, st, ent_rows, n_ent,
+                     q_rows, kp, qtrue, n_query, pk, m, entry_q, ids, n_entries, thr, list_v);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_link_truth_grouped(int model, int pred_kind, float margin, const float* d_ent_rows, int64_t n_ent,
+                                       const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr,
+                                       const int8_t* d_qmode, int64_t n_query, int dim, const int64_t* d_grp_qoff,
+                                       const int32_t* d_grp_q, int64_t n_groups, const int64_t* d_filt_off,
+                                       const int32_t* d_filt_ids, const int32_t* d_entry_q, int64_t n_entries,
+                                       const uint32_t* d_type_head, const uint32_t* d_type_tail,
+                                       float* d_list_scores, int32_t* d_counts, float* d_truth, void* stream) {
+  if (!valid_model(model)) return MMRE_ERR_MODEL;
+  if (pred_kind < 0 || pred_kind > 4) return MMRE_ERR_ARG;
+  if (!d_ent_rows || !d_q_rows || !d_q_true || !d_qr || !d_qmode || !d_counts || !d_truth) return MMRE_ERR_ARG;
+  if (!d_grp_qoff || !d_grp_q || !d_filt_off) return MMRE_ERR_ARG;
+  if (n_query <= 0 || n_ent <= 0 || dim <= 0 || n_groups <= 0 || n_groups > n_query || n_entries < 0)
+    return MMRE_ERR_ARG;
+  if (n_entries > 0 && (!d_filt_ids || !d_entry_q || !d_list_scores)) return MMRE_ERR_WORKSPACE;
+  if ((d_type_head == nullptr) != (d_type_tail == nullptr)) return MMRE_ERR_ARG;
+  if (n_ent >= (int64_t)INT32_MAX || n_query >= (int64_t)INT32_MAX) return MMRE_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  const int kp = plane_rows(dim);
+  int rc;
+#define MMRE_FS(OPV)                                                                                              \
+  launch_filter_scores<OPV>(st, d_ent_rows, n_ent, d_q_rows, kp, d_q_true, n_query, pred_kind, margin, d_entry_q, \
+                            d_filt_ids, n_entries, d_truth, d_list_scores)
+  switch (op_of_model(model)) {
+    case 0: rc = MMRE_FS(0); break;
+    case 1: rc = MMRE_FS(1); break;
+    case 2: rc = MMRE_FS(2); break;
+    case 3: rc = MMRE_FS(3); break;
+    default: rc = MMRE_FS(4); break;
+  }
+#undef MMRE_FS
+  if (rc) return rc;
+  const unsigned blocks = (unsigned)(n_groups < (1 << 20) ? n_groups : (1 << 20));
+  hipLaunchKernelGGL(k_filter_count, dim3(blocks), dim3(64), 0, st, d_grp_qoff, d_grp_q, n_groups, d_filt_off,
+                     d_filt_ids, d_list_scores, d_q_true, d_truth, d_qr, d_qmode, n_query, n_ent, d_type_head,
+                     d_type_tail, (n_ent + 31) / 32, d_counts);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
 extern "C" int mmre_link_truth(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
                                int64_t e_pad, const float* d_ent_rows, const float* d_q_km, const int32_t* d_q_true,
                                const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
@@ -748,17 +1070,18 @@ extern "C" int mmre_link_truth(int model, int pred_kind, float margin, const flo
   hipStream_t st = (hipStream_t)stream;
   const int kp = plane_rows(dim);
   const int64_t tw = (n_ent + 31) / 32;
-  MMRE_CHECK(hipMemsetAsync(d_counts, 0, sizeof(int32_t) * 4 * n_query, st));
-#define MMRE_AUX(OPV) launch_aux<OPV>(st, d_ent_rows, n_ent, d_q_km, q_pad, kp, d_q_true, d_qr, d_qmode, n_query, \
-                                      pred_kind, margin, d_truth, d_filt_off, d_filt_ids, d_type_head, d_type_tail, tw, d_counts)
+#define MMRE_TF(OPV)                                                                                              \
+  launch_truth_filter<OPV>(st, d_ent_rows, n_ent, d_q_km, q_pad, kp, nullptr, d_q_true, d_qr, d_qmode, n_query,   \
+                           pred_kind, margin, nullptr, nullptr, n_query, d_filt_off, d_filt_ids, d_type_head,      \
+                           d_type_tail, tw, d_truth, d_counts)
   switch (op_of_model(model)) {
-    case 0: return MMRE_AUX(0);
-    case 1: return MMRE_AUX(1);
-    case 2: return MMRE_AUX(2);
-    case 3: return MMRE_AUX(3);
-    default: return MMRE_AUX(4);
+    case 0: return MMRE_TF(0);
+    case 1: return MMRE_TF(1);
+    case 2: return MMRE_TF(2);
+    case 3: return MMRE_TF(3);
+    default: return MMRE_TF(4);
   }
-#undef MMRE_AUX
+#undef MMRE_TF
 }
 
 extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,

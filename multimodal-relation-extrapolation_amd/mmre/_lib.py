@@ -24,8 +24,10 @@ SIGNATURES = {
     "mmre_link_k": (I64, [I32, I32]),
     "mmre_link_pad": (I64, [I64]),
     "mmre_link_prepare_entities": (I32, [I32, I32, P, P, I64, I32, P, I64, P, P]),
-    "mmre_link_prepare_queries": (I32, [I32, I32, P, P, P, I64, I64, I32, F32, P, P, P, P, I64, P, I64, P, P, P]),
+    "mmre_link_prepare_queries": (I32, [I32, I32, P, P, P, I64, I64, I32, F32, P, P, P, P, I64, P, I64, P, P, P, P]),
     "mmre_link_truth": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, P, I64, I64, I32, P, P, P, P, P, P, P]),
+    "mmre_link_truth_grouped": (I32, [I32, I32, F32, P, I64, P, P, P, P, I64, I32, P, P, I64, P, P, P, I64, P, P, P,
+                                      P, P, P]),
     "mmre_link_sweep": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P]),
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
     "mmre_glibc_rand": (I32, [I64, I64, P]),

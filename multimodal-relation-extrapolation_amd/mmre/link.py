@@ -99,6 +99,32 @@ class FilterIndex:
             ids[dst] = gids
         return off, ids
 
+    def groups(self, qh, qr, qt, qmode, max_group: int = 64):
+        """Filter groups: queries with the same (mode, r, anchor) share their known-entity
+        list (Test.h:85 `_find` looks up (r, t) for head_batch, (h, r) for tail_batch).
+        Groups larger than `max_group` queries are split (one wave of the count kernel per
+        group). Returns (grp_qoff int64 [G+1], grp_q int32 [Q], off int64 [G+1], ids int32,
+        entry_q int32): the query partition, one CSR list per group and, per listed entity,
+        the group member whose query vector scores it -- for mmre_link_truth_grouped."""
+        qh, qr, qt, qmode = (np.asarray(x, np.int64) for x in (qh, qr, qt, qmode))
+        anchor = np.where(qmode == HEAD, qt, qh)
+        key = (qmode * self.n_rel + qr) * self.n_ent + anchor
+        _, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+        grp_q = np.argsort(inv, kind="stable").astype(np.int32)
+        # split each key's run of queries into pieces of <= max_group
+        starts = np.zeros(len(cnt), np.int64)
+        np.cumsum(cnt[:-1], out=starts[1:])
+        pieces = (cnt + max_group - 1) // max_group
+        piece_key = np.repeat(np.arange(len(cnt)), pieces)
+        piece_idx = np.arange(len(piece_key)) - np.repeat(np.cumsum(pieces) - pieces, pieces)
+        grp_qoff = np.empty(len(piece_key) + 1, np.int64)
+        grp_qoff[:-1] = starts[piece_key] + piece_idx * max_group
+        grp_qoff[-1] = len(grp_q)
+        first = grp_q[grp_qoff[:-1]]
+        off, ids = self.filters(qh[first], qr[first], qt[first], qmode[first])
+        entry_q = np.repeat(first, np.diff(off)).astype(np.int32)
+        return grp_qoff, grp_q, off, ids, entry_q
+
     def type_masks(self):
         if self.type_heads is None:
             return None
@@ -148,15 +174,18 @@ class LinkSweep:
         q_pad = int(_lib.lib().mmre_link_pad(n_query))
         dev = self.device
         return dict(q_km=torch.empty((self.K, q_pad), dtype=torch.float32, device=dev),
+                    q_rows=torch.empty((n_query, self.K), dtype=torch.float32, device=dev),
                     q_true=torch.empty(q_pad, dtype=torch.int32, device=dev),
                     counts=torch.empty((4, n_query), dtype=torch.int32, device=dev),
                     truth=torch.empty(n_query, dtype=torch.float32, device=dev), q_pad=q_pad)
 
     def run(self, qh, qr, qt, qmode, filt=None, type_masks=None, return_scores=False, buffers=None,
-            prepare=True, sweep_events=None):
-        """qh/qr/qt int64 and qmode int8 device tensors. filt: (off int64, ids int32) device CSR.
+            prepare=True, sweep_events=None, q_rows=True):
+        """qh/qr/qt int64 and qmode int8 device tensors. filt: per-query CSR (off int64, ids int32)
+        or filter groups (grp_qoff, grp_q, off, ids, entry_q), see FilterIndex.groups.
         sweep_events: optional (start, end) torch.cuda.Event pair recorded around the sweep kernel alone
-        (on the stream the kernels are launched on).
+        (on the stream the kernels are launched on). q_rows=False: no row-major query copy (the
+        per-query truth/filter kernel then gathers the query vectors from the k-major plane).
         Returns dict(counts=(4, Q) int32 [raw, filt, raw_tc, filt_tc], truth=(Q,), scores=(Q, E)|None)."""
         s = self.spec
         n = int(qh.shape[0])
@@ -164,17 +193,31 @@ class LinkSweep:
             self.prepare_entities()
         b = buffers if buffers is not None else self.alloc_queries(n)
         st = stream_ptr(self.device)
+        qrow = b["q_rows"] if q_rows else None   # None: truth kernel reads the k-major plane
         call("mmre_link_prepare_queries", self.model_id, int(bool(s.norm_flag)), ptr(self.ent_rows), ptr(self._rel),
              ptr(self._rel_im), self.n_ent, self.n_rel, s.dim, float(s.phase_denom), ptr(qh), ptr(qr), ptr(qt),
-             ptr(qmode), n, ptr(b["q_km"]), b["q_pad"], ptr(b["q_true"]), ptr(self.rel_work), st)
+             ptr(qmode), n, ptr(b["q_km"]), b["q_pad"], ptr(b["q_true"]), ptr(self.rel_work), ptr(qrow), st)
         scores = None
         if return_scores:
             scores = torch.empty((n, self.n_ent), dtype=torch.float32, device=self.device)
-        off, ids = (None, None) if filt is None else filt
         th, tt = (None, None) if type_masks is None else type_masks
-        call("mmre_link_truth", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
-             self.e_pad, ptr(self.ent_rows), ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(off),
-             ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
+        if filt is not None and len(filt) == 5 and q_rows:   # filter groups (FilterIndex.groups)
+            gqo, gq, off, ids, entry_q = filt
+            n_entries = int(ids.shape[0])
+            lv = b.get("list_scores")
+            if lv is None or lv.shape[0] < n_entries:
+                lv = b["list_scores"] = torch.empty(max(n_entries, 1), dtype=torch.float32, device=self.device)
+            call("mmre_link_truth_grouped", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_rows),
+                 self.n_ent, ptr(qrow), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, s.dim, ptr(gqo), ptr(gq),
+                 int(gqo.shape[0]) - 1, ptr(off), ptr(ids), ptr(entry_q), n_entries, ptr(th), ptr(tt), ptr(lv),
+                 ptr(b["counts"]), ptr(b["truth"]), st)
+        else:
+            if filt is not None and len(filt) == 5:   # groups -> per-query CSR is not derivable here
+                raise ValueError("filter groups need q_rows=True")
+            off, ids = (None, None) if filt is None else filt
+            call("mmre_link_truth", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
+                 self.e_pad, ptr(self.ent_rows), ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n,
+                 b["q_pad"], s.dim, ptr(off), ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
         if sweep_events is not None:
             sweep_events[0].record()
         call("mmre_link_sweep", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
@@ -185,16 +228,28 @@ class LinkSweep:
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
 
 
+def _rows_view(c):
+    """(4, n) int32 with unit element stride (row stride free): column slices of one
+    (4, 2n) count table are passed to the C reduction without a copy."""
+    c = np.asarray(c)
+    if c.dtype != np.int32 or c.ndim != 2 or c.strides[1] != 4 or c.strides[0] % 4:
+        c = np.ascontiguousarray(c, np.int32)
+    return c
+
+
 def link_metrics(head_counts: np.ndarray, tail_counts: np.ndarray):
     """Test.h:232-327 metric reduction (host C++ in libmmre, P14 float order).
     head_counts/tail_counts: (4, n) int32 = raw, filt, raw_tc, filt_tc."""
-    import ctypes
-    h = np.ascontiguousarray(head_counts, np.int32)
-    t = np.ascontiguousarray(tail_counts, np.int32)
+    h, t = _rows_view(head_counts), _rows_view(tail_counts)
     n = h.shape[1]
+    if t.shape[1] != n or h.shape[0] != 4 or t.shape[0] != 4:
+        raise ValueError("head/tail counts must both be (4, n)")
+    stride = h.strides[0] // 4
+    if t.strides[0] != h.strides[0]:
+        h, t = np.ascontiguousarray(h), np.ascontiguousarray(t)
+        stride = n
     out = np.zeros(20, np.float32)
-    call("mmre_link_metrics", h.ctypes.data_as(ctypes.c_void_p), t.ctypes.data_as(ctypes.c_void_p), n, n,
-         out.ctypes.data_as(ctypes.c_void_p))
+    call("mmre_link_metrics", h.ctypes.data, t.ctypes.data, n, stride, out.ctypes.data)
     return {g: {m: float(out[5 * gi + mi]) for mi, m in enumerate(METRIC_NAMES)} for gi, g in enumerate(GROUPS)}
 
 
@@ -212,8 +267,7 @@ def evaluate_link_prediction(spec: ScoreSpec, test_h, test_r, test_t, index: Fil
     filt = None
     masks = None
     if index is not None:
-        off, ids = index.filters(qh, qr, qt, qm)
-        filt = (torch.from_numpy(off).to(dev), torch.from_numpy(ids).to(dev))
+        filt = tuple(torch.from_numpy(a).to(dev) for a in index.groups(qh, qr, qt, qm))
         if type_constrain:
             tm = index.type_masks()
             masks = tuple(torch.from_numpy(m).to(dev) for m in tm)

@@ -97,8 +97,7 @@ class ShardedLinkEvaluation:
         self.filt = None
         self.masks_tc = None
         if index is not None:
-            off, ids = index.filters(qh[mine], qr[mine], qt[mine], qm[mine])
-            self.filt = (to(off), to(ids))
+            self.filt = tuple(to(a) for a in index.groups(qh[mine], qr[mine], qt[mine], qm[mine]))
             if type_constrain:
                 self.masks_tc = tuple(to(m) for m in index.type_masks())
         self.plan = ShardPlan(self.masks, dev) if self.world > 1 else None
@@ -117,7 +116,19 @@ class ShardedLinkEvaluation:
         local = self.local_runner(*self.q, self.filt, self.masks_tc, events)
         return gather_counts(local, self.plan, self.group) if self.world > 1 else local
 
-    def run(self, events=None):
+    def run(self, events=None, copy_counts=True):
+        """(metrics, counts (4, 2n) int32). copy_counts=False returns the reused pinned buffer
+        (overwritten by the next run)."""
         from .link import link_metrics
-        c = self.counts(events).cpu().numpy()
+        c = self.counts(events)
+        if c.is_cuda:  # D2H into a reused pinned buffer, then wait for this stream only
+            if getattr(self, "_host", None) is None or self._host.shape != c.shape:
+                self._host = torch.empty(c.shape, dtype=c.dtype, pin_memory=True)
+            self._host.copy_(c, non_blocking=True)
+            torch.cuda.current_stream(c.device).synchronize()
+            c = self._host.numpy()
+            if copy_counts:
+                c = c.copy()
+        else:
+            c = c.numpy()
         return link_metrics(c[:, :self.n], c[:, self.n:]), c

@@ -1,0 +1,51 @@
+#!/usr/bin/env python
+"""Where the bench step's time goes (C2 by default): full step vs GPU launches + sync vs
+D2H + host metric reduction. Diagnostic only; bench.py is the measurement of record."""
+import argparse
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "multimodal-relation-extrapolation_amd"), REPO]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mmre.link import FilterIndex, ScoreSpec, link_metrics  # noqa: E402
+from mmre.sharding import ShardedLinkEvaluation  # noqa: E402
+from mmre.workloads import zs_workload  # noqa: E402
+
+
+def timeit(fn, reps):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    w = zs_workload()
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], w["n_ent"], w["n_rel"])
+    spec = ScoreSpec(model="transe", ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=200, norm_flag=True)
+    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+    for _ in range(3):
+        ev.run(copy_counts=False)
+    full = timeit(lambda: ev.run(copy_counts=False), a.reps)
+    gpu = timeit(lambda: ev.counts(), a.reps)
+    c = ev.counts().cpu().numpy()
+    n = ev.n
+    t = time.perf_counter()
+    for _ in range(a.reps):
+        link_metrics(c[:, :n], c[:, n:])
+    met = (time.perf_counter() - t) / a.reps * 1e3
+    print(f"full step {full:.3f} ms | launches+GPU {gpu:.3f} ms | host metrics {met:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

@@ -124,6 +124,35 @@ def test_filter_index_and_type_masks():
         assert np.nonzero(bits)[0].tolist() == d.type_tails[r_]
 
 
+def test_filter_groups_partition():
+    """FilterIndex.groups: a partition of the queries into (mode, r, anchor) groups whose
+    shared list equals every member's own filter list."""
+    from mmre.data import OpenKEDataset
+    from mmre.link import FilterIndex
+    d = OpenKEDataset(os.path.join(GOLDEN, "data", "medium"))
+    idx = FilterIndex(*d.all_triples(), d.n_ent, d.n_rel)
+    h, r, t = d.test_list()
+    n = len(h)
+    qh, qr, qt = (np.concatenate([x, x]) for x in (h, r, t))
+    qm = np.r_[np.zeros(n, np.int8), np.ones(n, np.int8)]
+    off, ids = idx.filters(qh, qr, qt, qm)
+    gqo, gq, goff, gids, entry_q = idx.groups(qh, qr, qt, qm, max_group=3)
+    assert len(entry_q) == len(gids)
+    assert gqo[0] == 0 and gqo[-1] == 2 * n and np.all(np.diff(gqo) > 0) and np.all(np.diff(gqo) <= 3)
+    assert np.array_equal(np.sort(gq), np.arange(2 * n))
+    assert len(goff) == len(gqo) and goff[-1] == len(gids)
+    for g in range(len(gqo) - 1):
+        members = gq[gqo[g]:gqo[g + 1]]
+        lst = gids[goff[g]:goff[g + 1]].tolist()
+        m0 = members[0]
+        assert np.all(entry_q[goff[g]:goff[g + 1]] == m0)
+        for q in members:
+            assert qm[q] == qm[m0] and qr[q] == qr[m0]
+            assert (qt[q] == qt[m0]) if qm[q] == 0 else (qh[q] == qh[m0])
+            assert ids[off[q]:off[q + 1]].tolist() == lst
+    assert len(gqo) - 1 < 2 * n  # the synthetic test set shares keys
+
+
 def test_test_list_order_matches_reference(golden):
     """testList sorted by (r, h, t) (Reader.h:227): the reference Base.so's query order."""
     from mmre.data import OpenKEDataset

@@ -44,18 +44,18 @@ def _tables(g, name):
     return g[f"{name}.ent_embeddings.weight"], g[f"{name}.rel_embeddings.weight"], None, None
 
 
-def _run(spec, qh, qr, qt, qm, index=None, tc=False, scores=True):
+def _run(spec, qh, qr, qt, qm, index=None, tc=False, scores=True, grouped=True, q_rows=True):
     from mmre.link import LinkSweep
     dev = spec.ent.device
     filt = masks = None
     if index is not None:
-        off, ids = index.filters(qh, qr, qt, qm)
-        filt = (torch.from_numpy(off).to(dev), torch.from_numpy(ids).to(dev))
+        lists = index.groups(qh, qr, qt, qm) if grouped else index.filters(qh, qr, qt, qm)
+        filt = tuple(torch.from_numpy(a).to(dev) for a in lists)
         if tc:
             masks = tuple(torch.from_numpy(m).to(dev) for m in index.type_masks())
     res = LinkSweep(spec).run(*(torch.from_numpy(np.asarray(x, np.int64)).to(dev) for x in (qh, qr, qt)),
                               torch.from_numpy(np.asarray(qm, np.int8)).to(dev), filt=filt, type_masks=masks,
-                              return_scores=scores)
+                              return_scores=scores, q_rows=q_rows)
     torch.cuda.synchronize()
     out = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.items()}
     return out
@@ -63,7 +63,8 @@ def _run(spec, qh, qr, qt, qm, index=None, tc=False, scores=True):
 
 @pytest.mark.parametrize("name", list(GOLD_CFG))
 @pytest.mark.parametrize("tc", [0, 1])
-def test_golden_link_small(golden, oracle_mod, name, tc):
+@pytest.mark.parametrize("grouped", [0, 1])
+def test_golden_link_small(golden, oracle_mod, name, tc, grouped):
     from mmre.data import OpenKEDataset
     from mmre.link import FilterIndex, link_metrics
     g = golden("link_small")
@@ -77,7 +78,7 @@ def test_golden_link_small(golden, oracle_mod, name, tc):
     n = len(qh)
     QH, QR, QT = (np.concatenate([x, x]) for x in (qh, qr, qt))
     QM = np.concatenate([np.zeros(n, np.int8), np.ones(n, np.int8)])
-    out = _run(spec, QH, QR, QT, QM, index=index, tc=bool(tc))
+    out = _run(spec, QH, QR, QT, QM, index=index, tc=bool(tc), grouped=bool(grouped), q_rows=bool(grouped))
     okw = dict(ent_im=ent_im, rel_im=rel_im, norm_flag=c["norm"], margin=c["margin"])
     if c["model"] == "rotate":
         okw["phase_denom"] = spec.phase_denom
