@@ -404,7 +404,7 @@ __global__ __launch_bounds__(FT) void k_truth_filter(
 // Both rows stream from global 32 floats per round (RotatE 16 re + 16 im).
 template <int OP>
 __device__ float row_score(const float* __restrict__ qv, const float* __restrict__ ev, int kp) {
-  constexpr int W = (OP == 2) ? 16 : 32;
+  constexpr int W = (OP == 2) ? 16 : 32;  // 64 VGPRs of loads in flight per round
   const int kend = (OP == 2) ? kp : ((OP == 4) ? 2 * kp : kp);
   float acc = 0.0f;
   int k0 = 0;
@@ -492,9 +492,10 @@ __global__ __launch_bounds__(64) void k_filter_count(const int64_t* __restrict__
                                                      const uint32_t* __restrict__ type_head,
                                                      const uint32_t* __restrict__ type_tail, int64_t type_words,
                                                      int32_t* __restrict__ counts) {
-  __shared__ float s_v[64];
-  __shared__ int32_t s_id[64];
-  __shared__ uint8_t s_tb[64];
+  // staged list: id (-1 = invalid), score, type bit; read back 4 entries per LDS access
+  __shared__ __attribute__((aligned(16))) int32_t s_id[64];
+  __shared__ __attribute__((aligned(16))) float s_v[64];
+  __shared__ __attribute__((aligned(16))) int32_t s_tb[64];
   const int tid = threadIdx.x;
   for (int64_t g = blockIdx.x; g < n_groups; g += gridDim.x) {
     const int64_t qa = grp_qoff[g], qb = grp_qoff[g + 1];
@@ -512,21 +513,33 @@ __global__ __launch_bounds__(64) void k_filter_count(const int64_t* __restrict__
       for (int64_t lc = la; lc < lb; lc += 64) {
         const int nl = (int)((lb - lc) < 64 ? (lb - lc) : 64);
         __syncthreads();  // s_* reuse
-        if (tid < nl) {
-          const int64_t j = ids[lc + tid];
-          const bool ok = j >= 0 && j < n_ent;
-          s_id[tid] = ok ? (int32_t)j : -1;
-          s_v[tid] = list_v[lc + tid];
-          s_tb[tid] = (ok && tm) ? (uint8_t)type_bit(tm, type_words, r, j) : (uint8_t)0;
+        {
+          int32_t id = -1, tb = 0;
+          float v = 0.0f;
+          if (tid < nl) {
+            const int64_t j = ids[lc + tid];
+            if (j >= 0 && j < n_ent) {
+              id = (int32_t)j;
+              v = list_v[lc + tid];
+              tb = tm ? (int32_t)type_bit(tm, type_words, r, j) : 0;
+            }
+          }
+          s_id[tid] = id;  // entries nl..63 stay invalid: the loop below reads whole quads
+          s_v[tid] = v;
+          s_tb[tid] = tb;
         }
         __syncthreads();
         if (active) {
-          for (int i = 0; i < nl; ++i) {
-            const int32_t e = s_id[i];
-            if (e >= 0 && e != tr && s_v[i] < th) {
-              c += 1;
-              cc += s_tb[i];
-            }
+          for (int i = 0; i < nl; i += 4) {  // branch-free, 4 entries per LDS read
+            const int4 e = *reinterpret_cast<const int4*>(&s_id[i]);
+            const float4 v = *reinterpret_cast<const float4*>(&s_v[i]);
+            const int4 t = *reinterpret_cast<const int4*>(&s_tb[i]);
+            const int b0 = (e.x >= 0) & (e.x != tr) & (v.x < th);
+            const int b1 = (e.y >= 0) & (e.y != tr) & (v.y < th);
+            const int b2 = (e.z >= 0) & (e.z != tr) & (v.z < th);
+            const int b3 = (e.w >= 0) & (e.w != tr) & (v.w < th);
+            c += b0 + b1 + b2 + b3;
+            cc += (b0 & t.x) + (b1 & t.y) + (b2 & t.z) + (b3 & t.w);
           }
         }
       }

@@ -38,13 +38,21 @@ def main():
         ev.run(copy_counts=False)
     full = timeit(lambda: ev.run(copy_counts=False), a.reps)
     gpu = timeit(lambda: ev.counts(), a.reps)
+    host = torch.empty((4, 2 * ev.n), dtype=torch.int32, pin_memory=True)
+
+    def with_copy():
+        host.copy_(ev.counts(), non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+    d2h = timeit(with_copy, a.reps)
+    empty = timeit(lambda: torch.cuda.current_stream().synchronize(), a.reps)
     c = ev.counts().cpu().numpy()
     n = ev.n
     t = time.perf_counter()
     for _ in range(a.reps):
         link_metrics(c[:, :n], c[:, n:])
     met = (time.perf_counter() - t) / a.reps * 1e3
-    print(f"full step {full:.3f} ms | launches+GPU {gpu:.3f} ms | host metrics {met:.3f} ms")
+    print(f"full step {full:.3f} ms | launches+GPU {gpu:.3f} ms | +D2H+sync {d2h:.3f} ms | "
+          f"host metrics {met:.3f} ms | empty sync {empty:.4f} ms")
 
 
 if __name__ == "__main__":
