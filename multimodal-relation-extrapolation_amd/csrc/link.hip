@@ -14,7 +14,7 @@
 //   k_truth_filter    pred(truth) per query (the sweep's arithmetic) and the filtered-rank
 //                     correction, one workgroup per filter group (queries sharing a list)
 //   k_sweep_valu      TransE L1/L2, RotatE: VALU 8x8 register micro-tiles
-//   k_sweep_mfma      DistMult/ComplEx: v_mfma_f32_32x32x2_f32, ballot/popcount epilogue
+//   k_sweep_mfma      DistMult/ComplEx: v_mfma_f32_32x32x2_f32, register-counter epilogue
 #include <stdlib.h>
 
 #include "mmre_common.h"
@@ -747,59 +747,103 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 // ------------------------------------------------------------ MFMA sweep ---
 // DistMult / ComplEx: S = Q (queries x K) . E^T (K x entities) with the f32-input MFMA
 // v_mfma_f32_32x32x2_f32 (exact f32, a k-ordered fma chain: the canonical order).
+// Work units and the XCD-grouped persistent split are the VALU sweep's: (query tile of
+// 128) x (entity tile of 128), query-tile major within each XCD group's 1/8 of the table.
 // 4 waves as 2 (q) x 2 (e); each wave 64 x 64 = 2 x 2 blocks of 32 x 32 accumulators.
-// Epilogue: per accumulator register one ballot over "beats the truth"; the two 32-lane
-// halves are two query rows, so two popcounts give exact per-row counts.
+// Epilogue: each lane holds 32 query rows x 1 entity column of the 64 x 64 block; it
+// compares against the rows' thresholds (kept in registers for the whole query tile) and
+// bumps per-row register counters; the counters are reduced across the 32 column lanes
+// only when the workgroup leaves the query tile. The truth needs no exclusion test: its
+// score is bit-identical to the threshold (same canonical chain), so `< thr` rejects it.
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 template <bool TC, bool STORE>
-__global__ __launch_bounds__(NT) void k_sweep_mfma(
+__global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
-    int64_t q_pad, int64_t n_query, int ktot, int n_chunk, int et_per_chunk, int pred_kind, float margin,
-    const float* __restrict__ thr, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,
-    const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
-    const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
-    float* __restrict__ scores) {
+    int64_t q_pad, int64_t n_query, int ktot, int n_et, int n_groups, int pred_kind, float margin,
+    const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
+    const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
+    int32_t* __restrict__ counts, float* __restrict__ scores) {
   __shared__ float sq[2][KC][TQ];
   __shared__ float se[2][KC][TE];
-  __shared__ float s_thr[TQ];
-  __shared__ int32_t s_true[TQ];
   __shared__ int32_t s_rel[TC ? TQ : 1];
   __shared__ int8_t s_mode[TC ? TQ : 1];
-  __shared__ int32_t s_cnt[2][2][TQ];  // [we][raw|tc][q]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wq = wave >> 1, we = wave & 1;
-  const int chunk = blockIdx.x % n_chunk;
-  const int qtile = blockIdx.x / n_chunk;
-  const int64_t q0 = (int64_t)qtile * TQ;
-  const int n_et = (int)(e_pad / TE);
-  const int et_begin = chunk * et_per_chunk;
-  const int et_end = min(et_begin + et_per_chunk, n_et);
-  if (et_begin >= et_end) return;
+  const int lrow = lane >> 5, lcol = lane & 31;
+  const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
+  const int per_grp = gridDim.x / n_groups;
+  const int ex0 = (int)((int64_t)grp * n_et / n_groups), ex1 = (int)((int64_t)(grp + 1) * n_et / n_groups);
+  const int n_ex = ex1 - ex0;
+  const int units_g = (int)(q_pad / TQ) * n_ex;
+  const int u0 = (int)((int64_t)gmem * units_g / per_grp);
+  const int u1 = (int)((int64_t)(gmem + 1) * units_g / per_grp);
+  if (u0 >= u1) return;  // uniform over the workgroup
   const int nkc = ktot / KC;
-  const int nsteps = (et_end - et_begin) * nkc;
 
-  if (tid < TQ) {
-    int64_t q = q0 + tid;
-    bool v = q < n_query;
-    s_thr[tid] = v ? thr[q] : -INFINITY;
-    s_true[tid] = v ? qtrue[q] : -1;
+  // rows of this lane: ql(bi, r) = wq*64 + bi*32 + (r&3) + 8*(r>>2) + 4*lrow
+  float th[2][16];
+  int cnt[2][16], cnt_tc[TC ? 2 : 1][TC ? 16 : 1];
+  auto row_of = [&](int bi, int r) { return wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lrow; };
+  auto load_rows = [&](int qtile) {
+    const int64_t q0 = (int64_t)qtile * TQ;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + row_of(bi, r);
+        th[bi][r] = q < n_query ? thr[q] : -INFINITY;  // -inf: nothing beats a padded row
+        cnt[bi][r] = 0;
+        if constexpr (TC) cnt_tc[bi][r] = 0;
+      }
     if constexpr (TC) {
-      s_rel[tid] = v ? (int32_t)qr[q] : 0;
-      s_mode[tid] = v ? qmode[q] : 0;
+      __syncthreads();  // previous tile's s_rel/s_mode readers are done
+      if (tid < TQ) {
+        const int64_t q = q0 + tid;
+        s_rel[tid] = q < n_query ? (int32_t)qr[q] : 0;
+        s_mode[tid] = q < n_query ? qmode[q] : 0;
+      }
     }
-  }
-  for (int i = tid; i < 2 * 2 * TQ; i += NT) (&s_cnt[0][0][0])[i] = 0;
+  };
+  auto flush_rows = [&](int qtile) {
+    const int64_t q0 = (int64_t)qtile * TQ;
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        int c = cnt[bi][r];
+#pragma unroll
+        for (int sh = 1; sh < 32; sh <<= 1) c += __shfl_xor(c, sh);  // the 32 column lanes
+        int cc = 0;
+        if constexpr (TC) {
+          cc = cnt_tc[bi][r];
+#pragma unroll
+          for (int sh = 1; sh < 32; sh <<= 1) cc += __shfl_xor(cc, sh);
+        }
+        const int64_t q = q0 + row_of(bi, r);
+        if (lcol == 0 && q < n_query) {
+          if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
+          if constexpr (TC) {
+            if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
+          }
+        }
+      }
+  };
 
   const int srow = tid >> 5, sc4 = tid & 31;
   float4 rq, re;
-  auto gload = [&](int step) {
-    const int et = et_begin + step / nkc;
-    const int k = (step % nkc) * KC + srow;
-    rq = *reinterpret_cast<const float4*>(q_km + (int64_t)k * q_pad + q0 + sc4 * 4);
-    re = *reinterpret_cast<const float4*>(ent_km + (int64_t)k * e_pad + (int64_t)et * TE + sc4 * 4);
+  int ld_unit = u0, ld_kc = 0, ld_qt = u0 / n_ex, ld_et = ex0 + u0 % n_ex;
+  auto gload = [&]() {
+    const int k = ld_kc * KC + srow;
+    rq = *reinterpret_cast<const float4*>(q_km + (int64_t)k * q_pad + (int64_t)ld_qt * TQ + sc4 * 4);
+    re = *reinterpret_cast<const float4*>(ent_km + (int64_t)k * e_pad + (int64_t)ld_et * TE + sc4 * 4);
+    if (++ld_kc == nkc) {
+      ld_kc = 0;
+      ++ld_unit;
+      if (++ld_et == ex1) { ld_et = ex0; ++ld_qt; }
+    }
   };
   auto swrite = [&](int buf) {
     *reinterpret_cast<float4*>(&sq[buf][srow][sc4 * 4]) = rq;
@@ -814,72 +858,67 @@ __global__ __launch_bounds__(NT) void k_sweep_mfma(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
-  gload(0);
+  int cur_qt = u0 / n_ex, cur_et = ex0 + u0 % n_ex;
+  load_rows(cur_qt);
+  gload();
   swrite(0);
   __syncthreads();
 
-  const int lrow = lane >> 5, lcol = lane & 31;
-  for (int step = 0; step < nsteps; ++step) {
-    const int buf = step & 1;
-    if (step + 1 < nsteps) gload(step + 1);
+  int buf = 0;
+  for (int unit = u0; unit < u1; ++unit) {
+    for (int kc = 0; kc < nkc; ++kc) {
+      const bool more = ld_unit < u1;
+      if (more) gload();
 #pragma unroll
-    for (int kp2 = 0; kp2 < KC; kp2 += 2) {
-      const float a0 = sq[buf][kp2 + lrow][wq * 64 + lcol];
-      const float a1 = sq[buf][kp2 + lrow][wq * 64 + 32 + lcol];
-      const float b0 = se[buf][kp2 + lrow][we * 64 + lcol];
-      const float b1 = se[buf][kp2 + lrow][we * 64 + 32 + lcol];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if ((step + 1) % nkc == 0) {
-      const int64_t ebase = (int64_t)(et_begin + step / nkc) * TE + we * 64;
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi) {
+      for (int kp2 = 0; kp2 < KC; kp2 += 2) {
+        const float a0 = sq[buf][kp2 + lrow][wq * 64 + lcol];
+        const float a1 = sq[buf][kp2 + lrow][wq * 64 + 32 + lcol];
+        const float b0 = se[buf][kp2 + lrow][we * 64 + lcol];
+        const float b1 = se[buf][kp2 + lrow][we * 64 + 32 + lcol];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+      if (kc == nkc - 1) {  // unit finished: rank epilogue
+        const int64_t q0 = (int64_t)cur_qt * TQ;
+        const int64_t ebase = (int64_t)cur_et * TE + we * 64;
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) {
           const int64_t e = ebase + bj * 32 + lcol;
+          const bool ev = e < n_ent;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ql = wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lrow;
-            const float v = apply_pred(pred_kind, margin, acc[bi][bj][r]);
-            const bool better = (v < s_thr[ql]) && (e != s_true[ql]) && (e < n_ent);
-            const uint64_t m = __ballot(better);
-            if (lane == 0) {
-              const int qlo = wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2);
-              s_cnt[we][0][qlo] += __popcll(m & 0xffffffffull);
-              s_cnt[we][0][qlo + 4] += __popcll(m >> 32);
-            }
-            if constexpr (TC) {
-              const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-              const uint64_t mc = __ballot(better && type_bit(tm, type_words, s_rel[ql], e));
-              if (lane == 0) {
-                const int qlo = wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2);
-                s_cnt[we][1][qlo] += __popcll(mc & 0xffffffffull);
-                s_cnt[we][1][qlo + 4] += __popcll(mc >> 32);
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float v = apply_pred(pred_kind, margin, acc[bi][bj][r]);
+              const bool better = ev && (v < th[bi][r]);
+              cnt[bi][r] += better;
+              if constexpr (TC) {
+                const int ql = row_of(bi, r);
+                const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e);
               }
+              if constexpr (STORE) {
+                const int64_t q = q0 + row_of(bi, r);
+                if (q < n_query && ev) scores[q * n_ent + e] = v;
+              }
+              acc[bi][bj][r] = 0.0f;
             }
-            if constexpr (STORE) {
-              if (q0 + ql < n_query && e < n_ent) scores[(q0 + ql) * n_ent + e] = v;
-            }
-            acc[bi][bj][r] = 0.0f;
-          }
         }
+        const bool last = unit + 1 >= u1;
+        int next_qt = cur_qt, next_et = cur_et + 1;
+        if (next_et == ex1) { next_et = ex0; ++next_qt; }
+        if (last || next_qt != cur_qt) {  // uniform: leave this query tile
+          flush_rows(cur_qt);
+          if (!last) load_rows(next_qt);
+        }
+        cur_qt = next_qt;
+        cur_et = next_et;
       }
-    }
-    if (step + 1 < nsteps) swrite(buf ^ 1);
-    __syncthreads();
-  }
-  if (tid < TQ) {
-    const int64_t q = q0 + tid;
-    if (q < n_query) {
-      int c = s_cnt[0][0][tid] + s_cnt[1][0][tid];
-      if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
-      if constexpr (TC) {
-        int cc = s_cnt[0][1][tid] + s_cnt[1][1][tid];
-        if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
-      }
+      if (more) swrite(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
     }
   }
 }
@@ -1111,14 +1150,6 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
   const bool tc = d_type_head != nullptr;
   const bool store = d_scores != nullptr;
   const int op = op_of_model(model);
-  // grid: (query tiles) x (entity chunks); chunk count a multiple of 8 for XCD affinity
-  const int n_qt = (int)(q_pad / TQ);
-  const int n_et = (int)(e_pad / TE);
-  int n_chunk = (2048 + n_qt - 1) / n_qt;
-  n_chunk = (int)round_up(n_chunk, 8);
-  if (n_chunk > n_et) n_chunk = n_et;
-  const int etpc = (n_et + n_chunk - 1) / n_chunk;
-  const dim3 grid((unsigned)(n_qt * n_chunk));
   if (op <= 2) {
 #define MMRE_LV(OPV) launch_valu<OPV>(tc, store, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad, n_query, kp, pred_kind, \
                                       margin, d_truth, d_q_true, d_qr, d_qmode, d_type_head, d_type_tail, tw, d_counts, d_scores)
@@ -1128,10 +1159,16 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
 #undef MMRE_LV
   }
   const int ktot = n_planes(model) * kp;
-#define MMRE_MFMA(TCV, STV)                                                                                     \
-  hipLaunchKernelGGL((k_sweep_mfma<TCV, STV>), grid, dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,    \
-                     n_query, ktot, n_chunk, etpc, pred_kind, margin, d_truth, d_q_true, d_qr, d_qmode,         \
-                     d_type_head, d_type_tail, tw, d_counts, d_scores)
+  const int n_et = (int)(e_pad / TE);
+  // persistent XCD-grouped grid as for the VALU sweep (8 workgroups per resident slot)
+#define MMRE_MFMA(TCV, STV)                                                                                       \
+  do {                                                                                                            \
+    const int g = 8 * resident_groups((const void*)k_sweep_mfma<TCV, STV>, NT);                                   \
+    const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
+    hipLaunchKernelGGL((k_sweep_mfma<TCV, STV>), dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent,     \
+                       d_q_km, q_pad, n_query, ktot, n_et, ng, pred_kind, margin, d_truth, d_qr, d_qmode,        \
+                       d_type_head, d_type_tail, tw, d_counts, d_scores);                                        \
+  } while (0)
   if (tc) { if (store) MMRE_MFMA(true, true); else MMRE_MFMA(true, false); }
   else    { if (store) MMRE_MFMA(false, true); else MMRE_MFMA(false, false); }
 #undef MMRE_MFMA

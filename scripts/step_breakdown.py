@@ -51,6 +51,19 @@ def main():
     for _ in range(a.reps):
         link_metrics(c[:, :n], c[:, n:])
     met = (time.perf_counter() - t) / a.reps * 1e3
+    # host-side launch cost of one evaluation (no sync), and the metric reduction on pinned views
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(a.reps):
+        ev.counts()
+    launch = (time.perf_counter() - t) / a.reps * 1e3
+    torch.cuda.synchronize()
+    hv = host.numpy()
+    t = time.perf_counter()
+    for _ in range(a.reps):
+        link_metrics(hv[:, :n], hv[:, n:])
+    met_pinned = (time.perf_counter() - t) / a.reps * 1e3
+    print(f"launch-only (host) {launch:.3f} ms | metrics on pinned views {met_pinned:.3f} ms")
     print(f"full step {full:.3f} ms | launches+GPU {gpu:.3f} ms | +D2H+sync {d2h:.3f} ms | "
           f"host metrics {met:.3f} ms | empty sync {empty:.4f} ms")
 
