@@ -55,8 +55,10 @@ def bytes_per_triple(model, dim):
 
 
 def valu_ops_per_triple(model, dim):
-    """VALU lane-instructions per scored triple in the sweep's inner loop."""
-    return {"transe": 2 * dim, "transe_l2": 2 * dim, "rotate": 11 * dim}.get(model)
+    """VALU issue slots per scored triple in the sweep's inner loop: TransE L1
+    sub + add; RotatE 2 sub, 4 mul, 2 add, 2 fma, 3/4 of a min for the tiny-input check, and
+    v_rsq_f32 at quarter rate = 4 slots (measured, scripts/probes/trans_rate.hip)."""
+    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 16.75 * dim}.get(model)
 
 
 KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false>", "rotate": "k_sweep_valu<2, false, false>",

@@ -26,9 +26,13 @@ constexpr int TE = 128;   // entities per workgroup tile
 constexpr int KC = 8;     // K rows per LDS stage
 constexpr int NT = 256;   // threads per workgroup
 
-// rows per plane: TransE/DistMult use one plane of round_up(d, KC) rows;
-// ComplEx/RotatE use two planes (re, im) of round_up(d, KC) rows each.
-__host__ __device__ inline int plane_rows(int dim) { return (int)round_up(dim, KC); }
+// rows per plane: TransE/DistMult use one plane of plane_rows(model, d) rows;
+// ComplEx/RotatE use two planes (re, im) of plane_rows(model, d) rows each.
+constexpr int KCM = 16;   // K rows per LDS stage of the MFMA sweep
+// DistMult/ComplEx planes are padded to the MFMA sweep's 16-row stage (zero rows add exact
+// zeros to the fma chain); TransE/RotatE to the VALU sweep's 8.
+__host__ __device__ inline bool mfma_model(int model) { return model == MMRE_DISTMULT || model == MMRE_COMPLEX; }
+__host__ __device__ inline int plane_rows(int model, int dim) { return (int)round_up(dim, mfma_model(model) ? KCM : KC); }
 __host__ __device__ inline int n_planes(int model) { return (model == MMRE_COMPLEX || model == MMRE_ROTATE) ? 2 : 1; }
 
 // ------------------------------------------------------------------ prep ----
@@ -230,6 +234,19 @@ __device__ __forceinline__ float op_final(float acc) {
   if constexpr (OP == 1) return sqrtf(acc);
   else return acc;
 }
+// RotatE's |(dr, di)| = sqrt(v), v = dr*dr + di*di, correctly rounded, for the sweep's inner
+// loop, in full-rate f32 arithmetic only: y = v_rsq_f32(v), s = v*y, h = y/2, then one
+// Newton step s + (v - s*s)*h in fma form. Checked exhaustively on MI355X against IEEE
+// sqrtf over every float input (scripts/probes/sqrt_candidates.hip): exact for all
+// v in [2^-96, FLT_MAX]; it is not for v = 0, v < 2^-96 or v = inf, so the caller tracks
+// min(v) and the accumulators' NaN-ness and recomputes such a (rare) tile with sqrtf.
+__device__ __forceinline__ float rot_mag(float v, float y) {  // y = v_rsq_f32(v)
+  const float s = v * y, h = 0.5f * y;
+  const float e = __builtin_fmaf(-s, s, v);
+  return __builtin_fmaf(e, h, s);
+}
+constexpr float kRotMin = 0x1p-96f;
+
 __host__ __device__ inline int op_of_model(int model) {
   return model == MMRE_TRANSE_L1 ? 0 : model == MMRE_TRANSE_L2 ? 1 : model == MMRE_ROTATE ? 2
          : model == MMRE_DISTMULT ? 3 : 4;
@@ -609,16 +626,19 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
   };
 
   const int srow = tid >> 5, sc4 = tid & 31;
-  float4 rq[NPL], re[NPL];
+  float4 rq0, re0, rq1, re1;  // plane 0 / plane 1 (RotatE) staging: scalars, kept in VGPRs
   // staging position (unit, kc) of the next load, advanced incrementally (no divisions)
   int ld_unit = u0, ld_kc = 0, ld_qt = u0 / n_ex, ld_et = ex0 + u0 % n_ex;
   auto gload = [&]() {
     const int k = ld_kc * KC + srow;
     const int64_t q0 = (int64_t)ld_qt * TQ, e0 = (int64_t)ld_et * TE;
-#pragma unroll
-    for (int p = 0; p < NPL; ++p) {
-      rq[p] = *reinterpret_cast<const float4*>(q_km + (int64_t)(p * kp + k) * q_pad + q0 + sc4 * 4);
-      re[p] = *reinterpret_cast<const float4*>(ent_km + (int64_t)(p * kp + k) * e_pad + e0 + sc4 * 4);
+    const float* qp = q_km + (int64_t)k * q_pad + q0 + sc4 * 4;
+    const float* ep = ent_km + (int64_t)k * e_pad + e0 + sc4 * 4;
+    rq0 = *reinterpret_cast<const float4*>(qp);
+    re0 = *reinterpret_cast<const float4*>(ep);
+    if constexpr (NPL == 2) {
+      rq1 = *reinterpret_cast<const float4*>(qp + (int64_t)kp * q_pad);
+      re1 = *reinterpret_cast<const float4*>(ep + (int64_t)kp * e_pad);
     }
     if (++ld_kc == nkc) {
       ld_kc = 0;
@@ -627,10 +647,11 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     }
   };
   auto swrite = [&](int buf) {
-#pragma unroll
-    for (int p = 0; p < NPL; ++p) {
-      sq[buf][p][srow][sc4] = rq[p];
-      se[buf][p][srow][sc4] = re[p];
+    sq[buf][0][srow][sc4] = rq0;
+    se[buf][0][srow][sc4] = re0;
+    if constexpr (NPL == 2) {
+      sq[buf][NPL - 1][srow][sc4] = rq1;
+      se[buf][NPL - 1][srow][sc4] = re1;
     }
   };
 
@@ -647,6 +668,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 
   int cur_qt = u0 / n_ex, cur_et = ex0 + u0 % n_ex;
   int slot = 0;
+  uint32_t lo = 0xFFFFFFFFu;  // RotatE: min of the sqrt inputs' bits over this unit (see rot_mag)
   load_meta(cur_qt, 0);
   gload();
   swrite(0);
@@ -668,10 +690,24 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
           float4 y0 = se[buf][NPL - 1][kk][te], y1 = se[buf][NPL - 1][kk][16 + te];
           const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
           const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+          // two phases per row of 8: independent elements sit between each v_rsq_f32 and its
+          // use (no trans-use hazard padding)
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
+          for (int i = 0; i < 8; ++i) {
+            float v[8], y[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][j] = op_step<OP>(acc[i][j], qa[i], qb[i], xv[j], yv[j]);
+            for (int j = 0; j < 8; ++j) {
+              const float dr = qa[i] - xv[j], di = qb[i] - yv[j];
+              v[j] = dr * dr + di * di;
+              y[j] = __builtin_amdgcn_rsqf(v[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+              lo = min(lo, min(__float_as_uint(v[j]), __float_as_uint(v[j + 1])));  // v >= 0: bit order
+              acc[i][j] = acc[i][j] + rot_mag(v[j], y[j]);
+              acc[i][j + 1] = acc[i][j + 1] + rot_mag(v[j + 1], y[j + 1]);
+            }
+          }
         } else {
 #pragma unroll
           for (int i = 0; i < 8; ++i)
@@ -682,6 +718,36 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
       if (kc == nkc - 1) {  // unit finished: rank epilogue
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE;
+        if constexpr (OP == 2) {
+          bool bad = lo < __float_as_uint(kRotMin);  // v = 0 or v < 2^-96
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bad |= acc[i][j] != acc[i][j];  // v = inf (or a NaN input)
+          if (__ballot(bad)) {  // rare: redo this wave's tiles with the IEEE sqrtf
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) acc[i][j] = 0.0f;
+            for (int k = 0; k < kp; ++k) {
+              float qa[8], qb[8], xv[8], yv[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const int64_t ql = q0 + ((i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4));
+                const int64_t ec = ebase + ((i < 4) ? te * 4 + i : 64 + te * 4 + (i - 4));
+                qa[i] = q_km[(int64_t)k * q_pad + ql];
+                qb[i] = q_km[(int64_t)(kp + k) * q_pad + ql];
+                xv[i] = ent_km[(int64_t)k * e_pad + ec];
+                yv[i] = ent_km[(int64_t)(kp + k) * e_pad + ec];
+              }
+#pragma unroll
+              for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[i][j] = op_step<2>(acc[i][j], qa[i], qb[i], xv[j], yv[j]);
+            }
+          }
+          lo = 0xFFFFFFFFu;
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
@@ -764,8 +830,8 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
     const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
     int32_t* __restrict__ counts, float* __restrict__ scores) {
-  __shared__ float sq[2][KC][TQ];
-  __shared__ float se[2][KC][TE];
+  __shared__ float sq[2][KCM][TQ];
+  __shared__ float se[2][KCM][TE];
   __shared__ int32_t s_rel[TC ? TQ : 1];
   __shared__ int8_t s_mode[TC ? TQ : 1];
 
@@ -781,7 +847,7 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
   const int u0 = (int)((int64_t)gmem * units_g / per_grp);
   const int u1 = (int)((int64_t)(gmem + 1) * units_g / per_grp);
   if (u0 >= u1) return;  // uniform over the workgroup
-  const int nkc = ktot / KC;
+  const int nkc = ktot / KCM;
 
   // rows of this lane: ql(bi, r) = wq*64 + bi*32 + (r&3) + 8*(r>>2) + 4*lrow
   float th[2][16];
@@ -832,13 +898,17 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
       }
   };
 
-  const int srow = tid >> 5, sc4 = tid & 31;
-  float4 rq, re;
+  const int srow = tid >> 5, sc4 = tid & 31;  // rows srow and srow + 8 of the stage
+  float4 rq0, rq1, re0, re1;  // scalars, not an array: kept in VGPRs
   int ld_unit = u0, ld_kc = 0, ld_qt = u0 / n_ex, ld_et = ex0 + u0 % n_ex;
   auto gload = [&]() {
-    const int k = ld_kc * KC + srow;
-    rq = *reinterpret_cast<const float4*>(q_km + (int64_t)k * q_pad + (int64_t)ld_qt * TQ + sc4 * 4);
-    re = *reinterpret_cast<const float4*>(ent_km + (int64_t)k * e_pad + (int64_t)ld_et * TE + sc4 * 4);
+    const int k = ld_kc * KCM + srow;
+    const float* qp = q_km + (int64_t)k * q_pad + (int64_t)ld_qt * TQ + sc4 * 4;
+    const float* ep = ent_km + (int64_t)k * e_pad + (int64_t)ld_et * TE + sc4 * 4;
+    rq0 = *reinterpret_cast<const float4*>(qp);
+    rq1 = *reinterpret_cast<const float4*>(qp + 8 * q_pad);
+    re0 = *reinterpret_cast<const float4*>(ep);
+    re1 = *reinterpret_cast<const float4*>(ep + 8 * e_pad);
     if (++ld_kc == nkc) {
       ld_kc = 0;
       ++ld_unit;
@@ -846,8 +916,10 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     }
   };
   auto swrite = [&](int buf) {
-    *reinterpret_cast<float4*>(&sq[buf][srow][sc4 * 4]) = rq;
-    *reinterpret_cast<float4*>(&se[buf][srow][sc4 * 4]) = re;
+    *reinterpret_cast<float4*>(&sq[buf][srow][sc4 * 4]) = rq0;
+    *reinterpret_cast<float4*>(&sq[buf][srow + 8][sc4 * 4]) = rq1;
+    *reinterpret_cast<float4*>(&se[buf][srow][sc4 * 4]) = re0;
+    *reinterpret_cast<float4*>(&se[buf][srow + 8][sc4 * 4]) = re1;
   };
 
   floatx16 acc[2][2];
@@ -870,7 +942,7 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
       const bool more = ld_unit < u1;
       if (more) gload();
 #pragma unroll
-      for (int kp2 = 0; kp2 < KC; kp2 += 2) {
+      for (int kp2 = 0; kp2 < KCM; kp2 += 2) {
         const float a0 = sq[buf][kp2 + lrow][wq * 64 + lcol];
         const float a1 = sq[buf][kp2 + lrow][wq * 64 + 32 + lcol];
         const float b0 = se[buf][kp2 + lrow][we * 64 + lcol];
@@ -974,7 +1046,7 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
 
 using namespace mmre;
 
-extern "C" int64_t mmre_link_k(int model, int dim) { return (int64_t)n_planes(model) * plane_rows(dim); }
+extern "C" int64_t mmre_link_k(int model, int dim) { return (int64_t)n_planes(model) * plane_rows(model, dim); }
 extern "C" int64_t mmre_link_pad(int64_t n) { return round_up(n > 0 ? n : 1, 128); }
 
 static bool valid_model(int m) { return m >= MMRE_TRANSE_L1 && m <= MMRE_ROTATE; }
@@ -986,7 +1058,7 @@ extern "C" int mmre_link_prepare_entities(int model, int norm_flag, const float*
   if (!d_ent || !d_ent_km || !d_ent_rows || n_ent <= 0 || dim <= 0 || e_pad < n_ent || e_pad % TE) return MMRE_ERR_ARG;
   if (model == MMRE_COMPLEX && !d_ent_im) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const int kp = plane_rows(dim), kt = n_planes(model) * kp;
+  const int kp = plane_rows(model, dim), kt = n_planes(model) * kp;
   const int rb = stage_rows(kt);
   const size_t lds = sizeof(float) * (size_t)rb * (kt + 1);
   if (lds > 64 * 1024) return MMRE_ERR_SHAPE;
@@ -1010,7 +1082,7 @@ extern "C" int mmre_link_prepare_queries(int model, int norm_flag, const float* 
   const bool transe = model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2;
   if (transe && norm_flag && !d_rel_work) return MMRE_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  const int kp = plane_rows(dim), kt = n_planes(model) * kp;
+  const int kp = plane_rows(model, dim), kt = n_planes(model) * kp;
   const float* rel = d_rel;
   if (transe && norm_flag) {  // normalised relation rows (TransE.py:63-66) into d_rel_work (n_rel, dim)
     const int rb = stage_rows(kp);
@@ -1087,7 +1159,7 @@ extern "C" int mmre_link_truth_grouped(int model, int pred_kind, float margin, c
   if ((d_type_head == nullptr) != (d_type_tail == nullptr)) return MMRE_ERR_ARG;
   if (n_ent >= (int64_t)INT32_MAX || n_query >= (int64_t)INT32_MAX) return MMRE_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  const int kp = plane_rows(dim);
+  const int kp = plane_rows(model, dim);
   int rc;
 #define MMRE_FS(OPV)                                                                                              \
   launch_filter_scores<OPV>(st, d_ent_rows, n_ent, d_q_rows, kp, d_q_true, n_query, pred_kind, margin, d_entry_q, \
@@ -1120,7 +1192,7 @@ extern "C" int mmre_link_truth(int model, int pred_kind, float margin, const flo
   if (!d_ent_rows) return MMRE_ERR_ARG;
   if ((d_filt_off == nullptr) != (d_filt_ids == nullptr)) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const int kp = plane_rows(dim);
+  const int kp = plane_rows(model, dim);
   const int64_t tw = (n_ent + 31) / 32;
 #define MMRE_TF(OPV)                                                                                              \
   launch_truth_filter<OPV>(st, d_ent_rows, n_ent, d_q_km, q_pad, kp, nullptr, d_q_true, d_qr, d_qmode, n_query,   \
@@ -1145,7 +1217,7 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
                            d_type_head, d_type_tail, d_counts, d_truth);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  const int kp = plane_rows(dim);
+  const int kp = plane_rows(model, dim);
   const int64_t tw = (n_ent + 31) / 32;
   const bool tc = d_type_head != nullptr;
   const bool store = d_scores != nullptr;
@@ -1160,10 +1232,13 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
   }
   const int ktot = n_planes(model) * kp;
   const int n_et = (int)(e_pad / TE);
-  // persistent XCD-grouped grid as for the VALU sweep (8 workgroups per resident slot)
+  // persistent XCD-grouped grid as for the VALU sweep, 2 workgroups per resident slot (MI355X,
+  // KCM = 16: C3 1.20 / 1.24 / 1.22 / 1.24 ms and C5 36.5 / 36.5 / 36.5 / 36.6 ms at 1/2/3/4x)
 #define MMRE_MFMA(TCV, STV)                                                                                       \
   do {                                                                                                            \
-    const int g = 8 * resident_groups((const void*)k_sweep_mfma<TCV, STV>, NT);                                   \
+    int g = 2 * resident_groups((const void*)k_sweep_mfma<TCV, STV>, NT); /* flat 1-4x on C3/C5 */             \
+    static const char* gm = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */                      \
+    if (gm && gm[0] >= '1' && gm[0] <= '9') g = atoi(gm);                                                       \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL((k_sweep_mfma<TCV, STV>), dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent,     \
                        d_q_km, q_pad, n_query, ktot, n_et, ng, pred_kind, margin, d_truth, d_qr, d_qmode,        \

@@ -14,8 +14,13 @@ from mmre.workloads import zs_workload
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 model, dim, ds, norm = {"c2": ("transe", 200, "FB15K-237-ZS", True), "c3": ("complex", 200, "DB15K-ZS", False),
-                        "c4": ("rotate", 512, "FB15K-237-ZS", False)}[cfg]
-w = zs_workload(ds, model, dim)
+                        "c4": ("rotate", 512, "FB15K-237-ZS", False),
+                        "c5": ("distmult", 256, "synthetic-1M", False)}[cfg]
+if cfg == "c5":
+    from mmre.workloads import synthetic_large
+    w = synthetic_large()
+else:
+    w = zs_workload(ds, model, dim)
 dev = torch.device("cuda:0")
 n = len(w["test_h"])
 qh = np.r_[w["test_h"], w["test_h"]]; qr = np.r_[w["test_r"], w["test_r"]]; qt = np.r_[w["test_t"], w["test_t"]]
@@ -25,7 +30,7 @@ from mmre.link import rotate_phase_denom
 spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
                  ent_im=w["ent_im"].to(dev) if "ent_im" in w else None,
                  rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=norm,
-                 pred_kind={"transe": 0, "complex": 2, "rotate": 3}[model], margin=float(w.get("margin", 0)),
+                 pred_kind={"transe": 0, "complex": 2, "rotate": 3, "distmult": 2}[model], margin=float(w.get("margin", 0)),
                  phase_denom=rotate_phase_denom(6.0, 2.0, dim) if model == "rotate" else 0.0)
 sw = LinkSweep(spec)
 b = sw.alloc_queries(2 * n)
