@@ -200,3 +200,32 @@ def test_full_size_c2_properties(oracle_mod):
         o_pred = oracle_mod.link_predict("transe", mode, ent, rel, qh[s], qr[s], qt[s], norm_flag=True)
         o_c = oracle_mod.test_rank(mode, o_pred, qh[s], qr[s], qt[s], hrt)
         assert np.array_equal(c[:, s].T[:, :2], o_c[:, :2])
+
+
+def test_rotate_zero_and_tiny_magnitudes(oracle_mod):
+    """RotatE's fast magnitude is exact only for inputs >= 2^-96; tiles that see 0, tiny or
+    overflowing inputs are recomputed with sqrtf. Relation 0 has phase 0 (an exact identity
+    rotation), so a query's anchor scores v = 0 on every k, and near-copies of the anchor
+    score v ~ 1e-44 (subnormal) and ~1e-31 (below 2^-96): scores must stay bit-identical."""
+    rng = np.random.default_rng(11)
+    E, R, d, margin = 300, 5, 32, 6.0
+    er = (margin + 2.0) / (2 * d)
+    ent = rng.uniform(-er, er, (E, 2 * d)).astype(np.float32)
+    rel = rng.uniform(-(margin + 2.0) / d, (margin + 2.0) / d, (R, d)).astype(np.float32)
+    rel[0] = 0.0
+    ent[5] = ent[3]
+    ent[5, ::3] += np.float32(1e-22)       # dr ~ 1e-22 -> v ~ 1e-44 (subnormal)
+    ent[6] = ent[3]
+    ent[6, 1::4] += np.float32(3e-16)      # v ~ 1e-31 < 2^-96
+    ent[7] = ent[4]
+    qh = np.array([3, 3, 4, 10, 3, 4], np.int64)
+    qr = np.array([0, 0, 0, 1, 2, 0], np.int64)
+    qt = np.array([4, 3, 3, 12, 5, 4], np.int64)
+    qm = np.array([1, 0, 1, 0, 1, 0], np.int8)
+    spec = _spec_from("rotate", ent, rel, margin=margin, dim=d)
+    out = _run(spec, qh, qr, qt, qm)
+    for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+        sel = qm == mode_id
+        o_pred = oracle_mod.link_predict("rotate", mode, ent, rel, qh[sel], qr[sel], qt[sel], margin=margin,
+                                         phase_denom=spec.phase_denom)
+        assert np.array_equal(out["scores"][sel].view(np.uint32), o_pred.view(np.uint32))
