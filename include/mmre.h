@@ -243,6 +243,50 @@ int mmre_cosine_rank(const float* d_cand, int dim, const int64_t* d_cand_off, in
                      const float* d_rel_vecs, int n_samples, const int64_t* d_rel_of_query, float* d_scores,
                      int32_t* d_rank, void* stream);
 
+/* ====================================================================== *
+ *  ZSL Extractor (module/zsl_module.py:17-110) in eval mode, fused with   *
+ *  ZSLmodule.eval's cosine ranking (zsl_module.py:666-706). Replaces, per *
+ *  query, get_meta (:265-287) + Extractor(query, query, meta, meta)       *
+ *  (:690-694) + sklearn cosine_similarity(...).mean(1) (:699-701) +       *
+ *  argsort rank (:705-706). d = embed_dim in {64, 100, 128, 200, 256}.    *
+ * ====================================================================== */
+
+/* Floats of the packed-weight buffer for embed_dim `dim` (-1 if unsupported). */
+int64_t mmre_extractor_pack_size(int dim);
+/* Pack the Extractor's weights (nn.Linear layout (out, in) row-major, as in its
+ * state_dict: gcn_w (d/2, d) + bias, fc1 / fc2 (d/2, d) + bias, reshape_layer
+ * (d, 2d) + bias, support_encoder.proj1 (2d, d) + bias, proj2 (d, 2d) + bias,
+ * support_encoder.layer_norm weight / bias (d)) into MFMA lane order. */
+int mmre_extractor_pack(int dim, const float* d_gcn_w, const float* d_gcn_b, const float* d_fc1_w,
+                        const float* d_fc1_b, const float* d_fc2_w, const float* d_fc2_b, const float* d_rs_w,
+                        const float* d_rs_b, const float* d_p1_w, const float* d_p1_b, const float* d_p2_w,
+                        const float* d_p2_b, const float* d_ln_w, const float* d_ln_b, float* d_pack, void* stream);
+/* Per-node halves of reshape_layer's output (neighbor_encoder :47-59 and
+ * entity_encoder :61-67 folded through the linear reshape_layer :92-96):
+ *   d_left[n]  (as e1: left neighbours, fc1 part, + bias)   (n_nodes, d), or NULL
+ *   d_right[n] (as e2: fc2 part, right neighbours)          (n_nodes, d), or NULL
+ * for node n = symbol d_node_sym[n] with neighbour list d_conn[n][max_nb][2]
+ * (column 1 = neighbour symbol id, PAD = the zero last row of d_sym_emb; the
+ * layout of ZSLmodule.connections, :233-263) and degree d_deg[n] (float). */
+int mmre_extractor_nodes(int dim, const float* d_pack, const float* d_sym_emb, const int64_t* d_node_sym,
+                         const int64_t* d_conn, int max_nb, const float* d_deg, int64_t n_nodes, float* d_left,
+                         float* d_right, void* stream);
+/* Row r = (e1 = d_li[r], e2 = d_ri[r]): x = left[e1] + right[e2]; g = SupportEncoder(x)
+ * (submodule.py:254-258, nn.LayerNorm eps ln_eps). Writes d_out_g (n_rows, d) if
+ * non-NULL (the Extractor's query_g) and d_score[r] = g . t / (normalize ? |g| : 1)
+ * with t = d_targets[d_row_target[r]] (row 0 if d_row_target is NULL). */
+int mmre_extractor_encode(int dim, const float* d_pack, float ln_eps, const float* d_left, const int64_t* d_li,
+                          const float* d_right, const int64_t* d_ri, int64_t n_rows, const float* d_targets,
+                          const int64_t* d_row_target, int normalize, float* d_out_g, float* d_score, void* stream);
+/* d_targets[t] = mean_s v[t][s] / (normalize ? |v[t][s]| : 1) for d_vecs (n_sets, n_samples, dim),
+ * n_samples <= 64: the sklearn-normalised mean relation vector of ZSL scoring, or
+ * the support mean of Extractor.forward (:101). */
+int mmre_extractor_targets(const float* d_vecs, int64_t n_sets, int n_samples, int dim, int normalize,
+                           float* d_targets, void* stream);
+/* Rank of the first entry of each list (CSR d_off) in descending order:
+ * 1 + #(score > score[first]) (zsl_module.py:705-706, tie-free inputs). */
+int mmre_rank_desc(const float* d_scores, const int64_t* d_off, int64_t n_query, int32_t* d_rank, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,12 @@ SIGNATURES = {
                                      F32, I32, F32, P, P, P]),
     "mmre_candidate_rank_transe": (I32, [P, P, I32, P, P, I64, P, P, P, P, P]),
     "mmre_cosine_rank": (I32, [P, I32, P, I64, P, I32, P, P, P, P]),
+    "mmre_extractor_pack_size": (I64, [I32]),
+    "mmre_extractor_pack": (I32, [I32] + [P] * 15 + [P]),
+    "mmre_extractor_nodes": (I32, [I32, P, P, P, P, I32, P, I64, P, P, P]),
+    "mmre_extractor_encode": (I32, [I32, P, F32, P, P, P, P, I64, P, P, I32, P, P, P]),
+    "mmre_extractor_targets": (I32, [P, I64, I32, I32, I32, P, P]),
+    "mmre_rank_desc": (I32, [P, P, I64, P, P]),
 }
 
 ERRORS = {1: "bad argument", 2: "unknown model", 3: "unsupported shape", 4: "workspace too small"}

@@ -1,14 +1,209 @@
-"""Zero-shot evaluation ranking of ZSLmodule.eval (module/zsl_module.py:635-745).
+"""Zero-shot evaluation path of ZSLmodule (module/zsl_module.py): the Extractor
+(:17-110), the symbol / neighbourhood tables it reads (load_embed :208-232,
+build_connection :233-263, get_meta :265-287) and the evaluation ranking of
+ZSLmodule.eval (:635-745).
 
-`zsl_rank(candidate_vecs, cand_off, relation_vecs, rel_of_query)` runs the cosine-similarity
-ranking of every query on the GPU (csrc/candidates.hip): score = mean over the test_sample
-generated relation vectors of cos(candidate, relation) (sklearn cosine_similarity, :699-701),
-rank of the true candidate (row 0) in descending order (:705-706). `zsl_metrics` prints and
-returns Hits@10/5/1 and MRR as the reference does (:707-745). The Extractor that produces the
-candidate vectors (zsl_module.py:17-110) is the next component."""
+* `Extractor(embed_dim, num_symbols, embed)` keeps the reference's constructor, parameter
+  names (state_dict-compatible) and `forward(query, support, query_meta, support_meta) ->
+  (query_g, matching_scores)`. In eval mode forward runs on the GPU (csrc/extractor.hip):
+  per-row neighbour / entity encoders folded through reshape_layer, then the SupportEncoder
+  on MFMA. Training mode (dropout; pretrain_Extractor / the GAN loop) is not part of this build
+  and raises.
+* `ZSLGraph` builds symbol2id / symbol2vec / connections / e1_degrees exactly as the
+  reference does, with numpy instead of per-element Python loops.
+* `ZSLEvaluator.eval(relation_vecs, test_candidates)` is ZSLmodule.eval's ranking for every
+  query at once: Extractor vectors of all candidate pairs, mean cosine similarity with the
+  relation's generated vectors, rank of the true tail, Hits@10/5/1 and MRR printed as the
+  reference prints them.
+* `zsl_rank` ranks precomputed candidate vectors (csrc/candidates.hip).
+"""
+from collections import defaultdict
+
 import numpy as np
+import torch
+import torch.nn as nn
 
+from mmre._lib import MMREError
 from mmre.candidates import cosine_rank
+from mmre.extractor import ZSLRanker, _check_ids, encode, node_tables, pack_weights, targets
+from .submodule import SupportEncoder
+
+
+class Extractor(nn.Module):
+    """Matching metric based on KB embeddings (zsl_module.py:17-110)."""
+
+    def __init__(self, embed_dim, num_symbols, embed=None):
+        super().__init__()
+        self.embed_dim = int(embed_dim)
+        self.pad_idx = num_symbols
+        self.symbol_emb = nn.Embedding(num_symbols + 1, embed_dim, padding_idx=num_symbols)
+        self.num_symbols = num_symbols
+        self.gcn_w = nn.Linear(self.embed_dim, int(self.embed_dim / 2))
+        self.gcn_b = nn.Parameter(torch.zeros(self.embed_dim))  # declared, unused by forward (as in :29)
+        self.fc1 = nn.Linear(self.embed_dim, int(self.embed_dim / 2))
+        self.fc2 = nn.Linear(self.embed_dim, int(self.embed_dim / 2))
+        self.dropout = nn.Dropout(0.2)
+        self.dropout_e = nn.Dropout(0.2)
+        if embed is not None:
+            self.symbol_emb.weight.data.copy_(torch.as_tensor(np.asarray(embed), dtype=torch.float32))
+        self.symbol_emb.weight.requires_grad = False
+        self.reshape_layer = nn.Linear(self.embed_dim * 2, self.embed_dim)
+        self.support_encoder = SupportEncoder(self.embed_dim, 2 * self.embed_dim, dropout=0.2)
+
+    def _require_eval(self):
+        if self.training:
+            raise MMREError("Extractor runs in eval mode on this path (pretrain_Extractor / GAN training, "
+                            "zsl_module.py:289-600, are outside it): call .eval()")
+
+    def encode_pairs(self, pairs, meta, targets_=None, normalize=False, want_g=True):
+        """query_g (and optionally scores vs targets_) of (B, 2) symbol pairs with their meta."""
+        self._require_eval()
+        left_conn, left_deg, right_conn, right_deg = meta
+        n_sym = int(self.symbol_emb.weight.shape[0])
+        for ids, what in ((pairs, "symbol ids"), (left_conn[:, :, 1], "left neighbours"),
+                          (right_conn[:, :, 1], "right neighbours")):
+            _check_ids(ids, n_sym, what)
+        d = self.embed_dim
+        pack = pack_weights(self)
+        emb = self.symbol_emb.weight
+        left, _ = node_tables(pack, d, emb, pairs[:, 0], left_conn, left_deg, want_right=False)
+        _, right = node_tables(pack, d, emb, pairs[:, 1], right_conn, right_deg, want_left=False)
+        idx = torch.arange(pairs.shape[0], device=pairs.device)
+        return encode(pack, d, self.support_encoder.layer_norm.eps, left, idx, right, idx, targets=targets_,
+                      normalize=normalize, want_g=want_g, want_score=targets_ is not None)
+
+    def forward(self, query, support, query_meta=None, support_meta=None):
+        """query (B, 2), support (few, 2) symbol ids; metas from ZSLGraph.get_meta.
+        Returns (query_g (B, d), matching_scores = query_g . mean(support_g) squeezed)."""
+        support_g, _ = self.encode_pairs(support, support_meta)
+        s_mean = targets(support_g.unsqueeze(0), normalize=False)  # (1, d) = mean over support rows
+        query_g, scores = self.encode_pairs(query, query_meta, targets_=s_mean, normalize=False)
+        return query_g, scores.unsqueeze(1).squeeze()
+
+    def update(self, embed):
+        self.symbol_emb.weight.data.copy_(torch.as_tensor(np.asarray(embed), dtype=torch.float32))
+        self.symbol_emb.weight.requires_grad = False
+
+
+def weights_init(m):
+    """module/utils.py:119-123: xavier_normal_ weights and zero biases for every Linear."""
+    if "Linear" in m.__class__.__name__:
+        torch.nn.init.xavier_normal_(m.weight.data)
+        torch.nn.init.constant_(m.bias, 0.0)
+
+
+class ZSLGraph:
+    """Symbol tables and neighbourhoods of ZSLmodule (zsl_module.py:208-287).
+
+    rel2id / ent2id: the id maps (dict name -> id, iteration order matters: symbols are
+    numbered relations first, then entities, skipping "" and "OOV", PAD last); train_tasks /
+    test_tasks: {relation: [[e1, rel, e2], ...]}; ent_embs (n_nodes, d), rel_embs (n_rel, d)."""
+
+    def __init__(self, rel2id, ent2id, train_tasks, test_tasks, ent_embs, rel_embs, max_neighbor=50):
+        self.rel2id, self.ent2id = rel2id, ent2id
+        self.load_embed(ent_embs, rel_embs)
+        self.num_symbols = len(self.symbol2id) - 1
+        self.pad_id = self.num_symbols
+        self.num_ents = len(ent2id)
+        self.build_connection(train_tasks, test_tasks, max_=max_neighbor)
+
+    def load_embed(self, ent_embs, rel_embs):
+        """load_embed (:208-232)."""
+        ent = np.asarray(ent_embs.detach().cpu() if torch.is_tensor(ent_embs) else ent_embs)
+        rel = np.asarray(rel_embs.detach().cpu() if torch.is_tensor(rel_embs) else rel_embs)
+        rel_keys = [k for k in self.rel2id if k not in ("", "OOV")]
+        ent_keys = [k for k in self.ent2id if k not in ("", "OOV")]
+        self.symbol2id = {k: i for i, k in enumerate(rel_keys + ent_keys)}
+        self.symbol2id["PAD"] = len(rel_keys) + len(ent_keys)
+        rows = [rel[[self.rel2id[k] for k in rel_keys]].reshape(len(rel_keys), rel.shape[1]),
+                ent[[self.ent2id[k] for k in ent_keys]].reshape(len(ent_keys), rel.shape[1]),
+                np.zeros((1, rel.shape[1]))]
+        # the reference builds a float64 array from python lists of float32 values
+        self.symbol2vec = np.concatenate(rows, 0).astype(np.float64)
+
+    def build_connection(self, train_tasks, test_tasks, max_=100):
+        """build_connection (:233-263): each triple adds (rel, e2) to e1's list and (rel, e1)
+        to e2's, train tasks first then test tasks, in file order; lists cut at max_."""
+        s2i = self.symbol2id
+        nbrs = defaultdict(list)
+        for tasks in (train_tasks, test_tasks):
+            for rel in tasks.keys():
+                for e1, r, e2 in tasks[rel]:
+                    nbrs[e1].append((s2i[r], s2i[e2]))
+                    nbrs[e2].append((s2i[r], s2i[e1]))
+        conn = np.full((self.num_ents, max_, 2), self.pad_id, dtype=np.int64)
+        deg = np.zeros(self.num_ents, dtype=np.int64)
+        for ent, id_ in self.ent2id.items():
+            lst = nbrs.get(ent, [])[:max_]
+            deg[id_] = len(lst)
+            if lst:
+                conn[id_, :len(lst)] = np.asarray(lst, dtype=np.int64)
+        self.connections = conn
+        self.e1_degrees = deg
+        # symbol id of every entity id (ids of "" / "OOV" map to PAD)
+        self.ent_sym = np.full(self.num_ents, self.pad_id, dtype=np.int64)
+        for ent, id_ in self.ent2id.items():
+            if ent in s2i:
+                self.ent_sym[id_] = s2i[ent]
+        return {ent: int(deg[id_]) for ent, id_ in self.ent2id.items()}
+
+    def get_meta(self, left, right, device=None):
+        """get_meta (:265-287): (left_connections, left_degrees, right_connections, right_degrees)."""
+        left, right = np.asarray(left, np.int64), np.asarray(right, np.int64)
+        to = lambda a, dt: torch.as_tensor(a, dtype=dt, device=device)
+        return (to(self.connections[left], torch.int64), to(self.e1_degrees[left], torch.float32),
+                to(self.connections[right], torch.int64), to(self.e1_degrees[right], torch.float32))
+
+
+class ZSLEvaluator:
+    """ZSLmodule.eval's ranking (zsl_module.py:666-745) for all queries at once."""
+
+    def __init__(self, extractor: Extractor, graph: ZSLGraph, device=None):
+        extractor.eval()
+        self.graph = graph
+        self.ranker = ZSLRanker(extractor, graph.ent_sym, graph.connections, graph.e1_degrees, device=device)
+
+    def flatten(self, test_candidates, rel_order=None):
+        """test_candidates {rel: {"head\\trel\\ttrue": [true, cand...]}} -> device CSR of
+        (head id, tail id) rows, query -> relation-set index, and the relation order."""
+        e2id = self.graph.ent2id
+        rels = list(test_candidates.keys()) if rel_order is None else list(rel_order)
+        heads, tails, off, qset, qrel = [], [], [0], [], []
+        for ri, rel in enumerate(rels):
+            for e1_rel, cands in test_candidates[rel].items():
+                head = e1_rel.split("\t")[0]
+                h = e2id[head]
+                ids = [e2id[c] for c in cands]
+                heads.append(np.full(len(ids), h, np.int64))
+                tails.append(np.asarray(ids, np.int64))
+                off.append(off[-1] + len(ids))
+                qset.append(ri)
+                qrel.append(rel)
+        dev = self.ranker.left.device
+        to = lambda a: torch.as_tensor(np.concatenate(a) if isinstance(a, list) else a, device=dev)
+        return (to(heads), to(tails), torch.as_tensor(np.asarray(off, np.int64), device=dev),
+                torch.as_tensor(np.asarray(qset, np.int64), device=dev), rels, qrel)
+
+    def rank(self, relation_vecs, test_candidates, rel_order=None, return_scores=False):
+        """relation_vecs: {rel: (test_sample, d)} generated vectors (generate_model.generate,
+        :660-666) or a (n_rel, S, d) tensor in rel_order. Returns int32 ranks per query in
+        test_candidates order (and the query relations)."""
+        ch, ct, off, qset, rels, qrel = self.flatten(test_candidates, rel_order)
+        if isinstance(relation_vecs, dict):
+            rv = torch.stack([torch.as_tensor(relation_vecs[r]) for r in rels]).float()
+        else:
+            rv = torch.as_tensor(relation_vecs).float()
+        out = self.ranker.rank(ch, ct, off, rv, qset, return_scores=return_scores)
+        return out, qrel
+
+    def eval(self, relation_vecs, test_candidates, mode="test"):
+        (ranks, _), qrel = self.rank(relation_vecs, test_candidates, return_scores=True)
+        r = ranks.cpu().numpy()
+        per_rel = {}
+        qrel = np.asarray(qrel, dtype=object)
+        for rel in dict.fromkeys(qrel):
+            per_rel[rel] = qrel == rel
+        return zsl_metrics(r, mode, per_relation=per_rel)
 
 
 def zsl_rank(candidate_vecs, cand_off, relation_vecs, rel_of_query):
