@@ -25,7 +25,7 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "multimodal-relation-extrapolation_amd")
-for p in (PKG, REPO):
+for p in (PKG, REPO, os.path.join(REPO, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -45,7 +45,11 @@ CONFIGS = {
                workload="C4 FB15K-237-ZS RotatE d=512, filtered link prediction"),
     "c5": dict(dataset="synthetic-1M", model="distmult", dim=256, norm=False,
                workload="C5 synthetic |E|=1M DistMult d=256, 8,192 sweeps (MFMA f32)"),
+    "zsl": dict(dataset="FB15K-237-ZS", model="extractor", dim=200, norm=False,
+                workload="ZSL eval FB15K-237-ZS: Extractor (d=200, max_neighbor=50) + mean-cosine rank of "
+                         "17,596 queries x ~1,000 candidates (SURVEY 8(f) rank 1)"),
 }
+MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
 
 def bytes_per_triple(model, dim):
@@ -177,6 +181,148 @@ def cpu_baseline(w, n_sample: int):
                       f"{elapsed:.2f} s on {torch.get_num_threads()} threads"}
 
 
+def cpu_baseline_zsl(w, budget_s: float = 15.0, max_queries: int = 400):
+    """ZSLmodule.eval's per-query loop on the host cores (zsl_module.py:666-706): get_meta,
+    Extractor forward on torch CPU (the oracle's op-for-op restatement, eval mode), sklearn
+    cosine_similarity(...).mean(1), argsort rank; queries in order until the time budget."""
+    import zsl_extractor as ox
+    from sklearn.metrics.pairwise import cosine_similarity
+    d = w["dim"]
+    ref = ox.ExtractorRef(d, w["n_sym"], w["sym_emb"].numpy())
+    gen = torch.Generator().manual_seed(0)
+    with torch.no_grad():
+        for name, p in ref.named_parameters():
+            if p.dim() == 2 and not name.startswith("symbol_emb"):
+                p.copy_(torch.nn.init.xavier_normal_(torch.empty(p.shape), generator=gen))
+            elif name.endswith("bias"):
+                p.zero_()
+    off, ch, ct = w["off"], w["cand_head"], w["cand_tail"]
+    rv = w["rel_vecs"].numpy()
+    conn, deg, es = w["conn"], w["deg"], w["ent_sym"]
+    rows = 0
+    t0 = time.perf_counter()
+    q = 0
+    while q < min(max_queries, len(off) - 1) and time.perf_counter() - t0 < budget_s:
+        a, b = off[q], off[q + 1]
+        left, right = ch[a:b], ct[a:b]
+        pairs = torch.from_numpy(np.stack([es[left], es[right]], 1))
+        meta = (torch.LongTensor(np.stack([conn[i] for i in left])), torch.FloatTensor(deg[left]),
+                torch.LongTensor(np.stack([conn[i] for i in right])), torch.FloatTensor(deg[right]))
+        vecs, _ = ref(pairs, pairs, meta, meta)
+        scores = cosine_similarity(vecs.numpy(), rv[w["query_set"][q]]).mean(axis=1)
+        list(np.argsort(scores))[::-1].index(0)
+        rows += b - a
+        q += 1
+    el = time.perf_counter() - t0
+    return {"value": rows / el, "unit": "scored candidates/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"first {q} FB15K-237-ZS ZSL queries ({rows} candidate rows) through the ZSLmodule.eval loop "
+                      f"(oracle/zsl_extractor.py: torch {torch.__version__} CPU Extractor + sklearn cosine + argsort),"
+                      f" {el:.2f} s on {torch.get_num_threads()} threads"}
+
+
+def bench_zsl(args, world, rank, dev, dist):
+    """One step = one full ZSL evaluation (ZSLmodule.eval, zsl_module.py:635-745) of this rank's
+    relation shard: weight pack + per-entity node tables, normalised mean relation vectors, the
+    fused Extractor/SupportEncoder/cosine kernel over every candidate row, the descending rank,
+    (N>1) the all-gather of ranks, D2H and Hits@10/5/1 + MRR on the host."""
+    from mmre.extractor import encode, node_tables, pack_weights, rank_desc, targets
+    from mmre.sharding import lpt_partition
+    from mmre.workloads import zsl_workload
+    from module.zsl_module import Extractor, weights_init
+    w = zsl_workload(dim=CONFIGS["zsl"]["dim"])
+    d = w["dim"]
+    torch.manual_seed(0)
+    ex = Extractor(d, w["n_sym"], w["sym_emb"].numpy())
+    ex.apply(weights_init)
+    ex = ex.to(dev).eval()
+    nq = len(w["off"]) - 1
+    masks = lpt_partition(w["query_rel"], world)
+    mine = np.nonzero(masks[rank])[0]
+    off = w["off"]
+    lens = off[mine + 1] - off[mine]
+    rows = np.concatenate([np.arange(off[q], off[q + 1]) for q in mine]) if len(mine) else np.zeros(0, np.int64)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    ch, ct = to(w["cand_head"][rows]), to(w["cand_tail"][rows])
+    loff = to(np.r_[0, np.cumsum(lens)].astype(np.int64))
+    row_set = to(np.repeat(w["query_set"][mine], lens))
+    ent_sym, conn, deg = to(w["ent_sym"]), to(w["conn"]), to(w["deg"])
+    rel_vecs = w["rel_vecs"].to(dev)
+    n_rows = int(len(rows))
+    pad = max(int(m.sum()) for m in masks)
+    host = torch.empty(world * pad, dtype=torch.int32, pin_memory=True)
+
+    def step(ev=None):
+        pack = pack_weights(ex)
+        left, right = node_tables(pack, d, ex.symbol_emb.weight, ent_sym, conn, deg)
+        t = targets(rel_vecs, normalize=True)
+        if ev:
+            ev[0].record()
+        _, s = encode(pack, d, ex.support_encoder.layer_norm.eps, left, ch, right, ct, targets=t,
+                      row_target=row_set, normalize=True)
+        if ev:
+            ev[1].record()
+        r = rank_desc(s, loff)
+        if dist:
+            buf = torch.zeros(pad, dtype=torch.int32, device=dev)
+            buf[:len(mine)] = r
+            out = torch.empty(world * pad, dtype=torch.int32, device=dev)
+            dist.all_gather_into_tensor(out, buf)
+            r = out
+        host[:r.numel()].copy_(r, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        got = host.numpy()
+        full = np.empty(nq, np.int64)
+        for k in range(world):
+            ids = np.nonzero(masks[k])[0]
+            full[ids] = got[k * pad:k * pad + len(ids)]
+        return {"hits10": float((full <= 10).mean()), "hits5": float((full <= 5).mean()),
+                "hits1": float((full <= 1).mean()), "mrr": float((1.0 / full).mean())}
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m = None
+    for i in range(args.steps):
+        m = step(evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total = int(off[-1])
+    if rank == 0:
+        flops = 8.0 * d * d * n_rows  # proj1 (d -> 2d) + proj2 (2d -> d), 2 flops per MAC
+        ach = flops / (kern_ms * 1e-3) / 1e12
+        out = {"metric": f"scored candidates/sec, {CONFIGS['zsl']['workload']}", "value": total * args.steps / elapsed,
+               "unit": "scored candidates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+               "vs_baseline": None, "dtype": "f32",
+               "data": "real FB15K-237-ZS test triples + rel2candidates_all pools; synthetic train neighbourhoods, "
+                       "random-init Extractor (weights_init) and relation vectors",
+               "config": {"workload": CONFIGS["zsl"]["workload"], "n_queries": nq, "n_candidate_rows": total,
+                          "dim": d, "max_neighbor": w["max_nb"],
+                          "parallelism": f"relation-sharded x{world} (LPT), RCCL all-gather of ranks"},
+               "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
+                            "frac": ach * 1e12 / MFMA_F32_PEAK, "traffic": None,
+                            "kernel": "k_extractor_encode<200>", "kernel_ms": kern_ms,
+                            "flops_per_row": 8 * d * d, "rows_per_launch": n_rows},
+               "metrics": m}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_zsl(w)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -204,6 +350,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
+    if args.config == "zsl":
+        return bench_zsl(args, world, rank, dev, dist)
     if cfg["dataset"] == "synthetic-1M":
         w = synthetic_large()
     else:

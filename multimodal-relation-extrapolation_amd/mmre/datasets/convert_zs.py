@@ -35,8 +35,29 @@ def convert(name, out):
           "relations", len(set(r)))
 
 
+def convert_candidates(name, out):
+    """rel2candidates_all.json (the candidate pool gen_mode_candidates.py filters per test
+    triple, utils/gen_mode_candidates.py:27-34) for the test relations, as entity ids in the
+    order of test_tasks_zsl.json's relations (rel_ids) -- (n_test_rel, n_cand) with -1 for names
+    absent from entity2ids_zsl.json."""
+    d = os.path.join(SRC, name)
+    e2id = json.load(open(os.path.join(d, "entity2ids_zsl.json")))
+    r2id = json.load(open(os.path.join(d, "relation2ids.json")))
+    tasks = json.load(open(os.path.join(d, "test_tasks_zsl.json")))
+    cands = json.load(open(os.path.join(d, "rel2candidates_all.json")))
+    rels = list(tasks.keys())
+    width = max(len(cands[r]) for r in rels)
+    ids = np.full((len(rels), width), -1, np.int32)
+    for i, r in enumerate(rels):
+        for j, e in enumerate(cands[r]):
+            ids[i, j] = e2id.get(e, -1)
+    np.savez_compressed(os.path.join(OUT, out), rel_ids=np.array([r2id[r] for r in rels], np.int32), cand=ids)
+    print(name, "candidate pools", ids.shape, "unmapped", int((ids < 0).sum()))
+
+
 if __name__ == "__main__":
     if not os.path.isdir(SRC):
         sys.exit("reference data not available")
     convert("FB15K-237-ZS", "fb15k237zs_test.npz")
     convert("DB15K-ZS", "db15kzs_test.npz")
+    convert_candidates("FB15K-237-ZS", "fb15k237zs_cands.npz")

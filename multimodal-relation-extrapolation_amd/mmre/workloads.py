@@ -10,7 +10,9 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .data import load_zs_test, sorted_rel2
+import os
+
+from .data import DATASETS_DIR, load_zs_test, sorted_rel2
 
 FB15K237_TRAIN = 272_115
 
@@ -62,3 +64,79 @@ def synthetic_large(n_ent=1_000_000, n_rel=235, dim=256, n_query=8192, seed=0):
     w["test_t"] = rng.integers(0, n_ent, n_query // 2)
     w["filter_h"], w["filter_r"], w["filter_t"] = w["test_h"], w["test_r"], w["test_t"]
     return w
+
+
+def _first_k_per_key(keys, k):
+    """mask of the first k occurrences of each key, in input order."""
+    order = np.argsort(keys, kind="stable")
+    sk = keys[order]
+    start = np.r_[0, np.flatnonzero(sk[1:] != sk[:-1]) + 1]
+    rank = np.arange(len(sk)) - np.repeat(start, np.diff(np.r_[start, len(sk)]))
+    keep = np.zeros(len(keys), bool)
+    keep[order[rank < k]] = True
+    return keep
+
+
+def zsl_workload(dim: int = 200, max_nb: int = 50, test_sample: int = 20, n_train: int = FB15K237_TRAIN,
+                 seed: int = 0):
+    """ZSLmodule.eval at FB15K-237-ZS scale (zsl_module.py:635-745): every test triple is a query
+    whose candidate list is [true tail] + the relation's rel2candidates_all pool minus known tails
+    of (head, rel) (utils/gen_mode_candidates.py:27-34; e1rel_e2_all.json is not shipped, so the
+    known tails are the test triples'). Symbols are numbered relations first, then entities, PAD
+    last (load_embed, :208-232); neighbourhoods come from a synthetic train set over the seen
+    relations plus the test triples, first max_nb per entity (build_connection, :233-263).
+    Extractor weights: weights_init (xavier_normal_, zero bias; module/utils.py:119-123);
+    embeddings torch.rand (zsl_module.py:173-174); relation vectors ~ a shared direction per
+    relation + noise (shape of generate()'s output, test_sample rows)."""
+    z = load_zs_test("FB15K-237-ZS")
+    with np.load(os.path.join(DATASETS_DIR, "fb15k237zs_cands.npz"), allow_pickle=False) as c:
+        pool_rel, pools = c["rel_ids"].astype(np.int64), c["cand"].astype(np.int64)
+    E, R = int(z["n_ent"]), int(z["n_rel"])
+    h, r, t = (z[k].astype(np.int64) for k in ("h", "r", "t"))
+    rng = np.random.default_rng(seed + 5)
+    test_rels = np.unique(r)
+    seen = np.setdiff1d(np.arange(R), test_rels)
+    th, tr, tt = rng.integers(0, E, n_train), seen[rng.integers(0, len(seen), n_train)], rng.integers(0, E, n_train)
+    sym_ent = lambda e: R + e
+    # neighbour events in insertion order: train then test, each triple (e1 <- e2, e2 <- e1)
+    ah, ar, at = np.concatenate([th, h]), np.concatenate([tr, r]), np.concatenate([tt, t])
+    owner = np.stack([ah, at], 1).reshape(-1)
+    nb_rel = np.stack([ar, ar], 1).reshape(-1)
+    nb_sym = np.stack([sym_ent(at), sym_ent(ah)], 1).reshape(-1)
+    keep = _first_k_per_key(owner, max_nb)
+    owner, nb_rel, nb_sym = owner[keep], nb_rel[keep], nb_sym[keep]
+    slot = np.zeros(len(owner), np.int64)
+    order = np.argsort(owner, kind="stable")
+    so = owner[order]
+    start = np.r_[0, np.flatnonzero(so[1:] != so[:-1]) + 1]
+    slot[order] = np.arange(len(so)) - np.repeat(start, np.diff(np.r_[start, len(so)]))
+    pad = R + E
+    conn = np.full((E, max_nb, 2), pad, np.int64)
+    conn[owner, slot, 0] = nb_rel
+    conn[owner, slot, 1] = nb_sym
+    deg = np.bincount(owner, minlength=E).astype(np.float32)
+    # candidate lists
+    pool_of = {int(rr): pools[i][pools[i] >= 0] for i, rr in enumerate(pool_rel)}
+    known = {}
+    for a, b, c_ in zip(h.tolist(), r.tolist(), t.tolist()):
+        known.setdefault((a, b), set()).add(c_)
+    heads, tails, off, qset = [], [], [0], []
+    rel_index = {int(rr): i for i, rr in enumerate(pool_rel)}
+    for a, b, c_ in zip(h.tolist(), r.tolist(), t.tolist()):
+        p = pool_of[b]
+        bad = np.fromiter(known[(a, b)], np.int64)
+        p = p[~np.isin(p, bad)]
+        lst = np.concatenate([[c_], p])
+        heads.append(np.full(len(lst), a, np.int64))
+        tails.append(lst)
+        off.append(off[-1] + len(lst))
+        qset.append(rel_index[b])
+    gen = torch.Generator().manual_seed(seed)
+    sym_emb = torch.cat([torch.rand((R, dim), generator=gen), torch.rand((E, dim), generator=gen),
+                         torch.zeros((1, dim))])
+    rel_vecs = (torch.randn((len(pool_rel), 1, dim), generator=gen)
+                + 0.5 * torch.randn((len(pool_rel), test_sample, dim), generator=gen))
+    return dict(dim=dim, n_ent=E, n_rel=R, n_sym=R + E, sym_emb=sym_emb, ent_sym=R + np.arange(E), conn=conn,
+                deg=deg, cand_head=np.concatenate(heads), cand_tail=np.concatenate(tails),
+                off=np.asarray(off, np.int64), query_set=np.asarray(qset, np.int64), query_rel=r,
+                rel_vecs=rel_vecs, max_nb=max_nb, test_sample=test_sample)
