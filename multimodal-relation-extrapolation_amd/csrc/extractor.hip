@@ -41,10 +41,17 @@ struct XG {
   static constexpr int NY = (D + 15) / 16;         // output blocks of 16
   static constexpr int KC = (D + 3) / 4;           // input features per lane group (stage 1)
   static constexpr int S1 = (KC + 3) / 4 * 4;      // stage-1 steps, padded to float4 packs
+  // Weight stream: 1-KB pieces (64 lanes x float4) in the order the encode kernel consumes
+  // them -- stage 1: for s4, for b: W1 block b, steps 4*s4..4*s4+3; stage 2: for hb, for ob:
+  // W2 block ob, hidden features hb*16 + 4*(l/16) + q -- grouped in chunks of CH pieces
+  // (an even number NC of chunks, zero padded).
+  static constexpr int NP1 = (S1 / 4) * NH;
+  static constexpr int NP = NP1 + NH * NY;
+  static constexpr int CH = 8;    // 8-KB chunks: 2 float4 per thread of a 256-thread group
+  static constexpr int NC = ((NP + CH - 1) / CH + 1) / 2 * 2;
   // packed buffer offsets (floats)
-  static constexpr int64_t P1 = 0;                               // [NH][S1/4][64][4]  proj1
-  static constexpr int64_t P2 = P1 + (int64_t)NH * S1 * 64;      // [NH][NY][64][4]    proj2
-  static constexpr int64_t PB1 = P2 + (int64_t)NH * NY * 256;    // [NH*16] proj1 bias
+  static constexpr int64_t PS = 0;                               // [NC*CH][64][4] weight stream
+  static constexpr int64_t PB1 = PS + (int64_t)NC * CH * 256;    // [NH*16] proj1 bias
   static constexpr int64_t PB2 = PB1 + NH * 16;                  // [NY*16] proj2 bias
   static constexpr int64_t PLW = PB2 + NY * 16;                  // [NY*16] LayerNorm weight
   static constexpr int64_t PLB = PLW + NY * 16;                  // [NY*16] LayerNorm bias
@@ -75,20 +82,19 @@ __global__ __launch_bounds__(256) void k_extractor_pack(const float* __restrict_
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G::SIZE; i += stride) {
     float v = 0.0f;
-    if (i < G::P2) {  // proj1 A operand: lane l, step s -> W1[fb*16 + l%16][g*KC + s], g = l/16
-      const int64_t j = i - G::P1;
-      const int e = (int)(j & 3), lane = (int)((j >> 2) & 63);
-      const int64_t rest = j >> 8;  // fb * (S1/4) + s4
-      const int s4 = (int)(rest % (G::S1 / 4)), fb = (int)(rest / (G::S1 / 4));
-      const int s = s4 * 4 + e, row = fb * 16 + (lane & 15), col = (lane >> 4) * G::KC + s;
-      if (row < 2 * D && s < G::KC && col < D) v = p1_w[(int64_t)row * D + col];
-    } else if (i < G::PB1) {  // proj2 A operand: lane l, (hb, q) -> W2[ob*16 + l%16][hb*16 + 4*(l/16) + q]
-      const int64_t j = i - G::P2;
-      const int q = (int)(j & 3), lane = (int)((j >> 2) & 63);
-      const int64_t rest = j >> 8;  // hb * NY + ob
-      const int ob = (int)(rest % G::NY), hb = (int)(rest / G::NY);
-      const int row = ob * 16 + (lane & 15), col = hb * 16 + 4 * (lane >> 4) + q;
-      if (row < D && col < 2 * D) v = p2_w[(int64_t)row * (2 * D) + col];
+    if (i < G::PB1) {  // weight stream
+      const int64_t j = i - G::PS;
+      const int e = (int)(j & 3), lane = (int)((j >> 2) & 63), g = lane >> 4;
+      const int piece = (int)(j >> 8);
+      if (piece < G::NP1) {  // proj1: lane l, step s -> W1[b*16 + l%16][g*KC + s]
+        const int s4 = piece / G::NH, b = piece % G::NH;
+        const int st = s4 * 4 + e, row = b * 16 + (lane & 15), col = g * G::KC + st;
+        if (row < 2 * D && st < G::KC && col < D) v = p1_w[(int64_t)row * D + col];
+      } else if (piece < G::NP) {  // proj2: lane l, (hb, q) -> W2[ob*16 + l%16][hb*16 + 4g + q]
+        const int p2 = piece - G::NP1, hb = p2 / G::NY, ob = p2 % G::NY;
+        const int row = ob * 16 + (lane & 15), col = hb * 16 + 4 * g + e;
+        if (row < D && col < 2 * D) v = p2_w[(int64_t)row * (2 * D) + col];
+      }
     } else if (i < G::PB2) {
       const int f = (int)(i - G::PB1);
       v = f < 2 * D ? p1_b[f] : 0.0f;
@@ -219,8 +225,74 @@ __global__ __launch_bounds__(256) void k_extractor_nodes(const float* __restrict
 }
 
 // ---------------------------------------------------------------------------------------
-// Fused SupportEncoder + LayerNorm + cosine epilogue, 16 rows per wave.
+// Fused SupportEncoder + LayerNorm + cosine epilogue. Persistent workgroups of 4 waves take
+// tiles of 64 rows (16 per wave). The weight stream (650 KB at d = 200, identical for every
+// tile) flows through a 2 x 16-KB LDS ring shared by the 4 waves: each chunk is loaded into
+// registers one chunk ahead (4 x 16-B coalesced loads per thread) and written to LDS after
+// the barrier that frees its buffer, so every wave reads its A operands from LDS
+// (ds_read_b128, lane-linear, conflict-free) and L2 sees each weight byte once per 64 rows.
 // ---------------------------------------------------------------------------------------
+// Per-use opaque copy of a kernel-argument pointer: loads through it cannot be hoisted out of
+// the persistent tile loop (LICM would otherwise park every loop-invariant weight / bias load
+// of the fully unrolled body in registers for the kernel's lifetime).
+__device__ __forceinline__ const float* opaque(const float* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+template <int D>
+__device__ __forceinline__ void load_chunk(const floatx4* stream, int c, floatx4 (&st)[2]) {
+  // opaque base: keeps the compiler from hoisting the (loop-invariant) weight loads of every
+  // chunk out of the tile loop into registers -- they must stream through the LDS ring
+  asm volatile("" : "+s"(stream));
+  const floatx4* src = stream + (int64_t)c * (XG<D>::CH * 64) + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) st[j] = src[j * 256];
+}
+
+// One chunk of the weight stream (compile-time index CHK, so every accumulator / operand index
+// below is a constant: the register arrays never spill to scratch), then the next.
+template <int D, int CHK>
+__device__ __forceinline__ void run_chunks(floatx4 (&ring)[2][XG<D>::CH * 64], floatx4 (&st)[2],
+                                           const floatx4* stream, const floatx4* xs,
+                                           floatx4 (&hacc)[XG<D>::NH], floatx4 (&yacc)[XG<D>::NY],
+                                           const float* pack, int lane, int g) {
+  using G = XG<D>;
+  constexpr int NH = G::NH, NY = G::NY, CH = G::CH, NC = G::NC, NP1 = G::NP1, NP = G::NP;
+  __syncthreads();  // chunk CHK is in ring[CHK & 1]; everyone is done reading ring[(CHK + 1) & 1]
+#pragma unroll
+  for (int j = 0; j < 2; ++j) ring[(CHK + 1) & 1][j * 256 + threadIdx.x] = st[j];
+  load_chunk<D>(stream, (CHK + 2) % NC, st);  // the stream repeats for the next tile
+  const floatx4* buf = ring[CHK & 1] + lane;
+#pragma unroll
+  for (int slot = 0; slot < CH; ++slot) {
+    const int p = CHK * CH + slot;
+    if (p == NP1) {  // stage 1 done (accumulators started at the bias): relu; stage 2 starts at p2
+#pragma unroll
+      for (int b = 0; b < NH; ++b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) hacc[b][q] = fmaxf(hacc[b][q], 0.0f);
+      const floatx4* pb2 = reinterpret_cast<const floatx4*>(opaque(pack) + G::PB2);
+#pragma unroll
+      for (int b = 0; b < NY; ++b) yacc[b] = pb2[b * 4 + g];
+    }
+    if (p < NP1) {  // H^T = W1 . X^T
+      const int s4 = p / NH, b = p % NH;
+      const floatx4 a = buf[slot * 64];
+      const floatx4 xv = xs[s4 * 64];  // this lane's X[row][g*KC + 4*s4 .. +3]
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], xv[e], hacc[b], 0, 0, 0);
+    } else if (p < NP) {  // Y^T = W2 . H^T, B operand straight from the stage-1 accumulators
+      const int p2 = p - NP1, hb = p2 / NY, ob = p2 % NY;
+      const floatx4 a = buf[slot * 64];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q], hacc[hb][q], yacc[ob], 0, 0, 0);
+    }
+  }
+  if constexpr (CHK + 1 < NC) run_chunks<D, CHK + 1>(ring, st, stream, xs, hacc, yacc, pack, lane, g);
+}
+
 template <int D>
 __global__ __launch_bounds__(256, 2) void k_extractor_encode(const float* __restrict__ pack, float ln_eps,
                                                              const float* __restrict__ left,
@@ -231,134 +303,118 @@ __global__ __launch_bounds__(256, 2) void k_extractor_encode(const float* __rest
                                                              const int64_t* __restrict__ row_target, int normalize,
                                                              float* __restrict__ out_g, float* __restrict__ score) {
   using G = XG<D>;
-  constexpr int NH = G::NH, NY = G::NY, KC = G::KC, S1 = G::S1;
-  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 16;
-  if (r0 >= n_rows) return;  // whole wave exits together (no barriers in this kernel)
-  const int64_t row = r0 + c;
-  const bool valid = row < n_rows;
-  const float* lrow = left + (valid ? li[row] : 0) * D;
-  const float* rrow = right + (valid ? ri[row] : 0) * D;
+  constexpr int NH = G::NH, NY = G::NY, KC = G::KC, S1 = G::S1, CH = G::CH;
+  __shared__ floatx4 ring[2][CH * 64];
+  // lane-private stage-1 B operands, parked in LDS (lane-linear float4 per step group s4):
+  // keeps the 4*S1/4 x values out of the VGPR budget of the two accumulator sets
+  __shared__ floatx4 xlds[4][S1 / 4][64];
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15, wave = threadIdx.x >> 6;
+  const floatx4* stream = reinterpret_cast<const floatx4*>(pack + G::PS);
+  const int64_t n_tiles = (n_rows + 63) / 64;
 
-  // stage 1: H^T[NH*16][16] = W1 . X^T. B operand of step s = X[row][g*KC + s] (zero padded
-  // for s >= KC), read 4 steps at a time from the two L2-resident node tables.
-  floatx4 hacc[NH];
+  floatx4 st[2];
+  load_chunk<D>(stream, 0, st);
 #pragma unroll
-  for (int b = 0; b < NH; ++b) hacc[b] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-  const floatx4* p1 = reinterpret_cast<const floatx4*>(pack + G::P1) + lane;
-#pragma unroll
-  for (int s4 = 0; s4 < S1 / 4; ++s4) {
-    float x[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int s = 4 * s4 + e, k = g * KC + s;
-      x[e] = (valid && s < KC && k < D) ? lrow[k] + rrow[k] : 0.0f;
-    }
-#pragma unroll
-    for (int b = 0; b < NH; ++b) {
-      const floatx4 a = p1[((int64_t)b * (S1 / 4) + s4) * 64];
-      hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], x[0], hacc[b], 0, 0, 0);
-      hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], x[1], hacc[b], 0, 0, 0);
-      hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], x[2], hacc[b], 0, 0, 0);
-      hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], x[3], hacc[b], 0, 0, 0);
-    }
-  }
-  // bias + relu: lane holds hidden features b*16 + 4g + q of row c
-  const floatx4* pb1 = reinterpret_cast<const floatx4*>(pack + G::PB1);
-#pragma unroll
-  for (int b = 0; b < NH; ++b) {
-    const floatx4 bb = pb1[b * 4 + g];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) hacc[b][q] = fmaxf(hacc[b][q] + bb[q], 0.0f);
-  }
+  for (int j = 0; j < 2; ++j) ring[0][j * 256 + threadIdx.x] = st[j];
+  load_chunk<D>(stream, 1, st);
+  floatx4* xs = &xlds[wave][0][lane];
 
-  // stage 2: Y^T[NY*16][16] = W2 . H^T, contraction over (hb, q) with B = hacc[hb][q]
-  floatx4 yacc[NY];
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t row = tile * 64 + wave * 16 + c;
+    const bool valid = row < n_rows;
+    const int64_t rr = valid ? row : 0;
+    const float* lrow = left + li[rr] * D;
+    const float* rrow = right + ri[rr] * D;
+    // stage-1 B operand: X[row][g*KC + s] for s < KC (zero padded to S1); D % 4 == 0, so
+    // g*KC + s < D whenever s < KC
 #pragma unroll
-  for (int b = 0; b < NY; ++b) yacc[b] = floatx4{0.0f, 0.0f, 0.0f, 0.0f};
-  const floatx4* p2 = reinterpret_cast<const floatx4*>(pack + G::P2) + lane;
+    for (int s4 = 0; s4 < S1 / 4; ++s4) {
+      floatx4 v;
 #pragma unroll
-  for (int hb = 0; hb < NH; ++hb) {
+      for (int e = 0; e < 4; ++e) {
+        const int s = 4 * s4 + e;
+        const float t = s < KC ? lrow[g * KC + s] + rrow[g * KC + s] : 0.0f;
+        v[e] = valid ? t : 0.0f;
+      }
+      xs[s4 * 64] = v;  // read back only by this lane (no barrier needed)
+    }
+    floatx4 hacc[NH];  // proj1 accumulators start at the bias p1 (hidden b*16 + 4g + q)
+    const floatx4* pb1 = reinterpret_cast<const floatx4*>(opaque(pack) + G::PB1);
+#pragma unroll
+    for (int b = 0; b < NH; ++b) hacc[b] = pb1[b * 4 + g];
+    floatx4 yacc[NY];
+
+    run_chunks<D, 0>(ring, st, stream, xs, hacc, yacc, pack, lane, g);
+
+    // epilogue: y = acc (started at p2) + x (residual), LayerNorm over the D features of row
+    // c, which live in the 4 lanes c, c+16, c+32, c+48 (features ob*16 + 4g + q).
+    float sum = 0.0f;
 #pragma unroll
     for (int ob = 0; ob < NY; ++ob) {
-      const floatx4 a = p2[((int64_t)hb * NY + ob) * 64];
-      yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], hacc[hb][0], yacc[ob], 0, 0, 0);
-      yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], hacc[hb][1], yacc[ob], 0, 0, 0);
-      yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], hacc[hb][2], yacc[ob], 0, 0, 0);
-      yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], hacc[hb][3], yacc[ob], 0, 0, 0);
-    }
-  }
-
-  // epilogue: y = acc + p2 + x (residual), LayerNorm over the D features of row c, which
-  // live in the 4 lanes c, c+16, c+32, c+48 (features ob*16 + 4g + q).
-  const floatx4* pb2 = reinterpret_cast<const floatx4*>(pack + G::PB2);
-  float sum = 0.0f;
 #pragma unroll
-  for (int ob = 0; ob < NY; ++ob) {
-    const floatx4 bb = pb2[ob * 4 + g];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = ob * 16 + 4 * g + q;
-      const float res = (valid && f < D) ? lrow[f] + rrow[f] : 0.0f;
-      const float y = (f < D) ? yacc[ob][q] + bb[q] + res : 0.0f;
-      yacc[ob][q] = y;
-      sum += y;
-    }
-  }
-  sum += __shfl_xor(sum, 16);
-  sum += __shfl_xor(sum, 32);
-  const float mean = sum / (float)D;
-  float var = 0.0f;
-#pragma unroll
-  for (int ob = 0; ob < NY; ++ob) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = ob * 16 + 4 * g + q;
-      const float dlt = yacc[ob][q] - mean;
-      var += (f < D) ? dlt * dlt : 0.0f;
-    }
-  }
-  var += __shfl_xor(var, 16);
-  var += __shfl_xor(var, 32);
-  const float rstd = 1.0f / sqrtf(var / (float)D + ln_eps);
-  const floatx4* plw = reinterpret_cast<const floatx4*>(pack + G::PLW);
-  const floatx4* plb = reinterpret_cast<const floatx4*>(pack + G::PLB);
-  const float* tgt = targets ? targets + (row_target && valid ? row_target[row] : 0) * D : nullptr;
-  float dot = 0.0f, nz = 0.0f;
-#pragma unroll
-  for (int ob = 0; ob < NY; ++ob) {
-    const floatx4 w = plw[ob * 4 + g], bb = plb[ob * 4 + g];
-    floatx4 z;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int f = ob * 16 + 4 * g + q;
-      z[q] = (f < D) ? (yacc[ob][q] - mean) * rstd * w[q] + bb[q] : 0.0f;
-      if (tgt && f < D) dot += z[q] * tgt[f];
-      nz += z[q] * z[q];
-    }
-    if (out_g && valid) {
-      const int f0 = ob * 16 + 4 * g;
-      if (f0 + 3 < D && (D % 4) == 0) {
-        *reinterpret_cast<floatx4*>(out_g + row * D + f0) = z;
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (f0 + q < D) out_g[row * D + f0 + q] = z[q];
+      for (int q = 0; q < 4; ++q) {
+        const int f = ob * 16 + 4 * g + q;
+        const float res = (f < D) ? lrow[f] + rrow[f] : 0.0f;
+        const float y = (f < D) ? yacc[ob][q] + res : 0.0f;
+        yacc[ob][q] = y;
+        sum += y;
       }
     }
-  }
-  if (score) {
-    dot += __shfl_xor(dot, 16);
-    dot += __shfl_xor(dot, 32);
-    nz += __shfl_xor(nz, 16);
-    nz += __shfl_xor(nz, 32);
-    if (g == 0 && valid) {
-      float s = dot;
-      if (normalize) {
-        const float n = sqrtf(nz);
-        s = n > 0.0f ? dot / n : 0.0f;
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float mean = sum / (float)D;
+    float var = 0.0f;
+#pragma unroll
+    for (int ob = 0; ob < NY; ++ob) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = ob * 16 + 4 * g + q;
+        const float dlt = yacc[ob][q] - mean;
+        var += (f < D) ? dlt * dlt : 0.0f;
       }
-      score[row] = s;
+    }
+    var += __shfl_xor(var, 16);
+    var += __shfl_xor(var, 32);
+    const float rstd = 1.0f / sqrtf(var / (float)D + ln_eps);
+    const floatx4* plw = reinterpret_cast<const floatx4*>(opaque(pack) + G::PLW);
+    const floatx4* plb = reinterpret_cast<const floatx4*>(opaque(pack) + G::PLB);
+    const float* tgt = targets ? targets + (row_target ? row_target[rr] : 0) * D : nullptr;
+    float dot = 0.0f, nz = 0.0f;
+#pragma unroll
+    for (int ob = 0; ob < NY; ++ob) {
+      const floatx4 w = plw[ob * 4 + g], bb = plb[ob * 4 + g];
+      floatx4 z;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = ob * 16 + 4 * g + q;
+        z[q] = (f < D) ? (yacc[ob][q] - mean) * rstd * w[q] + bb[q] : 0.0f;
+        if (f < D) dot += z[q] * (tgt ? tgt[f] : 0.0f);
+        nz += z[q] * z[q];
+      }
+      if (out_g && valid) {
+        const int f0 = ob * 16 + 4 * g;
+        if (f0 + 3 < D && (D % 4) == 0) {
+          *reinterpret_cast<floatx4*>(out_g + row * D + f0) = z;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (f0 + q < D) out_g[row * D + f0 + q] = z[q];
+        }
+      }
+    }
+    if (score) {
+      dot += __shfl_xor(dot, 16);
+      dot += __shfl_xor(dot, 32);
+      nz += __shfl_xor(nz, 16);
+      nz += __shfl_xor(nz, 32);
+      if (g == 0 && valid) {
+        float sc = dot;
+        if (normalize) {
+          const float n = sqrtf(nz);
+          sc = n > 0.0f ? dot / n : 0.0f;
+        }
+        score[row] = sc;
+      }
     }
   }
 }
@@ -423,8 +479,20 @@ struct XDispatch {
   static int encode(const float* pack, float ln_eps, const float* left, const int64_t* li, const float* right,
                     const int64_t* ri, int64_t n_rows, const float* targets, const int64_t* row_target, int normalize,
                     float* out_g, float* score, hipStream_t st) {
-    const int64_t waves = (n_rows + 15) / 16;
-    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    const int64_t tiles = (n_rows + 63) / 64;
+    static int resident = 0;
+    if (!resident) {
+      int dev = 0, cus = 256, per = 0;
+      if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+      }
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k_extractor_encode<D>),
+                                                       256, 0) != hipSuccess || per <= 0)
+        per = 1;
+      resident = cus * per;
+    }
+    const unsigned blocks = (unsigned)(tiles < resident ? tiles : resident);
     hipLaunchKernelGGL(k_extractor_encode<D>, dim3(blocks), dim3(256), 0, st, pack, ln_eps, left, li, right, ri,
                        n_rows, targets, row_target, normalize, out_g, score);
     MMRE_CHECK_LAUNCH();
