@@ -264,30 +264,48 @@ __device__ __forceinline__ void run_chunks(floatx4 (&ring)[2][XG<D>::CH * 64], f
   for (int j = 0; j < 2; ++j) ring[(CHK + 1) & 1][j * 256 + threadIdx.x] = st[j];
   load_chunk<D>(stream, (CHK + 2) % NC, st);  // the stream repeats for the next tile
   const floatx4* buf = ring[CHK & 1] + lane;
-#pragma unroll
-  for (int slot = 0; slot < CH; ++slot) {
-    const int p = CHK * CH + slot;
-    if (p == NP1) {  // stage 1 done (accumulators started at the bias): relu; stage 2 starts at p2
-#pragma unroll
-      for (int b = 0; b < NH; ++b)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) hacc[b][q] = fmaxf(hacc[b][q], 0.0f);
-      const floatx4* pb2 = reinterpret_cast<const floatx4*>(opaque(pack) + G::PB2);
-#pragma unroll
-      for (int b = 0; b < NY; ++b) yacc[b] = pb2[b * 4 + g];
-    }
+  // one MFMA step e of piece p with A fragment a (p is a compile-time constant here)
+  auto step = [&](int p, const floatx4& a, const floatx4& xv, int e) {
     if (p < NP1) {  // H^T = W1 . X^T
-      const int s4 = p / NH, b = p % NH;
-      const floatx4 a = buf[slot * 64];
-      const floatx4 xv = xs[s4 * 64];  // this lane's X[row][g*KC + 4*s4 .. +3]
-#pragma unroll
-      for (int e = 0; e < 4; ++e) hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], xv[e], hacc[b], 0, 0, 0);
+      const int b = p % NH;
+      hacc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], xv[e], hacc[b], 0, 0, 0);
     } else if (p < NP) {  // Y^T = W2 . H^T, B operand straight from the stage-1 accumulators
       const int p2 = p - NP1, hb = p2 / NY, ob = p2 % NY;
-      const floatx4 a = buf[slot * 64];
+      yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], hacc[hb][e], yacc[ob], 0, 0, 0);
+    }
+  };
+  auto stage_switch = [&]() {  // stage 1 done (accumulators started at the bias): relu; stage 2 starts at p2
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        yacc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q], hacc[hb][q], yacc[ob], 0, 0, 0);
+    for (int b = 0; b < NH; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hacc[b][q] = fmaxf(hacc[b][q], 0.0f);
+    const floatx4* pb2 = reinterpret_cast<const floatx4*>(opaque(pack) + G::PB2);
+#pragma unroll
+    for (int b = 0; b < NY; ++b) yacc[b] = pb2[b * 4 + g];
+  };
+  // pieces in pairs: the two 4-step accumulation chains interleave, so no MFMA waits on the
+  // 40-cycle dependent latency of the one before it (16x16x4 f32 issues every 32 cycles)
+#pragma unroll
+  for (int slot = 0; slot < CH; slot += 2) {
+    const int p0 = CHK * CH + slot, p1 = p0 + 1;
+    if (p0 >= NP) break;
+    if (p0 == NP1) stage_switch();
+    const floatx4 a0 = buf[slot * 64];
+    const floatx4 a1 = buf[(slot + 1) * 64];
+    const floatx4 x0 = p0 < NP1 ? xs[(p0 / NH) * 64] : floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    const floatx4 x1 = p1 < NP1 ? xs[(p1 / NH) * 64] : floatx4{0.0f, 0.0f, 0.0f, 0.0f};
+    if (p1 == NP1) {  // the pair straddles the stage switch
+#pragma unroll
+      for (int e = 0; e < 4; ++e) step(p0, a0, x0, e);
+      stage_switch();
+#pragma unroll
+      for (int e = 0; e < 4; ++e) step(p1, a1, x1, e);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        step(p0, a0, x0, e);
+        step(p1, a1, x1, e);
+      }
     }
   }
   if constexpr (CHK + 1 < NC) run_chunks<D, CHK + 1>(ring, st, stream, xs, hacc, yacc, pack, lane, g);
