@@ -48,6 +48,9 @@ CONFIGS = {
     "zsl": dict(dataset="FB15K-237-ZS", model="extractor", dim=200, norm=False,
                 workload="ZSL eval FB15K-237-ZS: Extractor (d=200, max_neighbor=50) + mean-cosine rank of "
                          "17,596 queries x ~1,000 candidates (SURVEY 8(f) rank 1)"),
+    "gan": dict(dataset="FB15K-237-ZS", model="gan", dim=200, norm=False,
+                workload="ZSL GAN iteration FB15K-237-ZS (ZSLmodule.train, SURVEY 8(f) rank 3): 1 D step + 1 G step, "
+                         "G_batch_size 256 x gan_batch_rela 2 = 512 rows, d=200, 206 seen-relation centroids"),
 }
 MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
@@ -323,6 +326,139 @@ def bench_zsl(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def bench_gan(args, world, rank, dev, dist):
+    """One step = one GAN iteration of ZSLmodule.train (zsl_module.py:417-600) at the reference's
+    batch (G_batch_size 256 x gan_batch_rela 2): a Discriminator step (Extractor vectors of the
+    real and false pairs, generator in eval mode, 3 + 1 Discriminator calls with spectral-norm
+    power iterations, gradient penalty double backward, Adam) and a Generator step (generator
+    with power iteration + HIP backward, 3 Discriminator calls, visual-pivot loss, Adam), each
+    replayed from its hipGraph with noise / alpha drawn inside the graph."""
+    from mmre.extractor import ZSLRanker, encode
+    from mmre.gan import ZSLGANStep
+    from mmre.generator import RelationGenerator
+    from mmre.workloads import zsl_workload
+    from module.zsl_module import Discriminator, Extractor, weights_init
+    if world > 1:
+        raise SystemExit("bench --config gan is a single-GPU step (the GAN trains one model per process)")
+    w = zsl_workload(dim=200)
+    d, E = w["dim"], w["n_ent"]
+    torch.manual_seed(0)
+    ex = Extractor(d, w["n_sym"], w["sym_emb"].numpy())
+    ex.apply(weights_init)
+    ex = ex.to(dev).eval()
+    ranker = ZSLRanker(ex, w["ent_sym"], w["conn"], w["deg"], device=dev)
+    n_lab = 206
+    rng = np.random.default_rng(0)
+    # centroids: mean Extractor vector of 256 pairs per seen relation (zsl_module.py:371-383)
+    ph = torch.as_tensor(rng.integers(0, E, n_lab * 256), device=dev)
+    pt = torch.as_tensor(rng.integers(0, E, n_lab * 256), device=dev)
+    g, _ = encode(ranker.pack, d, ranker.ln_eps, ranker.left, ph, ranker.right, pt, want_g=True, want_score=False)
+    centroids = g.view(n_lab, 256, d).mean(1)
+    gen = RelationGenerator(384, 15, d).to(dev)
+    disc = Discriminator(dim=d).to(dev)
+    disc.apply(weights_init)
+    cls_table = torch.randn(w["n_rel"], 384, device=dev)
+    step = ZSLGANStep(gen, disc, cls_table, centroids, ranker, lr_G=1e-4, lr_D=1e-4, pretrain_margin=5.0,
+                      gan_batch_rela=2)
+    n = 512
+
+    def batch():
+        lab = np.repeat(rng.choice(n_lab, 2, replace=False), 256)
+        return {k: torch.as_tensor(v, device=dev) for k, v in dict(
+            rel=rng.integers(0, w["n_rel"], n), q_head=rng.integers(0, E, n), q_tail=rng.integers(0, E, n),
+            f_head=rng.integers(0, E, n), f_tail=rng.integers(0, E, n), labels=lab).items()}
+
+    b0 = batch()
+    step.replay("d", b0)  # eager first step + capture
+    step.replay("g", b0)
+
+    def one(bt):
+        step.replay("d", bt)
+        return step.replay("g", bt)
+
+    batches = [batch() for _ in range(args.warmup + args.steps)]
+    for i in range(args.warmup):
+        one(batches[i])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = one(batches[args.warmup + i])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # the same iteration launched eagerly (no graph), for the launch-overhead comparison
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    k_e = max(3, args.steps // 4)
+    for i in range(k_e):
+        bt = batches[i]
+        noise = torch.randn(n, 15, device=dev)
+        alpha = torch.rand(n, 1, device=dev)
+        step.d_step(bt["rel"], bt["q_head"], bt["q_tail"], bt["f_head"], bt["f_tail"], bt["labels"], noise, alpha)
+        step.g_step(bt["rel"], bt["q_head"], bt["q_tail"], bt["f_head"], bt["f_tail"], bt["labels"], noise)
+    torch.cuda.synchronize()
+    eager_ms = (time.perf_counter() - te) / k_e * 1e3
+    res = {"metric": f"GAN iterations/sec, {CONFIGS['gan']['workload']}", "value": args.steps / elapsed,
+           "unit": "iterations/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32",
+           "data": "real FB15K-237-ZS entity graph (synthetic train neighbourhoods), random-init Extractor / "
+                   "generator / Discriminator (weights_init), random relation CLS rows and batches",
+           "config": {"workload": CONFIGS["gan"]["workload"], "rows": n, "dim": d, "centroids": n_lab,
+                      "parallelism": "single GPU, hipGraph replay per D / G step"},
+           "eager_ms_per_step": eager_ms, "last_losses_G": [float(x) for x in out.cpu()]}
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_gan(w, centroids.cpu(), n_lab)
+    print(json.dumps(res), flush=True)
+
+
+def cpu_baseline_gan(w, centroids, n_lab, iters=3):
+    """The reference's GAN iteration on the host cores: Extractor forwards of the 4 x 512 real /
+    false pairs (oracle/zsl_extractor.py, eval) + one D step and one G step (oracle/zsl_gan.py
+    GANRef in float32: the op sequence of zsl_module.py:419-600)."""
+    import zsl_extractor as ox
+    import zsl_gan as og
+    from mmre.generator import RelationGenerator
+    from module.zsl_module import Discriminator
+    d, E = w["dim"], w["n_ent"]
+    ref = ox.ExtractorRef(d, w["n_sym"], w["sym_emb"].numpy())
+    gen, disc = RelationGenerator(384, 15, d), Discriminator(dim=d)
+    D = {k: v.detach().clone() for k, v in disc.state_dict().items()}
+    for k in D:
+        if not (k.endswith("weight_u") or k.endswith("weight_v")):
+            D[k].requires_grad_(True)
+    layers = [(L.weight_orig.detach().clone().requires_grad_(), L.bias.detach().clone().requires_grad_(),
+               L.weight_u.clone(), L.weight_v.clone())
+              for L in (gen.generate_fc_layer, gen.des_rel_map_layer1, gen.des_rel_map_layer2)]
+    G = (layers, gen.ln_a.detach().clone().requires_grad_(), gen.ln_b.detach().clone().requires_grad_())
+    gan = og.GANRef(D, G, centroids.float())
+    rng = np.random.default_rng(1)
+    conn, deg, es = w["conn"], w["deg"], w["ent_sym"]
+    n = 512
+
+    def vecs(h, t):
+        pairs = torch.from_numpy(np.stack([es[h], es[t]], 1))
+        meta = (torch.LongTensor(conn[h]), torch.FloatTensor(deg[h]), torch.LongTensor(conn[t]),
+                torch.FloatTensor(deg[t]))
+        with torch.no_grad():
+            return ref.encode(pairs, meta)
+
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        lab = torch.as_tensor(np.repeat(rng.choice(n_lab, 2, replace=False), 256))
+        cls_rows = torch.randn(n, 384)
+        for step in ("d", "g"):
+            h, t, fh, ft = (rng.integers(0, E, n) for _ in range(4))
+            real, neg = vecs(h, t), vecs(fh, ft)
+            if step == "d":
+                gan.d_step(cls_rows, real, neg, lab, torch.randn(n, 15), torch.rand(n, 1))
+            else:
+                gan.g_step(cls_rows, real, neg, lab, torch.randn(n, 15))
+    el = time.perf_counter() - t0
+    return {"value": iters / el, "unit": "iterations/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{iters} GAN iterations (torch {torch.__version__} CPU fp32: oracle Extractor + GANRef "
+                      f"D/G steps), {el:.2f} s on {torch.get_num_threads()} threads"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -352,6 +488,8 @@ def main():
     cfg = CONFIGS[args.config]
     if args.config == "zsl":
         return bench_zsl(args, world, rank, dev, dist)
+    if args.config == "gan":
+        return bench_gan(args, world, rank, dev, dist)
     if cfg["dataset"] == "synthetic-1M":
         w = synthetic_large()
     else:

@@ -227,6 +227,31 @@ int mmre_generator_forward(const float* d_noise, int noise_dim, const float* d_c
                            const float* d_w2, const float* d_b2, float* d_u2, float* d_v2, int out2,
                            const float* d_ln_a, const float* d_ln_b, float ln_eps, int power_iteration,
                            float sn_eps, float* d_out, float* d_work, void* stream);
+/* Floats of the activation buffer of mmre_generator_forward_save. */
+int64_t mmre_generator_acts_size(int64_t n_rows, int in0, int out0, int out1, int out2);
+/* Training forward: mmre_generator_forward that also keeps the layer outputs for the
+ * backward in d_acts = [x0 (N, in0) | h1 (N, out0) | h2 (N, out1) | h3 (N, out2) |
+ * W0/s0 (out0, in0) | W1/s1 (out1, out0) | W2/s2 (out2, out1)] (row-major, in0 =
+ * noise_dim + cls_dim); sigma[3] is left at d_work + 3 * 2048. */
+int mmre_generator_forward_save(const float* d_noise, int noise_dim, const float* d_cls, int cls_dim,
+                                int64_t n_rows, const float* d_w0, const float* d_b0, float* d_u0, float* d_v0,
+                                int out0, const float* d_w1, const float* d_b1, float* d_u1, float* d_v1, int out1,
+                                const float* d_w2, const float* d_b2, float* d_u2, float* d_v2, int out2,
+                                const float* d_ln_a, const float* d_ln_b, float ln_eps, int power_iteration,
+                                float sn_eps, float* d_out, float* d_work, float* d_acts, void* stream);
+/* Floats of the backward's workspace. */
+int64_t mmre_generator_backward_workspace(int64_t n_rows, int in0, int out0, int out1, int out2);
+/* Parameter gradients of the generator for loss_G.backward() (zsl_module.py:595; the
+ * grad_list of :356-357: weight_orig, bias of the three SN layers, layer_norm a_2 / b_2),
+ * written (not accumulated) from d_gout = dL/dout (N, out2). Spectral norm chain rule with
+ * the forward's u, v, sigma (u, v constant, spectral_norm.py:85-89):
+ *   dL/dW_orig = G / s - <G, W_orig> / s^2 * u v^T,  G = dL/d(W_orig / s). */
+int mmre_generator_backward(const float* d_gout, int64_t n_rows, int in0, int out0, int out1, int out2,
+                            const float* d_acts, const float* d_sigma, const float* d_w0, const float* d_u0,
+                            const float* d_v0, const float* d_w1, const float* d_u1, const float* d_v1,
+                            const float* d_w2, const float* d_u2, const float* d_v2, const float* d_ln_a,
+                            float ln_eps, float* d_gw0, float* d_gb0, float* d_gw1, float* d_gb1, float* d_gw2,
+                            float* d_gb2, float* d_gln_a, float* d_gln_b, float* d_work, void* stream);
 
 /* ====================================================================== *
  *  Candidate-list rankings.                                               *

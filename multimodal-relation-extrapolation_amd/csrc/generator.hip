@@ -7,11 +7,15 @@
 // Spectral norm (spectral_norm.py:39-89): s = u . (W v); in training mode one power
 // iteration first sets v = normalize(W^T u), u = normalize(W v) in place (eps 1e-12).
 //
-// k_sn_sigma: one workgroup per layer (the three mat-vecs), writes sigma[3] (+ u, v).
-// k_generator_mlp: one workgroup per 32 rows; the three layers run back to back on
-// v_mfma_f32_32x32x2_f32 with the activations kept in LDS (A operand) and the weights
-// read from global as W[c][k] / sigma -- the reference's normalised weight values --
-// as the B operand; bias add in the epilogue; LayerNormalization by one wave per row.
+// Forward launches (all small: N <= ~1k rows, so the design is about parallelism, not reuse):
+//   k_sn_sigma   one 1024-thread workgroup per layer: the power-iteration mat-vecs split over
+//                16 waves (column sums lane-parallel over 4 row quarters, row dots wave-parallel)
+//   k_sn_scale   W_hat = W_orig / sigma element-wise (the reference's normalised weight values),
+//                kept in the activation buffer for the backward
+//   k_gen_concat x0 = [noise | cls]
+//   k_linear     x W_hat^T + b: one wave per 32 x 32 output tile on v_mfma_f32_32x32x2_f32,
+//                operands batched 8 K-steps per load round (M/32 x N/32 waves per layer)
+//   k_gen_ln     LayerNormalization, one wave per row
 #include "mmre_common.h"
 
 namespace mmre {
@@ -37,138 +41,334 @@ struct SNLayer {
   int out, in;
 };
 
-// One workgroup per layer. scratch: >= in + out floats per layer (workspace).
-__global__ __launch_bounds__(256) void k_sn_sigma(SNLayer l0, SNLayer l1, SNLayer l2, int power_iteration, float eps,
-                                                  float* __restrict__ sigma, float* __restrict__ scratch) {
-  __shared__ float red[4];
+constexpr int SN_T = 1024;
+
+// One workgroup per layer. scratch: 2048 floats per layer (W v, then W^T u).
+__global__ __launch_bounds__(SN_T) void k_sn_sigma(SNLayer l0, SNLayer l1, SNLayer l2, int power_iteration,
+                                                   float eps, float* __restrict__ sigma, float* __restrict__ scratch) {
+  __shared__ float red[SN_T / 64];
+  __shared__ float part[4][1024];
   const SNLayer L = blockIdx.x == 0 ? l0 : (blockIdx.x == 1 ? l1 : l2);
   float* wv = scratch + blockIdx.x * 2048;  // W v   (out <= 1024)
   float* tv = wv + 1024;                    // W^T u (in <= 1024)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = SN_T / 64;
   if (power_iteration) {
-    for (int k = threadIdx.x; k < L.in; k += blockDim.x) {
+    // tv[k] = sum_o W[o][k] u[o]: 256 columns per pass x 4 quarters of the rows
+    const int q = threadIdx.x >> 8, tk = threadIdx.x & 255;
+    const int o0 = (int)((int64_t)q * L.out / 4), o1 = (int)((int64_t)(q + 1) * L.out / 4);
+    for (int k0 = 0; k0 < L.in; k0 += 256) {
+      const int k = k0 + tk;
       float s = 0.0f;
-      for (int o = 0; o < L.out; ++o) s += L.w[(int64_t)o * L.in + k] * L.u[o];
-      tv[k] = s;
+      if (k < L.in)
+        for (int o = o0; o < o1; ++o) s += L.w[(int64_t)o * L.in + k] * L.u[o];
+      part[q][tk] = s;
+      __syncthreads();
+      if (q == 0 && k < L.in) tv[k] = part[0][tk] + part[1][tk] + part[2][tk] + part[3][tk];
+      __syncthreads();
     }
-    __syncthreads();
     float ss = 0.0f;
-    for (int k = threadIdx.x; k < L.in; k += blockDim.x) ss += tv[k] * tv[k];
+    for (int k = threadIdx.x; k < L.in; k += SN_T) ss += tv[k] * tv[k];
     const float nv = fmaxf(sqrtf(block_sum(ss, red)), eps);
     __syncthreads();
-    for (int k = threadIdx.x; k < L.in; k += blockDim.x) L.v[k] = tv[k] / nv;
+    for (int k = threadIdx.x; k < L.in; k += SN_T) L.v[k] = tv[k] / nv;
     __syncthreads();
   }
-  for (int o = threadIdx.x; o < L.out; o += blockDim.x) {
+  // wv[o] = W[o] . v: one wave per row, lanes over k (coalesced)
+  for (int o = wave; o < L.out; o += nw) {
     float s = 0.0f;
-    for (int k = 0; k < L.in; ++k) s += L.w[(int64_t)o * L.in + k] * L.v[k];
-    wv[o] = s;
+    for (int k = lane; k < L.in; k += 64) s += L.w[(int64_t)o * L.in + k] * L.v[k];
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) s += __shfl_xor(s, sh);
+    if (lane == 0) wv[o] = s;
   }
   __syncthreads();
   if (power_iteration) {
     float ss = 0.0f;
-    for (int o = threadIdx.x; o < L.out; o += blockDim.x) ss += wv[o] * wv[o];
+    for (int o = threadIdx.x; o < L.out; o += SN_T) ss += wv[o] * wv[o];
     const float nu = fmaxf(sqrtf(block_sum(ss, red)), eps);
     __syncthreads();
-    for (int o = threadIdx.x; o < L.out; o += blockDim.x) L.u[o] = wv[o] / nu;
+    for (int o = threadIdx.x; o < L.out; o += SN_T) L.u[o] = wv[o] / nu;
     __syncthreads();
   }
   float dot = 0.0f;
-  for (int o = threadIdx.x; o < L.out; o += blockDim.x) dot += L.u[o] * wv[o];
+  for (int o = threadIdx.x; o < L.out; o += SN_T) dot += L.u[o] * wv[o];
   dot = block_sum(dot, red);
   if (threadIdx.x == 0) sigma[blockIdx.x] = dot;
 }
 
-constexpr int GM = 32;  // rows per workgroup
+// W_hat = W_orig / sigma for the three layers (one grid over their concatenation).
+__global__ __launch_bounds__(256) void k_sn_scale(const float* __restrict__ w0, int64_t n0,
+                                                  const float* __restrict__ w1, int64_t n1,
+                                                  const float* __restrict__ w2, int64_t n2,
+                                                  const float* __restrict__ sigma, float* __restrict__ out) {
+  const int64_t total = n0 + n1 + n2, stride = (int64_t)gridDim.x * blockDim.x;
+  const float s0 = sigma[0], s1 = sigma[1], s2 = sigma[2];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride)
+    out[i] = i < n0 ? w0[i] / s0 : (i < n0 + n1 ? w1[i - n0] / s1 : w2[i - n0 - n1] / s2);
+}
 
-// out_lds[i][c] = sum_k a_lds[i][k] * (W[c][k] / s) + b[c] for c < out (K padded to even).
-__device__ void mfma_layer(const float* a_lds, int lda, int in, const float* __restrict__ w,
-                           const float* __restrict__ bias, float s, int out, float* out_lds, int ldo) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int i = lane & 31, kh = lane >> 5;
-  const int n_tiles = (out + 31) / 32;
-  for (int tile = wave; tile < n_tiles; tile += nw) {
-    const int c = tile * 32 + i;  // B operand column for this lane
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-    const float* wrow = w + (int64_t)c * in;
-    for (int k0 = 0; k0 < in; k0 += 2) {
-      const int k = k0 + kh;
-      const float a = k < in ? a_lds[i * lda + k] : 0.0f;
-      const float b = (c < out && k < in) ? wrow[k] / s : 0.0f;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
-    }
-    const int col = tile * 32 + i;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (col < out) out_lds[row * ldo + col] = acc[r] + bias[col];
-    }
+__global__ __launch_bounds__(256) void k_gen_concat(const float* __restrict__ noise, int nd,
+                                                    const float* __restrict__ cls, int cd, int64_t n_rows,
+                                                    float* __restrict__ x0) {
+  const int in0 = nd + cd;
+  const int64_t total = n_rows * in0, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int64_t r = i / in0;
+    const int k = (int)(i % in0);
+    x0[i] = k < nd ? noise[r * nd + k] : cls[r * cd + (k - nd)];
   }
 }
 
-__global__ __launch_bounds__(256) void k_generator_mlp(const float* __restrict__ noise, int nd,
-                                                       const float* __restrict__ cls, int cd, int64_t n_rows,
-                                                       const float* __restrict__ w0, const float* __restrict__ b0,
-                                                       int o0, const float* __restrict__ w1,
-                                                       const float* __restrict__ b1, int o1,
-                                                       const float* __restrict__ w2, const float* __restrict__ b2,
-                                                       int o2, const float* __restrict__ sigma,
-                                                       const float* __restrict__ ln_a, const float* __restrict__ ln_b,
-                                                       float ln_eps, float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int in0 = nd + cd;
-  const int lda = in0 | 1, ld1 = o0 | 1, ld2 = o1 | 1, ld3 = o2 | 1;  // odd strides: conflict-free column reads
-  float* x0 = smem;                 // [GM][lda]
-  float* x1 = x0 + GM * lda;        // [GM][ld1]
-  float* x2 = x0;                   // reuse
-  float* x3 = x1;                   // reuse (o2 <= o0 checked on the host)
-  const int64_t r0 = (int64_t)blockIdx.x * GM;
-  for (int idx = threadIdx.x; idx < GM * in0; idx += blockDim.x) {
-    const int i = idx / in0, k = idx % in0;
-    const int64_t row = r0 + i;
-    float v = 0.0f;
-    if (row < n_rows) v = k < nd ? noise[row * nd + k] : cls[row * cd + (k - nd)];
-    x0[i * lda + k] = v;
-  }
-  __syncthreads();
-  mfma_layer(x0, lda, in0, w0, b0, sigma[0], o0, x1, ld1);
-  __syncthreads();
-  mfma_layer(x1, ld1, o0, w1, b1, sigma[1], o1, x2, ld2);
-  __syncthreads();
-  mfma_layer(x2, ld2, o1, w2, b2, sigma[2], o2, x3, ld3);
-  __syncthreads();
-  // LayerNormalization: one wave per row
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int i = wave; i < GM; i += nw) {
-    const int64_t row = r0 + i;
-    if (row >= n_rows) continue;
-    const float* z = x3 + i * ld3;
-    if (o2 == 1) {
-      if (lane == 0) out[row] = z[0];
-      continue;
+// C[m][n] = sum_k A[m][k] * W[n][k] + bias[n]  (A: M x K, W: N x K, both row-major).
+// One wave per 32 x 32 tile; each lane loads 8 K-steps of its A row / W row per round.
+constexpr int LK = 8;
+__global__ __launch_bounds__(64) void k_linear(const float* __restrict__ A, const float* __restrict__ W,
+                                               const float* __restrict__ bias, int M, int N, int K,
+                                               float* __restrict__ C) {
+  const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  const int m = m0 + i, n = n0 + i;
+  const float* ar = A + (int64_t)(m < M ? m : 0) * K;
+  const float* wr = W + (int64_t)(n < N ? n : 0) * K;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  for (int k0 = 0; k0 < K; k0 += 2 * LK) {
+    float a[LK], b[LK];
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      const int k = k0 + 2 * j + kh;
+      a[j] = (m < M && k < K) ? ar[k] : 0.0f;
+      b[j] = (n < N && k < K) ? wr[k] : 0.0f;
     }
-    float s = 0.0f;
-    for (int k = lane; k < o2; k += 64) s += z[k];
 #pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) s += __shfl_xor(s, sh);
-    const float mu = s / (float)o2;
-    float v = 0.0f;
-    for (int k = lane; k < o2; k += 64) v += (z[k] - mu) * (z[k] - mu);
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh);
-    const float sd = sqrtf(v / (float)(o2 - 1));
-    for (int k = lane; k < o2; k += 64) out[row * o2 + k] = (z[k] - mu) / (sd + ln_eps) * ln_a[k] + ln_b[k];
+    for (int j = 0; j < LK; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
   }
+  const float bb = n < N ? bias[n] : 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    if (row < M && n < N) C[(int64_t)row * N + n] = acc[r] + bb;
+  }
+}
+
+// LayerNormalization forward (submodule.py:68-77), one wave per row.
+__global__ __launch_bounds__(256) void k_gen_ln(const float* __restrict__ z, const float* __restrict__ ln_a,
+                                                const float* __restrict__ ln_b, float eps, int64_t n_rows, int D,
+                                                float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const float* zr = z + row * D;
+  if (D == 1) {
+    if (lane == 0) out[row] = zr[0];
+    return;
+  }
+  float s = 0.0f;
+  for (int k = lane; k < D; k += 64) s += zr[k];
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) s += __shfl_xor(s, sh);
+  const float mu = s / (float)D;
+  float v = 0.0f;
+  for (int k = lane; k < D; k += 64) v += (zr[k] - mu) * (zr[k] - mu);
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) v += __shfl_xor(v, sh);
+  const float sd = sqrtf(v / (float)(D - 1));
+  for (int k = lane; k < D; k += 64) out[row * D + k] = (zr[k] - mu) / (sd + eps) * ln_a[k] + ln_b[k];
+}
+
+// ----------------------------------------------------------------------------------------
+// Backward (training step of the generator, zsl_module.py:526-597: loss_G.backward()).
+// ----------------------------------------------------------------------------------------
+// LayerNormalization backward, one wave per row: out = (z - mu) / (sd + eps) * a + b with the
+// unbiased sd. With c = z - mu, d = sd + eps, g = dL/dout * a:
+//   dL/dz_k = (g_k - mean(g)) / d - c_k * sum_i(g_i c_i) / (d^2 * sd * (D - 1)).
+// Writes gz (N, D) and zhat (N, D) (for the a_2 gradient). D == 1: identity (submodule.py:69-70).
+__global__ __launch_bounds__(256) void k_gen_ln_bwd(const float* __restrict__ gout, const float* __restrict__ z,
+                                                    const float* __restrict__ ln_a, float eps, int64_t n_rows, int D,
+                                                    float* __restrict__ gz, float* __restrict__ zhat) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= n_rows) return;
+  const float* zr = z + row * D;
+  const float* gr = gout + row * D;
+  if (D == 1) {
+    if (lane == 0) { gz[row] = gr[0]; zhat[row] = 0.0f; }
+    return;
+  }
+  float s = 0.0f;
+  for (int k = lane; k < D; k += 64) s += zr[k];
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) s += __shfl_xor(s, sh);
+  const float mu = s / (float)D;
+  float v = 0.0f, sg = 0.0f, sgc = 0.0f;
+  for (int k = lane; k < D; k += 64) {
+    const float c = zr[k] - mu, g = gr[k] * ln_a[k];
+    v += c * c;
+    sg += g;
+    sgc += g * c;
+  }
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) {
+    v += __shfl_xor(v, sh);
+    sg += __shfl_xor(sg, sh);
+    sgc += __shfl_xor(sgc, sh);
+  }
+  const float sd = sqrtf(v / (float)(D - 1)), d = sd + eps;
+  const float mg = sg / (float)D;
+  const float coef = sgc / (d * d * sd * (float)(D - 1));
+  for (int k = lane; k < D; k += 64) {
+    const float c = zr[k] - mu;
+    gz[row * D + k] = (gr[k] * ln_a[k] - mg) / d - c * coef;
+    zhat[row * D + k] = c / d;
+  }
+}
+
+// out[j] = sum_n A[n][j] (* B[n][j]): 64 columns x 16 row slices per workgroup, fixed
+// summation order (deterministic).
+__global__ __launch_bounds__(1024) void k_colsum(const float* __restrict__ A, const float* __restrict__ B,
+                                                 int64_t n_rows, int width, float* __restrict__ out) {
+  __shared__ float part[16][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
+  const int64_t r0 = sl * n_rows / 16, r1 = (sl + 1) * n_rows / 16;
+  float t = 0.0f;
+  if (j < width)
+    for (int64_t n = r0; n < r1; ++n) t += B ? A[n * width + j] * B[n * width + j] : A[n * width + j];
+  part[sl][c] = t;
+  __syncthreads();
+  if (sl == 0 && j < width) {
+    float s = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += part[q][c];
+    out[j] = s;
+  }
+}
+
+// C[m][n] = alpha * sum_k A(m, k) B(k, n) with A(m, k) = A[m*sam + k*sak], B(k, n) = B[k*sbk + n*sbn];
+// one wave per 32 x 32 tile on v_mfma_f32_32x32x2_f32 (operands straight from L2: small GEMMs).
+__global__ __launch_bounds__(64) void k_gemm_f32(const float* __restrict__ A, int64_t sam, int64_t sak,
+                                                 const float* __restrict__ B, int64_t sbk, int64_t sbn, int M, int N,
+                                                 int64_t K, const float* __restrict__ div, float* __restrict__ C) {
+  const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int m = m0 + i, n = n0 + i;
+  for (int64_t k0 = 0; k0 < K; k0 += 2 * LK) {  // LK K-steps of operands per load round
+    float a[LK], b[LK];
+#pragma unroll
+    for (int j = 0; j < LK; ++j) {
+      const int64_t k = k0 + 2 * j + kh;
+      a[j] = (m < M && k < K) ? A[m * sam + k * sak] : 0.0f;
+      b[j] = (n < N && k < K) ? B[k * sbk + n * sbn] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < LK; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
+  }
+  const float d = div ? *div : 1.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    if (row < M && n < N) C[(int64_t)row * N + n] = div ? acc[r] / d : acc[r];
+  }
+}
+
+// Spectral-norm chain rule, in place (one workgroup per matrix): G = dL/d(W/s) ->
+// dL/dW = G / s - <G, W> / s^2 * u v^T   (u, v, s: the forward's values, spectral_norm.py:85-89).
+__global__ __launch_bounds__(1024) void k_sn_grad(float* __restrict__ G, const float* __restrict__ W,
+                                                  const float* __restrict__ u, const float* __restrict__ v,
+                                                  const float* __restrict__ sigma, int out, int in) {
+  __shared__ float red[16];
+  const int64_t n = (int64_t)out * in;
+  float t = 0.0f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) t += G[i] * W[i];
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) t += __shfl_xor(t, sh);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  float dot = 0.0f;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) dot += red[w];
+  const float s = *sigma, c = dot / (s * s);
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) G[i] = G[i] / s - c * u[i / in] * v[i % in];
+}
+
+// C (M x N) = A B / (*div if div), strided operands
+static int gemm(hipStream_t st, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                int M, int N, int64_t K, const float* div, float* C) {
+  dim3 grid((unsigned)((N + 31) / 32), (unsigned)((M + 31) / 32));
+  hipLaunchKernelGGL(k_gemm_f32, grid, dim3(64), 0, st, A, sam, sak, B, sbk, sbn, M, N, K, div, C);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
 }
 
 }  // namespace mmre
 
 using namespace mmre;
 
+// Forward workspace: mat-vec scratch (3 x 2048) + sigma[3] (at 3 * 2048) + the activations
+// and W_hat when the caller keeps none.
+static int64_t acts_floats(int64_t n, int in0, int o0, int o1, int o2) {
+  return n * ((int64_t)in0 + o0 + o1 + o2) + (int64_t)o0 * in0 + (int64_t)o1 * o0 + (int64_t)o2 * o1;
+}
+
 extern "C" int64_t mmre_generator_workspace(int64_t n_rows, int in0, int out0, int out1, int out2) {
-  (void)n_rows; (void)in0; (void)out0; (void)out1; (void)out2;
-  return 3 * 2048 + 16;  // mat-vec scratch + sigma[3]
+  return 3 * 2048 + 16 + acts_floats(n_rows, in0, out0, out1, out2);
+}
+
+extern "C" int64_t mmre_generator_acts_size(int64_t n_rows, int in0, int out0, int out1, int out2) {
+  return acts_floats(n_rows, in0, out0, out1, out2);
+}
+
+extern "C" int mmre_generator_forward_save(const float* d_noise, int noise_dim, const float* d_cls, int cls_dim,
+                                           int64_t n_rows, const float* d_w0, const float* d_b0, float* d_u0,
+                                           float* d_v0, int out0, const float* d_w1, const float* d_b1, float* d_u1,
+                                           float* d_v1, int out1, const float* d_w2, const float* d_b2, float* d_u2,
+                                           float* d_v2, int out2, const float* d_ln_a, const float* d_ln_b,
+                                           float ln_eps, int power_iteration, float sn_eps, float* d_out,
+                                           float* d_work, float* d_acts, void* stream) {
+  if (!d_noise || !d_cls || !d_w0 || !d_b0 || !d_u0 || !d_v0 || !d_w1 || !d_b1 || !d_u1 || !d_v1 || !d_w2 || !d_b2 ||
+      !d_u2 || !d_v2 || !d_ln_a || !d_ln_b || !d_out || !d_work)
+    return MMRE_ERR_ARG;
+  const int in0 = noise_dim + cls_dim;
+  if (n_rows <= 0 || noise_dim < 0 || cls_dim <= 0 || out0 <= 0 || out1 <= 0 || out2 <= 0) return MMRE_ERR_ARG;
+  if (in0 > 1024 || out0 > 1024 || out1 > 1024 || out2 > 1024) return MMRE_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  float* sigma = d_work + 3 * 2048;
+  float* acts = d_acts ? d_acts : d_work + 3 * 2048 + 16;
+  float* x0 = acts;
+  float* h1 = x0 + n_rows * in0;
+  float* h2 = h1 + n_rows * out0;
+  float* h3 = h2 + n_rows * out1;
+  float* wh0 = h3 + n_rows * out2;
+  float* wh1 = wh0 + (int64_t)out0 * in0;
+  float* wh2 = wh1 + (int64_t)out1 * out0;
+  SNLayer l0{d_w0, d_u0, d_v0, out0, in0}, l1{d_w1, d_u1, d_v1, out1, out0}, l2{d_w2, d_u2, d_v2, out2, out1};
+  hipLaunchKernelGGL(k_sn_sigma, dim3(3), dim3(SN_T), 0, st, l0, l1, l2, power_iteration, sn_eps, sigma, d_work);
+  MMRE_CHECK_LAUNCH();
+  const int64_t nw = (int64_t)out0 * in0 + (int64_t)out1 * out0 + (int64_t)out2 * out1;
+  hipLaunchKernelGGL(k_sn_scale, dim3((unsigned)((nw + 255) / 256 < 2048 ? (nw + 255) / 256 : 2048)), dim3(256), 0, st,
+                     d_w0, (int64_t)out0 * in0, d_w1, (int64_t)out1 * out0, d_w2, (int64_t)out2 * out1, sigma, wh0);
+  MMRE_CHECK_LAUNCH();
+  const int64_t nx = n_rows * in0;
+  hipLaunchKernelGGL(k_gen_concat, dim3((unsigned)((nx + 255) / 256 < 4096 ? (nx + 255) / 256 : 4096)), dim3(256), 0,
+                     st, d_noise, noise_dim, d_cls, cls_dim, n_rows, x0);
+  MMRE_CHECK_LAUNCH();
+  const unsigned mb = (unsigned)((n_rows + 31) / 32);
+  hipLaunchKernelGGL(k_linear, dim3((unsigned)((out0 + 31) / 32), mb), dim3(64), 0, st, x0, wh0, d_b0, (int)n_rows,
+                     out0, in0, h1);
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_linear, dim3((unsigned)((out1 + 31) / 32), mb), dim3(64), 0, st, h1, wh1, d_b1, (int)n_rows,
+                     out1, out0, h2);
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_linear, dim3((unsigned)((out2 + 31) / 32), mb), dim3(64), 0, st, h2, wh2, d_b2, (int)n_rows,
+                     out2, out1, h3);
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_gen_ln, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, st, h3, d_ln_a, d_ln_b, ln_eps,
+                     n_rows, out2, d_out);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
 }
 
 extern "C" int mmre_generator_forward(const float* d_noise, int noise_dim, const float* d_cls, int cls_dim,
@@ -177,22 +377,76 @@ extern "C" int mmre_generator_forward(const float* d_noise, int noise_dim, const
                                       int out1, const float* d_w2, const float* d_b2, float* d_u2, float* d_v2,
                                       int out2, const float* d_ln_a, const float* d_ln_b, float ln_eps,
                                       int power_iteration, float sn_eps, float* d_out, float* d_work, void* stream) {
-  if (!d_noise || !d_cls || !d_w0 || !d_b0 || !d_u0 || !d_v0 || !d_w1 || !d_b1 || !d_u1 || !d_v1 || !d_w2 || !d_b2 ||
-      !d_u2 || !d_v2 || !d_ln_a || !d_ln_b || !d_out || !d_work)
-    return MMRE_ERR_ARG;
-  const int in0 = noise_dim + cls_dim;
-  if (n_rows <= 0 || noise_dim < 0 || cls_dim <= 0 || out0 <= 0 || out1 <= 0 || out2 <= 0) return MMRE_ERR_ARG;
-  if (in0 > 1024 || out0 > 1024 || out1 > 1024 || out2 > out0 || (out1 | 1) > (in0 | 1)) return MMRE_ERR_SHAPE;
+  return mmre_generator_forward_save(d_noise, noise_dim, d_cls, cls_dim, n_rows, d_w0, d_b0, d_u0, d_v0, out0, d_w1,
+                                     d_b1, d_u1, d_v1, out1, d_w2, d_b2, d_u2, d_v2, out2, d_ln_a, d_ln_b, ln_eps,
+                                     power_iteration, sn_eps, d_out, d_work, nullptr, stream);
+}
+
+extern "C" int64_t mmre_generator_backward_workspace(int64_t n_rows, int in0, int out0, int out1, int out2) {
+  (void)in0;
+  return n_rows * (2 * (int64_t)out2 + out1 + out0);
+}
+
+extern "C" int mmre_generator_backward(const float* d_gout, int64_t n_rows, int in0, int out0, int out1, int out2,
+                                       const float* d_acts, const float* d_sigma, const float* d_w0,
+                                       const float* d_u0, const float* d_v0, const float* d_w1, const float* d_u1,
+                                       const float* d_v1, const float* d_w2, const float* d_u2, const float* d_v2,
+                                       const float* d_ln_a, float ln_eps, float* d_gw0, float* d_gb0, float* d_gw1,
+                                       float* d_gb1, float* d_gw2, float* d_gb2, float* d_gln_a, float* d_gln_b,
+                                       float* d_work, void* stream) {
+  const void* need[] = {d_gout, d_acts, d_sigma, d_w0, d_u0, d_v0, d_w1, d_u1, d_v1, d_w2, d_u2, d_v2, d_ln_a,
+                        d_gw0, d_gb0, d_gw1, d_gb1, d_gw2, d_gb2, d_gln_a, d_gln_b, d_work};
+  for (const void* p : need)
+    if (!p) return MMRE_ERR_ARG;
+  if (n_rows <= 0 || in0 <= 0 || out0 <= 0 || out1 <= 0 || out2 <= 0) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  float* sigma = d_work + 3 * 2048;
-  SNLayer l0{d_w0, d_u0, d_v0, out0, in0}, l1{d_w1, d_u1, d_v1, out1, out0}, l2{d_w2, d_u2, d_v2, out2, out1};
-  hipLaunchKernelGGL(k_sn_sigma, dim3(3), dim3(256), 0, st, l0, l1, l2, power_iteration, sn_eps, sigma, d_work);
+  const float* x0 = d_acts;
+  const float* h1 = x0 + n_rows * in0;
+  const float* h2 = h1 + n_rows * out0;
+  const float* h3 = h2 + n_rows * out1;
+  const float* wh0 = h3 + n_rows * out2;  // W_hat = W_orig / sigma of the forward
+  const float* wh1 = wh0 + (int64_t)out0 * in0;
+  const float* wh2 = wh1 + (int64_t)out1 * out0;
+  (void)wh0;
+  float* gz = d_work;                 // (N, out2)  dL/dh3
+  float* zhat = gz + n_rows * out2;   // (N, out2)
+  float* g2 = zhat + n_rows * out2;   // (N, out1)  dL/dh2
+  float* g1 = g2 + n_rows * out1;     // (N, out0)  dL/dh1
+  hipLaunchKernelGGL(k_gen_ln_bwd, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, st, d_gout, h3, d_ln_a, ln_eps,
+                     n_rows, out2, gz, zhat);
   MMRE_CHECK_LAUNCH();
-  const size_t lds = sizeof(float) * (size_t)GM * ((in0 | 1) + (out0 | 1));
-  if (lds > 160 * 1024) return MMRE_ERR_SHAPE;
-  const unsigned blocks = (unsigned)((n_rows + GM - 1) / GM);
-  hipLaunchKernelGGL(k_generator_mlp, dim3(blocks), dim3(256), lds, st, d_noise, noise_dim, d_cls, cls_dim, n_rows,
-                     d_w0, d_b0, out0, d_w1, d_b1, out1, d_w2, d_b2, out2, sigma, d_ln_a, d_ln_b, ln_eps, d_out);
-  MMRE_CHECK_LAUNCH();
+  auto colsum = [&](const float* A, const float* B, int width, float* out) -> int {
+    hipLaunchKernelGGL(k_colsum, dim3((unsigned)((width + 63) / 64)), dim3(1024), 0, st, A, B, n_rows, width, out);
+    MMRE_CHECK_LAUNCH();
+    return MMRE_OK;
+  };
+  int rc;
+  if (out2 == 1) {  // LayerNormalization is the identity: no a_2 / b_2 gradient
+    MMRE_CHECK(hipMemsetAsync(d_gln_a, 0, sizeof(float), st));
+    MMRE_CHECK(hipMemsetAsync(d_gln_b, 0, sizeof(float), st));
+  } else {
+    if ((rc = colsum(d_gout, zhat, out2, d_gln_a))) return rc;
+    if ((rc = colsum(d_gout, nullptr, out2, d_gln_b))) return rc;
+  }
+  auto sn = [&](float* G, const float* W, const float* u, const float* v, int layer, int o, int i) -> int {
+    hipLaunchKernelGGL(k_sn_grad, dim3(1), dim3(1024), 0, st, G, W, u, v, d_sigma + layer, o, i);
+    MMRE_CHECK_LAUNCH();
+    return MMRE_OK;
+  };
+  const int N = (int)n_rows;
+  // layer 2: h3 = h2 (W2/s2)^T + b2
+  if ((rc = colsum(gz, nullptr, out2, d_gb2))) return rc;
+  if ((rc = gemm(st, gz, 1, out2, h2, out1, 1, out2, out1, n_rows, nullptr, d_gw2))) return rc;   // gz^T h2
+  if ((rc = gemm(st, gz, out2, 1, wh2, out1, 1, N, out1, out2, nullptr, g2))) return rc;         // gz W_hat2
+  if ((rc = sn(d_gw2, d_w2, d_u2, d_v2, 2, out2, out1))) return rc;
+  // layer 1: h2 = h1 (W1/s1)^T + b1
+  if ((rc = colsum(g2, nullptr, out1, d_gb1))) return rc;
+  if ((rc = gemm(st, g2, 1, out1, h1, out0, 1, out1, out0, n_rows, nullptr, d_gw1))) return rc;
+  if ((rc = gemm(st, g2, out1, 1, wh1, out0, 1, N, out0, out1, nullptr, g1))) return rc;
+  if ((rc = sn(d_gw1, d_w1, d_u1, d_v1, 1, out1, out0))) return rc;
+  // layer 0: h1 = x0 (W0/s0)^T + b0 (no input gradient: noise and the frozen encoder's CLS)
+  if ((rc = colsum(g1, nullptr, out0, d_gb0))) return rc;
+  if ((rc = gemm(st, g1, 1, out0, x0, in0, 1, out0, in0, n_rows, nullptr, d_gw0))) return rc;
+  if ((rc = sn(d_gw0, d_w0, d_u0, d_v0, 0, out0, in0))) return rc;
   return MMRE_OK;
 }

@@ -46,6 +46,11 @@ SIGNATURES = {
     "mmre_generator_workspace": (I64, [I64, I32, I32, I32, I32]),
     "mmre_generator_forward": (I32, [P, I32, P, I32, I64, P, P, P, P, I32, P, P, P, P, I32, P, P, P, P, I32, P, P,
                                      F32, I32, F32, P, P, P]),
+    "mmre_generator_forward_save": (I32, [P, I32, P, I32, I64, P, P, P, P, I32, P, P, P, P, I32, P, P, P, P, I32,
+                                          P, P, F32, I32, F32, P, P, P, P]),
+    "mmre_generator_acts_size": (I64, [I64, I32, I32, I32, I32]),
+    "mmre_generator_backward_workspace": (I64, [I64, I32, I32, I32, I32]),
+    "mmre_generator_backward": (I32, [P, I64, I32, I32, I32, I32] + [P] * 12 + [F32] + [P] * 10),
     "mmre_candidate_rank_transe": (I32, [P, P, I32, P, P, I64, P, P, P, P, P]),
     "mmre_cosine_rank": (I32, [P, I32, P, I64, P, I32, P, P, P, P]),
     "mmre_extractor_pack_size": (I64, [I32]),

@@ -41,8 +41,20 @@ class RelationGenerator(nn.Module):
 
     def forward(self, cls: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
         """cls (N, reduced_dim), noise (N, noise_dim) -> (N, emb_dim). In training mode one
-        spectral-norm power iteration updates weight_u / weight_v in place first."""
+        spectral-norm power iteration updates weight_u / weight_v in place first. With autograd
+        recording and trainable parameters, the output carries the HIP backward
+        (mmre_generator_backward) to weight_orig / bias / layer-norm a, b."""
         require_cuda(cls, noise)
+        params = self._params()
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _GeneratorFn.apply(cls, noise, self, *params)
+        return self._run(cls, noise)
+
+    def _params(self):
+        L0, L1, L2 = self.generate_fc_layer, self.des_rel_map_layer1, self.des_rel_map_layer2
+        return [L0.weight_orig, L0.bias, L1.weight_orig, L1.bias, L2.weight_orig, L2.bias, self.ln_a, self.ln_b]
+
+    def _run(self, cls, noise, acts=None):
         n = int(cls.shape[0])
         L0, L1, L2 = self.generate_fc_layer, self.des_rel_map_layer1, self.des_rel_map_layer2
         dev = cls.device
@@ -56,14 +68,51 @@ class RelationGenerator(nn.Module):
         for L in (L0, L1, L2):
             if not (L.weight_u.is_contiguous() and L.weight_v.is_contiguous()):
                 raise ValueError("spectral-norm buffers must be contiguous")
-        call("mmre_generator_forward", ptr(noise_c), self.noise_dim, ptr(cls_c), self.reduced_dim, n,
+        call("mmre_generator_forward_save", ptr(noise_c), self.noise_dim, ptr(cls_c), self.reduced_dim, n,
              ptr(ws[0]), ptr(bs[0]), ptr(L0.weight_u), ptr(L0.weight_v), L0.out_features,
              ptr(ws[1]), ptr(bs[1]), ptr(L1.weight_u), ptr(L1.weight_v), L1.out_features,
              ptr(ws[2]), ptr(bs[2]), ptr(L2.weight_u), ptr(L2.weight_v), L2.out_features,
              ptr(c(self.ln_a)), ptr(c(self.ln_b)), float(self.ln_eps), int(self.training), float(L0.eps),
-             ptr(out), ptr(work), stream_ptr(dev))
+             ptr(out), ptr(work), ptr(acts), stream_ptr(dev))
+        if acts is not None:
+            return out, work[3 * 2048:3 * 2048 + 3].clone()
         return out
 
     def generate(self, cls: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
         """UnifiedModel.generate with the CLS already computed (model.py:679-686)."""
         return self.forward(cls, noise)
+
+
+class _GeneratorFn(torch.autograd.Function):
+    """Generator forward (training form: activations kept) + its HIP backward. u, v and sigma
+    are the values this forward used (cloned: a later forward updates u, v in place, as the
+    reference's spectral_norm.py:74-85 clones them for the same reason)."""
+
+    @staticmethod
+    def forward(ctx, cls, noise, gen, w0, b0, w1, b1, w2, b2, ln_a, ln_b):
+        n = int(cls.shape[0])
+        L0, L1, L2 = gen.generate_fc_layer, gen.des_rel_map_layer1, gen.des_rel_map_layer2
+        in0 = L0.in_features
+        acts = torch.empty(int(lib().mmre_generator_acts_size(n, in0, L0.out_features, L1.out_features,
+                                                              L2.out_features)), dtype=torch.float32, device=cls.device)
+        out, sigma = gen._run(cls, noise, acts=acts)
+        uv = [t.detach().clone() for L in (L0, L1, L2) for t in (L.weight_u, L.weight_v)]
+        ctx.gen_dims = (n, in0, L0.out_features, L1.out_features, L2.out_features, float(gen.ln_eps))
+        ctx.save_for_backward(acts, sigma, w0, w1, w2, ln_a, *uv)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        acts, sigma, w0, w1, w2, ln_a, u0, v0, u1, v1, u2, v2 = ctx.saved_tensors
+        n, in0, o0, o1, o2, eps = ctx.gen_dims
+        dev = gout.device
+        c = lambda t: t.detach().contiguous().float()
+        g = [torch.empty_like(w0), torch.empty(o0, device=dev), torch.empty_like(w1), torch.empty(o1, device=dev),
+             torch.empty_like(w2), torch.empty(o2, device=dev), torch.empty(o2, device=dev),
+             torch.empty(o2, device=dev)]
+        work = torch.empty(int(lib().mmre_generator_backward_workspace(n, in0, o0, o1, o2)), dtype=torch.float32,
+                           device=dev)
+        call("mmre_generator_backward", ptr(c(gout)), n, in0, o0, o1, o2, ptr(acts), ptr(sigma), ptr(c(w0)),
+             ptr(u0), ptr(v0), ptr(c(w1)), ptr(u1), ptr(v1), ptr(c(w2)), ptr(u2), ptr(v2), ptr(c(ln_a)), eps,
+             *[ptr(t) for t in g], ptr(work), stream_ptr(dev))
+        return (None, None, None, *g)

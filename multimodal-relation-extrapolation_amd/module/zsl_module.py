@@ -22,11 +22,12 @@ from collections import defaultdict
 import numpy as np
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from mmre._lib import MMREError
 from mmre.candidates import cosine_rank
 from mmre.extractor import ZSLRanker, _check_ids, encode, node_tables, pack_weights, targets
-from .submodule import SupportEncoder
+from .submodule import LayerNormalization, SupportEncoder
 
 
 class Extractor(nn.Module):
@@ -83,6 +84,29 @@ class Extractor(nn.Module):
     def update(self, embed):
         self.symbol_emb.weight.data.copy_(torch.as_tensor(np.asarray(embed), dtype=torch.float32))
         self.symbol_emb.weight.requires_grad = False
+
+
+class Discriminator(nn.Module):
+    """Discriminator (zsl_module.py:112-138): spectral-normalised fc_middle (d -> d, leaky_relu,
+    LayerNormalization) shared by the sample and the class centroids, spectral-normalised fc_TF
+    (d -> 1) for the WGAN critic, and class scores against the centroids. Same parameter and
+    buffer names (fc_middle.weight_orig / weight_u / weight_v / bias, fc_TF.*, layer_norm.a_2 /
+    b_2). Runs as torch-ROCm autograd on the device inside the GAN step's hipGraph
+    (mmre.gan): its double backward (the gradient penalty) is the reason it is not a fused
+    kernel."""
+
+    def __init__(self, dropout=0.3, dim=200):
+        super().__init__()
+        self.fc_middle = nn.utils.spectral_norm(nn.Linear(dim, dim))
+        self.fc_TF = nn.utils.spectral_norm(nn.Linear(dim, 1))
+        self.layer_norm = LayerNormalization(dim)
+
+    def forward(self, ep_vec, centroid_matrix):
+        middle_vec = self.layer_norm(F.leaky_relu(self.fc_middle(ep_vec)))
+        centroid_matrix = self.layer_norm(F.leaky_relu(self.fc_middle(centroid_matrix)))
+        logit_TF = self.fc_TF(middle_vec)
+        class_scores = torch.matmul(middle_vec, centroid_matrix.t())
+        return middle_vec, logit_TF, class_scores
 
 
 def weights_init(m):

@@ -25,7 +25,7 @@ def test_generator_matches_reference(golden, tag):
     out = gen(torch.from_numpy(g[f"{tag}_cls"]).to(dev), torch.from_numpy(g[f"{tag}_noise"]).to(dev))
     torch.cuda.synchronize()
     ref = g[f"{tag}_out"]
-    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-4 * max(1.0, np.abs(ref).max())
+    assert np.abs(out.detach().cpu().numpy() - ref).max() <= 1e-4 * max(1.0, np.abs(ref).max())
     for i, L in enumerate([gen.generate_fc_layer, gen.des_rel_map_layer1, gen.des_rel_map_layer2]):
         assert np.allclose(L.weight_u.cpu().numpy(), g[f"{tag}_u{i}_after"], atol=1e-5)
         assert np.allclose(L.weight_v.cpu().numpy(), g[f"{tag}_v{i}_after"], atol=1e-5)
