@@ -230,6 +230,75 @@ class ZSLEvaluator:
         return zsl_metrics(r, mode, per_relation=per_rel)
 
 
+def train_generate_decription(train_tasks, rel2candidates, e1rel_e2, ent2id, rel2id, rela2label, batch_size,
+                              gan_batch_rela, rng=None):
+    """Batch generator of ZSLmodule.train (module/utils.py:625-689) as id arrays: per batch,
+    gan_batch_rela shuffled train relations with > 20 candidates, batch_size query triples each
+    (with replacement when the relation has fewer), one false tail per query drawn from the
+    relation's candidates (known to ent2id, not a known tail of (head, rel), not the true tail).
+    Yields dict(rel, q_head, q_tail, f_head, f_tail, labels) of int64 numpy arrays: relation id
+    per row (the description row, utils.py:686), entity ids (ent2id) and label ids. Draws come
+    from `rng` (a random.Random; the reference uses the unseeded module-level `random`)."""
+    import random as _random
+    rng = rng if rng is not None else _random.Random()
+    pool = list(train_tasks.keys())
+    while True:
+        out = {k: [] for k in ("rel", "q_head", "q_tail", "f_head", "f_tail", "labels")}
+        rng.shuffle(pool)
+        for query in pool[:gan_batch_rela]:
+            cands = rel2candidates[query]
+            if len(cands) <= 20:
+                continue
+            triples = list(train_tasks[query])
+            rng.shuffle(triples)
+            if not triples:
+                continue
+            picked = ([rng.choice(triples) for _ in range(batch_size)] if len(triples) < batch_size
+                      else rng.sample(triples, batch_size))
+            for h, r, t in picked:
+                while True:
+                    noise = rng.choice(cands)
+                    if noise in ent2id and noise not in e1rel_e2[h + r] and noise != t:
+                        break
+                out["rel"].append(rel2id[query])
+                out["q_head"].append(ent2id[h])
+                out["q_tail"].append(ent2id[t])
+                out["f_head"].append(ent2id[h])
+                out["f_tail"].append(ent2id[noise])
+                out["labels"].append(rela2label[query])
+        yield {k: np.asarray(v, np.int64) for k, v in out.items()}
+
+
+def gan_train(step, batches, train_times, D_epoch=1, G_epoch=1, loss_every=50, device=None, graphs=True):
+    """The loop of ZSLmodule.train (zsl_module.py:417-609) over `batches` (an iterator of
+    train_generate_decription dicts) with a mmre.gan.ZSLGANStep; prints the reference's
+    'Epoch: ...' line every loss_every epochs. Each D / G step replays its hipGraph."""
+    from collections import deque
+    D_every, G_every = D_epoch * loss_every, G_epoch * loss_every
+    D_losses = deque([], D_every)
+    G_losses = deque([], G_every)
+    dev = device if device is not None else step.device
+    for epoch in range(train_times):
+        for _ in range(D_epoch):
+            b = {k: torch.as_tensor(v, device=dev) for k, v in next(batches).items()}
+            d = step.replay("d", b) if graphs else step.d_step(
+                b["rel"], b["q_head"], b["q_tail"], b["f_head"], b["f_tail"], b["labels"],
+                torch.randn(len(b["rel"]), step.G.noise_dim, device=dev), torch.rand(len(b["rel"]), 1, device=dev))
+            D_losses.append(d.detach().cpu().numpy().copy())
+        for _ in range(G_epoch):
+            b = {k: torch.as_tensor(v, device=dev) for k, v in next(batches).items()}
+            g = step.replay("g", b) if graphs else step.g_step(
+                b["rel"], b["q_head"], b["q_tail"], b["f_head"], b["f_tail"], b["labels"],
+                torch.randn(len(b["rel"]), step.G.noise_dim, device=dev))
+            G_losses.append(g.detach().cpu().numpy().copy())
+        if epoch % loss_every == 0 and epoch != 0:
+            Dm, Gm = np.mean(D_losses, 0), np.mean(G_losses, 0)
+            # D: loss, real, real-class, fake, fake-class; G: loss, fake, class, real-class, VP
+            print("Epoch: %d, D_loss: %.2f [%.2f, %.2f, %.2f, %.2f], G_loss: %.2f [%.2f, %.2f, %.2f, %.2f]"
+                  % (epoch, Dm[0], Dm[1], Dm[2], Dm[3], Dm[4], Gm[0], Gm[1], Gm[2], Gm[3], Gm[4]))
+    return step
+
+
 def zsl_rank(candidate_vecs, cand_off, relation_vecs, rel_of_query):
     return cosine_rank(candidate_vecs, cand_off, relation_vecs, rel_of_query)
 

@@ -49,3 +49,38 @@ def test_extractor_requires_eval_mode():
     ex.train()
     with pytest.raises(MMREError):
         ex.encode_pairs(torch.zeros((1, 2), dtype=torch.long), None)
+
+
+def test_gan_batch_generator_invariants():
+    """train_generate_decription (module/utils.py:625-689): batch layout, false tails drawn from
+    the relation's candidates, never a known tail of (head, rel) nor the true tail."""
+    import random
+    from module.zsl_module import train_generate_decription
+    g = make_graph(seed=6)
+    ents = g["ents"]
+    tasks = g["train_tasks"]
+    rng = random.Random(0)
+    rel2cands = {r: rng.sample(ents, 40) for r in tasks}
+    rel2cands[list(tasks)[0]] = ents[:10]  # <= 20 candidates: skipped like the reference
+    e1rel_e2 = {}
+    for r, tr in tasks.items():
+        for h, rr, t in tr:
+            e1rel_e2.setdefault(h + rr, []).append(t)
+    for h, rr, t in (x for tr in tasks.values() for x in tr):
+        e1rel_e2.setdefault(h + rr, [])
+    rela2label = {r: i for i, r in enumerate(sorted(tasks))}
+    gen = train_generate_decription(tasks, rel2cands, e1rel_e2, g["ent2id"], g["rel2id"], rela2label, 16, 2,
+                                    rng=random.Random(1))
+    inv = {i: e for e, i in g["ent2id"].items()}
+    inv_rel = {i: r for r, i in g["rel2id"].items()}
+    for _ in range(20):
+        b = next(gen)
+        n = len(b["rel"])
+        assert n in (0, 16, 32) and all(len(v) == n for v in b.values())
+        for i in range(n):
+            rel = inv_rel[int(b["rel"][i])]
+            h, t, f = inv[int(b["q_head"][i])], inv[int(b["q_tail"][i])], inv[int(b["f_tail"][i])]
+            assert b["f_head"][i] == b["q_head"][i] and rela2label[rel] == b["labels"][i]
+            assert [h, rel, t] in tasks[rel]
+            assert f in rel2cands[rel] and f != t and f not in e1rel_e2[h + rel]
+            assert len(rel2cands[rel]) > 20
