@@ -51,6 +51,10 @@ CONFIGS = {
     "gan": dict(dataset="FB15K-237-ZS", model="gan", dim=200, norm=False,
                 workload="ZSL GAN iteration FB15K-237-ZS (ZSLmodule.train, SURVEY 8(f) rank 3): 1 D step + 1 G step, "
                          "G_batch_size 256 x gan_batch_rela 2 = 512 rows, d=200, 206 seen-relation centroids"),
+    "m3ae": dict(dataset="FB15K-237-ZS", model="m3ae", dim=200, norm=False,
+                 workload="UnifiedModel.generate over the 235 FB15K-237-ZS relation descriptions x test_sample 20 "
+                          "(4,700 rows of 320 tokens): frozen M3AE-small text encoder (d 384, 12 blocks) + SN "
+                          "generator + LayerNormalization (SURVEY 8(f) rank 4)"),
 }
 MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 
@@ -459,6 +463,138 @@ def cpu_baseline_gan(w, centroids, n_lab, iters=3):
                       f"D/G steps), {el:.2f} s on {torch.get_num_threads()} threads"}
 
 
+def _generator_cpu(gen, cls, noise):
+    """UnifiedModel.generate's MLP on the host (model.py:680-685), eval mode: SN weights
+    W / (u . W v) (spectral_norm.py:87-89), three Linear layers, LayerNormalization with the
+    unbiased std (submodule.py:68-77)."""
+    import torch.nn.functional as F
+    x = torch.cat([noise, cls], 1)
+    for L in (gen.generate_fc_layer, gen.des_rel_map_layer1, gen.des_rel_map_layer2):
+        W = L.weight_orig.detach().cpu()
+        sigma = torch.dot(L.weight_u.cpu(), torch.mv(W, L.weight_v.cpu()))
+        x = F.linear(x, W / sigma, L.bias.detach().cpu())
+    mu, sd = x.mean(-1, keepdim=True), x.std(-1, keepdim=True)
+    return (x - mu.expand_as(x)) / (sd.expand_as(x) + gen.ln_eps) * gen.ln_a.detach().cpu() + gen.ln_b.detach().cpu()
+
+
+def cpu_baseline_m3ae(enc, gen, w, budget_s: float = 15.0):
+    """The reference's generate() on the host cores, relation by relation as ZSLmodule.eval calls
+    it (zsl_module.py:662-667): test_sample rows of the 320-token description through the M3AE
+    encoder over the full padded sequence (oracle/m3ae_text.py, torch CPU fp32) + the generator
+    MLP, until the time budget."""
+    import m3ae_text as om
+    sd = {k: v.detach().cpu() for k, v in enc.state_dict().items()}
+    S = w["test_sample"]
+    g = torch.Generator().manual_seed(0)
+    rows, r = 0, 0
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        while r < w["tok"].shape[0] and time.perf_counter() - t0 < budget_s:
+            tok = w["tok"][r:r + 1].repeat(S, 1)
+            msk = w["mask"][r:r + 1].repeat(S, 1)
+            cls, _ = om.forward_representation_text(sd, tok, msk, enc.num_heads)
+            _generator_cpu(gen, cls[:, 0], 0.1 * torch.randn(S, 15, generator=g))
+            rows += S
+            r += 1
+    el = time.perf_counter() - t0
+    return {"value": rows / el, "unit": "relation embeddings/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"first {r} FB15K-237-ZS relation descriptions x {S} rows ({rows} rows of 320 tokens) through "
+                      f"M3AE-small forward_representation over the padded rows + generator MLP (oracle/m3ae_text.py, "
+                      f"torch {torch.__version__} CPU fp32), {el:.2f} s on {torch.get_num_threads()} threads"}
+
+
+def bench_m3ae(args, world, rank, dev, dist):
+    """One step = UnifiedModel.generate (model.py:674-686) for every FB15K-237-ZS relation
+    description x test_sample 20 (the ZSLmodule.eval expansion, zsl_module.py:662-666): 4,700
+    description rows of 320 tokens -> row dedupe + padding-free HIP M3AE-small encoder -> CLS
+    (N, 384) -> SN generator + LayerNormalization (HIP) -> (N, 200), D2H. N > 1: descriptions
+    round-robin over ranks (independent rows, no collective)."""
+    from mmre._lib import call, ptr, stream_ptr
+    from mmre.generator import RelationGenerator
+    from mmre.m3ae import M3AETextEncoder, dedupe_rows
+    from mmre.workloads import description_workload
+    w = description_workload()
+    R = int(w["tok"].shape[0])
+    S = w["test_sample"]
+    mine = np.arange(rank, R, world)
+    torch.manual_seed(0)
+    enc = M3AETextEncoder(w["vocab"], model_type="small").to(dev)
+    gen = RelationGenerator(384, 15, 200).to(dev).eval()
+    tok = w["tok"][mine].repeat_interleave(S, 0).to(dev)
+    msk = w["mask"][mine].repeat_interleave(S, 0).to(dev)
+    n = int(tok.shape[0])
+    noise = 0.1 * torch.randn(n, 15, device=dev)
+    host = torch.empty((n, 200), pin_memory=True)
+
+    def step():
+        with torch.no_grad():
+            out = gen(enc.encode(tok, msk), noise)
+        host.copy_(out, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    # roofline: the dominant kernel, fc1 (+GELU) of a block over the packed rows, timed alone
+    u, m, _ = dedupe_rows(tok, msk)
+    packed = int((m <= 0).sum().item()) + int(u.shape[0])
+    d, hid = enc.emb_dim, 4 * enc.emb_dim
+    A = torch.randn(packed, d, device=dev)
+    fc1 = enc.encoder.blocks[0].transformer_mlp.fc1
+    Hout = torch.empty(packed, hid, device=dev)
+    st = stream_ptr(dev)
+    launch = lambda: call("mmre_m3ae_linear", 1, ptr(A), packed, d, ptr(fc1.weight), hid, ptr(fc1.bias), None,
+                          ptr(Hout), st)
+    for _ in range(3):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 50
+    e0.record()
+    for _ in range(reps):
+        launch()
+    e1.record()
+    torch.cuda.synchronize()
+    k_ms = e0.elapsed_time(e1) / reps
+    flops = 2.0 * packed * d * hid
+    ach = flops / (k_ms * 1e-3) / 1e12
+    if rank == 0:
+        out = {"metric": f"relation embeddings generated/sec, {CONFIGS['m3ae']['workload']}",
+               "value": R * S * args.steps / elapsed, "unit": "relation embeddings/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+               "data": "real FB15K-237-ZS relation-description lengths (synthetic token ids: no BERT vocabulary "
+                       "offline), random-init M3AE-small encoder and generator",
+               "config": {"workload": CONFIGS["m3ae"]["workload"], "descriptions": R, "rows": R * S,
+                          "tokens_per_row": int(w["tok"].shape[1]), "packed_rows_per_rank0": packed,
+                          "parallelism": f"descriptions round-robin x{world}, no collective"},
+               "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
+                            "frac": ach * 1e12 / MFMA_F32_PEAK, "traffic": None,
+                            "kernel": "k_m3ae_linear<1>", "kernel_ms": k_ms, "shape": [packed, d, hid],
+                            "flops_per_launch": flops,
+                            "note": "fc1+GELU of one block over the packed (unpadded) rows of the unique "
+                                    "descriptions; the reference's padded rows and repeated descriptions are "
+                                    "never computed"}}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline_m3ae(enc, gen, w)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -490,6 +626,8 @@ def main():
         return bench_zsl(args, world, rank, dev, dist)
     if args.config == "gan":
         return bench_gan(args, world, rank, dev, dist)
+    if args.config == "m3ae":
+        return bench_m3ae(args, world, rank, dev, dist)
     if cfg["dataset"] == "synthetic-1M":
         w = synthetic_large()
     else:

@@ -312,6 +312,51 @@ int mmre_extractor_targets(const float* d_vecs, int64_t n_sets, int n_samples, i
  * 1 + #(score > score[first]) (zsl_module.py:705-706, tie-free inputs). */
 int mmre_rank_desc(const float* d_scores, const int64_t* d_off, int64_t n_query, int32_t* d_rank, void* stream);
 
+/* ====================================================================== *
+ *  Frozen M3AE text encoder: the producer of the generator's CLS input.   *
+ *  Replaces MaskedMultimodalAutoencoder.forward_representation(image=None,*
+ *  text, text_padding_mask, deterministic=True) (module/model.py:323-356) *
+ *  over Transformer/Block/Attention/TransformerMLP (module/submodule.py:  *
+ *  128-238), as called by UnifiedModel.generate (model.py:674-679) and    *
+ *  forward_relation_emb (model.py:599-604). Only the CLS row is returned. *
+ *  Padded tokens (mask > 0) and, in the last block, non-CLS rows are not  *
+ *  computed: they cannot reach the CLS output (masked logit -1e7 has      *
+ *  softmax weight exactly 0). d in {384, 768, 1024, 1280}, head dim 64/80,*
+ *  len <= mmre_m3ae_max_len().                                            *
+ * ====================================================================== */
+
+/* Longest description row (tokens) the encoder accepts. */
+int mmre_m3ae_max_len(void);
+/* d_off[0] = 0, d_off[b+1] = d_off[b] + 1 + #{p : !(d_mask[b][p] > 0)}: the packed row range
+ * [d_off[b], d_off[b+1]) of sequence b (CLS row first). d_mask (n_seq, len) float32. */
+int mmre_m3ae_rows(const float* d_mask, int64_t n_seq, int64_t len, int32_t* d_off, void* stream);
+/* Floats of the workspace mmre_m3ae_encode needs for n_rows = d_off[n_seq] packed rows. */
+int64_t mmre_m3ae_workspace(int64_t n_rows, int64_t n_seq, int d);
+/* CLS vectors d_cls (n_seq, d) of the description rows d_tokens (n_seq, len) int32 /
+ * d_mask (n_seq, len) float32 (> 0 = padding, module/data.py:252-270). h_params: HOST array
+ * of 4 + 12 * depth + 2 DEVICE pointers, fp32 row-major as in the reference state dict:
+ *   text_embedding.weight (vocab, d), the sin-cos position table (>= len, d)
+ *   (get_1d_sincos_pos_embed, model.py:113-133), encoder_text_type_embedding (d), cls_token (d);
+ *   per block i: layer_norm1.{weight,bias}, attention.qkv_linear.{weight (3d, d), bias},
+ *   attention.fc.{weight, bias}, layer_norm2.{weight,bias}, transformer_mlp.fc1.{weight (4d, d),
+ *   bias}, transformer_mlp.fc2.{weight (d, 4d), bias};
+ *   encoder.layer_norm.{weight, bias}.
+ * d_off / n_rows / max_rows: from mmre_m3ae_rows (max_rows = largest per-sequence row count). */
+int mmre_m3ae_encode(const float* const* h_params, int depth, int d, int heads, float ln_eps,
+                     const int32_t* d_tokens, const float* d_mask, int64_t n_seq, int64_t len, int64_t vocab,
+                     const int32_t* d_off, int64_t n_rows, int max_rows, float* d_work, int64_t work_floats,
+                     float* d_cls, void* stream);
+/* The encoder's building blocks (also exported for tests): nn.LayerNorm over rows;
+ * out = a w^T + bias (epilogue 0), GELU(.) (1, F.gelu erf form), resid + (.) (2; resid may
+ * alias out), n % 128 == 0, k % 32 == 0; packed multi-head attention over d_off sequences
+ * (qkv rows [q | k | v]; cls_only: query row 0 of each sequence only, written to out row b). */
+int mmre_m3ae_layernorm(const float* d_x, int64_t n_rows, int d, const float* d_w, const float* d_b, float eps,
+                        float* d_y, void* stream);
+int mmre_m3ae_linear(int epilogue, const float* d_a, int64_t m, int k, const float* d_w, int n, const float* d_bias,
+                     const float* d_resid, float* d_out, void* stream);
+int mmre_m3ae_attention(const float* d_qkv, const int32_t* d_off, int64_t n_seq, int max_rows, int heads,
+                        int head_dim, float scale, int cls_only, float* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

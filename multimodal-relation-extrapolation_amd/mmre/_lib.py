@@ -59,6 +59,13 @@ SIGNATURES = {
     "mmre_extractor_encode": (I32, [I32, P, F32, P, P, P, P, I64, P, P, I32, P, P, P]),
     "mmre_extractor_targets": (I32, [P, I64, I32, I32, I32, P, P]),
     "mmre_rank_desc": (I32, [P, P, I64, P, P]),
+    "mmre_m3ae_max_len": (I32, []),
+    "mmre_m3ae_rows": (I32, [P, I64, I64, P, P]),
+    "mmre_m3ae_workspace": (I64, [I64, I64, I32]),
+    "mmre_m3ae_encode": (I32, [P, I32, I32, I32, F32, P, P, I64, I64, I64, P, I64, I32, P, I64, P, P]),
+    "mmre_m3ae_layernorm": (I32, [P, I64, I32, P, P, F32, P, P]),
+    "mmre_m3ae_linear": (I32, [I32, P, I64, I32, P, I32, P, P, P, P]),
+    "mmre_m3ae_attention": (I32, [P, P, I64, I32, I32, I32, F32, I32, P, P]),
 }
 
 ERRORS = {1: "bad argument", 2: "unknown model", 3: "unsupported shape", 4: "workspace too small"}

@@ -55,9 +55,35 @@ def convert_candidates(name, out):
     print(name, "candidate pools", ids.shape, "unmapped", int((ids < 0).sum()))
 
 
+def convert_descriptions(name, out, max_len=320, vocab=30522, first_id=1000):
+    """rel_description_zsl (one description per relation id, the rel_des_file that
+    MMKGDataset.generate_batch indexes by relation, module/data.py:274, 301-304) as synthetic
+    token rows: the BERT tokenizer (module/data.py:256-263, add_special_tokens=False,
+    padding='max_length', truncation at unpaired_tokenizer_max_length = 320) is not available
+    offline, so each description is split the way BERT's basic tokenizer splits (lower case,
+    words and single punctuation marks) and every piece gets a stable id in [first_id, vocab).
+    Lengths are therefore the pre-token counts (WordPiece can only add pieces). Writes tok
+    (R, max_len) int32 with 0 on padded positions and n_tok (R,) int32."""
+    import re
+    import zlib
+    d = os.path.join(SRC, name)
+    lines = open(os.path.join(d, "rel_description_zsl")).read().splitlines()
+    tok = np.zeros((len(lines), max_len), np.int32)
+    n_tok = np.zeros(len(lines), np.int32)
+    for i, line in enumerate(lines):
+        pieces = re.findall(r"\w+|[^\w\s]", line.lower())[:max_len]
+        ids = [first_id + zlib.crc32(p.encode()) % (vocab - first_id) for p in pieces]
+        tok[i, :len(ids)] = ids
+        n_tok[i] = len(ids)
+    np.savez_compressed(os.path.join(OUT, out), tok=tok, n_tok=n_tok, vocab=np.array(vocab))
+    print(name, "descriptions", len(lines), "tokens min/mean/max", n_tok.min(), round(float(n_tok.mean()), 1),
+          n_tok.max())
+
+
 if __name__ == "__main__":
     if not os.path.isdir(SRC):
         sys.exit("reference data not available")
     convert("FB15K-237-ZS", "fb15k237zs_test.npz")
     convert("DB15K-ZS", "db15kzs_test.npz")
     convert_candidates("FB15K-237-ZS", "fb15k237zs_cands.npz")
+    convert_descriptions("FB15K-237-ZS", "fb15k237zs_desc.npz")

@@ -140,3 +140,16 @@ def zsl_workload(dim: int = 200, max_nb: int = 50, test_sample: int = 20, n_trai
                 deg=deg, cand_head=np.concatenate(heads), cand_tail=np.concatenate(tails),
                 off=np.asarray(off, np.int64), query_set=np.asarray(qset, np.int64), query_rel=r,
                 rel_vecs=rel_vecs, max_nb=max_nb, test_sample=test_sample)
+
+
+def description_workload(test_sample: int = 20):
+    """The 235 FB15K-237-ZS relation descriptions as 320-token rows (mmre/datasets/
+    fb15k237zs_desc.npz, written by convert_zs.convert_descriptions: real description lengths,
+    synthetic token ids since the BERT vocabulary is not available offline), padded like
+    MMKGDataset._text_prepro (module/data.py:252-270: mask 1.0 on padded positions), and the
+    ZSLmodule.eval expansion of each description to test_sample rows (zsl_module.py:662-666)."""
+    with np.load(os.path.join(DATASETS_DIR, "fb15k237zs_desc.npz"), allow_pickle=False) as z:
+        tok, n_tok, vocab = z["tok"], z["n_tok"], int(z["vocab"])
+    mask = (np.arange(tok.shape[1])[None, :] >= n_tok[:, None]).astype(np.float32)
+    return dict(tok=torch.from_numpy(tok), mask=torch.from_numpy(mask), n_tok=n_tok, vocab=vocab,
+                test_sample=test_sample)
