@@ -509,9 +509,10 @@ def bench_m3ae(args, world, rank, dev, dist):
     description rows of 320 tokens -> row dedupe + padding-free HIP M3AE-small encoder -> CLS
     (N, 384) -> SN generator + LayerNormalization (HIP) -> (N, 200), D2H. N > 1: descriptions
     round-robin over ranks (independent rows, no collective)."""
-    from mmre._lib import call, ptr, stream_ptr
+    from mmre._lib import call, lib, ptr, stream_ptr
     from mmre.generator import RelationGenerator
-    from mmre.m3ae import M3AETextEncoder, dedupe_rows
+    _lib_m3ae_plan_size = lib().mmre_m3ae_plan_size
+    from mmre.m3ae import M3AETextEncoder
     from mmre.workloads import description_workload
     w = description_workload()
     R = int(w["tok"].shape[0])
@@ -550,8 +551,9 @@ def bench_m3ae(args, world, rank, dev, dist):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # roofline: the dominant kernel, fc1 (+GELU) of a block over the packed rows, timed alone
-    u, m, _ = dedupe_rows(tok, msk)
-    packed = int((m <= 0).sum().item()) + int(u.shape[0])
+    plan = torch.empty(int(_lib_m3ae_plan_size(n)), dtype=torch.int32, device=dev)
+    call("mmre_m3ae_plan", ptr(tok), ptr(msk), n, int(tok.shape[1]), 1, w["vocab"], ptr(plan), stream_ptr(dev))
+    n_unique, packed = (int(v) for v in plan[3 * n + 1:3 * n + 3].cpu())
     d, hid = enc.emb_dim, 4 * enc.emb_dim
     A = torch.randn(packed, d, device=dev)
     fc1 = enc.encoder.blocks[0].transformer_mlp.fc1
@@ -579,7 +581,8 @@ def bench_m3ae(args, world, rank, dev, dist):
                "data": "real FB15K-237-ZS relation-description lengths (synthetic token ids: no BERT vocabulary "
                        "offline), random-init M3AE-small encoder and generator",
                "config": {"workload": CONFIGS["m3ae"]["workload"], "descriptions": R, "rows": R * S,
-                          "tokens_per_row": int(w["tok"].shape[1]), "packed_rows_per_rank0": packed,
+                          "tokens_per_row": int(w["tok"].shape[1]), "unique_descriptions_rank0": n_unique,
+                          "packed_rows_rank0": packed,
                           "parallelism": f"descriptions round-robin x{world}, no collective"},
                "roofline": {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
                             "frac": ach * 1e12 / MFMA_F32_PEAK, "traffic": None,

@@ -321,19 +321,26 @@ int mmre_rank_desc(const float* d_scores, const int64_t* d_off, int64_t n_query,
  *  forward_relation_emb (model.py:599-604). Only the CLS row is returned. *
  *  Padded tokens (mask > 0) and, in the last block, non-CLS rows are not  *
  *  computed: they cannot reach the CLS output (masked logit -1e7 has      *
- *  softmax weight exactly 0). d in {384, 768, 1024, 1280}, head dim 64/80,*
- *  len <= mmre_m3ae_max_len().                                            *
+ *  softmax weight exactly 0); a row equal to the previous row on its      *
+ *  unpadded tokens is encoded once. d in {384, 768, 1024, 1280}, head dim *
+ *  64 or 80, len <= mmre_m3ae_max_len().                                  *
  * ====================================================================== */
 
 /* Longest description row (tokens) the encoder accepts. */
 int mmre_m3ae_max_len(void);
-/* d_off[0] = 0, d_off[b+1] = d_off[b] + 1 + #{p : !(d_mask[b][p] > 0)}: the packed row range
- * [d_off[b], d_off[b+1]) of sequence b (CLS row first). d_mask (n_seq, len) float32. */
-int mmre_m3ae_rows(const float* d_mask, int64_t n_seq, int64_t len, int32_t* d_off, void* stream);
-/* Floats of the workspace mmre_m3ae_encode needs for n_rows = d_off[n_seq] packed rows. */
-int64_t mmre_m3ae_workspace(int64_t n_rows, int64_t n_seq, int d);
-/* CLS vectors d_cls (n_seq, d) of the description rows d_tokens (n_seq, len) int32 /
- * d_mask (n_seq, len) float32 (> 0 = padding, module/data.py:252-270). h_params: HOST array
+/* Int32 elements of the plan buffer for n_seq rows (6 n_seq + 5). */
+int64_t mmre_m3ae_plan_size(int64_t n_seq);
+/* Plan of an encode: per input row of d_tokens (n_seq, len) int32 / d_mask (n_seq, len) float32
+ * (> 0 = padding, module/data.py:252-270): uniq[b] (the unique sequence it maps to; a row equal
+ * to row b-1 on its padding pattern and unpadded tokens shares b-1's when dedupe != 0), the
+ * unique sequences' source rows and packed row offsets (1 + unpadded tokens each, CLS row
+ * first), and at d_plan[3 n_seq + 1 ..] info = {n_unique, n_rows, max_rows, unpadded token ids
+ * outside [0, vocab)}. The host reads info (4 ints) to size the encode. */
+int mmre_m3ae_plan(const int32_t* d_tokens, const float* d_mask, int64_t n_seq, int64_t len, int dedupe,
+                   int64_t vocab, int32_t* d_plan, void* stream);
+/* Floats of the workspace mmre_m3ae_encode needs for info's n_rows / n_unique. */
+int64_t mmre_m3ae_workspace(int64_t n_rows, int64_t n_unique, int d);
+/* CLS vectors d_cls (n_seq, d) of the description rows planned by mmre_m3ae_plan. h_params: HOST array
  * of 4 + 12 * depth + 2 DEVICE pointers, fp32 row-major as in the reference state dict:
  *   text_embedding.weight (vocab, d), the sin-cos position table (>= len, d)
  *   (get_1d_sincos_pos_embed, model.py:113-133), encoder_text_type_embedding (d), cls_token (d);
@@ -341,14 +348,14 @@ int64_t mmre_m3ae_workspace(int64_t n_rows, int64_t n_seq, int d);
  *   attention.fc.{weight, bias}, layer_norm2.{weight,bias}, transformer_mlp.fc1.{weight (4d, d),
  *   bias}, transformer_mlp.fc2.{weight (d, 4d), bias};
  *   encoder.layer_norm.{weight, bias}.
- * d_off / n_rows / max_rows: from mmre_m3ae_rows (max_rows = largest per-sequence row count). */
+ * n_unique / n_rows / max_rows: the plan's info. */
 int mmre_m3ae_encode(const float* const* h_params, int depth, int d, int heads, float ln_eps,
                      const int32_t* d_tokens, const float* d_mask, int64_t n_seq, int64_t len, int64_t vocab,
-                     const int32_t* d_off, int64_t n_rows, int max_rows, float* d_work, int64_t work_floats,
-                     float* d_cls, void* stream);
+                     const int32_t* d_plan, int64_t n_unique, int64_t n_rows, int max_rows, float* d_work,
+                     int64_t work_floats, float* d_cls, void* stream);
 /* The encoder's building blocks (also exported for tests): nn.LayerNorm over rows;
  * out = a w^T + bias (epilogue 0), GELU(.) (1, F.gelu erf form), resid + (.) (2; resid may
- * alias out), n % 128 == 0, k % 32 == 0; packed multi-head attention over d_off sequences
+ * alias out), n % 64 == 0, k % 32 == 0; packed multi-head attention over d_off sequences
  * (qkv rows [q | k | v]; cls_only: query row 0 of each sequence only, written to out row b). */
 int mmre_m3ae_layernorm(const float* d_x, int64_t n_rows, int d, const float* d_w, const float* d_b, float eps,
                         float* d_y, void* stream);

@@ -60,9 +60,10 @@ SIGNATURES = {
     "mmre_extractor_targets": (I32, [P, I64, I32, I32, I32, P, P]),
     "mmre_rank_desc": (I32, [P, P, I64, P, P]),
     "mmre_m3ae_max_len": (I32, []),
-    "mmre_m3ae_rows": (I32, [P, I64, I64, P, P]),
+    "mmre_m3ae_plan_size": (I64, [I64]),
+    "mmre_m3ae_plan": (I32, [P, P, I64, I64, I32, I64, P, P]),
     "mmre_m3ae_workspace": (I64, [I64, I64, I32]),
-    "mmre_m3ae_encode": (I32, [P, I32, I32, I32, F32, P, P, I64, I64, I64, P, I64, I32, P, I64, P, P]),
+    "mmre_m3ae_encode": (I32, [P, I32, I32, I32, F32, P, P, I64, I64, I64, P, I64, I64, I32, P, I64, P, P]),
     "mmre_m3ae_layernorm": (I32, [P, I64, I32, P, P, F32, P, P]),
     "mmre_m3ae_linear": (I32, [I32, P, I64, I32, P, I32, P, P, P, P]),
     "mmre_m3ae_attention": (I32, [P, P, I64, I32, I32, I32, F32, I32, P, P]),

@@ -9,10 +9,10 @@ loads with ``load_reference_state_dict`` (image / decoder tensors are ignored).
 
 The encoder runs padding-free: only the CLS row and the unpadded tokens of each description
 are computed (a padded key's logit is -1e7, its softmax weight exactly 0, and every other op
-is row-wise), and the last block runs on the CLS rows alone. Identical description rows (the
-reference repeats one description test_sample / G_batch_size times, zsl_module.py:662-665,
-utils.py:686) are encoded once: the frozen encoder is a deterministic function of the
-unpadded tokens, so deduplication is exact. There is no fallback: without libmmre_hip.so every
+is row-wise), and the last block runs on the CLS rows alone. A description row equal to the
+previous one (the reference repeats one description test_sample / G_batch_size times,
+zsl_module.py:662-665, utils.py:686) is encoded once: the frozen encoder is a deterministic
+function of the unpadded tokens, so deduplication is exact. There is no fallback: without libmmre_hip.so every
 call raises.
 """
 from __future__ import annotations
@@ -39,15 +39,6 @@ def sincos_pos_embed_1d(embed_dim: int, length: int) -> torch.Tensor:
     pos = torch.arange(length, dtype=torch.float32).view(-1)
     out = torch.einsum("m,d->md", pos, omega)
     return torch.cat([torch.sin(out), torch.cos(out)], dim=1)
-
-
-def dedupe_rows(text: torch.Tensor, text_padding_mask: torch.Tensor):
-    """Unique description rows up to padding: a row is the sequence of (position, token) of its
-    unpadded entries (mask > 0 is padding, submodule.py:177). Returns (tokens int32, mask f32,
-    inverse) with tokens[inverse] == the input rows on every unpadded position."""
-    key = torch.where(text_padding_mask > 0, torch.full_like(text, -1, dtype=torch.int64), text.to(torch.int64))
-    uniq, inv = torch.unique(key, dim=0, return_inverse=True)
-    return uniq.clamp_min(0).to(torch.int32).contiguous(), (uniq < 0).to(torch.float32).contiguous(), inv
 
 
 class _Attention(nn.Module):  # submodule.py:148-162, use_bias=True (Block, :199)
@@ -141,44 +132,34 @@ class M3AETextEncoder(nn.Module):
     @torch.no_grad()
     def encode(self, text: torch.Tensor, text_padding_mask: torch.Tensor, dedupe: bool = True) -> torch.Tensor:
         """CLS vectors (B, D) of description rows text (B, L) int token ids and
-        text_padding_mask (B, L) float (> 0 = padding)."""
+        text_padding_mask (B, L) float (> 0 = padding). dedupe: a row equal to the previous row
+        on its unpadded tokens reuses that row's CLS (exact; the reference's repeats are
+        adjacent, zsl_module.py:662-665)."""
         require_cuda(text, text_padding_mask)
         if text.dim() != 2 or tuple(text_padding_mask.shape) != tuple(text.shape):
             raise ValueError("text and text_padding_mask must both be (B, L)")
         B, L = (int(s) for s in text.shape)
         if L > int(lib().mmre_m3ae_max_len()):
             raise MMREError(f"description rows of {L} tokens exceed the encoder's {lib().mmre_m3ae_max_len()}")
+        dev = text.device
         if B == 0:
-            return torch.empty((0, self.emb_dim), dtype=torch.float32, device=text.device)
-        mask = text_padding_mask.to(torch.float32)
-        valid = ~(mask > 0)
-        bad = valid & ((text < 0) | (text >= self.text_vocab_size))
-        if bool(bad.any()):
-            raise MMREError("token id outside [0, text_vocab_size) on an unpadded position")
-        if dedupe and B > 1:
-            tok, msk, inv = dedupe_rows(text, mask)
-        else:
-            tok, msk, inv = text.to(torch.int32).contiguous(), mask.contiguous(), None
-        cls = self.encode_unique(tok, msk)
-        return cls if inv is None else cls.index_select(0, inv)
-
-    def encode_unique(self, tok: torch.Tensor, msk: torch.Tensor) -> torch.Tensor:
-        """One mmre_m3ae_rows + mmre_m3ae_encode pass over already-validated rows."""
-        S, L = (int(s) for s in tok.shape)
-        dev = tok.device
+            return torch.empty((0, self.emb_dim), dtype=torch.float32, device=dev)
+        tok = text.to(torch.int32).contiguous()
+        msk = text_padding_mask.to(torch.float32).contiguous()
         st = stream_ptr(dev)
-        off = torch.empty(S + 1, dtype=torch.int32, device=dev)
-        call("mmre_m3ae_rows", ptr(msk), S, L, ptr(off), st)
-        off_h = off.cpu()  # sizes the packed rows (one D2H of S + 1 ints)
-        n_rows = int(off_h[-1])
-        max_rows = int((off_h[1:] - off_h[:-1]).max())
-        work = torch.empty(int(lib().mmre_m3ae_workspace(n_rows, S, self.emb_dim)), dtype=torch.float32, device=dev)
-        out = torch.empty((S, self.emb_dim), dtype=torch.float32, device=dev)
+        plan = torch.empty(int(lib().mmre_m3ae_plan_size(B)), dtype=torch.int32, device=dev)
+        call("mmre_m3ae_plan", ptr(tok), ptr(msk), B, L, int(bool(dedupe)), self.text_vocab_size, ptr(plan), st)
+        n_unique, n_rows, max_rows, n_bad = (int(v) for v in plan[3 * B + 1:3 * B + 5].cpu())  # sizes the encode
+        if n_bad:
+            raise MMREError(f"{n_bad} token ids outside [0, text_vocab_size) on unpadded positions")
+        work = torch.empty(int(lib().mmre_m3ae_workspace(n_rows, n_unique, self.emb_dim)), dtype=torch.float32,
+                           device=dev)
+        out = torch.empty((B, self.emb_dim), dtype=torch.float32, device=dev)
         params = self.param_list(L, dev)
         arr = (ctypes.c_void_p * len(params))(*[t.data_ptr() for t in params])
         call("mmre_m3ae_encode", ctypes.cast(arr, ctypes.c_void_p), self.depth, self.emb_dim, self.num_heads, LN_EPS,
-             ptr(tok), ptr(msk), S, L, self.text_vocab_size, ptr(off), n_rows, max_rows, ptr(work), work.numel(),
-             ptr(out), st)
+             ptr(tok), ptr(msk), B, L, self.text_vocab_size, ptr(plan), n_unique, n_rows, max_rows, ptr(work),
+             work.numel(), ptr(out), st)
         return out
 
     def forward(self, text, text_padding_mask):

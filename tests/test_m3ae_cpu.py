@@ -1,5 +1,5 @@
 """CPU checks of the M3AE text-encoder path: the host pieces (position
-table, row deduplication, reference parameter names, state-dict loading), the oracle's padding
+table, reference parameter names, state-dict loading), the oracle's padding
 invariances -- the property the padding-free HIP path relies on -- and the C ABI exports and
 argument checks (nothing is launched)."""
 import ctypes
@@ -69,19 +69,6 @@ def test_load_reference_state_dict_ignores_decoder():
         other.load_reference_state_dict(full)
 
 
-def test_dedupe_rows_ignores_padded_positions():
-    from mmre.m3ae import dedupe_rows
-    tok = torch.tensor([[5, 6, 7, 9], [5, 6, 1, 2], [5, 6, 7, 3], [4, 6, 7, 9]], dtype=torch.int32)
-    msk = torch.tensor([[0, 0, 0, 1], [0, 0, 1, 1], [0, 0, 0, 1], [0, 0, 0, 1]], dtype=torch.float32)
-    u, m, inv = dedupe_rows(tok, msk)
-    assert u.shape[0] == 3  # rows 0 and 2 differ only on a padded position
-    assert inv[0] == inv[2] and len({int(inv[0]), int(inv[1]), int(inv[3])}) == 3
-    for b in range(4):
-        valid = msk[b] <= 0
-        assert torch.equal(m[inv[b]], msk[b])
-        assert torch.equal(u[inv[b]][valid], tok[b][valid])
-
-
 def test_oracle_padding_is_inert():
     """What the padding-free HIP path relies on: the CLS output does not depend on the token ids
     at padded positions (bit-identical: their softmax weights are exactly 0), and a right-padded
@@ -107,7 +94,7 @@ def test_oracle_padding_is_inert():
 def test_m3ae_c_abi_exports_and_argument_checks():
     from mmre import _lib
     L = ctypes.CDLL(_lib.LIB_PATH)
-    for n in ("mmre_m3ae_max_len", "mmre_m3ae_rows", "mmre_m3ae_workspace", "mmre_m3ae_encode",
+    for n in ("mmre_m3ae_max_len", "mmre_m3ae_plan_size", "mmre_m3ae_plan", "mmre_m3ae_workspace", "mmre_m3ae_encode",
               "mmre_m3ae_layernorm", "mmre_m3ae_linear", "mmre_m3ae_attention"):
         assert hasattr(L, n)
     lib = _lib.lib()
@@ -116,15 +103,18 @@ def test_m3ae_c_abi_exports_and_argument_checks():
     dummy = ctypes.c_void_p(16)
     # shape / argument errors come back as status codes before any launch
     assert lib.mmre_m3ae_linear(0, dummy, 10, 100, dummy, 384, dummy, None, dummy, None) == 3  # k % 32
-    assert lib.mmre_m3ae_linear(0, dummy, 10, 384, dummy, 200, dummy, None, dummy, None) == 3  # n % 128
+    assert lib.mmre_m3ae_linear(0, dummy, 10, 384, dummy, 200, dummy, None, dummy, None) == 3  # n % 64
     assert lib.mmre_m3ae_linear(2, dummy, 10, 384, dummy, 384, dummy, None, dummy, None) == 1  # no residual
     assert lib.mmre_m3ae_layernorm(dummy, 4, 200, dummy, dummy, 1e-5, dummy, None) == 3
     assert lib.mmre_m3ae_attention(dummy, dummy, 2, 400, 6, 64, 0.125, 0, dummy, None) == 3  # rows > max
     assert lib.mmre_m3ae_attention(dummy, dummy, 2, 10, 6, 32, 0.125, 0, dummy, None) == 3  # head dim
-    assert lib.mmre_m3ae_rows(dummy, 2, 400, dummy, None) == 1  # len > max_len
+    assert lib.mmre_m3ae_plan_size(10) == 65
+    assert lib.mmre_m3ae_plan(dummy, dummy, 2, 400, 1, 10, dummy, None) == 1  # len > max_len
     params = (ctypes.c_void_p * 30)(*([16] * 30))
     assert lib.mmre_m3ae_encode(ctypes.cast(params, ctypes.c_void_p), 2, 200, 4, 1e-5, dummy, dummy, 1, 8, 10,
-                                dummy, 9, 9, dummy, 10 ** 6, dummy, None) == 3  # d = 200 unsupported
+                                dummy, 1, 9, 9, dummy, 10 ** 6, dummy, None) == 3  # d = 200 unsupported
+    assert lib.mmre_m3ae_encode(ctypes.cast(params, ctypes.c_void_p), 2, 384, 6, 1e-5, dummy, dummy, 2, 8, 10,
+                                dummy, 3, 9, 9, dummy, 10 ** 6, dummy, None) == 1  # n_unique > n_seq
 
 
 def test_encoder_needs_device_tensors():

@@ -110,7 +110,7 @@ def test_attention_matches_float64(heads, hd):
 @pytest.mark.parametrize("L,lens,holes", [(64, [0, 1, 7, 33, 64], True), (320, [12, 320, 3], False)])
 def test_encoder_matches_oracle(L, lens, holes):
     """CLS of the padding-free / CLS-only HIP encoder vs the oracle over the full padded rows,
-    with empty, full and interior-padded rows; dedupe is exact (bit-identical rows)."""
+    with empty, full and interior-padded rows; the dedupe of adjacent repeats is exact."""
     import m3ae_text as om
     vocab = 500
     enc = _encoder(vocab, depth=2)
@@ -121,13 +121,16 @@ def test_encoder_matches_oracle(L, lens, holes):
     cls = enc.encode(tok_d, msk_d)
     torch.cuda.synchronize()
     _close(cls, ref[:, 0])
-    # duplicated rows (different ids on padded positions) go through dedupe: bit-identical
+    # adjacent repeats (different ids on padded positions) are encoded once; rows are
+    # independent of their packing: everything bit-identical
     tok2 = torch.where(msk_d > 0, torch.randint_like(tok_d, 0, vocab), tok_d)
-    rep = enc.encode(torch.cat([tok_d, tok2, tok_d]), torch.cat([msk_d, msk_d, msk_d]))
+    rep = enc.encode(torch.stack([tok_d, tok2, tok_d], 1).flatten(0, 1), msk_d.repeat_interleave(3, 0))
+    far = enc.encode(torch.cat([tok_d, tok2, tok_d]), torch.cat([msk_d, msk_d, msk_d]))
     nodup = enc.encode(tok_d, msk_d, dedupe=False)
     torch.cuda.synchronize()
     n = len(lens)
-    assert torch.equal(rep[:n], cls) and torch.equal(rep[n:2 * n], cls) and torch.equal(nodup, cls)
+    assert torch.equal(rep, cls.repeat_interleave(3, 0)) and torch.equal(far, cls.repeat(3, 1))
+    assert torch.equal(nodup, cls)
 
 
 def test_encoder_small_full_depth():
@@ -172,3 +175,27 @@ def test_generate_end_to_end():
     torch.cuda.synchronize()
     assert out.shape == (20, 200)
     _close(out, ref)
+
+
+def test_plan_dedupes_adjacent_repeats_and_counts_bad_ids():
+    """mmre_m3ae_plan: a row equal to the previous one on its padding pattern and unpadded tokens
+    (ids on padded positions may differ) shares its unique sequence; packed offsets count the
+    CLS row + unpadded tokens; unpadded ids outside [0, vocab) are counted."""
+    from mmre._lib import call, lib, ptr, stream_ptr
+    L = 8
+    rows = [([1, 2, 3, 0, 0, 0, 0, 0], 3), ([1, 2, 3, 9, 9, 9, 9, 9], 3), ([1, 2, 3, 0, 0, 0, 0, 0], 4),
+            ([1, 2, 3, 0, 0, 0, 0, 0], 4), ([5, 5, 5, 5, 5, 5, 5, 5], 8), ([1, 2, 3, 0, 0, 0, 0, 0], 3)]
+    tok = torch.tensor([r for r, _ in rows], dtype=torch.int32, device=DEV)
+    msk = torch.tensor([[0.0] * n + [1.0] * (L - n) for _, n in rows], device=DEV)
+    B = len(rows)
+    plan = torch.full((int(lib().mmre_m3ae_plan_size(B)),), -7, dtype=torch.int32, device=DEV)
+    call("mmre_m3ae_plan", ptr(tok), ptr(msk), B, L, 1, 10, ptr(plan), stream_ptr(DEV))
+    p = plan.cpu().numpy()
+    assert list(p[:B]) == [0, 0, 1, 1, 2, 3]                  # uniq
+    assert list(p[B:B + 4]) == [0, 2, 4, 5]                   # src rows of the unique sequences
+    assert list(p[2 * B:2 * B + 5]) == [0, 4, 9, 18, 22]      # packed offsets
+    assert list(p[3 * B + 1:3 * B + 5]) == [4, 22, 9, 0]      # n_unique, n_rows, max_rows, bad ids
+    call("mmre_m3ae_plan", ptr(tok), ptr(msk), B, L, 0, 5, ptr(plan), stream_ptr(DEV))  # no dedupe, vocab 5
+    p = plan.cpu().numpy()
+    assert list(p[:B]) == list(range(B))
+    assert list(p[3 * B + 1:3 * B + 5]) == [6, 4 + 4 + 5 + 5 + 9 + 4, 9, 8]  # the eight 5s are out of range
