@@ -28,7 +28,11 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="time one rank's share of a W-way relation-sharded step (no collective)")
     a = ap.parse_args()
+    if a.emulate_world:
+        return emulate(a)
     dev = torch.device("cuda:0")
     w = zs_workload()
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], w["n_ent"], w["n_rel"])
@@ -66,6 +70,42 @@ def main():
     print(f"launch-only (host) {launch:.3f} ms | metrics on pinned views {met_pinned:.3f} ms")
     print(f"full step {full:.3f} ms | launches+GPU {gpu:.3f} ms | +D2H+sync {d2h:.3f} ms | "
           f"host metrics {met:.3f} ms | empty sync {empty:.4f} ms")
+
+
+def emulate(a):
+    """Per-rank cost of a W-way relation-sharded C2 step on this one GPU: each rank's LPT share
+    swept and reduced alone (the all-gather is not included)."""
+    from mmre.link import HEAD, TAIL, LinkSweep
+    from mmre.sharding import lpt_partition
+    dev = torch.device("cuda:0")
+    w = zs_workload()
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], w["n_ent"], w["n_rel"])
+    spec = ScoreSpec(model="transe", ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=200, norm_flag=True)
+    th, tr, tt = (np.asarray(x, np.int64) for x in (w["test_h"], w["test_r"], w["test_t"]))
+    n = len(th)
+    qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
+    qm = np.concatenate([np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)])
+    masks = lpt_partition(qr, a.emulate_world)
+    to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    worst = 0.0
+    for k, m in enumerate(masks):
+        q = [to(x[m]) for x in (qh, qr, qt, qm)]
+        filt = tuple(to(x) for x in index.groups(qh[m], qr[m], qt[m], qm[m]))
+        sw = LinkSweep(spec)
+        bufs = sw.alloc_queries(int(m.sum()))
+        host = torch.empty((4, int(m.sum())), dtype=torch.int32, pin_memory=True)
+        ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+
+        def step():
+            c = sw.run(*q, filt=filt, buffers=bufs, sweep_events=ev)["counts"]
+            host.copy_(c, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+        for _ in range(3):
+            step()
+        ms = timeit(step, a.reps)
+        worst = max(worst, ms)
+        print(f"rank {k}: {int(m.sum())} sweeps, step {ms:.3f} ms, sweep kernel {ev[0].elapsed_time(ev[1]):.3f} ms")
+    print(f"world {a.emulate_world}: slowest rank {worst:.3f} ms (+ all-gather + metric reduction)")
 
 
 if __name__ == "__main__":
