@@ -300,6 +300,7 @@ __global__ __launch_bounds__(256, 2) void k_m3ae_linear(const float* __restrict_
   const int ar = tid & 63, aq = tid >> 6;   // A stage: row ar, k quads aq and aq + 4
   const int br = tid % BN, bq = tid / BN;   // W stage: row br, k quads bq + BSTEP i
   // rows past M load row M - 1 (no branches in the load path); their outputs are never stored
+  const int nkt = K / LK;
   const float* Ap = A + min(m0 + ar, M - 1) * (int64_t)K;
   const float* Bp = W + (int64_t)(n0 + br) * K;
   // two register stages: the loads of K step s are issued two steps before they are written to
@@ -352,7 +353,6 @@ __global__ __launch_bounds__(256, 2) void k_m3ae_linear(const float* __restrict_
     }                                                                                               \
   } while (0)
   // K step s lives in LDS buffer s & 1 and register stage s & 1
-  const int nkt = K / LK;
   M3_GLOAD(0, ra00, ra01, rb00, rb01, rb02, rb03);
   if (nkt > 1) M3_GLOAD(1, ra10, ra11, rb10, rb11, rb12, rb13);
   M3_SWRITE(0, ra00, ra01, rb00, rb01, rb02, rb03);
@@ -516,11 +516,13 @@ int launch_linear(int epi, const float* A, int64_t M, int K, const float* W, int
   if (epi < 0 || epi > 2 || !A || !W || !bias || !out || (epi == 2 && !resid)) return MMRE_ERR_ARG;
   if (M == 0) return MMRE_OK;
   const int64_t mt = (M + LM - 1) / LM;
-  // 64 x 128 tiles once they fill the chip twice over (256 CUs), else 64 x 64 (twice the groups)
-  if (N % 128 == 0 && mt * (N / 128) >= 512)
-    launch_linear_bn<128>(epi, mt, st, A, M, K, W, N, bias, resid, out);
-  else
-    launch_linear_bn<64>(epi, mt, st, A, M, K, W, N, bias, resid, out);
+  // 64 x 64 tiles: measured faster than 64 x 128 on every encoder shape at 2,261 rows
+  // (scripts/m3ae_gemm_ab.py; an in-workgroup split-K was no faster either); 64 x 128 only
+  // once the grid holds 8 tiles per CU
+  static const char* force = getenv("MMRE_M3AE_TILE");  // experiments: "128" or "64"
+  const bool wide = N % 128 == 0 && (force && force[0] ? force[0] == '1' : mt * (N / 128) >= 2048);
+  if (wide) launch_linear_bn<128>(epi, mt, st, A, M, K, W, N, bias, resid, out);
+  else launch_linear_bn<64>(epi, mt, st, A, M, K, W, N, bias, resid, out);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
