@@ -364,6 +364,20 @@ int mmre_m3ae_linear(int epilogue, const float* d_a, int64_t m, int k, const flo
 int mmre_m3ae_attention(const float* d_qkv, const int32_t* d_off, int64_t n_seq, int max_rows, int heads,
                         int head_dim, float scale, int cls_only, float* d_out, void* stream);
 
+/* ====================================================================== *
+ *  Small fp32 GEMM of the GAN step's Discriminator (zsl_module.py:112-138: *
+ *  its SN linears and class scores) and of their autograd, the gradient   *
+ *  penalty's double backward included (module/utils.py:692-707).          *
+ *  d_c (m, n) row-major = A B with A(i, k) = d_a[i sam + k sak],          *
+ *  B(k, j) = d_b[k sbk + j sbn] (transposes are strides). 32 x 32 MFMA    *
+ *  tiles, K split into mmre_gemm_splits slices when the tiles alone do    *
+ *  not fill the chip; the slices' partials (d_work, splits x m x n floats)*
+ *  are summed in slice order.                                             *
+ * ====================================================================== */
+int mmre_gemm_splits(int64_t m, int64_t n, int64_t k);
+int mmre_gemm_f32(const float* d_a, int64_t sam, int64_t sak, const float* d_b, int64_t sbk, int64_t sbn, int64_t m,
+                  int64_t n, int64_t k, float* d_work, int64_t work_floats, float* d_c, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

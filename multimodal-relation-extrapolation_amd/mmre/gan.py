@@ -10,7 +10,9 @@ Here:
     is frozen during GAN training; mmre.extractor);
   * generator forward + backward: HIP (mmre_generator_forward_save / _backward, spectral-norm
     chain rule included);
-  * Discriminator, gradient penalty and Adam: torch-ROCm autograd on the device;
+  * Discriminator, gradient penalty and Adam: autograd on the device, every matrix product
+    (and its derivatives, the penalty's double backward included) on the split-K HIP GEMM of
+    mmre.gemm -- a library GEMM ran each of these 200-512-sided products on one workgroup;
   * each D step and G step is captured once into a hipGraph (torch.cuda.CUDAGraph on ROCm)
     over static input buffers and replayed: one graph launch per step instead of ~200 kernel
     launches. Noise and the GP's alpha are drawn inside the graph (graph-safe Philox).
@@ -21,6 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from .extractor import encode
+from .gemm import mm
 
 
 def _cls_scores(class_scores, labels):
@@ -110,7 +113,7 @@ class ZSLGANStep:
         # |mean(sample rows of the label) - centroid|_2, summed, / gan_batch_rela
         onehot = F.one_hot(labels, self.n_labels).to(sample.dtype)          # (N, L)
         cnt = onehot.sum(0)                                                  # (L,)
-        means = (onehot.t() @ sample) / cnt.clamp(min=1).unsqueeze(1)        # (L, d)
+        means = mm(onehot.t(), sample) / cnt.clamp(min=1).unsqueeze(1)       # (L, d)
         dist = ((means - self.centroids) ** 2).sum(1).sqrt()
         loss_vp = torch.where(cnt > 0, dist, torch.zeros_like(dist)).sum() * (1.0 / self.gan_batch_rela)
         loss = loss_fake + loss_cls + 3.0 * loss_vp

@@ -27,6 +27,7 @@ import torch.nn.functional as F
 from mmre._lib import MMREError
 from mmre.candidates import cosine_rank
 from mmre.extractor import ZSLRanker, _check_ids, encode, node_tables, pack_weights, targets
+from mmre.gemm import mm, sn_linear
 from .submodule import LayerNormalization, SupportEncoder
 
 
@@ -91,9 +92,10 @@ class Discriminator(nn.Module):
     LayerNormalization) shared by the sample and the class centroids, spectral-normalised fc_TF
     (d -> 1) for the WGAN critic, and class scores against the centroids. Same parameter and
     buffer names (fc_middle.weight_orig / weight_u / weight_v / bias, fc_TF.*, layer_norm.a_2 /
-    b_2). Runs as torch-ROCm autograd on the device inside the GAN step's hipGraph
-    (mmre.gan): its double backward (the gradient penalty) is the reason it is not a fused
-    kernel."""
+    b_2). Runs as autograd on the device inside the GAN step's hipGraph (mmre.gan): its
+    products (x W^T of both layers, the class scores) and all their derivatives -- the gradient
+    penalty's double backward included -- run on the split-K HIP GEMM of mmre.gemm; the
+    element-wise parts (leaky_relu, LayerNormalization, the SN power iteration) stay torch ops."""
 
     def __init__(self, dropout=0.3, dim=200):
         super().__init__()
@@ -102,10 +104,10 @@ class Discriminator(nn.Module):
         self.layer_norm = LayerNormalization(dim)
 
     def forward(self, ep_vec, centroid_matrix):
-        middle_vec = self.layer_norm(F.leaky_relu(self.fc_middle(ep_vec)))
-        centroid_matrix = self.layer_norm(F.leaky_relu(self.fc_middle(centroid_matrix)))
-        logit_TF = self.fc_TF(middle_vec)
-        class_scores = torch.matmul(middle_vec, centroid_matrix.t())
+        middle_vec = self.layer_norm(F.leaky_relu(sn_linear(self.fc_middle, ep_vec)))
+        centroid_matrix = self.layer_norm(F.leaky_relu(sn_linear(self.fc_middle, centroid_matrix)))
+        logit_TF = sn_linear(self.fc_TF, middle_vec)
+        class_scores = mm(middle_vec, centroid_matrix.t())
         return middle_vec, logit_TF, class_scores
 
 
