@@ -368,15 +368,33 @@ int mmre_m3ae_attention(const float* d_qkv, const int32_t* d_off, int64_t n_seq,
  *  Small fp32 GEMM of the GAN step's Discriminator (zsl_module.py:112-138: *
  *  its SN linears and class scores) and of their autograd, the gradient   *
  *  penalty's double backward included (module/utils.py:692-707).          *
- *  d_c (m, n) row-major = A B with A(i, k) = d_a[i sam + k sak],          *
- *  B(k, j) = d_b[k sbk + j sbn] (transposes are strides). 32 x 32 MFMA    *
- *  tiles, K split into mmre_gemm_splits slices when the tiles alone do    *
- *  not fill the chip; the slices' partials (d_work, splits x m x n floats)*
- *  are summed in slice order.                                             *
+ *  d_c (m, n) row-major = A B (+ d_bias[n] when given) with               *
+ *  A(i, k) = d_a[i sam + k sak], B(k, j) = d_b[k sbk + j sbn] (transposes *
+ *  are strides). One launch: 32 x 32 MFMA tiles, K split over             *
+ *  mmre_gemm_splits(m, n, k) waves of a workgroup, summed in slice order. *
  * ====================================================================== */
 int mmre_gemm_splits(int64_t m, int64_t n, int64_t k);
 int mmre_gemm_f32(const float* d_a, int64_t sam, int64_t sak, const float* d_b, int64_t sbk, int64_t sbn, int64_t m,
-                  int64_t n, int64_t k, float* d_work, int64_t work_floats, float* d_c, void* stream);
+                  int64_t n, int64_t k, const float* d_bias, float* d_c, void* stream);
+
+/* Spectral normalisation of one weight (torch.nn.utils.spectral_norm's compute_weight, the
+ * reference's SN layers: module/spectral_norm.py:39-89; Discriminator zsl_module.py:115-118).
+ * power_iteration != 0 (training mode): one power iteration first updates d_u (out), d_v (in)
+ * in place (v = normalize(W^T u), u = normalize(W v), eps). Then sigma = u . (W v),
+ * d_w_hat = W / sigma, and d_u_snap / d_v_snap = the u, v used (for the backward).
+ * d_work: 2048 floats. out, in <= 1024. */
+int mmre_sn_weight(const float* d_w, int out, int in, float* d_u, float* d_v, int power_iteration, float eps,
+                   float* d_sigma, float* d_u_snap, float* d_v_snap, float* d_w_hat, float* d_work, void* stream);
+/* d_gw = G / s - <G, W> / s^2 u v^T for G = d_g = dL/dW_hat (u, v, s from mmre_sn_weight). */
+int mmre_sn_weight_backward(const float* d_g, const float* d_w, int out, int in, const float* d_u, const float* d_v,
+                            const float* d_sigma, float* d_gw, void* stream);
+/* LayerNormalization (module/submodule.py:58-77): (z - mean) / (std_unbiased + eps) * a + b
+ * per row of d_z (n_rows, d); d == 1 is the identity. */
+int mmre_layernorm_unbiased(const float* d_z, int64_t n_rows, int d, const float* d_a, const float* d_b, float eps,
+                            float* d_out, void* stream);
+/* Its backward for dL/dout = d_g: d_gz (n_rows, d), d_ga, d_gb (d). d_work: n_rows * d floats. */
+int mmre_layernorm_unbiased_backward(const float* d_g, const float* d_z, int64_t n_rows, int d, const float* d_a,
+                                     float eps, float* d_gz, float* d_ga, float* d_gb, float* d_work, void* stream);
 
 #ifdef __cplusplus
 }

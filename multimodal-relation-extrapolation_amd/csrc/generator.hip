@@ -13,8 +13,8 @@
 //   k_sn_scale   W_hat = W_orig / sigma element-wise (the reference's normalised weight values),
 //                kept in the activation buffer for the backward
 //   k_gen_concat x0 = [noise | cls]
-//   k_linear     x W_hat^T + b: one wave per 32 x 32 output tile on v_mfma_f32_32x32x2_f32,
-//                operands batched 8 K-steps per load round (M/32 x N/32 waves per layer)
+//   linears      x W_hat^T + b on the split-K GEMM of gemm.hip (32 x 32 MFMA tiles, bias in its
+//                epilogue)
 //   k_gen_ln     LayerNormalization, one wave per row
 #include "mmre_common.h"
 
@@ -43,14 +43,10 @@ struct SNLayer {
 
 constexpr int SN_T = 1024;
 
-// One workgroup per layer. scratch: 2048 floats per layer (W v, then W^T u).
-__global__ __launch_bounds__(SN_T) void k_sn_sigma(SNLayer l0, SNLayer l1, SNLayer l2, int power_iteration,
-                                                   float eps, float* __restrict__ sigma, float* __restrict__ scratch) {
-  __shared__ float red[SN_T / 64];
-  __shared__ float part[4][1024];
-  const SNLayer L = blockIdx.x == 0 ? l0 : (blockIdx.x == 1 ? l1 : l2);
-  float* wv = scratch + blockIdx.x * 2048;  // W v   (out <= 1024)
-  float* tv = wv + 1024;                    // W^T u (in <= 1024)
+// sigma of one layer by one SN_T-thread workgroup (returned to every thread); in training
+// mode the power iteration first updates L.u, L.v in place. wv / tv: 1024 floats each of scratch.
+__device__ float sn_sigma_layer(const SNLayer& L, int power_iteration, float eps, float* __restrict__ wv,
+                                float* __restrict__ tv, float* red, float (*part)[1024]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = SN_T / 64;
   if (power_iteration) {
     // tv[k] = sum_o W[o][k] u[o]: 256 columns per pass x 4 quarters of the rows
@@ -59,8 +55,10 @@ __global__ __launch_bounds__(SN_T) void k_sn_sigma(SNLayer l0, SNLayer l1, SNLay
     for (int k0 = 0; k0 < L.in; k0 += 256) {
       const int k = k0 + tk;
       float s = 0.0f;
-      if (k < L.in)
+      if (k < L.in) {
+#pragma unroll 8
         for (int o = o0; o < o1; ++o) s += L.w[(int64_t)o * L.in + k] * L.u[o];
+      }
       part[q][tk] = s;
       __syncthreads();
       if (q == 0 && k < L.in) tv[k] = part[0][tk] + part[1][tk] + part[2][tk] + part[3][tk];
@@ -92,8 +90,36 @@ __global__ __launch_bounds__(SN_T) void k_sn_sigma(SNLayer l0, SNLayer l1, SNLay
   }
   float dot = 0.0f;
   for (int o = threadIdx.x; o < L.out; o += SN_T) dot += L.u[o] * wv[o];
-  dot = block_sum(dot, red);
-  if (threadIdx.x == 0) sigma[blockIdx.x] = dot;
+  return block_sum(dot, red);
+}
+
+// One workgroup per layer. scratch: 2048 floats per layer (W v, then W^T u).
+__global__ __launch_bounds__(SN_T) void k_sn_sigma(SNLayer l0, SNLayer l1, SNLayer l2, int power_iteration,
+                                                   float eps, float* __restrict__ sigma, float* __restrict__ scratch) {
+  __shared__ float red[SN_T / 64];
+  __shared__ float part[4][1024];
+  const SNLayer L = blockIdx.x == 0 ? l0 : (blockIdx.x == 1 ? l1 : l2);
+  float* wv = scratch + blockIdx.x * 2048;
+  const float s = sn_sigma_layer(L, power_iteration, eps, wv, wv + 1024, red, part);
+  if (threadIdx.x == 0) sigma[blockIdx.x] = s;
+}
+
+// spectral_norm.compute_weight (spectral_norm.py:39-89, torch.nn.utils.spectral_norm) of one
+// layer in one launch: power iteration (training mode), sigma, W_hat = W / sigma, and copies
+// of the u, v the weight was normalised with (the autograd snapshot: later calls update the
+// buffers in place).
+__global__ __launch_bounds__(SN_T) void k_sn_weight(SNLayer L, int power_iteration, float eps,
+                                                    float* __restrict__ sigma, float* __restrict__ scratch,
+                                                    float* __restrict__ u_snap, float* __restrict__ v_snap,
+                                                    float* __restrict__ w_hat) {
+  __shared__ float red[SN_T / 64];
+  __shared__ float part[4][1024];
+  const float s = sn_sigma_layer(L, power_iteration, eps, scratch, scratch + 1024, red, part);
+  if (threadIdx.x == 0) sigma[0] = s;
+  const int64_t n = (int64_t)L.out * L.in;
+  for (int64_t i = threadIdx.x; i < n; i += SN_T) w_hat[i] = L.w[i] / s;
+  for (int o = threadIdx.x; o < L.out; o += SN_T) u_snap[o] = L.u[o];
+  for (int k = threadIdx.x; k < L.in; k += SN_T) v_snap[k] = L.v[k];
 }
 
 // W_hat = W_orig / sigma for the three layers (one grid over their concatenation).
@@ -116,39 +142,6 @@ __global__ __launch_bounds__(256) void k_gen_concat(const float* __restrict__ no
     const int64_t r = i / in0;
     const int k = (int)(i % in0);
     x0[i] = k < nd ? noise[r * nd + k] : cls[r * cd + (k - nd)];
-  }
-}
-
-// C[m][n] = sum_k A[m][k] * W[n][k] + bias[n]  (A: M x K, W: N x K, both row-major).
-// One wave per 32 x 32 tile; each lane loads 8 K-steps of its A row / W row per round.
-constexpr int LK = 8;
-__global__ __launch_bounds__(64) void k_linear(const float* __restrict__ A, const float* __restrict__ W,
-                                               const float* __restrict__ bias, int M, int N, int K,
-                                               float* __restrict__ C) {
-  const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
-  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
-  const int m = m0 + i, n = n0 + i;
-  const float* ar = A + (int64_t)(m < M ? m : 0) * K;
-  const float* wr = W + (int64_t)(n < N ? n : 0) * K;
-  floatx16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  for (int k0 = 0; k0 < K; k0 += 2 * LK) {
-    float a[LK], b[LK];
-#pragma unroll
-    for (int j = 0; j < LK; ++j) {
-      const int k = k0 + 2 * j + kh;
-      a[j] = (m < M && k < K) ? ar[k] : 0.0f;
-      b[j] = (n < N && k < K) ? wr[k] : 0.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < LK; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
-  }
-  const float bb = n < N ? bias[n] : 0.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-    if (row < M && n < N) C[(int64_t)row * N + n] = acc[r] + bb;
   }
 }
 
@@ -245,41 +238,11 @@ __global__ __launch_bounds__(1024) void k_colsum(const float* __restrict__ A, co
   }
 }
 
-// C[m][n] = alpha * sum_k A(m, k) B(k, n) with A(m, k) = A[m*sam + k*sak], B(k, n) = B[k*sbk + n*sbn];
-// one wave per 32 x 32 tile on v_mfma_f32_32x32x2_f32 (operands straight from L2: small GEMMs).
-__global__ __launch_bounds__(64) void k_gemm_f32(const float* __restrict__ A, int64_t sam, int64_t sak,
-                                                 const float* __restrict__ B, int64_t sbk, int64_t sbn, int M, int N,
-                                                 int64_t K, const float* __restrict__ div, float* __restrict__ C) {
-  const int lane = threadIdx.x, i = lane & 31, kh = lane >> 5;
-  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
-  floatx16 acc;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-  const int m = m0 + i, n = n0 + i;
-  for (int64_t k0 = 0; k0 < K; k0 += 2 * LK) {  // LK K-steps of operands per load round
-    float a[LK], b[LK];
-#pragma unroll
-    for (int j = 0; j < LK; ++j) {
-      const int64_t k = k0 + 2 * j + kh;
-      a[j] = (m < M && k < K) ? A[m * sam + k * sak] : 0.0f;
-      b[j] = (n < N && k < K) ? B[k * sbk + n * sbn] : 0.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < LK; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], b[j], acc, 0, 0, 0);
-  }
-  const float d = div ? *div : 1.0f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-    if (row < M && n < N) C[(int64_t)row * N + n] = div ? acc[r] / d : acc[r];
-  }
-}
-
-// Spectral-norm chain rule, in place (one workgroup per matrix): G = dL/d(W/s) ->
+// Spectral-norm chain rule (one workgroup per matrix; GW may alias G): G = dL/d(W/s) ->
 // dL/dW = G / s - <G, W> / s^2 * u v^T   (u, v, s: the forward's values, spectral_norm.py:85-89).
-__global__ __launch_bounds__(1024) void k_sn_grad(float* __restrict__ G, const float* __restrict__ W,
+__global__ __launch_bounds__(1024) void k_sn_grad(const float* G, const float* __restrict__ W,
                                                   const float* __restrict__ u, const float* __restrict__ v,
-                                                  const float* __restrict__ sigma, int out, int in) {
+                                                  const float* __restrict__ sigma, int out, int in, float* GW) {
   __shared__ float red[16];
   const int64_t n = (int64_t)out * in;
   float t = 0.0f;
@@ -291,16 +254,13 @@ __global__ __launch_bounds__(1024) void k_sn_grad(float* __restrict__ G, const f
   float dot = 0.0f;
   for (int w = 0; w < (int)(blockDim.x >> 6); ++w) dot += red[w];
   const float s = *sigma, c = dot / (s * s);
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) G[i] = G[i] / s - c * u[i / in] * v[i % in];
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) GW[i] = G[i] / s - c * u[i / in] * v[i % in];
 }
 
-// C (M x N) = A B / (*div if div), strided operands
+// C (M x N) = A B / (*div if div), strided operands (the split-K GEMM of gemm.hip)
 static int gemm(hipStream_t st, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
                 int M, int N, int64_t K, const float* div, float* C) {
-  dim3 grid((unsigned)((N + 31) / 32), (unsigned)((M + 31) / 32));
-  hipLaunchKernelGGL(k_gemm_f32, grid, dim3(64), 0, st, A, sam, sak, B, sbk, sbn, M, N, K, div, C);
-  MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  return gemm_launch(st, A, sam, sak, B, sbk, sbn, M, N, K, div, nullptr, C, nullptr, nullptr);
 }
 
 }  // namespace mmre
@@ -355,16 +315,13 @@ extern "C" int mmre_generator_forward_save(const float* d_noise, int noise_dim, 
   hipLaunchKernelGGL(k_gen_concat, dim3((unsigned)((nx + 255) / 256 < 4096 ? (nx + 255) / 256 : 4096)), dim3(256), 0,
                      st, d_noise, noise_dim, d_cls, cls_dim, n_rows, x0);
   MMRE_CHECK_LAUNCH();
-  const unsigned mb = (unsigned)((n_rows + 31) / 32);
-  hipLaunchKernelGGL(k_linear, dim3((unsigned)((out0 + 31) / 32), mb), dim3(64), 0, st, x0, wh0, d_b0, (int)n_rows,
-                     out0, in0, h1);
-  MMRE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_linear, dim3((unsigned)((out1 + 31) / 32), mb), dim3(64), 0, st, h1, wh1, d_b1, (int)n_rows,
-                     out1, out0, h2);
-  MMRE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_linear, dim3((unsigned)((out2 + 31) / 32), mb), dim3(64), 0, st, h2, wh2, d_b2, (int)n_rows,
-                     out2, out1, h3);
-  MMRE_CHECK_LAUNCH();
+  // x W_hat^T + b: B(k, n) = W_hat[n][k]
+  int rc;
+  if ((rc = gemm_launch(st, x0, in0, 1, wh0, 1, in0, n_rows, out0, in0, nullptr, d_b0, h1, nullptr, nullptr))) return rc;
+  if ((rc = gemm_launch(st, h1, out0, 1, wh1, 1, out0, n_rows, out1, out0, nullptr, d_b1, h2, nullptr, nullptr)))
+    return rc;
+  if ((rc = gemm_launch(st, h2, out1, 1, wh2, 1, out1, n_rows, out2, out1, nullptr, d_b2, h3, nullptr, nullptr)))
+    return rc;
   hipLaunchKernelGGL(k_gen_ln, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, st, h3, d_ln_a, d_ln_b, ln_eps,
                      n_rows, out2, d_out);
   MMRE_CHECK_LAUNCH();
@@ -429,7 +386,7 @@ extern "C" int mmre_generator_backward(const float* d_gout, int64_t n_rows, int 
     if ((rc = colsum(d_gout, nullptr, out2, d_gln_b))) return rc;
   }
   auto sn = [&](float* G, const float* W, const float* u, const float* v, int layer, int o, int i) -> int {
-    hipLaunchKernelGGL(k_sn_grad, dim3(1), dim3(1024), 0, st, G, W, u, v, d_sigma + layer, o, i);
+    hipLaunchKernelGGL(k_sn_grad, dim3(1), dim3(1024), 0, st, G, W, u, v, d_sigma + layer, o, i, G);
     MMRE_CHECK_LAUNCH();
     return MMRE_OK;
   };
@@ -448,5 +405,53 @@ extern "C" int mmre_generator_backward(const float* d_gout, int64_t n_rows, int 
   if ((rc = colsum(g1, nullptr, out0, d_gb0))) return rc;
   if ((rc = gemm(st, g1, 1, out0, x0, in0, 1, out0, in0, n_rows, nullptr, d_gw0))) return rc;
   if ((rc = sn(d_gw0, d_w0, d_u0, d_v0, 0, out0, in0))) return rc;
+  return MMRE_OK;
+}
+
+extern "C" int mmre_sn_weight(const float* d_w, int out, int in, float* d_u, float* d_v, int power_iteration,
+                              float eps, float* d_sigma, float* d_u_snap, float* d_v_snap, float* d_w_hat,
+                              float* d_work, void* stream) {
+  if (!d_w || !d_u || !d_v || !d_sigma || !d_u_snap || !d_v_snap || !d_w_hat || !d_work || out <= 0 || in <= 0)
+    return MMRE_ERR_ARG;
+  if (out > 1024 || in > 1024) return MMRE_ERR_SHAPE;
+  SNLayer L{d_w, d_u, d_v, out, in};
+  hipLaunchKernelGGL(k_sn_weight, dim3(1), dim3(SN_T), 0, (hipStream_t)stream, L, power_iteration, eps, d_sigma,
+                     d_work, d_u_snap, d_v_snap, d_w_hat);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_sn_weight_backward(const float* d_g, const float* d_w, int out, int in, const float* d_u,
+                                       const float* d_v, const float* d_sigma, float* d_gw, void* stream) {
+  if (!d_g || !d_w || !d_u || !d_v || !d_sigma || !d_gw || out <= 0 || in <= 0) return MMRE_ERR_ARG;
+  hipLaunchKernelGGL(k_sn_grad, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_g, d_w, d_u, d_v, d_sigma, out, in,
+                     d_gw);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_layernorm_unbiased(const float* d_z, int64_t n_rows, int d, const float* d_a, const float* d_b,
+                                       float eps, float* d_out, void* stream) {
+  if (!d_z || !d_a || !d_b || !d_out || n_rows < 0 || d <= 0) return MMRE_ERR_ARG;
+  if (n_rows == 0) return MMRE_OK;
+  hipLaunchKernelGGL(k_gen_ln, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, d_z, d_a, d_b,
+                     eps, n_rows, d, d_out);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_layernorm_unbiased_backward(const float* d_g, const float* d_z, int64_t n_rows, int d,
+                                                const float* d_a, float eps, float* d_gz, float* d_ga, float* d_gb,
+                                                float* d_work, void* stream) {
+  if (!d_g || !d_z || !d_a || !d_gz || !d_ga || !d_gb || !d_work || n_rows <= 0 || d <= 0) return MMRE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_gen_ln_bwd, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, st, d_g, d_z, d_a, eps, n_rows,
+                     d, d_gz, d_work);
+  MMRE_CHECK_LAUNCH();
+  const dim3 g((unsigned)((d + 63) / 64));
+  hipLaunchKernelGGL(k_colsum, g, dim3(1024), 0, st, d_g, d_work, n_rows, d, d_ga);
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_colsum, g, dim3(1024), 0, st, d_g, nullptr, n_rows, d, d_gb);
+  MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }

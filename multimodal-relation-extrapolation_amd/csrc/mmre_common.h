@@ -24,6 +24,13 @@ constexpr int kWave = 64;
 
 __host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Small split-K fp32 GEMM (gemm.hip): C = A B / (*div if div) + bias, strided operands;
+// tile_dot[t] = sum over output tile t of C * Wd when both are given. One launch.
+int gemm_launch(hipStream_t st, const float* A, int64_t sam, int64_t sak, const float* B, int64_t sbk, int64_t sbn,
+                int64_t M, int64_t N, int64_t K, const float* div, const float* bias, float* C, const float* Wd,
+                float* tile_dot);
+int64_t gemm_tiles(int64_t M, int64_t N);
+
 // Row width of the k-major entity / query planes for a model.
 __host__ __device__ inline int model_k(int model, int dim) {
   return (model == MMRE_COMPLEX || model == MMRE_ROTATE) ? 2 * dim : dim;

@@ -68,7 +68,11 @@ SIGNATURES = {
     "mmre_m3ae_linear": (I32, [I32, P, I64, I32, P, I32, P, P, P, P]),
     "mmre_m3ae_attention": (I32, [P, P, I64, I32, I32, I32, F32, I32, P, P]),
     "mmre_gemm_splits": (I32, [I64, I64, I64]),
-    "mmre_gemm_f32": (I32, [P, I64, I64, P, I64, I64, I64, I64, I64, P, I64, P, P]),
+    "mmre_gemm_f32": (I32, [P, I64, I64, P, I64, I64, I64, I64, I64, P, P, P]),
+    "mmre_sn_weight": (I32, [P, I32, I32, P, P, I32, F32, P, P, P, P, P, P]),
+    "mmre_sn_weight_backward": (I32, [P, P, I32, I32, P, P, P, P, P]),
+    "mmre_layernorm_unbiased": (I32, [P, I64, I32, P, P, F32, P, P]),
+    "mmre_layernorm_unbiased_backward": (I32, [P, P, I64, I32, P, F32, P, P, P, P, P]),
 }
 
 ERRORS = {1: "bad argument", 2: "unknown model", 3: "unsupported shape", 4: "workspace too small"}

@@ -10,9 +10,10 @@ Here:
     is frozen during GAN training; mmre.extractor);
   * generator forward + backward: HIP (mmre_generator_forward_save / _backward, spectral-norm
     chain rule included);
-  * Discriminator, gradient penalty and Adam: autograd on the device, every matrix product
-    (and its derivatives, the penalty's double backward included) on the split-K HIP GEMM of
-    mmre.gemm -- a library GEMM ran each of these 200-512-sided products on one workgroup;
+  * Discriminator, gradient penalty and Adam: autograd on the device with the Discriminator's
+    pieces on HIP (mmre.gemm): every matrix product and its derivatives (the penalty's double
+    backward included) on the split-K GEMM -- a library GEMM ran each of these 200-512-sided
+    products on one workgroup -- the spectral-norm weight in one launch, LayerNormalization;
   * each D step and G step is captured once into a hipGraph (torch.cuda.CUDAGraph on ROCm)
     over static input buffers and replayed: one graph launch per step instead of ~200 kernel
     launches. Noise and the GP's alpha are drawn inside the graph (graph-safe Philox).
@@ -96,7 +97,19 @@ class ZSLGANStep:
                             loss_fake_cls.detach()])
 
     def g_step(self, rel, q_head, q_tail, f_head, f_tail, labels, noise):
-        """One Generator step (zsl_module.py:511-600). Returns loss_G and its parts."""
+        """One Generator step (zsl_module.py:511-600). Returns loss_G and its parts. The
+        Discriminator's parameter gradients of loss_G, which the reference computes and then
+        clears (Discriminator.zero_grad(), zsl_module.py:600), are not computed."""
+        frozen = [p for p in self.D.parameters() if p.requires_grad]
+        for p in frozen:
+            p.requires_grad_(False)
+        try:
+            return self._g_step(rel, q_head, q_tail, f_head, f_tail, labels, noise)
+        finally:
+            for p in frozen:
+                p.requires_grad_(True)
+
+    def _g_step(self, rel, q_head, q_tail, f_head, f_tail, labels, noise):
         self.D.eval()
         self.G.train()
         sample = self.G(self.cls_table.index_select(0, rel), noise)

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from mmre._lib import MMREError
 from mmre.candidates import cosine_rank
 from mmre.extractor import ZSLRanker, _check_ids, encode, node_tables, pack_weights, targets
-from mmre.gemm import mm, sn_linear
+from mmre.gemm import layer_norm, mm, sn_linear
 from .submodule import LayerNormalization, SupportEncoder
 
 
@@ -92,10 +92,11 @@ class Discriminator(nn.Module):
     LayerNormalization) shared by the sample and the class centroids, spectral-normalised fc_TF
     (d -> 1) for the WGAN critic, and class scores against the centroids. Same parameter and
     buffer names (fc_middle.weight_orig / weight_u / weight_v / bias, fc_TF.*, layer_norm.a_2 /
-    b_2). Runs as autograd on the device inside the GAN step's hipGraph (mmre.gan): its
-    products (x W^T of both layers, the class scores) and all their derivatives -- the gradient
-    penalty's double backward included -- run on the split-K HIP GEMM of mmre.gemm; the
-    element-wise parts (leaky_relu, LayerNormalization, the SN power iteration) stay torch ops."""
+    b_2). Runs as autograd on the device inside the GAN step's hipGraph (mmre.gan) with its
+    pieces on HIP kernels (mmre.gemm): the spectral-norm weight (power iteration, sigma, W /
+    sigma) in one launch per call, the products x W^T + b and the class scores -- and all their
+    derivatives, the gradient penalty's double backward included -- on the split-K GEMM, the
+    LayerNormalization forward and first-order backward in HIP; leaky_relu stays a torch op."""
 
     def __init__(self, dropout=0.3, dim=200):
         super().__init__()
@@ -104,8 +105,8 @@ class Discriminator(nn.Module):
         self.layer_norm = LayerNormalization(dim)
 
     def forward(self, ep_vec, centroid_matrix):
-        middle_vec = self.layer_norm(F.leaky_relu(sn_linear(self.fc_middle, ep_vec)))
-        centroid_matrix = self.layer_norm(F.leaky_relu(sn_linear(self.fc_middle, centroid_matrix)))
+        middle_vec = layer_norm(self.layer_norm, F.leaky_relu(sn_linear(self.fc_middle, ep_vec)))
+        centroid_matrix = layer_norm(self.layer_norm, F.leaky_relu(sn_linear(self.fc_middle, centroid_matrix)))
         logit_TF = sn_linear(self.fc_TF, middle_vec)
         class_scores = mm(middle_vec, centroid_matrix.t())
         return middle_vec, logit_TF, class_scores
