@@ -189,6 +189,11 @@ class LinkSweep:
         Returns dict(counts=(4, Q) int32 [raw, filt, raw_tc, filt_tc], truth=(Q,), scores=(Q, E)|None)."""
         s = self.spec
         n = int(qh.shape[0])
+        if n == 0:  # e.g. a rank that owns no test relation (world > #relations): nothing to sweep
+            z = torch.empty((4, 0), dtype=torch.int32, device=self.device)
+            return dict(counts=z, truth=torch.empty(0, dtype=torch.float32, device=self.device),
+                        scores=torch.empty((0, self.n_ent), dtype=torch.float32, device=self.device)
+                        if return_scores else None)
         if prepare or not self.prepared:
             self.prepare_entities()
         b = buffers if buffers is not None else self.alloc_queries(n)

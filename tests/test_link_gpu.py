@@ -229,3 +229,33 @@ def test_rotate_zero_and_tiny_magnitudes(oracle_mod):
         o_pred = oracle_mod.link_predict("rotate", mode, ent, rel, qh[sel], qr[sel], qt[sel], margin=margin,
                                          phase_denom=spec.phase_denom)
         assert np.array_equal(out["scores"][sel].view(np.uint32), o_pred.view(np.uint32))
+
+
+@pytest.mark.parametrize("model", ["transe", "distmult"])
+def test_tiny_tables_and_empty_query_set(oracle_mod, model):
+    """Edge sizes: a single-entity table (every sweep's only candidate is its truth: rank 0),
+    two entities, and an empty query set (a rank owning no test relation) that launches nothing."""
+    from mmre.link import FilterIndex
+    rng = np.random.default_rng(3)
+    for E in (1, 2):
+        ent = rng.uniform(-0.5, 0.5, (E, 8)).astype(np.float32)
+        rel = rng.uniform(-0.5, 0.5, (2, 8)).astype(np.float32)
+        qh = np.zeros(4, np.int64) if E == 1 else np.array([0, 1, 0, 1])
+        qr = np.array([0, 1, 0, 1], np.int64)
+        qt = np.zeros(4, np.int64) if E == 1 else np.array([1, 0, 1, 0])
+        qm = np.array([0, 0, 1, 1], np.int8)
+        spec = _spec_from(model, ent, rel, norm=model == "transe")
+        index = FilterIndex(qh, qr, qt, E, 2)
+        out = _run(spec, qh, qr, qt, qm, index=index)
+        hrt = oracle_mod.sorted_hrt(qh, qr, qt)
+        for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+            sel = qm == mode_id
+            o = oracle_mod.link_predict(model, mode, ent, rel, qh[sel], qr[sel], qt[sel], norm_flag=model == "transe")
+            assert np.array_equal(out["scores"][sel], o)
+            oc = oracle_mod.test_rank(mode, o, qh[sel], qr[sel], qt[sel], hrt)
+            assert np.array_equal(out["counts"][:, sel].T[:, :2], oc[:, :2])
+        if E == 1:
+            assert (out["counts"] == 0).all()
+    e = np.zeros(0, np.int64)
+    out = _run(spec, e, e, e, np.zeros(0, np.int8), index=index)
+    assert out["counts"].shape == (4, 0) and out["scores"].shape == (0, 2)

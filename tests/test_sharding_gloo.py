@@ -37,7 +37,15 @@ def _oracle_runner(ent, rel, hrt):
     return run
 
 
-def _worker(rank, world, port, res_path):
+def _test_list(d, keep_rel):
+    h, r, t = d.test_list()
+    if keep_rel:  # only the first `keep_rel` test relations: ranks beyond them own no query
+        sel = np.isin(r, np.unique(r)[:keep_rel])
+        h, r, t = h[sel], r[sel], t[sel]
+    return h, r, t
+
+
+def _worker(rank, world, port, res_path, keep_rel=None):
     sys.path[:0] = [PKG, os.path.join(REPO, "oracle"), REPO]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -50,19 +58,20 @@ def _worker(rank, world, port, res_path):
     rel = rng.uniform(-0.5, 0.5, (d.n_rel, 16)).astype(np.float32)
     trip = np.concatenate([d.train, d.valid, d.test])
     hrt = oracle.sorted_hrt(trip[:, 0], trip[:, 2], trip[:, 1])
-    h, r, t = d.test_list()
+    h, r, t = _test_list(d, keep_rel)
     ev = ShardedLinkEvaluation(None, h, r, t, device="cpu", local_runner=_oracle_runner(ent, rel, hrt))
     metrics, counts = ev.run()
     np.save(f"{res_path}_{rank}.npy", counts)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_counts_equal_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,keep_rel", [(2, None), (3, None), (3, 2)])
+def test_sharded_counts_equal_single_rank(tmp_path, world, keep_rel):
+    """keep_rel=2 at world 3: one rank owns no relation and joins the all-gather empty."""
     import oracle
     port = _free_port()
     res = str(tmp_path / "counts")
-    mp.spawn(_worker, args=(world, port, res), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, res, keep_rel), nprocs=world, join=True)
     outs = [np.load(f"{res}_{k}.npy") for k in range(world)]
     for o in outs[1:]:
         assert np.array_equal(o, outs[0])  # every rank holds the full table
@@ -75,7 +84,7 @@ def test_sharded_counts_equal_single_rank(tmp_path, world):
     rel = rng.uniform(-0.5, 0.5, (d.n_rel, 16)).astype(np.float32)
     trip = np.concatenate([d.train, d.valid, d.test])
     hrt = oracle.sorted_hrt(trip[:, 0], trip[:, 2], trip[:, 1])
-    h, r, t = d.test_list()
+    h, r, t = _test_list(d, keep_rel)
     single = _oracle_runner(ent, rel, hrt)(*(torch.from_numpy(np.concatenate([x, x])) for x in (h, r, t)),
                                            torch.from_numpy(np.r_[np.zeros(len(h), np.int8), np.ones(len(h), np.int8)]),
                                            None, None).numpy()
