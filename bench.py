@@ -648,20 +648,27 @@ def main():
     ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
     n_local = int(ev.masks[rank].sum())
 
-    def step(events=None):
-        return ev.run(events, copy_counts=False)[0]
+    def steps(n, evs=None):
+        # evaluation i + 1 is enqueued before the host reduces evaluation i's metrics, so that
+        # reduction overlaps the next sweep; every evaluation's metrics are reduced in the loop
+        metrics, pending = None, None
+        for i in range(n):
+            ticket = ev.launch(evs[i] if evs else None)
+            if pending is not None:
+                metrics = ev.finish(pending, copy_counts=False)[0]
+            pending = ticket
+        if pending is not None:
+            metrics = ev.finish(pending, copy_counts=False)[0]
+        return metrics
 
-    for _ in range(args.warmup):
-        step()
+    steps(args.warmup)
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    metrics = None
-    for i in range(args.steps):
-        metrics = step(evs[i])
+    metrics = steps(args.steps, evs)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

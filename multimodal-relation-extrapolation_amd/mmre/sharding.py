@@ -116,19 +116,43 @@ class ShardedLinkEvaluation:
         local = self.local_runner(*self.q, self.filt, self.masks_tc, events)
         return gather_counts(local, self.plan, self.group) if self.world > 1 else local
 
-    def run(self, events=None, copy_counts=True):
-        """(metrics, counts (4, 2n) int32). copy_counts=False returns the reused pinned buffer
-        (overwritten by the next run)."""
-        from .link import link_metrics
+    def launch(self, events=None):
+        """Enqueue one evaluation -- sweep, (world > 1) all-gather, and the D2H of the count
+        table into the next of two pinned buffers -- without waiting for it. Returns a ticket
+        for finish(). At most two tickets may be outstanding (the pinned buffers alternate), so
+        the host metric reduction of evaluation i can run while the GPU sweeps i + 1."""
+        if getattr(self, "_outstanding", 0) >= 2:
+            raise RuntimeError("ShardedLinkEvaluation: finish() a ticket before launching a third")
         c = self.counts(events)
-        if c.is_cuda:  # D2H into a reused pinned buffer, then wait for this stream only
-            if getattr(self, "_host", None) is None or self._host.shape != c.shape:
-                self._host = torch.empty(c.shape, dtype=c.dtype, pin_memory=True)
-            self._host.copy_(c, non_blocking=True)
-            torch.cuda.current_stream(c.device).synchronize()
-            c = self._host.numpy()
+        if not c.is_cuda:
+            return (c.numpy(), None)
+        hosts = getattr(self, "_hosts", None)
+        if hosts is None or hosts[0].shape != c.shape:
+            hosts = self._hosts = [torch.empty(c.shape, dtype=c.dtype, pin_memory=True) for _ in range(2)]
+            self._next = 0
+            self._outstanding = 0
+        h = hosts[self._next]
+        self._next ^= 1
+        h.copy_(c, non_blocking=True)
+        done = torch.cuda.Event()
+        done.record(torch.cuda.current_stream(c.device))
+        self._outstanding += 1
+        return (h, done)
+
+    def finish(self, ticket, copy_counts=True):
+        """Wait for a launch() ticket's counts (its own event only) and run the Test.h metric
+        reduction: (metrics, counts (4, 2n) int32). copy_counts=False returns the pinned
+        buffer itself (reused two launches later)."""
+        from .link import link_metrics
+        c, done = ticket
+        if done is not None:
+            done.synchronize()
+            self._outstanding -= 1
+            c = c.numpy()
             if copy_counts:
                 c = c.copy()
-        else:
-            c = c.numpy()
         return link_metrics(c[:, :self.n], c[:, self.n:]), c
+
+    def run(self, events=None, copy_counts=True):
+        """(metrics, counts (4, 2n) int32) of one evaluation, synchronously."""
+        return self.finish(self.launch(events), copy_counts)

@@ -259,3 +259,36 @@ def test_tiny_tables_and_empty_query_set(oracle_mod, model):
     e = np.zeros(0, np.int64)
     out = _run(spec, e, e, e, np.zeros(0, np.int8), index=index)
     assert out["counts"].shape == (4, 0) and out["scores"].shape == (0, 2)
+
+
+def test_pipelined_launch_finish_matches_run():
+    """ShardedLinkEvaluation.launch/finish (two evaluations in flight, alternating pinned
+    buffers, as bench.py drives it) gives the same counts and metrics as run(), for two
+    different model snapshots whose tickets overlap."""
+    from mmre.data import OpenKEDataset
+    from mmre.link import FilterIndex
+    from mmre.sharding import ShardedLinkEvaluation
+    ds = OpenKEDataset(os.path.join(GOLDEN, "data", "small"))
+    h, r, t = ds.test_list()
+    index = FilterIndex(*ds.all_triples(), ds.n_ent, ds.n_rel)
+    rng = np.random.default_rng(3)
+    evs = []
+    for _ in range(2):
+        ent = rng.uniform(-0.3, 0.3, (ds.n_ent, 64)).astype(np.float32)
+        rel = rng.uniform(-0.3, 0.3, (ds.n_rel, 64)).astype(np.float32)
+        evs.append(ShardedLinkEvaluation(_spec_from("transe", ent, rel, norm=True, dim=64), h, r, t, index=index,
+                                         device="cuda:0"))
+    ref = [e.run() for e in evs]
+    ev = evs[0]
+    a = ev.launch()
+    b = ev.launch()
+    with pytest.raises(RuntimeError):
+        ev.launch()  # a third ticket would overwrite a pinned buffer still unread
+    ma, ca = ev.finish(a)
+    mb, cb = ev.finish(b)
+    assert np.array_equal(ca, ref[0][1]) and np.array_equal(cb, ref[0][1])
+    assert ma == ref[0][0] and mb == ref[0][0]
+    # overlapping tickets of two snapshots keep their own buffers
+    ta, tb = evs[0].launch(), evs[1].launch()
+    (m0, c0), (m1, c1) = evs[0].finish(ta), evs[1].finish(tb)
+    assert np.array_equal(c0, ref[0][1]) and np.array_equal(c1, ref[1][1]) and m1 == ref[1][0]
