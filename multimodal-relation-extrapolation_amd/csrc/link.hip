@@ -1019,6 +1019,14 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   // CUs that run at different speeds (C2 on MI355X: 1,024 groups 4.0 ms, 8,192 3.43 ms,
   // 16,384 3.30 ms, 30,528 (one unit each) 3.36 ms).
   int g = 16 * resident_groups((const void*)k_sweep_valu<OP, TCV, STV>, NT);
+  // Small sweeps (a rank's share under relation sharding): no more workgroups than the
+  // busiest XCD group has units, so every workgroup gets at most one unit and no empty
+  // workgroups are dispatched (C2 at 8-way: 4,380 sweeps 0.52 -> 0.47 ms; 4-way 0.89 -> 0.85).
+  {
+    const int64_t q_tiles = q_pad / TQ;
+    const int64_t units = (n_et >= 8) ? 8 * q_tiles * ((n_et + 7) / 8) : q_tiles * n_et;
+    if (units < g) g = (int)(units > 0 ? units : 1);
+  }
   // MMRE_SWEEP_GRID (experiments): "tiles" = one workgroup per (query tile, 1/8 of the
   // entity tiles); a number = that many persistent workgroups.
   static const char* gmode = getenv("MMRE_SWEEP_GRID");
