@@ -134,8 +134,12 @@ def cpu_baseline(w, n_sample: int):
         tmp = tempfile.mkdtemp(prefix="mmre_cpu_")
         trn = np.stack([w["filter_h"][:-len(w["test_h"])], w["filter_t"][:-len(w["test_h"])],
                         w["filter_r"][:-len(w["test_h"])]], 1)
-        for name, arr in (("train2id.txt", trn), ("valid2id.txt", np.zeros((0, 3), np.int64)),
-                          ("test2id.txt", np.stack([th, tt, tr], 1))):
+        # one valid triple, a copy of a test triple already in the filter set (a duplicate in
+        # Base.so's tripleList changes no filtered rank): Reader.h:255-256 reads validList[0]
+        # and validList[validTotal - 1] unguarded, so validTotal = 0 indexes a zero-size calloc
+        # and crashes the process intermittently
+        tst = np.stack([th, tt, tr], 1)
+        for name, arr in (("train2id.txt", trn), ("valid2id.txt", tst[:1]), ("test2id.txt", tst)):
             with open(os.path.join(tmp, name), "w") as f:
                 f.write(f"{len(arr)}\n")
                 np.savetxt(f, arr, fmt="%d")
