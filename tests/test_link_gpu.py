@@ -292,3 +292,45 @@ def test_pipelined_launch_finish_matches_run():
     ta, tb = evs[0].launch(), evs[1].launch()
     (m0, c0), (m1, c1) = evs[0].finish(ta), evs[1].finish(tb)
     assert np.array_equal(c0, ref[0][1]) and np.array_equal(c1, ref[1][1]) and m1 == ref[1][0]
+
+
+@pytest.mark.parametrize("config", ["c3", "c4", "c5"])
+def test_full_size_configs(oracle_mod, config):
+    """BASELINE configs C3 (DB15K-ZS ComplEx d=200, MFMA), C4 (FB15K-237-ZS RotatE d=512) and C5
+    (synthetic |E| = 1M DistMult d=256, MFMA) at full size, through the bench's workloads:
+    size-independent properties on every sweep (filtered <= raw <= E - 1, raw - filtered <= the
+    query's filter list) + bit-exact counts and truth scores vs the oracle on a seeded subset."""
+    from mmre.link import FilterIndex
+    from mmre.workloads import synthetic_large, zs_workload
+    if config == "c5":
+        w = synthetic_large()
+    else:
+        w = zs_workload(*{"c3": ("DB15K-ZS", "complex", 200), "c4": ("FB15K-237-ZS", "rotate", 512)}[config])
+    model, E, R = w["model"], int(w["n_ent"]), int(w["n_rel"])
+    np_ = lambda k: None if k not in w else w[k].numpy()
+    ent, rel, ent_im, rel_im = np_("ent"), np_("rel"), np_("ent_im"), np_("rel_im")
+    margin = w.get("margin")
+    spec = _spec_from(model, ent, rel, ent_im, rel_im, margin=margin, dim=w["dim"], eps=w.get("epsilon", 2.0))
+    h, r, t = (np.asarray(w[k], np.int64) for k in ("test_h", "test_r", "test_t"))
+    n = len(h)
+    qh, qr, qt = np.concatenate([h, h]), np.concatenate([r, r]), np.concatenate([t, t])
+    qm = np.concatenate([np.zeros(n, np.int8), np.ones(n, np.int8)])
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, R)
+    out = _run(spec, qh, qr, qt, qm, index=index, scores=False)
+    c = out["counts"]
+    assert np.all(c[0] >= c[1]) and np.all(c[1] >= 0) and np.all(c[0] <= E - 1)
+    off, _ = index.filters(qh, qr, qt, qm)
+    assert np.all(c[0] - c[1] <= np.diff(off))
+    rng = np.random.default_rng(1)
+    sub = rng.choice(2 * n, 8 if config == "c5" else 24, replace=False)
+    hrt = oracle_mod.sorted_hrt(w["filter_h"], w["filter_r"], w["filter_t"])
+    okw = dict(ent_im=ent_im, rel_im=rel_im, norm_flag=False, margin=margin, phase_denom=spec.phase_denom)
+    for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+        s = np.sort(sub[qm[sub] == mode_id])
+        if len(s) == 0:
+            continue
+        o_pred = oracle_mod.link_predict(model, mode, ent, rel, qh[s], qr[s], qt[s], **okw)
+        o_c = oracle_mod.test_rank(mode, o_pred, qh[s], qr[s], qt[s], hrt)
+        assert np.array_equal(c[:, s].T[:, :2], o_c[:, :2])
+        truth_ids = qh[s] if mode_id == 0 else qt[s]
+        assert np.array_equal(out["truth"][s], o_pred[np.arange(len(s)), truth_ids])
