@@ -135,10 +135,12 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
                                                       const int64_t* __restrict__ qh, const int64_t* __restrict__ qr,
                                                       const int64_t* __restrict__ qt, const int8_t* __restrict__ qmode,
                                                       int64_t n_query, float* __restrict__ out, int64_t q_pad,
-                                                      int32_t* __restrict__ qtrue, float* __restrict__ q_rows) {
+                                                      int32_t* __restrict__ qtrue, float* __restrict__ q_rows,
+                                                      int rel_norm) {
   extern __shared__ float lds[];
   __shared__ int64_t s_anchor[32], s_rel[32];
   __shared__ int s_head[32];
+  __shared__ float s_rnorm[32];
   const int np = n_planes(model);
   const int kt = np * kp, ls = kt + 1;
   const int lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
@@ -156,6 +158,22 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
     s_anchor[threadIdx.x] = a;
     s_rel[threadIdx.x] = r;
     s_head[threadIdx.x] = head;
+    if (rel_norm) {  // TransE norm_flag: F.normalize of the relation row (TransE.py:63-66), in
+                     // k_prep_rows' canonical order, so r / |r| is bit-identical to its output
+      const float* rp = rel + r * dim;
+      float ss = 0.0f;
+      int k = 0;
+      for (; k + 16 <= dim; k += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = rp[k + u];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) ss = ss + v[u] * v[u];
+      }
+      for (; k < dim; ++k) ss = ss + rp[k] * rp[k];
+      const float nr = sqrtf(ss);
+      s_rnorm[threadIdx.x] = nr < 1e-12f ? 1e-12f : nr;
+    }
   }
   __syncthreads();
   for (int i = slot; i < rb; i += 8) {
@@ -181,7 +199,7 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
       if (model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2) {
         // head_batch: score = h + (r - t) -> q = -(r - t); tail_batch: (h + r) - t -> q = h + r
         // (TransE.py:71-74). |q - e| reproduces both element-wise bit-for-bit.
-        const float b = rel[r * dim + k];
+        const float b = rel_norm ? rel[r * dim + k] / s_rnorm[i] : rel[r * dim + k];
         x[k] = head ? -(b - x[k]) : (x[k] + b);
       } else if (model == MMRE_DISTMULT) {  // head: h*(r*t) ; tail: (h*r)*t  (DistMult.py:37-42)
         const float b = rel[r * dim + k];
@@ -1091,21 +1109,15 @@ extern "C" int mmre_link_prepare_queries(int model, int norm_flag, const float* 
   if (transe && norm_flag && !d_rel_work) return MMRE_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const int kp = plane_rows(model, dim), kt = n_planes(model) * kp;
-  const float* rel = d_rel;
-  if (transe && norm_flag) {  // normalised relation rows (TransE.py:63-66) into d_rel_work (n_rel, dim)
-    const int rb = stage_rows(kp);
-    hipLaunchKernelGGL(k_prep_rows, dim3((unsigned)((n_rel + rb - 1) / rb)), dim3(256),
-                       sizeof(float) * (size_t)rb * (kp + 1), st, model, 1, d_rel, (const float*)nullptr, n_rel, dim,
-                       kp, rb, (float*)nullptr, (int64_t)0, d_rel_work, dim);
-    MMRE_CHECK_LAUNCH();
-    rel = d_rel_work;
-  }
+  // TransE norm_flag: each query block normalises its relation rows itself (no separate
+  // relation-prep launch; d_rel_work stays part of the ABI as caller-provided scratch)
+  const int rel_norm = (transe && norm_flag) ? 1 : 0;
   const int rb = stage_rows(kt);
   const size_t lds = sizeof(float) * (size_t)rb * (kt + 1);
   if (lds > 64 * 1024) return MMRE_ERR_SHAPE;
   hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((q_pad + rb - 1) / rb)), dim3(256), lds, st, model, d_ent_rows,
-                     rel, d_rel_im, dim, kp, rb, phase_denom, d_qh, d_qr, d_qt, d_qmode, n_query, d_q_km, q_pad,
-                     d_q_true, d_q_rows);
+                     d_rel, d_rel_im, dim, kp, rb, phase_denom, d_qh, d_qr, d_qt, d_qmode, n_query, d_q_km, q_pad,
+                     d_q_true, d_q_rows, rel_norm);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
