@@ -125,7 +125,7 @@ class ShardedLinkEvaluation:
             raise RuntimeError("ShardedLinkEvaluation: finish() a ticket before launching a third")
         c = self.counts(events)
         if not c.is_cuda:
-            return (c.numpy(), None)
+            return [c.numpy(), None]
         hosts = getattr(self, "_hosts", None)
         if hosts is None or hosts[0].shape != c.shape:
             hosts = self._hosts = [torch.empty(c.shape, dtype=c.dtype, pin_memory=True) for _ in range(2)]
@@ -137,7 +137,7 @@ class ShardedLinkEvaluation:
         done = torch.cuda.Event()
         done.record(torch.cuda.current_stream(c.device))
         self._outstanding += 1
-        return (h, done)
+        return [h, done]
 
     def finish(self, ticket, copy_counts=True):
         """Wait for a launch() ticket's counts (its own event only) and run the Test.h metric
@@ -145,6 +145,9 @@ class ShardedLinkEvaluation:
         buffer itself (reused two launches later)."""
         from .link import link_metrics
         c, done = ticket
+        if c is None:
+            raise RuntimeError("ShardedLinkEvaluation: this ticket was already finished")
+        ticket[0] = None
         if done is not None:
             done.synchronize()
             self._outstanding -= 1

@@ -286,6 +286,8 @@ def test_pipelined_launch_finish_matches_run():
         ev.launch()  # a third ticket would overwrite a pinned buffer still unread
     ma, ca = ev.finish(a)
     mb, cb = ev.finish(b)
+    with pytest.raises(RuntimeError):
+        ev.finish(b)  # a ticket is finished once
     assert np.array_equal(ca, ref[0][1]) and np.array_equal(cb, ref[0][1])
     assert ma == ref[0][0] and mb == ref[0][0]
     # overlapping tickets of two snapshots keep their own buffers
