@@ -15,7 +15,6 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
-import contextlib
 import ctypes
 import json
 import os
@@ -37,6 +36,9 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9   # 256 CUs x 4 SIMD-32 x 2.4 GHz (lane-ops/s)
 
 CONFIGS = {
+    "c1": dict(dataset="FB15K-237-ZS", model="transe", dim=100, norm=True, n_test=1000,
+               workload="C1 FB15K-237-ZS TransE d=100 p=1 norm_flag, filtered link prediction of the first 1,000 "
+                        "test triples (Test.h order)"),
     "c2": dict(dataset="FB15K-237-ZS", model="transe", dim=200, norm=True,
                workload="C2 FB15K-237-ZS TransE d=200 p=1 norm_flag, filtered link prediction"),
     "c3": dict(dataset="DB15K-ZS", model="complex", dim=200, norm=False,
@@ -92,124 +94,121 @@ def pmc_traffic(config: str, model: str):
     return None, None
 
 
-@contextlib.contextmanager
-def stdout_to_stderr():
-    """Base.so printf()s to fd 1; keep rank 0's stdout a single JSON line."""
-    sys.stdout.flush()
-    saved = os.dup(1)
-    os.dup2(2, 1)
-    try:
-        yield
-    finally:
-        sys.stdout.flush()
-        os.dup2(saved, 1)
-        os.close(saved)
+REF_SAMPLE = {"c1": 1000, "c2": 1000, "c3": 1000, "c4": 10, "c5": 24}   # test triples in the CPU leg
 
 
-def cpu_baseline(w, n_sample: int, use_reference: bool = True):
-    """The reference's CPU path on this host's cores: the OpenKE Tester loop
-    (Tester.py:70-91) = Base.so getHeadBatch -> TransE.predict on torch CPU (the op sequence of
-    TransE.py:62-76: gather, F.normalize, h + (r - t) / (h + r) - t, torch.norm p=1) ->
-    Base.so testHead/testTail. Base.so is the reference's own C++ (oracle/_ref, compiled from
-    /root/reference/OpenKE/openke/base/Base.cpp); without it the oracle's ranker is used."""
-    import torch.nn.functional as F
-    E, d = w["n_ent"], w["dim"]
-    ent, rel = w["ent"].float(), w["rel"].float()
+def ref_tester_leg(w, n_sample: int, timeout_s: int = 600):
+    """The reference's CPU path on this host's cores, as a child process (oracle/ref_tester.py:
+    the OpenKE Tester loop with the reference's own Base.so ranker -- oracle/_ref, compiled
+    from /root/reference/OpenKE/openke/base/Base.cpp -- and the reference models' predict op
+    sequences on torch CPU). The first n_sample test triples (Test.h order) are its test set;
+    train2id holds the rest of the workload's filter set, so Base.so filters with exactly the
+    triples the GPU evaluation filters with. Returns the child's result (per-query raw /
+    filtered counts read from Base.so's rank accumulators, near ties, Base.so's metrics, time),
+    or None if the reference library is absent or the child fails."""
+    import shutil
+    import subprocess
     ref_so = os.path.join(REPO, "oracle", "_ref", "Base.so")
-    kind = "reference" if use_reference and os.path.exists(ref_so) else "port"
-    n = min(n_sample, len(w["test_h"]))
-    th, tr, tt = w["test_h"][:n], w["test_r"][:n], w["test_t"][:n]
-
-    def predict(ph, pt, pr, mode):
-        h = F.normalize(ent[ph], 2, -1)
-        r = F.normalize(rel[pr], 2, -1)
-        t = F.normalize(ent[pt], 2, -1)
-        h = h.view(-1, r.shape[0], h.shape[-1])
-        t = t.view(-1, r.shape[0], t.shape[-1])
-        r = r.view(-1, r.shape[0], r.shape[-1])
-        s = h + (r - t) if mode == "head_batch" else (h + r) - t
-        return torch.norm(s, 1, -1).flatten().cpu().data.numpy()
-
-    if kind == "reference":
-        tmp = tempfile.mkdtemp(prefix="mmre_cpu_")
-        trn = np.stack([w["filter_h"][:-len(w["test_h"])], w["filter_t"][:-len(w["test_h"])],
-                        w["filter_r"][:-len(w["test_h"])]], 1)
-        # one valid triple, a copy of a test triple already in the filter set (a duplicate in
-        # Base.so's tripleList changes no filtered rank): Reader.h:255-256 reads validList[0]
-        # and validList[validTotal - 1] unguarded, so validTotal = 0 indexes a zero-size calloc
-        # and crashes the process intermittently
+    if not os.path.exists(ref_so):
+        print("cpu_baseline: oracle/_ref/Base.so absent (build() compiles it where /root/reference exists)",
+              file=sys.stderr)
+        return None
+    n = min(int(n_sample), len(w["test_h"]))
+    tmp = tempfile.mkdtemp(prefix="mmre_ref_")
+    try:
+        th, tr, tt = (np.asarray(w[k][:n], np.int64) for k in ("test_h", "test_r", "test_t"))
+        fh, fr, ft = (np.asarray(w[k], np.int64) for k in ("filter_h", "filter_r", "filter_t"))
+        # filter set minus one copy of each sampled test triple -> train2id
+        keep = np.ones(len(fh), bool)
+        key = (fh * w["n_rel"] + fr) * w["n_ent"] + ft
+        skey = (th * w["n_rel"] + tr) * w["n_ent"] + tt
+        pos = {}
+        for i, k in enumerate(key.tolist()):
+            pos.setdefault(k, i)
+        for k in skey.tolist():
+            if k in pos:
+                keep[pos.pop(k)] = False
+        trn = np.stack([fh[keep], ft[keep], fr[keep]], 1)
         tst = np.stack([th, tt, tr], 1)
+        # one valid triple, a copy of a sampled test triple (already in the filter set): Reader.h:255-256
+        # reads validList[0] unguarded, so an empty valid2id.txt crashes Base.so intermittently
         for name, arr in (("train2id.txt", trn), ("valid2id.txt", tst[:1]), ("test2id.txt", tst)):
             with open(os.path.join(tmp, name), "w") as f:
                 f.write(f"{len(arr)}\n")
                 np.savetxt(f, arr, fmt="%d")
-        for name, cnt in (("entity2id.txt", E), ("relation2id.txt", w["n_rel"])):
+        for name, cnt in (("entity2id.txt", w["n_ent"]), ("relation2id.txt", w["n_rel"])):
             with open(os.path.join(tmp, name), "w") as f:
                 f.write(f"{cnt}\n")
-        lib = ctypes.CDLL(ref_so)
-        P, I = ctypes.c_void_p, ctypes.c_int64
-        lib.setInPath.argtypes = [ctypes.c_char_p]
-        lib.getHeadBatch.argtypes = [P, P, P]
-        lib.getTailBatch.argtypes = [P, P, P]
-        lib.testHead.argtypes = [P, I, I]
-        lib.testTail.argtypes = [P, I, I]
-        lib.test_link_prediction.argtypes = [I]
-        with stdout_to_stderr():
-            lib.setInPath((tmp + "/").encode())
-            lib.importTrainFiles()
-            lib.importTestFiles()
-            lib.initTest()
-        ph, pt, pr = (np.zeros(E, np.int64) for _ in range(3))
-        t0 = time.perf_counter()
-        with stdout_to_stderr():
-            for idx in range(n):
-                lib.getHeadBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
-                s = predict(torch.from_numpy(ph), torch.from_numpy(pt[:1]), torch.from_numpy(pr[:1]), "head_batch")
-                lib.testHead(s.ctypes.data, idx, 0)
-                lib.getTailBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
-                s = predict(torch.from_numpy(ph[:1]), torch.from_numpy(pt), torch.from_numpy(pr[:1]), "tail_batch")
-                lib.testTail(s.ctypes.data, idx, 0)
-            lib.test_link_prediction(0)
-        elapsed = time.perf_counter() - t0
-    else:
-        import oracle
-        hrt = oracle.sorted_hrt(w["filter_h"], w["filter_r"], w["filter_t"])
-        t0 = time.perf_counter()
-        for i in range(n):
-            for mode in ("head_batch", "tail_batch"):
-                if mode == "head_batch":
-                    s = predict(torch.arange(E), torch.tensor([tt[i]]), torch.tensor([tr[i]]), mode)
-                else:
-                    s = predict(torch.tensor([th[i]]), torch.arange(E), torch.tensor([tr[i]]), mode)
-                oracle.test_rank(mode, s[None, :], th[i:i + 1], tr[i:i + 1], tt[i:i + 1], hrt)
-        elapsed = time.perf_counter() - t0
-    triples = 2 * n * E
-    return {"value": triples / elapsed, "unit": "scored triples/s", "cores": torch.get_num_threads(),
-            "kind": kind,
-            "sample": f"{n} FB15K-237-ZS test triples x {{head,tail}} = {2 * n} sweeps x {E} entities through the "
-                      f"OpenKE Tester loop (torch {torch.__version__} CPU TransE.predict op sequence + "
-                      f"{'reference Base.so' if kind == 'reference' else 'oracle'} testHead/testTail), "
-                      f"{elapsed:.2f} s on {torch.get_num_threads()} threads"}
-
-
-def cpu_baseline_isolated(config: str, w, n_sample: int):
-    """cpu_baseline in a child process (CPU only, it never touches the GPU): the reference's
-    Base.so is C++ with unguarded indexing, so a crash inside it must not take
-    the bench line with it. If the child fails, the oracle's ranker ("port") is timed here."""
-    import subprocess
-    cfg = CONFIGS[config]
-    code = ("import json, sys; sys.argv = ['bench.py']; import bench; from mmre.workloads import zs_workload; "
-            f"w = zs_workload({cfg['dataset']!r}, {cfg['model']!r}, {cfg['dim']}); "
-            f"print('CPU_BASELINE ' + json.dumps(bench.cpu_baseline(w, {int(n_sample)})), flush=True)")
-    try:
-        r = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=600)
-        for line in r.stdout.splitlines():
-            if line.startswith("CPU_BASELINE "):
-                return json.loads(line[len("CPU_BASELINE "):])
-        print(f"cpu_baseline child failed (rc {r.returncode}); timing the oracle port instead", file=sys.stderr)
+        tables = {"ent": w["ent"].numpy(), "rel": w["rel"].numpy()}
+        if "ent_im" in w:
+            tables.update(ent_im=w["ent_im"].numpy(), rel_im=w["rel_im"].numpy())
+        np.savez(os.path.join(tmp, "tables.npz"), **tables)
+        meta = dict(model=w["model"], dim=w["dim"], norm_flag=bool(w.get("norm_flag", False)),
+                    margin=w.get("margin"), epsilon=w.get("epsilon"), threads=torch.get_num_threads())
+        with open(os.path.join(tmp, "meta.json"), "w") as f:
+            json.dump(meta, f)
+        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "ref_tester.py"), tmp], cwd=REPO,
+                           capture_output=True, text=True, timeout=timeout_s)
+        if r.returncode != 0 or not os.path.exists(os.path.join(tmp, "result.npz")):
+            print(f"cpu_baseline: ref_tester failed (rc {r.returncode}): {r.stderr[-800:]}", file=sys.stderr)
+            return None
+        with np.load(os.path.join(tmp, "result.npz"), allow_pickle=False) as z:
+            out = {k: z[k] for k in z.files}
+        out["n"] = n
+        return out
     except subprocess.TimeoutExpired:
-        print("cpu_baseline child timed out; timing the oracle port instead", file=sys.stderr)
-    return cpu_baseline(w, n_sample, use_reference=False)
+        print("cpu_baseline: ref_tester timed out", file=sys.stderr)
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def cpu_baseline_block(ref, w):
+    E, n = int(ref["n_ent"]), int(ref["n"])
+    el = float(ref["elapsed"])
+    note = ""
+    if w["model"] == "rotate":
+        note = (" RotatE: ~99% of the reference's CPU time is torch.norm over the size-2 stacked dim "
+                "(RotatE.py:74-75), a CPU pathology of the reference path that inflates GPU/CPU ratios.")
+    return {"value": 2 * n * E / el, "unit": "scored triples/s", "cores": int(ref["threads"]), "kind": "reference",
+            "sample": f"first {n} {w['dataset']} test triples (Test.h order) x {{head,tail}} = {2 * n} sweeps x {E} "
+                      f"entities through the OpenKE Tester loop: reference Base.so getHeadBatch/testHead/testTail "
+                      f"(oracle/_ref) + the reference {w['model']} predict op sequence on torch {torch.__version__} "
+                      f"CPU (oracle/ref_tester.py), {el:.2f} s on {int(ref['threads'])} threads.{note}"}
+
+
+def parity_block(ref, counts, n_total, w):
+    """GPU per-query counts vs the reference Base.so's on the cpu_baseline sample: raw and
+    filtered counts query by query, the sample's hit@{1,3,10} / MR / MRR from both sides (the
+    GPU's through the P14 reduction of its counts, Base.so's from getTestLink*), and whether
+    every mismatch lies within that sweep's near ties (entities within tie_rel x max|score| of
+    the truth on the reference scores: the only ones a different summation order can move)."""
+    from mmre.link import link_metrics
+    n = int(ref["n"])
+    q = ref["q"]
+    same_q = bool(np.array_equal(q[:, 0], w["test_h"][:n]) and np.array_equal(q[:, 1], w["test_r"][:n])
+                  and np.array_equal(q[:, 2], w["test_t"][:n]))
+    gh = counts[:, :n].T.astype(np.int64)                  # (n, 4) raw, filt, raw_tc, filt_tc
+    gt = counts[:, n_total:n_total + n].T.astype(np.int64)
+    ref_c = ref["counts"]                                   # (2, n, 2) [head|tail][q][raw, filt]
+    gpu_c = np.stack([gh[:, :2], gt[:, :2]])
+    diff = np.abs(gpu_c - ref_c)                            # (2, n, 2)
+    ties = ref["near_ties"][:, :, None]                     # (2, n, 1)
+    mism = diff != 0
+    unexplained = mism & (diff > ties)
+    gm = link_metrics(counts[:, :n], counts[:, n_total:n_total + n])["filter"]
+    rm = ref["metrics"]  # MRR, MR, hit10, hit3, hit1 (filter, Test.h:232-327)
+    gpu_vals = np.array([gm["mrr"], gm["mr"], gm["hit10"], gm["hit3"], gm["hit1"]], np.float32)
+    return {"source": "reference Base.so Tester loop on the cpu_baseline sample (oracle/ref_tester.py)",
+            "test_triples": n, "sweeps": 2 * n, "queries_match": same_q,
+            "raw_mismatches": int(mism[:, :, 0].sum()), "filt_mismatches": int(mism[:, :, 1].sum()),
+            "unexplained_mismatches": int(unexplained.sum()),
+            "near_tie_sweeps": int((ref["near_ties"] > 0).sum()), "tie_rel": float(ref["tie_rel"]),
+            "hit1_gpu": float(gm["hit1"]), "hit3_gpu": float(gm["hit3"]), "hit10_gpu": float(gm["hit10"]),
+            "mr_gpu": float(gm["mr"]), "mrr_gpu": float(gm["mrr"]),
+            "hit1_ref": float(rm[4]), "hit3_ref": float(rm[3]), "hit10_ref": float(rm[2]), "mr_ref": float(rm[1]),
+            "mrr_ref": float(rm[0]),
+            "metrics_bit_equal": bool(np.array_equal(gpu_vals.view(np.uint32), rm.astype(np.float32).view(np.uint32)))}
 
 
 def cpu_baseline_zsl(w, budget_s: float = 15.0, max_queries: int = 400):
@@ -628,13 +627,16 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-sample", type=int, default=1000, help="test triples in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="test triples in the CPU-baseline / parity sample (0: per-config default)")
+    ap.add_argument("--train-steps", type=int, default=300,
+                    help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     from mmre.link import FilterIndex, ScoreSpec, rotate_phase_denom
     from mmre.sharding import ShardedLinkEvaluation
-    from mmre.workloads import synthetic_large, zs_workload
+    from mmre.workloads import synthetic_large, train_transe, zs_workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -658,8 +660,16 @@ def main():
     if cfg["dataset"] == "synthetic-1M":
         w = synthetic_large()
     else:
-        w = zs_workload(cfg["dataset"], cfg["model"], cfg["dim"])
+        w = zs_workload(cfg["dataset"], cfg["model"], cfg["dim"], n_test=cfg.get("n_test"))
+    w["norm_flag"] = cfg["norm"]
     model, dim = cfg["model"], cfg["dim"]
+    if model == "transe" and args.train_steps > 0:
+        train_transe(w, dev, steps=args.train_steps)
+        if dist:  # every rank evaluates rank 0's tables (float atomics make training run-dependent)
+            for k in ("ent", "rel"):
+                t = w[k].to(dev)
+                dist.broadcast(t, 0)
+                w[k] = t.cpu()
     E = w["n_ent"]
     n = len(w["test_h"])
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
@@ -672,11 +682,11 @@ def main():
     ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
     n_local = int(ev.masks[rank].sum())
 
-    def steps(n, evs=None):
+    def steps(k, evs=None):
         # evaluation i + 1 is enqueued before the host reduces evaluation i's metrics, so that
         # reduction overlaps the next sweep; every evaluation's metrics are reduced in the loop
         metrics, pending = None, None
-        for i in range(n):
+        for i in range(k):
             ticket = ev.launch(evs[i] if evs else None)
             if pending is not None:
                 metrics = ev.finish(pending, copy_counts=False)[0]
@@ -697,48 +707,67 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if n_local else 0.0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    _, counts = ev.run()  # one more evaluation outside the timed region: the counts the parity check reads
 
     total_triples = 2 * n * E
     value = total_triples * args.steps / elapsed
     if rank == 0:
         bpt = bytes_per_triple(model, dim)
-        achieved = n_local * E * bpt / (sweep_ms * 1e-3) / 1e9
+        triples_launch = n_local * E
+        tps = triples_launch / (sweep_ms * 1e-3) if sweep_ms > 0 else 0.0
         traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
-        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes per launch",
-                "traffic_source": tsrc, "kernel": KERNEL_NAMES[model], "kernel_ms": sweep_ms,
-                "bytes_per_triple": bpt, "triples_per_launch": n_local * E,
-                "note": "algorithmic bytes per SURVEY 8(d); the sweep reuses each entity row across a "
-                        "128-query LDS tile, so frac > 1 is expected -- the binding roof for TransE/RotatE "
-                        "is VALU (valu_frac), for DistMult/ComplEx f32 MFMA"}
         if model in ("distmult", "complex"):
-            fl = 2.0 * dim * (2 if model == "complex" else 1) * n_local * E / (sweep_ms * 1e-3)
-            roof["mfma_achieved_tflops"] = fl / 1e12
-            roof["mfma_frac"] = fl / 157.3e12
-        vo = valu_ops_per_triple(model, dim)
-        if vo:
-            tps = n_local * E / (sweep_ms * 1e-3)
-            roof["valu_bound_triples_per_s"] = VALU_LANE_OPS / vo
-            roof["valu_frac"] = tps / (VALU_LANE_OPS / vo)
+            flops = 2.0 * dim * (2 if model == "complex" else 1)
+            ach = tps * flops / 1e12
+            roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
+                    "frac": ach * 1e12 / MFMA_F32_PEAK, "flops_per_triple": flops}
+        else:
+            ops = valu_ops_per_triple(model, dim)
+            ach = tps * ops / 1e12
+            roof = {"bound": "valu", "achieved": ach, "peak": VALU_LANE_OPS / 1e12,
+                    "unit": "TOP/s (VALU lane-ops: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz)",
+                    "frac": ach * 1e12 / VALU_LANE_OPS, "valu_ops_per_triple": ops}
+        roof.update({
+            "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE)",
+            "traffic_source": tsrc, "kernel": KERNEL_NAMES[model], "kernel_ms": sweep_ms,
+            "triples_per_launch": triples_launch, "bytes_per_triple": bpt,
+            "hbm_algorithmic_x": tps * bpt / (HBM_PEAK_GBS * 1e9),
+            "hbm_measured_GBs": (traffic / (sweep_ms * 1e-3) / 1e9) if traffic and sweep_ms else None,
+            "note": "binding roof: VALU for TransE/RotatE (|q-e| per element: sub + add-with-abs), f32 MFMA for "
+                    "DistMult/ComplEx. hbm_algorithmic_x = SURVEY 8(d) algorithmic bytes (one entity row per "
+                    "scored triple) / 8 TB/s: > 1 because each entity row is reused across a 128-query LDS tile; "
+                    "the measured HBM traffic is in traffic / hbm_measured_GBs"})
+        data = {"c1": "synthetic TransE tables trained on the FB15K-237-ZS test triples",
+                "c2": "synthetic TransE tables trained on the FB15K-237-ZS test triples",
+                "c5": "synthetic 1M-entity DistMult tables (OpenKE xavier init, seed 0) and 4,096 random test "
+                      "triples (= the filter set)"}.get(args.config, f"synthetic {model} tables (OpenKE init, seed 0)")
+        if args.config != "c5":
+            data += (f" ({args.train_steps} steps of this build's HIP trainer: bit-exact OpenKE sampler + fused margin"
+                     f" loss, SGD 1.0, margin 5, neg 25)" if "trained" in w else "") + \
+                f" over the real {w['dataset']} test triples; filter set = all test triples + 272,115 synthetic train"
         out = {"metric": METRIC if args.config == "c2" else f"scored triples/sec, {cfg['workload']}",
                "value": value, "unit": "scored triples/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "strong", "vs_baseline": None, "dtype": "f32",
-               "data": "synthetic tables (OpenKE xavier/uniform init, seed 0) over the real test triples; "
-                       "filter set = test + 272,115 synthetic train triples",
+               "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
                "config": {"workload": cfg["workload"], "n_entities": E, "dim": dim, "n_sweeps": 2 * n,
                           "parallelism": f"relation-sharded x{world} (LPT), RCCL all-gather of rank counts"},
                "roofline": roof,
-               "parity": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
-                          "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
-                          "mr": metrics["filter"]["mr"]}}
-        if world == 1 and not args.no_cpu_baseline and model == "transe":
-            out["cpu_baseline"] = cpu_baseline_isolated(args.config, w, args.cpu_sample)
+               "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
+                           "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
+                           "mr": metrics["filter"]["mr"]},
+               "parity": None}
+        if "trained" in w:
+            out["config"]["tables"] = w["trained"]
+        if world == 1 and not args.no_cpu_baseline:
+            ref = ref_tester_leg(w, args.cpu_sample or REF_SAMPLE[args.config])
+            if ref is not None:
+                out["cpu_baseline"] = cpu_baseline_block(ref, w)
+                out["parity"] = parity_block(ref, counts, n, w)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -190,6 +190,9 @@ class LinkSweep:
         s = self.spec
         n = int(qh.shape[0])
         if n == 0:  # e.g. a rank that owns no test relation (world > #relations): nothing to sweep
+            if sweep_events is not None:  # keep the caller's timing events valid (an empty interval)
+                sweep_events[0].record()
+                sweep_events[1].record()
             z = torch.empty((4, 0), dtype=torch.int32, device=self.device)
             return dict(counts=z, truth=torch.empty(0, dtype=torch.float32, device=self.device),
                         scores=torch.empty((0, self.n_ent), dtype=torch.float32, device=self.device)

@@ -99,7 +99,11 @@ class ShardedLinkEvaluation:
         if index is not None:
             self.filt = tuple(to(a) for a in index.groups(qh[mine], qr[mine], qt[mine], qm[mine]))
             if type_constrain:
-                self.masks_tc = tuple(to(m) for m in index.type_masks())
+                tm = index.type_masks()
+                if tm is None:
+                    raise ValueError("type_constrain=True needs the FilterIndex's type constraints "
+                                     "(type_constrain.txt, Reader.h:266-317)")
+                self.masks_tc = tuple(to(m) for m in tm)
         self.plan = ShardPlan(self.masks, dev) if self.world > 1 else None
         if local_runner is None:
             from .link import LinkSweep
@@ -118,42 +122,44 @@ class ShardedLinkEvaluation:
 
     def launch(self, events=None):
         """Enqueue one evaluation -- sweep, (world > 1) all-gather, and the D2H of the count
-        table into the next of two pinned buffers -- without waiting for it. Returns a ticket
-        for finish(). At most two tickets may be outstanding (the pinned buffers alternate), so
-        the host metric reduction of evaluation i can run while the GPU sweeps i + 1."""
-        if getattr(self, "_outstanding", 0) >= 2:
+        table into a free one of two pinned buffers -- without waiting for it. Returns a ticket
+        for finish(). Each ticket owns its buffer until it is finished (in any order), so at
+        most two may be outstanding: the host metric reduction of evaluation i runs while the
+        GPU sweeps i + 1."""
+        free = getattr(self, "_free", None)
+        if free is not None and not free:
             raise RuntimeError("ShardedLinkEvaluation: finish() a ticket before launching a third")
         c = self.counts(events)
         if not c.is_cuda:
-            return [c.numpy(), None]
+            return [c.numpy(), None, None]
         hosts = getattr(self, "_hosts", None)
         if hosts is None or hosts[0].shape != c.shape:
+            if free is not None and len(free) != 2:
+                raise RuntimeError("ShardedLinkEvaluation: count shape changed with tickets outstanding")
             hosts = self._hosts = [torch.empty(c.shape, dtype=c.dtype, pin_memory=True) for _ in range(2)]
-            self._next = 0
-            self._outstanding = 0
-        h = hosts[self._next]
-        self._next ^= 1
+            free = self._free = [0, 1]
+        slot = free.pop(0)
+        h = hosts[slot]
         h.copy_(c, non_blocking=True)
         done = torch.cuda.Event()
         done.record(torch.cuda.current_stream(c.device))
-        self._outstanding += 1
-        return [h, done]
+        return [h, done, slot]
 
     def finish(self, ticket, copy_counts=True):
         """Wait for a launch() ticket's counts (its own event only) and run the Test.h metric
-        reduction: (metrics, counts (4, 2n) int32). copy_counts=False returns the pinned
-        buffer itself (reused two launches later)."""
+        reduction: (metrics, counts (4, 2n) int32). The ticket's pinned buffer is free again
+        afterwards; copy_counts=False returns that buffer itself (valid until the next launch)."""
         from .link import link_metrics
-        c, done = ticket
+        c, done, slot = ticket
         if c is None:
             raise RuntimeError("ShardedLinkEvaluation: this ticket was already finished")
         ticket[0] = None
         if done is not None:
             done.synchronize()
-            self._outstanding -= 1
             c = c.numpy()
             if copy_counts:
                 c = c.copy()
+            self._free.append(slot)
         return link_metrics(c[:, :self.n], c[:, self.n:]), c
 
     def run(self, events=None, copy_counts=True):

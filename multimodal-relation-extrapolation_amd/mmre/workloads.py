@@ -23,7 +23,9 @@ def xavier(rows, cols, gen):
 
 
 def zs_workload(dataset: str = "FB15K-237-ZS", model: str = "transe", dim: int = 200, seed: int = 0,
-                margin: float = 6.0, epsilon: float = 2.0, n_train: int = FB15K237_TRAIN):
+                margin: float = 6.0, epsilon: float = 2.0, n_train: int = FB15K237_TRAIN, n_test: int | None = None):
+    """n_test: evaluate only the first n_test test triples in Test.h order (C1: 1,000); the
+    filter set keeps every test triple."""
     z = load_zs_test(dataset)
     E, R = int(z["n_ent"]), int(z["n_rel"])
     gen = torch.Generator().manual_seed(seed)
@@ -50,6 +52,8 @@ def zs_workload(dataset: str = "FB15K-237-ZS", model: str = "transe", dim: int =
     w["filter_h"] = np.concatenate([th, h])
     w["filter_r"] = np.concatenate([tr, r])
     w["filter_t"] = np.concatenate([tt, t])
+    if n_test is not None:
+        w["test_h"], w["test_r"], w["test_t"] = h[:n_test], r[:n_test], t[:n_test]
     return w
 
 
@@ -59,10 +63,45 @@ def synthetic_large(n_ent=1_000_000, n_rel=235, dim=256, n_query=8192, seed=0):
     rng = np.random.default_rng(seed + 1)
     w = dict(dataset="synthetic-1M", model="distmult", dim=dim, n_ent=n_ent, n_rel=n_rel,
              ent=xavier(n_ent, dim, gen), rel=xavier(n_rel, dim, gen))
-    w["test_h"] = rng.integers(0, n_ent, n_query // 2)
-    w["test_r"] = rng.integers(0, n_rel, n_query // 2)
-    w["test_t"] = rng.integers(0, n_ent, n_query // 2)
+    h = rng.integers(0, n_ent, n_query // 2)
+    r = rng.integers(0, n_rel, n_query // 2)
+    t = rng.integers(0, n_ent, n_query // 2)
+    # Test.h order (testList sorted by (r, h, t), Reader.h:227)
+    w["test_h"], w["test_r"], w["test_t"] = sorted_rel2(np.stack([h, t, r], 1))
     w["filter_h"], w["filter_r"], w["filter_t"] = w["test_h"], w["test_r"], w["test_t"]
+    return w
+
+
+def train_transe(w, device, steps: int = 300, batch: int = 2721, neg: int = 25, margin: float = 5.0,
+                 lr: float = 1.0, bern: bool = True):
+    """Give the evaluation non-degenerate tables: `steps` OpenKE TransE training steps
+    (OpenKE/examples/train_transe_FB15K237.py: p=1, norm_flag, MarginLoss(5.0), neg_ent 25,
+    bern, SGD alpha 1.0) on the workload's test triples, through this build's own training
+    path -- the bit-exact GPU sampler (mmre.sampler.OpenKESampler) and the fused HIP loss
+    (mmre.ns.fused_ns_loss) -- so the truths rank near the top instead of around E / 2.
+    Replaces w["ent"] / w["rel"] (CPU float32) and records the steps in w["trained"]."""
+    from .data import TrainIndex
+    from .ns import NSSpec, fused_ns_loss
+    from .sampler import OpenKESampler
+    if w["model"] != "transe":
+        raise ValueError("train_transe trains TransE tables")
+    dev = torch.device(device)
+    idx = TrainIndex(w["test_h"], w["test_t"], w["test_r"], w["n_ent"], w["n_rel"])
+    smp = OpenKESampler(idx, dev, bern=bern)
+    ent = w["ent"].to(dev).clone().requires_grad_(True)
+    rel = w["rel"].to(dev).clone().requires_grad_(True)
+    spec = NSSpec("transe", w["dim"], norm_flag=bool(w.get("norm_flag", True)))
+    opt = torch.optim.SGD([ent, rel], lr=lr)
+    loss = None
+    for _ in range(int(steps)):
+        b = smp.sample(batch, neg)
+        loss, _ = fused_ns_loss(spec, ent, rel, b["batch_h"], b["batch_t"], b["batch_r"], batch, neg, margin)
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        opt.step()
+    w["ent"], w["rel"] = ent.detach().cpu(), rel.detach().cpu()
+    w["trained"] = dict(steps=int(steps), batch=int(batch), neg=int(neg), margin=float(margin), lr=float(lr),
+                        bern=bool(bern), final_loss=None if loss is None else float(loss.detach().cpu()))
     return w
 
 

@@ -1,0 +1,241 @@
+"""ref_tester.py -- TEST INFRASTRUCTURE ONLY: the reference's CPU link-prediction path, run
+as the bench's `cpu_baseline` leg and as the full-size parity checker of the GPU counts.
+
+It is the OpenKE Tester loop (OpenKE/openke/config/Tester.py:70-91) on this host's cores:
+
+    getHeadBatch (Test.h:36-43) -> model.predict on torch CPU -> testHead (Test.h:65-127)
+    getTailBatch (Test.h:46-53) -> model.predict on torch CPU -> testTail (Test.h:130-192)
+    test_link_prediction (Test.h:232-327) -> getTestLink{MRR,MR,Hit10,Hit3,Hit1}
+
+with the reference's own ranker: ``oracle/_ref/Base.so``, compiled by ``oracle/Makefile``
+from /root/reference/OpenKE/openke/base/Base.cpp (the checker, never the product). The
+``predict_*`` functions below are the reference models' torch op sequences, unchanged in
+order and dtype (TransE.py:46-74 + 88-94, DistMult.py:34-55 + 70-72, ComplEx.py:20-40 +
+60-62, RotatE.py:45-91); ``tests/test_oracle_golden.py`` pins them bit-for-bit against the
+reference's own predictions in tests/golden/link_small.npz.
+
+Per query it also reads Base.so's rank deltas (l_rank / l_filter_rank / r_rank /
+r_filter_rank are float globals holding sums of exact integers below 2^24), so the GPU's
+per-query counts can be compared with the reference's one by one. After the timed loop it
+counts each sweep's near ties on the reference scores -- entities whose score lies within
+``tie_rel`` x max|score| of the truth's -- the only entities whose side of the strict `<`
+(Test.h:83, :147) a different float summation order can flip.
+
+Usage (a child process of bench.py: Base.so is C++ with unguarded indexing):
+    python oracle/ref_tester.py <workdir>
+<workdir> holds the OpenKE files (entity2id / relation2id / train2id / valid2id / test2id),
+tables.npz (ent, rel[, ent_im, rel_im]) and meta.json (model, dim, norm_flag, margin,
+epsilon, threads); the result goes to <workdir>/result.npz.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_BASE_SO = os.path.join(HERE, "_ref", "Base.so")
+
+
+# ----------------------------------------------------------- reference predict --
+def predict_transe(ent, rel, ph, pt, pr, mode, norm_flag=True, p_norm=1, margin=None):
+    """TransE.forward + predict (TransE.py:46-74, 88-94): gather, F.normalize(2, -1),
+    view(-1, R, d), h + (r - t) for head_batch else (h + r) - t, torch.norm(p, -1);
+    predict = margin - (margin - score) with a margin, the score otherwise."""
+    import torch
+    import torch.nn.functional as F
+    h, t, r = ent[ph], ent[pt], rel[pr]
+    if norm_flag:
+        h = F.normalize(h, 2, -1)
+        r = F.normalize(r, 2, -1)
+        t = F.normalize(t, 2, -1)
+    h = h.view(-1, r.shape[0], h.shape[-1])
+    t = t.view(-1, r.shape[0], t.shape[-1])
+    r = r.view(-1, r.shape[0], r.shape[-1])
+    s = h + (r - t) if mode == "head_batch" else (h + r) - t
+    score = torch.norm(s, p_norm, -1).flatten()
+    if margin is not None:
+        m = torch.tensor([margin], dtype=torch.float32)
+        score = m - (m - score)  # forward returns margin - score (:70-71), predict margin - forward (:90-91)
+    return score.cpu().data.numpy()
+
+
+def predict_distmult(ent, rel, ph, pt, pr, mode):
+    """DistMult._calc + predict (DistMult.py:34-55, 70-72)."""
+    import torch
+    h, t, r = ent[ph], ent[pt], rel[pr]
+    h = h.view(-1, r.shape[0], h.shape[-1])
+    t = t.view(-1, r.shape[0], t.shape[-1])
+    r = r.view(-1, r.shape[0], r.shape[-1])
+    s = h * (r * t) if mode == "head_batch" else (h * r) * t
+    score = torch.sum(s, -1).flatten()
+    return (-score).cpu().data.numpy()
+
+
+def predict_complex(ent_re, ent_im, rel_re, rel_im, ph, pt, pr, mode):
+    """ComplEx._calc + predict (ComplEx.py:20-40, 60-62): no mode handling, broadcast."""
+    import torch
+    h_re, h_im, t_re, t_im = ent_re[ph], ent_im[ph], ent_re[pt], ent_im[pt]
+    r_re, r_im = rel_re[pr], rel_im[pr]
+    score = torch.sum(h_re * t_re * r_re + h_im * t_im * r_re + h_re * t_im * r_im - h_im * t_re * r_im, -1)
+    return (-score).cpu().data.numpy()
+
+
+def predict_rotate(ent, rel, ph, pt, pr, mode, margin, epsilon, dim):
+    """RotatE._calc + forward + predict (RotatE.py:45-91): phase = r / (range / pi),
+    rotate, stack, norm(dim=0).sum(-1), forward = margin - score, predict = -forward."""
+    import torch
+    pi = 3.14159265358979323846
+    rel_range = torch.tensor([(margin + epsilon) / dim], dtype=torch.float32)
+    h, t, r = ent[ph], ent[pt], rel[pr]
+    re_head, im_head = torch.chunk(h, 2, dim=-1)
+    re_tail, im_tail = torch.chunk(t, 2, dim=-1)
+    phase = r / (rel_range.item() / pi)
+    re_rel, im_rel = torch.cos(phase), torch.sin(phase)
+    R = re_rel.shape[0]
+    re_head = re_head.view(-1, R, re_head.shape[-1]).permute(1, 0, 2)
+    re_tail = re_tail.view(-1, R, re_tail.shape[-1]).permute(1, 0, 2)
+    im_head = im_head.view(-1, R, im_head.shape[-1]).permute(1, 0, 2)
+    im_tail = im_tail.view(-1, R, im_tail.shape[-1]).permute(1, 0, 2)
+    im_rel = im_rel.view(-1, R, im_rel.shape[-1]).permute(1, 0, 2)
+    re_rel = re_rel.view(-1, R, re_rel.shape[-1]).permute(1, 0, 2)
+    if mode == "head_batch":
+        re_s = re_rel * re_tail + im_rel * im_tail
+        im_s = re_rel * im_tail - im_rel * re_tail
+        re_s = re_s - re_head
+        im_s = im_s - im_head
+    else:
+        re_s = re_head * re_rel - im_head * im_rel
+        im_s = re_head * im_rel + im_head * re_rel
+        re_s = re_s - re_tail
+        im_s = im_s - im_tail
+    score = torch.stack([re_s, im_s], dim=0).norm(dim=0).sum(dim=-1).permute(1, 0).flatten()
+    m = torch.tensor([margin], dtype=torch.float32)
+    return (-(m - score)).cpu().data.numpy()
+
+
+def make_predict(meta, tables):
+    """predict(ph, pt, pr, mode) -> float32 numpy for the model named in meta."""
+    import torch
+    T = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in tables.items()}
+    model = meta["model"]
+    if model in ("transe", "transe_l2"):
+        p = 1 if model == "transe" else 2
+        return lambda ph, pt, pr, mode: predict_transe(T["ent"], T["rel"], ph, pt, pr, mode,
+                                                       norm_flag=meta.get("norm_flag", True), p_norm=p,
+                                                       margin=meta.get("transe_margin"))
+    if model == "distmult":
+        return lambda ph, pt, pr, mode: predict_distmult(T["ent"], T["rel"], ph, pt, pr, mode)
+    if model == "complex":
+        return lambda ph, pt, pr, mode: predict_complex(T["ent"], T["ent_im"], T["rel"], T["rel_im"], ph, pt, pr,
+                                                        mode)
+    if model == "rotate":
+        return lambda ph, pt, pr, mode: predict_rotate(T["ent"], T["rel"], ph, pt, pr, mode, meta["margin"],
+                                                       meta["epsilon"], meta["dim"])
+    raise ValueError(f"unknown model {model}")
+
+
+# ------------------------------------------------------------------ Tester loop --
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """Base.so printf()s to fd 1."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def _fglob(lib, name):
+    return ctypes.c_float.in_dll(lib, name).value
+
+
+def near_ties(scores, truth, tie_rel):
+    """#{j != truth : |s_j - s_truth| <= tie_rel * max_j |s_j|} per sweep."""
+    s = np.asarray(scores, np.float64)
+    st = s[np.arange(s.shape[0]), truth][:, None]
+    tol = tie_rel * np.max(np.abs(s), axis=1, keepdims=True)
+    close = np.abs(s - st) <= tol
+    close[np.arange(s.shape[0]), truth] = False
+    return close.sum(1)
+
+
+def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
+    import torch
+    with open(os.path.join(workdir, "meta.json")) as f:
+        meta = json.load(f)
+    if meta.get("threads"):
+        torch.set_num_threads(int(meta["threads"]))
+    with np.load(os.path.join(workdir, "tables.npz"), allow_pickle=False) as z:
+        tables = {k: z[k] for k in z.files}
+    predict = make_predict(meta, tables)
+    lib = ctypes.CDLL(base_so)
+    P, I = ctypes.c_void_p, ctypes.c_int64
+    lib.setInPath.argtypes = [ctypes.c_char_p]
+    lib.getHeadBatch.argtypes = [P, P, P]
+    lib.getTailBatch.argtypes = [P, P, P]
+    lib.testHead.argtypes = [P, I, I]
+    lib.testTail.argtypes = [P, I, I]
+    lib.test_link_prediction.argtypes = [I]
+    for g in ("getTestLinkMRR", "getTestLinkMR", "getTestLinkHit10", "getTestLinkHit3", "getTestLinkHit1"):
+        getattr(lib, g).argtypes = [I]
+        getattr(lib, g).restype = ctypes.c_float
+    lib.getEntityTotal.restype = I
+    lib.getTestTotal.restype = I
+    with stdout_to_stderr():
+        lib.setInPath((workdir.rstrip("/") + "/").encode())
+        lib.importTrainFiles()
+        lib.importTestFiles()
+        lib.initTest()
+    E, n = int(lib.getEntityTotal()), int(lib.getTestTotal())
+    ph, pt, pr = (np.zeros(E, np.int64) for _ in range(3))
+    counts = np.zeros((2, n, 2), np.int64)       # [head|tail][query][raw, filt]
+    q = np.zeros((n, 3), np.int64)               # (h, r, t) as Base.so's testList holds them
+    scores = np.zeros((2, n, E), np.float32)
+    keys = (("l_rank", "l_filter_rank"), ("r_rank", "r_filter_rank"))
+    t0 = time.perf_counter()
+    with stdout_to_stderr():
+        for idx in range(n):
+            lib.getHeadBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
+            s = np.ascontiguousarray(predict(torch.from_numpy(ph), torch.from_numpy(pt[:1]),
+                                             torch.from_numpy(pr[:1]), "head_batch"), np.float32)
+            before = [_fglob(lib, k) for k in keys[0]]
+            lib.testHead(s.ctypes.data, idx, 0)
+            counts[0, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[0], before)]
+            q[idx, 1], q[idx, 2] = pr[0], pt[0]
+            scores[0, idx] = s
+            lib.getTailBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
+            s = np.ascontiguousarray(predict(torch.from_numpy(ph[:1]), torch.from_numpy(pt),
+                                             torch.from_numpy(pr[:1]), "tail_batch"), np.float32)
+            before = [_fglob(lib, k) for k in keys[1]]
+            lib.testTail(s.ctypes.data, idx, 0)
+            counts[1, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[1], before)]
+            q[idx, 0] = ph[0]
+            scores[1, idx] = s
+        lib.test_link_prediction(0)
+        elapsed = time.perf_counter() - t0
+        metrics = np.array([lib.getTestLinkMRR(0), lib.getTestLinkMR(0), lib.getTestLinkHit10(0),
+                            lib.getTestLinkHit3(0), lib.getTestLinkHit1(0)], np.float32)
+    ties = np.stack([near_ties(scores[0], q[:, 0], tie_rel), near_ties(scores[1], q[:, 2], tie_rel)])
+    if not all(math.isfinite(float(m)) for m in metrics):
+        raise RuntimeError("Base.so returned non-finite metrics")
+    out = dict(counts=counts, q=q, metrics=metrics, near_ties=ties, elapsed=np.float64(elapsed),
+               threads=np.int64(torch.get_num_threads()), n_ent=np.int64(E), tie_rel=np.float64(tie_rel))
+    np.savez(os.path.join(workdir, "result.npz"), **out)
+    return out
+
+
+if __name__ == "__main__":
+    r = run_tester(sys.argv[1])
+    print(f"ref_tester: {r['counts'].shape[1]} test triples x 2 sweeps in {float(r['elapsed']):.2f} s "
+          f"on {int(r['threads'])} threads")

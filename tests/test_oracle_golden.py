@@ -190,3 +190,43 @@ def test_margin_loss_and_regul(golden, oracle_mod):
     # P9 aliasing: the reported gcn_loss IS struct_loss (margin + 0.5 * regul)
     assert abs(g["gcn_loss"] - g["struct_loss"]) < 1e-7
     assert abs(oracle_mod.margin_loss(g["p"], g["n"], 3.0, adv_temperature=2.0) - g["adv_loss"]) < 1e-5
+
+
+REF_TESTER_META = {
+    "transe": dict(model="transe", norm_flag=True, dim=32),
+    "transe_nonorm_margin": dict(model="transe", norm_flag=False, transe_margin=5.0, dim=32),
+    "transe_l2": dict(model="transe_l2", norm_flag=True, dim=32),
+    "distmult": dict(model="distmult", dim=32),
+    "complex": dict(model="complex", dim=24),
+    "rotate": dict(model="rotate", margin=6.0, epsilon=2.0, dim=16),
+}
+
+
+@pytest.mark.parametrize("name", sorted(REF_TESTER_META))
+def test_ref_tester_predict_is_the_reference(golden, name):
+    """oracle/ref_tester.py (the bench's cpu_baseline and full-size parity checker) scores
+    bit-identically to the reference models' own predict() (golden link_small)."""
+    import torch
+    import ref_tester
+    g = golden("link_small")
+    ent, rel, ent_im, rel_im = _tables(g, name)
+    tables = {"ent": ent, "rel": rel}
+    if ent_im is not None:
+        tables.update(ent_im=ent_im, rel_im=rel_im)
+    predict = ref_tester.make_predict(REF_TESTER_META[name], tables)
+    E = int(g["E"])
+    all_e = torch.arange(E)
+    for mode, key in (("head_batch", "head"), ("tail_batch", "tail")):
+        ref = g[f"{name}_pred_{key}"]
+        for i in range(0, len(g["qh"]), 7):
+            h, r, t = (torch.tensor([int(g[k][i])]) for k in ("qh", "qr", "qt"))
+            s = predict(all_e, t, r, mode) if mode == "head_batch" else predict(h, all_e, r, mode)
+            np.testing.assert_array_equal(s, ref[i])
+
+
+def test_ref_tester_near_ties():
+    import ref_tester
+    s = np.array([[1.0, 1.00005, 2.0, 0.99999], [3.0, -3.0, 2.9999, 5.0]], np.float32)
+    got = ref_tester.near_ties(s, np.array([0, 2]), 1e-4)
+    # row 0: tol 2e-4 -> entities 1 and 3 are near; row 1: tol 5e-4 -> entity 0 is near
+    np.testing.assert_array_equal(got, [2, 1])
