@@ -91,24 +91,29 @@ class _SNWeight(torch.autograd.Function):
         return gw, None, None, None, None
 
 
-def _sn_hook(mod):
+def _sn_eps(mod) -> float:
+    """eps of a spectral-normalised layer: a torch.nn.utils.spectral_norm hook (n_power_iterations
+    1, dim 0, on 'weight') or mmre.generator.SNLinear's own state (same parameter names)."""
     for hook in mod._forward_pre_hooks.values():
         if isinstance(hook, SpectralNorm):
-            return hook
-    raise MMREError(f"{type(mod).__name__} has no spectral_norm hook")
+            if hook.n_power_iterations != 1 or hook.dim != 0 or hook.name != "weight":
+                raise MMREError("sn_weight: spectral_norm with n_power_iterations=1, dim=0 on 'weight' only")
+            return float(hook.eps)
+    if all(hasattr(mod, a) for a in ("weight_orig", "weight_u", "weight_v", "eps")):
+        return float(mod.eps)
+    raise MMREError(f"{type(mod).__name__} is not spectral-normalised")
 
 
 def sn_weight(mod) -> torch.Tensor:
-    """W_orig / sigma of a torch.nn.utils.spectral_norm layer, as its forward pre-hook computes
-    it (one power iteration on weight_u / weight_v in training mode), in one launch."""
-    hook = _sn_hook(mod)
-    if hook.n_power_iterations != 1 or hook.dim != 0 or hook.name != "weight":
-        raise MMREError("sn_weight: spectral_norm with n_power_iterations=1, dim=0 on 'weight' only")
+    """W_orig / sigma of a spectral-normalised layer, as spectral_norm's forward pre-hook
+    computes it (one power iteration on weight_u / weight_v in training mode,
+    spectral_norm.py:74-89), in one launch."""
+    eps = _sn_eps(mod)
     w = mod.weight_orig
     require_cuda(w)
     if w.dim() != 2:
         raise MMREError("sn_weight: 2-d weights only")
-    return _SNWeight.apply(w, mod.weight_u, mod.weight_v, mod.training, hook.eps)
+    return _SNWeight.apply(w, mod.weight_u, mod.weight_v, mod.training, eps)
 
 
 def sn_linear(mod, x: torch.Tensor) -> torch.Tensor:

@@ -25,9 +25,27 @@ class SNLinear(nn.Module):
         self.in_features, self.out_features, self.eps = in_features, out_features, eps
 
 
+class LayerNormalization(nn.Module):
+    """LayerNormalization (module/submodule.py:58-77): parameters a_2 / b_2, unbiased std, eps
+    added to the std, identity when z.size(1) == 1. Standalone calls run the HIP kernel
+    (mmre.gemm.layer_norm, differentiable); inside the generator it is fused into
+    csrc/generator.hip."""
+
+    def __init__(self, d_hid: int, eps: float = 1e-3):
+        super().__init__()
+        self.eps = eps
+        self.a_2 = nn.Parameter(torch.ones(d_hid), requires_grad=True)
+        self.b_2 = nn.Parameter(torch.zeros(d_hid), requires_grad=True)
+
+    def forward(self, z):
+        from .gemm import layer_norm
+        return layer_norm(self, z)
+
+
 class RelationGenerator(nn.Module):
     """generate_fc_layer (in -> red), des_rel_map_layer1 (red -> D), des_rel_map_layer2 (D -> D),
-    layer_norm (D): the exact module names of UnifiedModel (model.py:544-549, 554)."""
+    layer_norm (D): the module names, and so the state-dict keys, of UnifiedModel
+    (model.py:544-549, 555): *.weight_orig / weight_u / weight_v / bias, layer_norm.a_2 / b_2."""
 
     def __init__(self, reduced_dim: int = 384, noise_dim: int = 15, emb_dim: int = 200, ln_eps: float = 1e-3):
         super().__init__()
@@ -35,9 +53,19 @@ class RelationGenerator(nn.Module):
         self.generate_fc_layer = SNLinear(reduced_dim + noise_dim, reduced_dim)
         self.des_rel_map_layer1 = SNLinear(reduced_dim, emb_dim)
         self.des_rel_map_layer2 = SNLinear(emb_dim, emb_dim)
-        self.ln_a = nn.Parameter(torch.ones(emb_dim))
-        self.ln_b = nn.Parameter(torch.zeros(emb_dim))
-        self.ln_eps = ln_eps
+        self.layer_norm = LayerNormalization(emb_dim, eps=ln_eps)
+
+    @property
+    def ln_a(self):
+        return self.layer_norm.a_2
+
+    @property
+    def ln_b(self):
+        return self.layer_norm.b_2
+
+    @property
+    def ln_eps(self):
+        return float(self.layer_norm.eps)
 
     def forward(self, cls: torch.Tensor, noise: torch.Tensor) -> torch.Tensor:
         """cls (N, reduced_dim), noise (N, noise_dim) -> (N, emb_dim). In training mode one

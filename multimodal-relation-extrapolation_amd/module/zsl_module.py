@@ -16,7 +16,17 @@ ZSLmodule.eval (:635-745).
   relation's generated vectors, rank of the true tail, Hits@10/5/1 and MRR printed as the
   reference prints them.
 * `zsl_rank` ranks precomputed candidate vectors (csrc/candidates.hip).
+* `ZSLmodule(args, data_path, r2id, e2id, device, dataset)` is the reference's class
+  (:140-790) over the pieces above: `update_embed`, `get_meta`, `train(generate_model)` (the
+  adversarial loop on mmre.gan.ZSLGANStep, hipGraph-replayed D / G steps, then save + eval),
+  `eval(generate_model, mode, meta, load_pretrain)` -> (hits10, hits5, mrr) with every
+  relation's generate() in one batched call and every candidate ranked in one launch
+  sequence, `save` / `load` / `save_pretrain` / `load_pretrain`. The Extractor's own
+  pretraining (`pretrain_Extractor`, :289-348: Extractor training with dropout) is outside
+  this path; the Extractor keeps its current (or load_pretrain'ed) weights.
 """
+import json
+import os
 from collections import defaultdict
 
 import numpy as np
@@ -29,6 +39,7 @@ from mmre.candidates import cosine_rank
 from mmre.extractor import ZSLRanker, _check_ids, encode, node_tables, pack_weights, targets
 from mmre.gemm import layer_norm, mm, sn_linear
 from .submodule import LayerNormalization, SupportEncoder
+from .utils import weights_init  # noqa: F401  (module/utils.py:119-123; re-exported, zsl_module imports utils *)
 
 
 class Extractor(nn.Module):
@@ -110,13 +121,6 @@ class Discriminator(nn.Module):
         logit_TF = sn_linear(self.fc_TF, middle_vec)
         class_scores = mm(middle_vec, centroid_matrix.t())
         return middle_vec, logit_TF, class_scores
-
-
-def weights_init(m):
-    """module/utils.py:119-123: xavier_normal_ weights and zero biases for every Linear."""
-    if "Linear" in m.__class__.__name__:
-        torch.nn.init.xavier_normal_(m.weight.data)
-        torch.nn.init.constant_(m.bias, 0.0)
 
 
 class ZSLGraph:
@@ -323,3 +327,193 @@ def zsl_metrics(ranks, mode="test", per_relation=None):
     print("MAP: {:.3f}".format(mrr.mean()))
     print("###################################")
     return float(h10.mean()), float(h5.mean()), float(mrr.mean())
+
+
+def _read_json(path):
+    with open(path) as f:
+        return json.load(f)
+
+
+class ZSLmodule(nn.Module):
+    """ZSLmodule (zsl_module.py:140-790). data_path holds the reference's files:
+    train_tasks_zsl.json, test_tasks_zsl.json, rel2candidates_all.json, e1rel_e2_all.json and
+    <mode>_candidates.json for eval; dataset provides generate_batch([], relation ids) ->
+    rel_des / rel_des_padding_mask (module.data.ZSDataset), num_nodes and num_relations."""
+
+    def __init__(self, args, data_path, r2id, e2id, device, dataset, pretrain_margin=3.0):
+        super().__init__()
+        for k, v in vars(args).items():
+            if not hasattr(nn.Module, k):  # the reference's setattr would shadow nn.Module.cuda etc.
+                setattr(self, k, v)
+        self.args = args
+        self.data_path = data_path
+        self.train_tasks = _read_json(os.path.join(data_path, "train_tasks_zsl.json"))
+        self.test_tasks = _read_json(os.path.join(data_path, "test_tasks_zsl.json"))
+        self.rel2id = r2id
+        self.ent2id = e2id
+        self.device = torch.device(device)
+        self.prertain_margin = pretrain_margin  # (sic, :151) stored, unused by the reference as well
+        self.rel2candidates = _read_json(os.path.join(data_path, "rel2candidates_all.json"))
+        self.e1rel_e2 = _read_json(os.path.join(data_path, "e1rel_e2_all.json"))
+        self.test_noises = 0.1 * torch.randn(self.test_sample, self.noise_dim).to(self.device)
+        self.meta = not self.no_meta
+        self.label_num = len(self.train_tasks.keys())
+        batch_data = dataset.generate_batch([], torch.arange(0, len(self.rel2id)))
+        self.des_tokens, self.des_pad_masks = batch_data["rel_des"], batch_data["rel_des_padding_mask"]
+        self.rela2label = {rela: i for i, rela in enumerate(sorted(self.train_tasks.keys()))}
+        ent_embs = torch.rand((dataset.num_nodes, self.emb_dim))
+        rel_embs = torch.rand((dataset.num_relations, self.emb_dim))
+        print("##LOADING PRE-TRAINED EMBEDDING")
+        print("##BUILDING CONNECTION MATRIX")
+        self.graph = ZSLGraph(r2id, e2id, self.train_tasks, self.test_tasks, ent_embs, rel_embs,
+                              max_neighbor=self.max_neighbor)
+        self.num_symbols = self.graph.num_symbols
+        self.pad_id = self.num_symbols
+        self.num_ents = len(self.ent2id.keys())
+        self.Extractor = Extractor(self.emb_dim, self.num_symbols, embed=self.graph.symbol2vec)
+        self.Extractor.to(self.device)
+        self.Extractor.apply(weights_init)
+        self.Discriminator = Discriminator(dim=self.emb_dim)
+        self.Discriminator.to(self.device)
+        self.Discriminator.apply(weights_init)
+        self.centroid_matrix = None
+        self.gan_step = None
+
+    # symbol tables (load_embed / build_connection, :209-268)
+    @property
+    def symbol2id(self):
+        return self.graph.symbol2id
+
+    @property
+    def symbol2vec(self):
+        return self.graph.symbol2vec
+
+    @property
+    def connections(self):
+        return self.graph.connections
+
+    @property
+    def e1_degrees(self):
+        return self.graph.e1_degrees
+
+    def load_embed(self, ent_embs, rel_embs):
+        print("##LOADING PRE-TRAINED EMBEDDING")
+        self.graph.load_embed(ent_embs, rel_embs)
+
+    def update_embed(self, ent_embs, rel_embs):
+        """:235-237: new symbol table from the entity / relation embeddings, into the Extractor."""
+        self.load_embed(ent_embs, rel_embs)
+        self.Extractor.update(self.graph.symbol2vec)
+
+    def get_meta(self, left, right):
+        return self.graph.get_meta(left, right, device=self.device)
+
+    # ---------------------------------------------------------------- training
+    def pretrain_Extractor(self):
+        print("##EXTRACTOR PRETRAINING (zsl_module.py:289-348) is outside this build's path: "
+              "the Extractor keeps its current weights")
+
+    def _ranker(self):
+        self.Extractor.eval()
+        return ZSLRanker(self.Extractor, self.graph.ent_sym, self.graph.connections, self.graph.e1_degrees,
+                         device=self.device)
+
+    def _centroids(self, ranker):
+        """centroid_matrix (:353-383): the mean Extractor vector of every train relation's pairs
+        (centroid_generate, utils.py:615-623), row rela2label[relation]; one encode launch."""
+        heads, tails, labels = [], [], []
+        for rel, triples in self.train_tasks.items():
+            heads += [self.ent2id[t[0]] for t in triples]
+            tails += [self.ent2id[t[2]] for t in triples]
+            labels += [self.rela2label[rel]] * len(triples)
+        dev = self.device
+        h, t, lab = (torch.as_tensor(x, dtype=torch.int64, device=dev) for x in (heads, tails, labels))
+        g, _ = encode(ranker.pack, ranker.dim, ranker.ln_eps, ranker.left, h, ranker.right, t, want_g=True,
+                      want_score=False)
+        sums = torch.zeros((len(self.train_tasks), self.emb_dim), dtype=torch.float32, device=dev)
+        sums.index_add_(0, lab, g)
+        cnt = torch.bincount(lab, minlength=len(self.train_tasks)).clamp(min=1).to(torch.float32)
+        return sums / cnt.unsqueeze(1)
+
+    def train(self, generate_model=None):
+        """:350-633. train() without a model is nn.Module.train() (mode switch)."""
+        if generate_model is None or isinstance(generate_model, bool):
+            return super().train(True if generate_model is None else generate_model)
+        import random
+        from mmre.gan import ZSLGANStep
+        print("\n##START ADVERSARIAL TRAINING...")
+        self.pretrain_Extractor()
+        grad_list = ["generate_fc_layer.weight_orig", "generate_fc_layer.bias", "des_rel_map_layer1.weight_orig",
+                     "des_rel_map_layer1.bias", "des_rel_map_layer2.weight_orig", "des_rel_map_layer2.bias",
+                     "layer_norm.a_2", "layer_norm.b_2"]
+        for name, param in generate_model.named_parameters():
+            param.requires_grad = name in grad_list
+        ranker = self._ranker()
+        self.centroid_matrix = self._centroids(ranker)
+        dev = self.device
+        cls_table = generate_model.M3AEmodel.encode(self.des_tokens.to(dev), self.des_pad_masks.to(dev))
+        self.gan_step = ZSLGANStep(generate_model.generator, self.Discriminator, cls_table, self.centroid_matrix,
+                                   ranker, lr_G=self.lr_maximum, lr_D=self.lr_D, pretrain_margin=self.pretrain_margin,
+                                   gan_batch_rela=self.gan_batch_rela)
+        print("##LOADING TRAINING DATA")
+        batches = train_generate_decription(self.train_tasks, self.rel2candidates, self.e1rel_e2, self.ent2id,
+                                            self.rel2id, self.rela2label, self.G_batch_size, self.gan_batch_rela,
+                                            rng=random.Random())
+        gan_train(self.gan_step, batches, self.train_times, D_epoch=self.D_epoch, G_epoch=self.G_epoch,
+                  loss_every=self.loss_every, device=dev)
+        self.save(generate_model)
+        return self.eval(generate_model, mode="test", meta=self.meta)
+
+    # ---------------------------------------------------------------- evaluation
+    def relation_vectors(self, generate_model, relations):
+        """generate() of test_sample rows per relation with the fixed test noises (:662-667),
+        all relations in one call (eval mode: every row depends on its own CLS and noise only)."""
+        dev = self.device
+        S = int(self.test_sample)
+        ids = torch.as_tensor([self.rel2id[r] for r in relations], dtype=torch.int64)
+        tok = self.des_tokens[ids].repeat_interleave(S, 0).to(dev)
+        msk = self.des_pad_masks[ids].repeat_interleave(S, 0).to(dev)
+        noise = self.test_noises.repeat(len(relations), 1)
+        with torch.no_grad():
+            out = generate_model.generate(tok, msk, noise)
+        return out.view(len(relations), S, -1)
+
+    def eval(self, generate_model=None, mode="test", meta=True, load_pretrain=False):
+        """:635-745 -> (hits10, hits5, mrr); prints the reference's per-relation and final
+        lines. eval() without a model is nn.Module.eval() (mode switch)."""
+        if generate_model is None:
+            return super().eval()
+        if load_pretrain:
+            self.load_pretrain()
+            self.load(generate_model)
+        generate_model.eval()
+        self.Discriminator.eval()
+        self.Extractor.eval()
+        print("##EVALUATING ON %s DATA" % mode.upper())
+        if not meta:
+            raise MMREError("ZSLmodule.eval scores candidates only with meta=True (zsl_module.py:690-703)")
+        test_candidates = _read_json(self.data_path + "/" + mode + "_candidates.json")
+        rels = list(test_candidates.keys())
+        vecs = self.relation_vectors(generate_model, rels)
+        evaluator = ZSLEvaluator(self.Extractor, self.graph, device=self.device)
+        return evaluator.eval(dict(zip(rels, vecs)), test_candidates, mode)
+
+    # ---------------------------------------------------------------- checkpoints (:205-207, 747-755)
+    def save(self, generate_model):
+        os.makedirs(self.save_path, exist_ok=True)
+        torch.save(generate_model.state_dict(), os.path.join(self.save_path, "Generator"))
+        torch.save(self.Discriminator.state_dict(), os.path.join(self.save_path, "Discriminator"))
+
+    def load(self, generate_model):
+        generate_model.load_state_dict(torch.load(os.path.join(self.save_path, "Generator"),
+                                                  map_location=self.device, weights_only=True))
+        self.Discriminator.load_state_dict(torch.load(os.path.join(self.save_path, "Discriminator"),
+                                                      map_location=self.device, weights_only=True))
+
+    def save_pretrain(self):
+        os.makedirs(self.save_path, exist_ok=True)
+        torch.save(self.Extractor.state_dict(), os.path.join(self.save_path, "Extractor"))
+
+    def load_pretrain(self):
+        self.Extractor.load_state_dict(torch.load(os.path.join(self.save_path, "Extractor"),
+                                                  map_location=self.device, weights_only=True))

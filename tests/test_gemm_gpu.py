@@ -105,8 +105,19 @@ def test_layer_norm_first_and_second_order():
         ln.a_2.normal_(1.0, 0.2)
         ln.b_2.normal_(0.0, 0.2)
     z0, up = torch.randn(300, 200) * 3 + 1, torch.randn(300, 200)
-    lref = LayerNormalization(200).double()
-    lref.load_state_dict({k: v.double() for k, v in ln.state_dict().items()})
+    import torch.nn as nn
+    import zsl_gan
+
+    class _RefLN(nn.Module):  # the reference formula in float64 torch ops (oracle/zsl_gan.py)
+        def __init__(self):
+            super().__init__()
+            self.a_2 = nn.Parameter(ln.a_2.detach().double().clone())
+            self.b_2 = nn.Parameter(ln.b_2.detach().double().clone())
+
+        def forward(self, z):
+            return zsl_gan.layer_norm_ref(z, self.a_2, self.b_2, ln.eps)
+
+    lref = _RefLN()
     zr = z0.double().requires_grad_()
     out_r = lref(zr)
     (out_r * up.double()).sum().backward()

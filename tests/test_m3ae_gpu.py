@@ -158,25 +158,6 @@ def test_encoder_rejects_bad_ids():
     assert torch.isfinite(enc.encode(tok, msk)).all()
 
 
-def test_generate_end_to_end():
-    """UnifiedModel.generate(description_tokens, des_padding_mask, noise) (model.py:674-686):
-    frozen encoder CLS -> SN generator -> LayerNormalization, 20 rows of one description."""
-    import m3ae_text as om
-    from module.model import UnifiedModelGenerator
-    vocab = 300
-    enc = _encoder(vocab, depth=2)
-    tok, msk = _rows([11], 320, vocab, seed=9)
-    ref_cls, _ = om.forward_representation_text(enc.state_dict(), tok, msk, 6)
-    torch.manual_seed(1)
-    model = UnifiedModelGenerator(emb_dim=200, noise_dim=15, encoder=enc.to(DEV)).to(DEV).eval()
-    noise = 0.1 * torch.randn(20, 15, device=DEV)
-    out = model.generate(tok.to(DEV).repeat(20, 1), msk.to(DEV).repeat(20, 1), noise)
-    ref = model.generate_from_cls(ref_cls[:, 0].to(DEV).repeat(20, 1), noise)
-    torch.cuda.synchronize()
-    assert out.shape == (20, 200)
-    _close(out, ref)
-
-
 def test_plan_dedupes_adjacent_repeats_and_counts_bad_ids():
     """mmre_m3ae_plan: a row equal to the previous one on its padding pattern and unpadded tokens
     (ids on padded positions may differ) shares its unique sequence; packed offsets count the
