@@ -50,6 +50,9 @@ CONFIGS = {
     "zsl": dict(dataset="FB15K-237-ZS", model="extractor", dim=200, norm=False,
                 workload="ZSL eval FB15K-237-ZS: Extractor (d=200, max_neighbor=50) + mean-cosine rank of "
                          "17,596 queries x ~1,000 candidates (SURVEY 8(f) rank 1)"),
+    "ns": dict(dataset="FB15K-237-ZS", model="ns", dim=200, norm=True,
+               workload="C2 training step FB15K-237-ZS TransE d=200 p=1 norm_flag: OpenKE sampler (B=2,721 positives, "
+                        "neg_ent 25, bern) + fused margin loss (MarginLoss 5.0) forward + backward + SGD step"),
     "gan": dict(dataset="FB15K-237-ZS", model="gan", dim=200, norm=False,
                 workload="ZSL GAN iteration FB15K-237-ZS (ZSLmodule.train, SURVEY 8(f) rank 3): 1 D step + 1 G step, "
                          "G_batch_size 256 x gan_batch_rela 2 = 512 rows, d=200, 206 seen-relation centroids"),
@@ -177,12 +180,26 @@ def cpu_baseline_block(ref, w):
                       f"CPU (oracle/ref_tester.py), {el:.2f} s on {int(ref['threads'])} threads.{note}"}
 
 
-def parity_block(ref, counts, n_total, w):
+def sample_scores(spec, w, n, dev):
+    """GPU model.predict values of the sample's 2n sweeps ([head block | tail block], (2n, E)):
+    the same query-prep + sweep kernels as the evaluation, with the score write-back on."""
+    from mmre.link import HEAD, TAIL, LinkSweep
+    th, tr, tt = (np.asarray(w[k][:n], np.int64) for k in ("test_h", "test_r", "test_t"))
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    qm = np.concatenate([np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)])
+    res = LinkSweep(spec).run(to(np.r_[th, th]), to(np.r_[tr, tr]), to(np.r_[tt, tt]), to(qm), return_scores=True)
+    return res["scores"].cpu().numpy()
+
+
+def parity_block(ref, counts, n_total, w, gpu_scores=None):
     """GPU per-query counts vs the reference Base.so's on the cpu_baseline sample: raw and
     filtered counts query by query, the sample's hit@{1,3,10} / MR / MRR from both sides (the
     GPU's through the P14 reduction of its counts, Base.so's from getTestLink*), and whether
-    every mismatch lies within that sweep's near ties (entities within tie_rel x max|score| of
-    the truth on the reference scores: the only ones a different summation order can move)."""
+    every mismatch is explained by the measured score error: with gpu_scores (the GPU's
+    predict values of the same sweeps), a sweep's tie window is 2 x max_j |s_gpu_j - s_ref_j|
+    around the truth's reference score, and a mismatch is explained when |count difference|
+    <= #entities inside it (a strict `<` can only flip for those). Without gpu_scores the
+    reference-side screen near_ties (tie_rel x max|score|) is used."""
     from mmre.link import link_metrics
     n = int(ref["n"])
     q = ref["q"]
@@ -193,22 +210,38 @@ def parity_block(ref, counts, n_total, w):
     ref_c = ref["counts"]                                   # (2, n, 2) [head|tail][q][raw, filt]
     gpu_c = np.stack([gh[:, :2], gt[:, :2]])
     diff = np.abs(gpu_c - ref_c)                            # (2, n, 2)
-    ties = ref["near_ties"][:, :, None]                     # (2, n, 1)
+    out = {"source": "reference Base.so Tester loop on the cpu_baseline sample (oracle/ref_tester.py)",
+           "test_triples": n, "sweeps": 2 * n, "queries_match": same_q}
+    if gpu_scores is not None and "scores" in ref:
+        rs = ref["scores"].reshape(2 * n, -1).astype(np.float64)
+        gs = np.asarray(gpu_scores, np.float64)
+        truth = np.r_[q[:, 0], q[:, 2]]
+        delta = np.abs(gs - rs)
+        out["score_err_max"] = float(delta.max())
+        out["score_err_rel"] = float((delta / np.maximum(1.0, np.abs(rs))).max())
+        window = 2.0 * delta.max(axis=1) + 1e-30
+        st = rs[np.arange(2 * n), truth][:, None]
+        inside = np.abs(rs - st) <= window[:, None]
+        inside[np.arange(2 * n), truth] = False
+        ties = inside.sum(1).reshape(2, n)[:, :, None]
+        out["tie_window"] = "2 x measured max |s_gpu - s_ref| per sweep"
+    else:
+        ties = ref["near_ties"][:, :, None]
+        out["tie_window"] = f"tie_rel {float(ref['tie_rel'])} x max|s_ref| per sweep"
     mism = diff != 0
     unexplained = mism & (diff > ties)
     gm = link_metrics(counts[:, :n], counts[:, n_total:n_total + n])["filter"]
     rm = ref["metrics"]  # MRR, MR, hit10, hit3, hit1 (filter, Test.h:232-327)
     gpu_vals = np.array([gm["mrr"], gm["mr"], gm["hit10"], gm["hit3"], gm["hit1"]], np.float32)
-    return {"source": "reference Base.so Tester loop on the cpu_baseline sample (oracle/ref_tester.py)",
-            "test_triples": n, "sweeps": 2 * n, "queries_match": same_q,
-            "raw_mismatches": int(mism[:, :, 0].sum()), "filt_mismatches": int(mism[:, :, 1].sum()),
-            "unexplained_mismatches": int(unexplained.sum()),
-            "near_tie_sweeps": int((ref["near_ties"] > 0).sum()), "tie_rel": float(ref["tie_rel"]),
-            "hit1_gpu": float(gm["hit1"]), "hit3_gpu": float(gm["hit3"]), "hit10_gpu": float(gm["hit10"]),
-            "mr_gpu": float(gm["mr"]), "mrr_gpu": float(gm["mrr"]),
-            "hit1_ref": float(rm[4]), "hit3_ref": float(rm[3]), "hit10_ref": float(rm[2]), "mr_ref": float(rm[1]),
-            "mrr_ref": float(rm[0]),
-            "metrics_bit_equal": bool(np.array_equal(gpu_vals.view(np.uint32), rm.astype(np.float32).view(np.uint32)))}
+    out.update({"raw_mismatches": int(mism[:, :, 0].sum()), "filt_mismatches": int(mism[:, :, 1].sum()),
+                "unexplained_mismatches": int(unexplained.sum()), "near_tie_sweeps": int((ties[:, :, 0] > 0).sum()),
+                "hit1_gpu": float(gm["hit1"]), "hit3_gpu": float(gm["hit3"]), "hit10_gpu": float(gm["hit10"]),
+                "mr_gpu": float(gm["mr"]), "mrr_gpu": float(gm["mrr"]),
+                "hit1_ref": float(rm[4]), "hit3_ref": float(rm[3]), "hit10_ref": float(rm[2]), "mr_ref": float(rm[1]),
+                "mrr_ref": float(rm[0]),
+                "metrics_bit_equal": bool(np.array_equal(gpu_vals.view(np.uint32),
+                                                         rm.astype(np.float32).view(np.uint32)))})
+    return out
 
 
 def cpu_baseline_zsl(w, budget_s: float = 15.0, max_queries: int = 400):
@@ -351,6 +384,142 @@ def bench_zsl(args, world, rank, dev, dist):
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def bench_ns(args, world, rank, dev, dist):
+    """One step = one OpenKE training step at the C2 training shape (Trainer.train_one_step,
+    Trainer.py:43-54, over the loader's Base.cpp sampling): a bit-exact GPU sampler batch
+    (mmre.sampler.OpenKESampler: B = 2,721 positives x (1 + neg_ent) rows, bern), the fused
+    negative-sampling margin loss forward + backward into the dense tables (mmre.ns), SGD.
+    Training triples = the C2 filter set (272,115 synthetic + the test triples). N > 1: data
+    parallel replicas (each rank its own sampler stream; no gradient exchange is timed)."""
+    import ref_trainer  # noqa: F401  (import check of the CPU leg before timing)
+    from mmre.data import TrainIndex
+    from mmre.ns import NSSpec, fused_ns_loss
+    from mmre.sampler import OpenKESampler
+    from mmre.workloads import zs_workload
+    w = zs_workload("FB15K-237-ZS", "transe", 200)
+    E, R, d = w["n_ent"], w["n_rel"], w["dim"]
+    B, k, margin = 2721, args.ns_neg, 5.0
+    idx = TrainIndex(w["filter_h"], w["filter_t"], w["filter_r"], E, R)
+    smp = OpenKESampler(idx, dev, bern=True, seed_skip=8 * rank)
+    ent = w["ent"].to(dev).requires_grad_(True)
+    rel = w["rel"].to(dev).requires_grad_(True)
+    spec = NSSpec("transe", d, norm_flag=True)
+    opt = torch.optim.SGD([ent, rel], lr=1.0)
+    n_rows = B * (1 + k)
+    bufs = [dict(batch_h=torch.empty(n_rows, dtype=torch.int64, device=dev),
+                 batch_t=torch.empty(n_rows, dtype=torch.int64, device=dev),
+                 batch_r=torch.empty(n_rows, dtype=torch.int64, device=dev),
+                 batch_y=torch.empty(n_rows, dtype=torch.float32, device=dev)) for _ in range(2)]
+
+    def step(i, ev=None):
+        b = smp.sample(B, k, out=bufs[i & 1])
+        opt.zero_grad(set_to_none=True)
+        if ev:
+            ev[0].record()
+        loss, _ = fused_ns_loss(spec, ent, rel, b["batch_h"], b["batch_t"], b["batch_r"], B, k, margin)
+        if ev:
+            ev[1].record()
+        loss.backward()
+        if ev:
+            ev[2].record()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i, evs[i])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
+    bwd_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank == 0:
+        # SURVEY 8(d): forward bytes = B*3*4d (positive h, r, t) + B*k*4d (one corrupted row per
+        # negative) + B(1+k)*3*8 (int64 ids); the backward writes the same bytes again
+        fwd_bytes = B * 3 * 4 * d + B * k * 4 * d + n_rows * 3 * 8
+        ach = 2 * fwd_bytes / ((fwd_ms + bwd_ms) * 1e-3) / 1e9
+        out = {"metric": f"training triples/sec, {CONFIGS['ns']['workload']}",
+               "value": n_rows * args.steps * world / elapsed, "unit": "training triples/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic TransE tables (OpenKE xavier init, seed 0); training triples = 272,115 synthetic "
+                       "+ the FB15K-237-ZS test triples",
+               "config": {"workload": CONFIGS["ns"]["workload"], "batch": B, "neg_ent": k, "rows_per_step": n_rows,
+                          "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}"},
+               "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                            "kernel": "k_ns_transe_fused<4, false> (+ k_row_norms, k_ns_reduce; forward_ms holds them, "
+                                      "backward_ms the upstream-gradient scaling)",
+                            "kernel_ms": fwd_ms + bwd_ms, "forward_ms": fwd_ms, "backward_ms": bwd_ms,
+                            "algorithmic_bytes": 2 * fwd_bytes,
+                            # the gradient scatter: one d-float row of f32 atomic adds per corrupted row plus
+                            # three per positive; MI355X_MICROARCH.md 'Global float atomics': ~1.3 TB/s chip-wide
+                            "atomic_bytes": B * (k + 3) * 4 * d,
+                            "atomic_roof_GBs": 1300.0,
+                            "atomic_frac": B * (k + 3) * 4 * d / ((fwd_ms + bwd_ms) * 1e-3) / 1.3e12},
+               "last_loss": float(loss.detach())}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def ref_trainer_leg(w, B, k, margin, steps=30, timeout_s=600):
+    """The reference's training step on this host's cores (oracle/ref_trainer.py in a child
+    process): reference Base.so sampling + the TransE / strategy / MarginLoss op sequence on
+    torch CPU + backward + SGD, `steps` steps on the same training triples."""
+    import shutil
+    import subprocess
+    ref_so = os.path.join(REPO, "oracle", "_ref", "Base.so")
+    if not os.path.exists(ref_so):
+        return None
+    tmp = tempfile.mkdtemp(prefix="mmre_reftrain_")
+    try:
+        trn = np.stack([w["filter_h"], w["filter_t"], w["filter_r"]], 1)
+        with open(os.path.join(tmp, "train2id.txt"), "w") as f:
+            f.write(f"{len(trn)}\n")
+            np.savetxt(f, trn, fmt="%d")
+        for name, cnt in (("entity2id.txt", w["n_ent"]), ("relation2id.txt", w["n_rel"])):
+            with open(os.path.join(tmp, name), "w") as f:
+                f.write(f"{cnt}\n")
+        meta = dict(dim=w["dim"], batch=B, neg=k, margin=margin, norm_flag=True, bern=True, steps=steps,
+                    threads=torch.get_num_threads(), sampler_threads=8)
+        with open(os.path.join(tmp, "meta.json"), "w") as f:
+            json.dump(meta, f)
+        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "ref_trainer.py"), tmp], cwd=REPO,
+                           capture_output=True, text=True, timeout=timeout_s)
+        if r.returncode != 0:
+            print(f"cpu_baseline: ref_trainer failed (rc {r.returncode}): {r.stderr[-800:]}", file=sys.stderr)
+            return None
+        with open(os.path.join(tmp, "result.json")) as f:
+            res = json.load(f)
+    except subprocess.TimeoutExpired:
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    el = res["elapsed"]
+    tm = res["times"]
+    return {"value": res["rows_per_step"] * res["steps"] / el, "unit": "training triples/s", "cores": res["threads"],
+            "kind": "reference",
+            "sample": f"{res['steps']} training steps of B={B} x (1+{k}) rows: reference Base.so sampling (8 pthreads) "
+                      f"+ TransE/NegativeSampling/MarginLoss op sequence on torch {torch.__version__} CPU + backward + "
+                      f"SGD (oracle/ref_trainer.py), {el:.2f} s on {res['threads']} threads (sampling "
+                      f"{tm['sampling']:.2f} s, forward {tm['forward']:.2f} s, backward+step {tm['backward_step']:.2f} s)"}
 
 
 def bench_gan(args, world, rank, dev, dist):
@@ -631,6 +800,7 @@ def main():
                     help="test triples in the CPU-baseline / parity sample (0: per-config default)")
     ap.add_argument("--train-steps", type=int, default=300,
                     help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
+    ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -655,6 +825,8 @@ def main():
         return bench_zsl(args, world, rank, dev, dist)
     if args.config == "gan":
         return bench_gan(args, world, rank, dev, dist)
+    if args.config == "ns":
+        return bench_ns(args, world, rank, dev, dist)
     if args.config == "m3ae":
         return bench_m3ae(args, world, rank, dev, dist)
     if cfg["dataset"] == "synthetic-1M":
@@ -767,7 +939,8 @@ def main():
             ref = ref_tester_leg(w, args.cpu_sample or REF_SAMPLE[args.config])
             if ref is not None:
                 out["cpu_baseline"] = cpu_baseline_block(ref, w)
-                out["parity"] = parity_block(ref, counts, n, w)
+                gs = sample_scores(spec, w, int(ref["n"]), dev)
+                out["parity"] = parity_block(ref, counts, n, w, gpu_scores=gs)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

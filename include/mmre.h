@@ -196,13 +196,28 @@ int mmre_ns_forward(int model, int norm_flag, float model_margin, int use_model_
                     float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
                     float* d_work, void* stream);
 /* Backward of the forward above: accumulates d(loss)/d(table) * d_grad_loss[0]
- * into the dense gradient tables (float atomics). */
+ * into the dense gradient tables (float atomics); d_grad_loss NULL means 1. */
 int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
                      const float* d_ent_im, const float* d_rel, const float* d_rel_im, int dim,
                      float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r, int64_t batch,
                      int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
                      const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
                      float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
+
+/* Forward + gradient in one pass, for training: everything mmre_ns_forward computes, plus
+ * d(loss)/d(tables) for an upstream gradient of 1, ACCUMULATED into the (caller-zeroed)
+ * dense gradient tables; the caller scales them by the actual upstream gradient. TransE
+ * (L1 / L2, dim <= 512, neg <= 32) runs one fused launch over a norm pre-pass; other models
+ * run the forward and the backward above. Replaces strategy NegativeSampling.forward +
+ * loss.backward() (NegativeSampling.py:23-32, Trainer.py:43-54) for one batch.
+ * d_work: >= mmre_ns_fused_workspace(B, k, n_ent, n_rel) floats. */
+int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel);
+int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
+                             const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent,
+                             int64_t n_rel, int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,
+                             const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
+                             float regul_rate, float* d_score, float* d_loss, float* d_grad_ent, float* d_grad_ent_im,
+                             float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
 
 /* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
  * batch = n_rows, neg = 0, d_loss = NULL. Its backward: accumulate

@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void k_ns_backward(NSArgs A, const float* __re
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * NS_WAVES + (threadIdx.x >> 6);
   if (b >= A.B) return;
-  const float G = grad_loss[0];
+  const float G = grad_loss ? grad_loss[0] : 1.0f;
   const float p = score[b];
   float mx = -INFINITY, den = 0.0f;
   if (A.adv_t > 0.0f) {
@@ -309,6 +309,635 @@ __global__ __launch_bounds__(256) void k_rows_backward(NSArgs A, const float* __
   if (row >= A.B) return;
   const float g = grad_score[row];
   if (g != 0.0f) row_backward(A, row, lane, g, 0.0f, 0.0f, gent, gent_im, grel, grel_im);
+}
+
+// ---------------------------------------------------------------------------------------
+// TransE fast path (L1 / L2, with or without norm_flag; dim <= 512).
+// One workgroup of NSW waves per positive: every wave loads the positive's h, r, t rows once
+// into registers (element lane + 64 c in slot c: every load and every gradient atomic
+// instruction covers 64 consecutive floats) with their norms;
+// the negatives j = w, w + NSW, ... of the positive are spread over the waves. A negative
+// shares the positive's relation and one of its entities (Base.cpp:111-124: head OR tail
+// corruption), so per negative only the corrupted row is read and normalised -- the shared
+// rows are the register copies (a row that shares nothing is read in full, so any
+// [pos | neg_1 | ... | neg_k] batch is handled). The backward accumulates the gradients of
+// the shared rows in registers across the positive's negatives and issues atomics only for
+// corrupted rows plus one per shared row at the end: k + 3 row atomics per positive instead
+// of 3 (k + 1). Per-row arithmetic is the generic path's: x = (h/|h| + r/|r|) - t/|t|.
+// ---------------------------------------------------------------------------------------
+constexpr int NSW = 4;  // waves per positive
+
+__device__ __forceinline__ void wave_sum3(float& a, float& b, float& c) {
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    a += __shfl_xor(a, s);
+    b += __shfl_xor(b, s);
+    c += __shfl_xor(c, s);
+  }
+}
+
+template <int NC>
+struct Vec {
+  float v[NC];  // element lane + 64 c of the row in v[c] (zero past the row's end)
+};
+
+template <int NC>
+__device__ __forceinline__ void vload(Vec<NC>& o, const float* row, int d, int lane) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = lane + c * kWave;
+    o.v[c] = i < d ? row[i] : 0.0f;
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ float vsq(const Vec<NC>& a) {
+  float s = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) s += a.v[c] * a.v[c];
+  return s;
+}
+
+// x = (h / nh + r / nr) - t / nt per element (the forward's association, TransE.py:55-58)
+__device__ __forceinline__ float tx(float h, float r, float t, float nh, float nr, float nt) {
+  return (h / nh + r / nr) - t / nt;
+}
+
+// |x|_1 or |x|_2^2 partial of this lane (padding elements are 0 - 0 = 0)
+template <int NC, bool L2>
+__device__ __forceinline__ float row_partial(const Vec<NC>& h, const Vec<NC>& r, const Vec<NC>& t, float nh, float nr,
+                                             float nt) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float x = tx(h.v[c], r.v[c], t.v[c], nh, nr, nt);
+    acc += L2 ? x * x : fabsf(x);
+  }
+  return acc;
+}
+
+// the per-row inputs of one wave: each of h, r, t is the positive's register copy or a row
+// read for this row (with its squared norm)
+template <int NC>
+struct RowCtx {
+  Vec<NC> h, r, t;
+  float sh, sr, st;   // squared raw norms
+  bool own_h, own_r, own_t;
+};
+
+// Split in two so that the loads of two rows are in flight before either is reduced.
+template <int NC>
+__device__ __forceinline__ void row_ctx_load(RowCtx<NC>& o, const NSArgs& A, int64_t row, int64_t ph, int64_t pr,
+                                             int64_t pt, const RowCtx<NC>& P, int lane) {
+  const int d = A.dim;
+  const int64_t h = A.h[row], r = A.r[row], t = A.t[row];
+  o.own_h = h == ph;
+  o.own_r = r == pr;
+  o.own_t = t == pt;
+  o.sh = o.sr = o.st = 0.0f;
+  if (o.own_h) o.h = P.h; else vload(o.h, A.ent + h * d, d, lane);
+  if (o.own_r) o.r = P.r; else vload(o.r, A.rel + r * d, d, lane);
+  if (o.own_t) o.t = P.t; else vload(o.t, A.ent + t * d, d, lane);
+}
+
+template <int NC>
+__device__ __forceinline__ void row_ctx_norms(RowCtx<NC>& o, const RowCtx<NC>& P) {
+  float a = o.own_h ? 0.f : vsq(o.h), b = o.own_r ? 0.f : vsq(o.r), c = o.own_t ? 0.f : vsq(o.t);
+  if (!(o.own_h && o.own_r && o.own_t)) wave_sum3(a, b, c);
+  o.sh = o.own_h ? P.sh : a;
+  o.sr = o.own_r ? P.sr : b;
+  o.st = o.own_t ? P.st : c;
+}
+
+__device__ __forceinline__ float norm_of(float sq, int norm_flag) { return norm_flag ? fmaxf(sqrtf(sq), 1e-12f) : 1.0f; }
+
+template <int NC, bool L2>
+__device__ __forceinline__ float row_fwd(const NSArgs& A, const RowCtx<NC>& R, int lane) {
+  const float nh = norm_of(R.sh, A.norm_flag), nr = norm_of(R.sr, A.norm_flag), nt = norm_of(R.st, A.norm_flag);
+  float acc = row_partial<NC, L2>(R.h, R.r, R.t, nh, nr, nt);
+  acc = wave_sum(acc);
+  if (L2) acc = sqrtf(acc);
+  return A.use_model_margin ? A.model_margin - acc : acc;
+}
+
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_transe_forward(NSArgs A, float* __restrict__ score,
+                                                           float* __restrict__ part) {
+  __shared__ float s_n[NS_MAXK];
+  __shared__ float s_sq[NSW][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  const int d = A.dim;
+  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
+  RowCtx<NC> P;
+  vload(P.h, A.ent + ph * d, d, lane);
+  vload(P.r, A.rel + pr * d, d, lane);
+  vload(P.t, A.ent + pt * d, d, lane);
+  P.sh = vsq(P.h); P.sr = vsq(P.r); P.st = vsq(P.t);
+  wave_sum3(P.sh, P.sr, P.st);
+  P.own_h = P.own_r = P.own_t = true;
+  const float p = row_fwd<NC, L2>(A, P, lane);
+  float qh = 0.f, qt = 0.f, qr = 0.f;  // regularization: sums of squared raw rows handled by this wave
+  if (w == 0) {
+    if (lane == 0) score[b] = p;
+    qh = P.sh; qt = P.st; qr = P.sr;
+  }
+  int64_t j = w;
+  for (; j + NSW < A.K; j += 2 * NSW) {  // two negatives per step: both rows in flight together
+    const int64_t row0 = b + (j + 1) * A.B, row1 = row0 + NSW * A.B;
+    RowCtx<NC> R0, R1;
+    row_ctx_load(R0, A, row0, ph, pr, pt, P, lane);
+    row_ctx_load(R1, A, row1, ph, pr, pt, P, lane);
+    row_ctx_norms(R0, P);
+    row_ctx_norms(R1, P);
+    const float n0 = row_fwd<NC, L2>(A, R0, lane);
+    const float n1 = row_fwd<NC, L2>(A, R1, lane);
+    if (lane == 0) { score[row0] = n0; s_n[j] = n0; score[row1] = n1; s_n[j + NSW] = n1; }
+    qh += R0.sh + R1.sh; qt += R0.st + R1.st; qr += R0.sr + R1.sr;
+  }
+  if (j < A.K) {
+    const int64_t row = b + (j + 1) * A.B;
+    RowCtx<NC> R;
+    row_ctx_load(R, A, row, ph, pr, pt, P, lane);
+    row_ctx_norms(R, P);
+    const float n = row_fwd<NC, L2>(A, R, lane);
+    if (lane == 0) { score[row] = n; s_n[j] = n; }
+    qh += R.sh; qt += R.st; qr += R.sr;
+  }
+  if (lane == 0) { s_sq[w][0] = qh; s_sq[w][1] = qt; s_sq[w][2] = qr; }
+  __syncthreads();
+  if (w != 0) return;
+  // hinge max(p - n, -m) over the negatives, self-adversarial weights softmax(-n T) (detached)
+  const float m = A.loss_margin;
+  float loss = 0.0f;
+  if (A.adv_t > 0.0f) {
+    float mx = -INFINITY;
+    for (int64_t j = lane; j < A.K; j += kWave) mx = fmaxf(mx, -s_n[j] * A.adv_t);
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+    float den = 0.0f, num = 0.0f;
+    for (int64_t j = lane; j < A.K; j += kWave) {
+      const float e = expf(-s_n[j] * A.adv_t - mx);
+      den += e;
+      num += e * fmaxf(p - s_n[j], -m);
+    }
+    wave_sum3(den, num, loss);
+    loss = num / den;
+  } else {
+    for (int64_t j = lane; j < A.K; j += kWave) loss += fmaxf(p - s_n[j], -m);
+    loss = wave_sum(loss);
+  }
+  if (lane == 0) {
+    float a = 0.f, c = 0.f, e = 0.f;
+    for (int i = 0; i < NSW; ++i) { a += s_sq[i][0]; c += s_sq[i][1]; e += s_sq[i][2]; }
+    float* o = part + b * 7;
+    o[0] = loss;
+    o[1] = A.regul_rate != 0.0f ? a : 0.0f;
+    o[2] = A.regul_rate != 0.0f ? c : 0.0f;
+    o[3] = A.regul_rate != 0.0f ? e : 0.0f;
+    o[4] = o[5] = o[6] = 0.0f;
+  }
+}
+
+// dy (gradient w.r.t. the normalised row y = v / max(|v|, eps)) -> gradient w.r.t. v:
+// (dy - y (y . dy)) / |v| when |v| > eps, dy / eps otherwise; then + reg * v. Atomically
+// added, one instruction per 64 consecutive floats (256 contiguous bytes).
+template <int NC>
+__device__ __forceinline__ void scatter_row(float* g, int64_t id, int d, int lane, const Vec<NC>& v, float sq,
+                                            const Vec<NC>& dy, int norm_flag, float reg) {
+  float* o = g + id * d;
+  if (norm_flag) {
+    const float nv = sqrtf(sq);
+    const float cv = fmaxf(nv, 1e-12f);
+    float dot = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dot += (v.v[c] / cv) * dy.v[c];
+    dot = wave_sum(dot);
+    const float scale = nv > 1e-12f ? 1.0f / nv : 1.0f / 1e-12f;
+    const float proj = nv > 1e-12f ? dot : 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + c * kWave;
+      if (i < d) atomicAdd(o + i, (dy.v[c] - (v.v[c] / cv) * proj) * scale + reg * v.v[c]);
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + c * kWave;
+      if (i < d) atomicAdd(o + i, dy.v[c] + reg * v.v[c]);
+    }
+  }
+}
+
+// gx = d(loss)/dx for one row (g = d(loss)/d(raw score s)): g sign(x) (L1), g x / |x| (L2)
+template <int NC, bool L2>
+__device__ __forceinline__ void row_gx(Vec<NC>& gx, const NSArgs& A, const RowCtx<NC>& R, float g, int lane) {
+  const float nh = norm_of(R.sh, A.norm_flag), nr = norm_of(R.sr, A.norm_flag), nt = norm_of(R.st, A.norm_flag);
+  float s = 0.0f;
+  if (L2) {
+    s = row_partial<NC, true>(R.h, R.r, R.t, nh, nr, nt);
+    s = sqrtf(wave_sum(s));
+  }
+  const float gs = L2 ? (s > 0.0f ? g / s : 0.0f) : g;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float x = tx(R.h.v[c], R.r.v[c], R.t.v[c], nh, nr, nt);
+    gx.v[c] = L2 ? gs * x : g * (float)((x > 0.0f) - (x < 0.0f));
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ void vadd(Vec<NC>& a, const Vec<NC>& b, float s) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) a.v[c] += s * b.v[c];
+}
+
+// one negative row's backward: shared rows accumulate in registers, the others are scattered
+template <int NC, bool L2>
+__device__ __forceinline__ void neg_backward(const NSArgs& A, const RowCtx<NC>& R, int64_t row, float g, int lane,
+                                             float reg_ent, float reg_rel, float* gent, float* grel, Vec<NC>& Gh,
+                                             Vec<NC>& Gr, Vec<NC>& Gt, float& oh, float& orr, float& ot) {
+  const int d = A.dim;
+  Vec<NC> gx;
+  row_gx<NC, L2>(gx, A, R, g, lane);
+  if (R.own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; }
+  else scatter_row(gent, A.h[row], d, lane, R.h, R.sh, gx, A.norm_flag, reg_ent);
+  if (R.own_r) { vadd(Gr, gx, 1.0f); orr += 1.0f; }
+  else scatter_row(grel, A.r[row], d, lane, R.r, R.sr, gx, A.norm_flag, reg_rel);
+  if (R.own_t) { vadd(Gt, gx, -1.0f); ot += 1.0f; }
+  else {
+    Vec<NC> dt;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dt.v[c] = -gx.v[c];
+    scatter_row(gent, A.t[row], d, lane, R.t, R.st, dt, A.norm_flag, reg_ent);
+  }
+}
+
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const float* __restrict__ score,
+                                                            const float* __restrict__ grad_loss, float* gent,
+                                                            float* grel) {
+  __shared__ float s_c[NS_MAXK];               // d(loss)/d(forward score) of each negative
+  __shared__ float s_gp;                       // ... of the positive
+  __shared__ float s_acc[NSW - 1][3][NC * kWave];
+  __shared__ float s_occ[NSW][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  const int d = A.dim;
+  const float G = grad_loss ? grad_loss[0] : 1.0f;  // NULL: upstream gradient 1
+  const float p = score[b];
+  if (w == 0) {  // coefficients (same formulas as k_ns_backward)
+    float mx = -INFINITY, den = 0.0f;
+    if (A.adv_t > 0.0f) {
+      for (int64_t j = lane; j < A.K; j += kWave) mx = fmaxf(mx, -score[b + (j + 1) * A.B] * A.adv_t);
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+      for (int64_t j = lane; j < A.K; j += kWave) den += expf(-score[b + (j + 1) * A.B] * A.adv_t - mx);
+      den = wave_sum(den);
+    }
+    float gp = 0.0f;
+    for (int64_t j = lane; j < A.K; j += kWave) {
+      const float n = score[b + (j + 1) * A.B];
+      const float x = p - n, m = -A.loss_margin;
+      const float ind = x > m ? 1.0f : (x == m ? 0.5f : 0.0f);
+      const float c = A.adv_t > 0.0f ? G * (expf(-n * A.adv_t - mx) / den) / (float)A.B : G / (float)(A.B * A.K);
+      s_c[j] = c * ind;
+      gp += c * ind;
+    }
+    gp = wave_sum(gp);
+    if (lane == 0) s_gp = gp;
+  }
+  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
+  RowCtx<NC> P;
+  vload(P.h, A.ent + ph * d, d, lane);
+  vload(P.r, A.rel + pr * d, d, lane);
+  vload(P.t, A.ent + pt * d, d, lane);
+  P.sh = vsq(P.h); P.sr = vsq(P.r); P.st = vsq(P.t);
+  wave_sum3(P.sh, P.sr, P.st);
+  P.own_h = P.own_r = P.own_t = true;
+  const double N = (double)A.B * (1.0 + (double)A.K);
+  const float reg_ent = A.regul_rate != 0.0f ? (float)(G * A.regul_rate * 2.0 / (3.0 * N * d)) : 0.0f;
+  const float reg_rel = reg_ent;
+  __syncthreads();
+  const float sgn = A.use_model_margin ? -1.0f : 1.0f;   // forward = m - s
+  Vec<NC> Gh, Gr, Gt, gx;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) Gh.v[c] = Gr.v[c] = Gt.v[c] = 0.0f;
+  float oh = 0.f, orr = 0.f, ot = 0.f;  // occurrences of the shared rows (regularization)
+  if (w == 0) {
+    row_gx<NC, L2>(gx, A, P, sgn * s_gp, lane);
+    vadd(Gh, gx, 1.0f); vadd(Gr, gx, 1.0f); vadd(Gt, gx, -1.0f);
+    oh = orr = ot = 1.0f;
+  }
+  int64_t j = w;
+  for (; j + NSW < A.K; j += 2 * NSW) {  // two negatives per step: both rows in flight together
+    const int64_t row0 = b + (j + 1) * A.B, row1 = row0 + NSW * A.B;
+    RowCtx<NC> R0, R1;
+    row_ctx_load(R0, A, row0, ph, pr, pt, P, lane);
+    row_ctx_load(R1, A, row1, ph, pr, pt, P, lane);
+    row_ctx_norms(R0, P);
+    row_ctx_norms(R1, P);
+    neg_backward<NC, L2>(A, R0, row0, -sgn * s_c[j], lane, reg_ent, reg_rel, gent, grel, Gh, Gr, Gt, oh, orr, ot);
+    neg_backward<NC, L2>(A, R1, row1, -sgn * s_c[j + NSW], lane, reg_ent, reg_rel, gent, grel, Gh, Gr, Gt, oh, orr,
+                         ot);
+  }
+  if (j < A.K) {
+    const int64_t row = b + (j + 1) * A.B;
+    RowCtx<NC> R;
+    row_ctx_load(R, A, row, ph, pr, pt, P, lane);
+    row_ctx_norms(R, P);
+    neg_backward<NC, L2>(A, R, row, -sgn * s_c[j], lane, reg_ent, reg_rel, gent, grel, Gh, Gr, Gt, oh, orr, ot);
+  }
+  // combine the shared-row accumulators of the waves, then one scatter per shared row
+  if (w > 0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      s_acc[w - 1][0][c * kWave + lane] = Gh.v[c];
+      s_acc[w - 1][1][c * kWave + lane] = Gr.v[c];
+      s_acc[w - 1][2][c * kWave + lane] = Gt.v[c];
+    }
+  }
+  if (lane == 0) { s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot; }
+  __syncthreads();
+  if (w != 0) return;
+  for (int i = 0; i < NSW - 1; ++i) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      Gh.v[c] += s_acc[i][0][c * kWave + lane];
+      Gr.v[c] += s_acc[i][1][c * kWave + lane];
+      Gt.v[c] += s_acc[i][2][c * kWave + lane];
+    }
+  }
+  float nh = 0.f, nr = 0.f, nt = 0.f;
+  for (int i = 0; i < NSW; ++i) { nh += s_occ[i][0]; nr += s_occ[i][1]; nt += s_occ[i][2]; }
+  scatter_row(gent, ph, d, lane, P.h, P.sh, Gh, A.norm_flag, reg_ent * nh);
+  scatter_row(grel, pr, d, lane, P.r, P.sr, Gr, A.norm_flag, reg_rel * nr);
+  scatter_row(gent, pt, d, lane, P.t, P.st, Gt, A.norm_flag, reg_ent * nt);
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused forward + gradient (TransE fast path, K <= NSW * NSF_MAXJ). The margin loss's
+// d(loss)/d(score) of every row depends only on its own positive's scores (hinge indicator,
+// self-adversarial softmax over the positive's negatives), so the workgroup that scores a
+// positive can also emit its gradients, per unit upstream gradient: the rows are read ONCE
+// (kept in registers between the scoring and the gradient pass), the row norms come from a
+// pre-pass (one scalar per entity / relation instead of a wave reduction per row), and the
+// gradient atomics of one positive overlap the gathers of the others in the same launch.
+// The caller scales the gradient tables by the upstream gradient in the backward.
+// ---------------------------------------------------------------------------------------
+constexpr int NSF_MAXJ = 8;
+
+__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ tab, int64_t n, int d,
+                                                   float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* p = tab + row * d;
+  float s = 0.0f;
+  for (int i = lane; i < d; i += kWave) s += p[i] * p[i];
+  s = wave_sum(s);
+  if (lane == 0) out[row] = sqrtf(s);
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int src) {
+  const int lo = __shfl((int)(uint32_t)(uint64_t)v, src), hi = __shfl((int)((uint64_t)v >> 32), src);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+template <int NC>
+__device__ __forceinline__ void vnorm(Vec<NC>& o, const Vec<NC>& v, float c) {
+#pragma unroll
+  for (int q = 0; q < NC; ++q) o.v[q] = v.v[q] / c;
+}
+
+// x of a row given the normalised positive rows and the normalised corrupted row (code 0: h,
+// 1: t, 2: r, 3: none), |x|_1 or |x|_2^2 partial of this lane; x kept for the gradient
+template <int NC, bool L2>
+__device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Vec<NC>& rn, const Vec<NC>& tn,
+                                         const Vec<NC>& cn, int code) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) {
+    const float h = code == 0 ? cn.v[q] : hn.v[q];
+    const float r = code == 2 ? cn.v[q] : rn.v[q];
+    const float t = code == 1 ? cn.v[q] : tn.v[q];
+    const float e = (h + r) - t;
+    x.v[q] = e;
+    acc += L2 ? e * e : fabsf(e);
+  }
+  return acc;
+}
+
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
+                                                         const float* __restrict__ nrm_r, float* __restrict__ score,
+                                                         float* __restrict__ part, float* gent, float* grel) {
+  __shared__ float s_n[NSW * NSF_MAXJ];
+  __shared__ float s_c[NSW * NSF_MAXJ];
+  __shared__ float s_gp;
+  __shared__ float s_sq[NSW][3];
+  __shared__ float s_acc[NSW - 1][3][NC * kWave];
+  __shared__ float s_occ[NSW][3];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  const int d = A.dim;
+  const int nf = A.norm_flag;
+  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
+  // this wave's negatives j = w + NSW u, u < nj; lane u holds negative u's row ids
+  const int nj = w < A.K ? (int)((A.K - w + NSW - 1) / NSW) : 0;
+  int64_t my_h = 0, my_t = 0, my_r = 0;
+  if (lane < nj) {
+    const int64_t row = b + (w + NSW * (int64_t)lane + 1) * A.B;
+    my_h = A.h[row]; my_t = A.t[row]; my_r = A.r[row];
+  }
+  Vec<NC> Ph, Pr, Pt;
+  vload(Ph, A.ent + ph * d, d, lane);
+  vload(Pr, A.rel + pr * d, d, lane);
+  vload(Pt, A.ent + pt * d, d, lane);
+  const float nph = nrm_e[ph], npr = nrm_r[pr], npt = nrm_e[pt];
+  // issue every corrupted-row load of the wave before any arithmetic
+  Vec<NC> C[NSF_MAXJ];
+  float cnr[NSF_MAXJ];
+  int code[NSF_MAXJ];
+#pragma unroll
+  for (int u = 0; u < NSF_MAXJ; ++u) {
+    code[u] = 3;
+    cnr[u] = 0.0f;
+    if (u < nj) {
+      const int64_t h = readlane64(my_h, u), t = readlane64(my_t, u), r = readlane64(my_r, u);
+      const bool oh = h == ph, ot = t == pt, orr = r == pr;
+      if (orr && ot && !oh) { code[u] = 0; vload(C[u], A.ent + h * d, d, lane); cnr[u] = nrm_e[h]; }
+      else if (orr && oh && !ot) { code[u] = 1; vload(C[u], A.ent + t * d, d, lane); cnr[u] = nrm_e[t]; }
+      else if (oh && ot && !orr) { code[u] = 2; vload(C[u], A.rel + r * d, d, lane); cnr[u] = nrm_r[r]; }
+      else if (!(oh && ot && orr)) code[u] = 4;  // shares less than two rows: generic path
+    }
+  }
+  const float ch = nf ? fmaxf(nph, 1e-12f) : 1.0f, cr = nf ? fmaxf(npr, 1e-12f) : 1.0f;
+  const float ct = nf ? fmaxf(npt, 1e-12f) : 1.0f;
+  Vec<NC> hn, rn, tn, x, cn;
+  vnorm(hn, Ph, ch); vnorm(rn, Pr, cr); vnorm(tn, Pt, ct);
+  float p_raw = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
+  if (L2) p_raw = sqrtf(p_raw);
+  const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
+  RowCtx<NC> P;  // for the generic-row helpers
+  P.h = Ph; P.r = Pr; P.t = Pt; P.sh = nph * nph; P.sr = npr * npr; P.st = npt * npt;
+  P.own_h = P.own_r = P.own_t = true;
+  float qh = 0.f, qt = 0.f, qr = 0.f;
+  if (w == 0) {
+    if (lane == 0) score[b] = p;
+    qh = P.sh; qt = P.st; qr = P.sr;
+  }
+  float sraw[NSF_MAXJ];
+#pragma unroll
+  for (int u = 0; u < NSF_MAXJ; ++u) {
+    sraw[u] = 0.0f;
+    if (u >= nj) continue;
+    const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
+    float n;
+    if (code[u] == 4) {
+      RowCtx<NC> R;
+      row_ctx_load(R, A, row, ph, pr, pt, P, lane);
+      row_ctx_norms(R, P);
+      n = row_fwd<NC, L2>(A, R, lane);
+      qh += R.sh; qt += R.st; qr += R.sr;
+    } else {
+      const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
+      if (code[u] != 3) vnorm(cn, C[u], cc);
+      float sv = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]));
+      if (L2) sv = sqrtf(sv);
+      sraw[u] = sv;
+      n = A.use_model_margin ? A.model_margin - sv : sv;
+      const float sq = cnr[u] * cnr[u];
+      qh += code[u] == 0 ? sq : P.sh;
+      qt += code[u] == 1 ? sq : P.st;
+      qr += code[u] == 2 ? sq : P.sr;
+    }
+    if (lane == 0) { score[row] = n; s_n[j] = n; }
+  }
+  if (lane == 0) { s_sq[w][0] = qh; s_sq[w][1] = qt; s_sq[w][2] = qr; }
+  __syncthreads();
+  if (w == 0) {  // loss partial and d(loss)/d(forward score) of every row, per unit upstream gradient
+    const float m = A.loss_margin;
+    const bool have = lane < A.K;
+    const float nj_ = have ? s_n[lane] : 0.0f;
+    float loss, gp;
+    if (A.adv_t > 0.0f) {
+      float mx = have ? -nj_ * A.adv_t : -INFINITY;
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+      const float e = have ? expf(-nj_ * A.adv_t - mx) : 0.0f;
+      float den = e, num = have ? e * fmaxf(p - nj_, -m) : 0.0f, z = 0.0f;
+      wave_sum3(den, num, z);
+      loss = num / den;
+      const float x_ = p - nj_;
+      const float ind = x_ > -m ? 1.0f : (x_ == -m ? 0.5f : 0.0f);
+      const float c = have ? (e / den) / (float)A.B * ind : 0.0f;
+      if (have) s_c[lane] = c;
+      gp = wave_sum(c);
+    } else {
+      loss = wave_sum(have ? fmaxf(p - nj_, -m) : 0.0f);
+      const float x_ = p - nj_;
+      const float ind = x_ > -m ? 1.0f : (x_ == -m ? 0.5f : 0.0f);
+      const float c = have ? ind / (float)(A.B * A.K) : 0.0f;
+      if (have) s_c[lane] = c;
+      gp = wave_sum(c);
+    }
+    if (lane == 0) {
+      s_gp = gp;
+      float a = 0.f, c2 = 0.f, e2 = 0.f;
+      for (int i = 0; i < NSW; ++i) { a += s_sq[i][0]; c2 += s_sq[i][1]; e2 += s_sq[i][2]; }
+      float* o = part + b * 7;
+      o[0] = loss;
+      o[1] = A.regul_rate != 0.0f ? a : 0.0f;
+      o[2] = A.regul_rate != 0.0f ? c2 : 0.0f;
+      o[3] = A.regul_rate != 0.0f ? e2 : 0.0f;
+      o[4] = o[5] = o[6] = 0.0f;
+    }
+  }
+  __syncthreads();
+  // gradient pass (upstream gradient 1)
+  const double N = (double)A.B * (1.0 + (double)A.K);
+  const float reg = A.regul_rate != 0.0f ? (float)(A.regul_rate * 2.0 / (3.0 * N * d)) : 0.0f;
+  const float sgn = A.use_model_margin ? -1.0f : 1.0f;
+  Vec<NC> Gh, Gr, Gt, gx;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) Gh.v[q] = Gr.v[q] = Gt.v[q] = 0.0f;
+  float oh = 0.f, orr = 0.f, ot = 0.f;
+  if (w == 0) {
+    const float g = sgn * s_gp;
+    p_raw = fused_x<NC, L2>(x, hn, rn, tn, hn, 3);  // x of the positive again (registers)
+    const float gs = L2 ? (p_raw > 0.0f ? g / sqrtf(wave_sum(p_raw)) : 0.0f) : g;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      const float gv = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
+      Gh.v[q] += gv; Gr.v[q] += gv; Gt.v[q] -= gv;
+    }
+    oh = orr = ot = 1.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < NSF_MAXJ; ++u) {
+    if (u >= nj) continue;
+    const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
+    const float g = -sgn * s_c[j];
+    if (code[u] == 4) {
+      RowCtx<NC> R;
+      row_ctx_load(R, A, row, ph, pr, pt, P, lane);
+      row_ctx_norms(R, P);
+      neg_backward<NC, L2>(A, R, row, g, lane, reg, reg, gent, grel, Gh, Gr, Gt, oh, orr, ot);
+      continue;
+    }
+    const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
+    if (code[u] != 3) vnorm(cn, C[u], cc);
+    fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]);
+    const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
+#pragma unroll
+    for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
+    if (code[u] != 0) { vadd(Gh, gx, 1.0f); oh += 1.0f; }
+    if (code[u] != 2) { vadd(Gr, gx, 1.0f); orr += 1.0f; }
+    if (code[u] != 1) { vadd(Gt, gx, -1.0f); ot += 1.0f; }
+    if (code[u] == 0) scatter_row(gent, readlane64(my_h, u), d, lane, C[u], cnr[u] * cnr[u], gx, nf, reg);
+    else if (code[u] == 2) scatter_row(grel, readlane64(my_r, u), d, lane, C[u], cnr[u] * cnr[u], gx, nf, reg);
+    else if (code[u] == 1) {
+#pragma unroll
+      for (int q = 0; q < NC; ++q) gx.v[q] = -gx.v[q];
+      scatter_row(gent, readlane64(my_t, u), d, lane, C[u], cnr[u] * cnr[u], gx, nf, reg);
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      s_acc[w - 1][0][q * kWave + lane] = Gh.v[q];
+      s_acc[w - 1][1][q * kWave + lane] = Gr.v[q];
+      s_acc[w - 1][2][q * kWave + lane] = Gt.v[q];
+    }
+  }
+  if (lane == 0) { s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot; }
+  __syncthreads();
+  if (w != 0) return;
+  for (int i = 0; i < NSW - 1; ++i) {
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      Gh.v[q] += s_acc[i][0][q * kWave + lane];
+      Gr.v[q] += s_acc[i][1][q * kWave + lane];
+      Gt.v[q] += s_acc[i][2][q * kWave + lane];
+    }
+  }
+  float kh = 0.f, kr = 0.f, kt = 0.f;
+  for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
+  scatter_row(gent, ph, d, lane, Ph, P.sh, Gh, nf, reg * kh);
+  scatter_row(grel, pr, d, lane, Pr, P.sr, Gr, nf, reg * kr);
+  scatter_row(gent, pt, d, lane, Pt, P.st, Gt, nf, reg * kt);
+}
+
+// which TransE fast-path instance fits: elements per lane (0: none, generic path)
+static int transe_fast_nc(const NSArgs& A) {
+  if (A.model != MMRE_TRANSE_L1 && A.model != MMRE_TRANSE_L2) return 0;
+  if (A.K > NS_MAXK) return 0;
+  if (A.dim <= 64) return 1;
+  if (A.dim <= 128) return 2;
+  if (A.dim <= 256) return 4;
+  if (A.dim <= 512) return 8;
+  return 0;
 }
 
 static int ns_args(NSArgs& A, int model, int norm_flag, float model_margin, int use_model_margin, const float* ent,
@@ -348,8 +977,23 @@ extern "C" int mmre_ns_forward(int model, int norm_flag, float model_margin, int
   if (!d_score || !d_work) return MMRE_ERR_ARG;
   if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_ns_forward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A, d_score,
-                     d_work);
+  const int nc = transe_fast_nc(A);
+  const dim3 grid((unsigned)batch), blk(256);
+  const bool l2 = model == MMRE_TRANSE_L2;
+#define MMRE_NS_FWD(NC_)                                                                              \
+  do {                                                                                                \
+    if (l2) hipLaunchKernelGGL((k_ns_transe_forward<NC_, true>), grid, blk, 0, st, A, d_score, d_work); \
+    else hipLaunchKernelGGL((k_ns_transe_forward<NC_, false>), grid, blk, 0, st, A, d_score, d_work);   \
+  } while (0)
+  if (nc == 1) MMRE_NS_FWD(1);
+  else if (nc == 2) MMRE_NS_FWD(2);
+  else if (nc == 4) MMRE_NS_FWD(4);
+  else if (nc == 8) MMRE_NS_FWD(8);
+  else {
+    hipLaunchKernelGGL(k_ns_forward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
+                       d_score, d_work);
+  }
+#undef MMRE_NS_FWD
   MMRE_CHECK_LAUNCH();
   if (d_loss) {
     hipLaunchKernelGGL(k_ns_reduce, dim3(1), dim3(256), 0, st, A, d_work, d_loss);
@@ -370,11 +1014,28 @@ extern "C" int mmre_ns_backward(int model, int norm_flag, float model_margin, in
   int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                    phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
   if (rc) return rc;
-  if (!d_score || !d_grad_loss || !d_grad_ent || !d_grad_rel) return MMRE_ERR_ARG;
+  if (!d_score || !d_grad_ent || !d_grad_rel) return MMRE_ERR_ARG;  // d_grad_loss NULL: upstream gradient 1
   if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_ns_backward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
-                     d_score, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
+  const int nc = transe_fast_nc(A);
+  const dim3 grid((unsigned)batch), blk(256);
+  const bool l2 = model == MMRE_TRANSE_L2;
+#define MMRE_NS_BWD(NC_, L2_)                                                                               \
+  hipLaunchKernelGGL((k_ns_transe_backward<NC_, L2_>), grid, blk, 0, st, A, d_score, d_grad_loss, d_grad_ent, \
+                     d_grad_rel)
+  if (nc == 1) {
+    if (l2) MMRE_NS_BWD(1, true); else MMRE_NS_BWD(1, false);
+  } else if (nc == 2) {
+    if (l2) MMRE_NS_BWD(2, true); else MMRE_NS_BWD(2, false);
+  } else if (nc == 4) {
+    if (l2) MMRE_NS_BWD(4, true); else MMRE_NS_BWD(4, false);
+  } else if (nc == 8) {
+    if (l2) MMRE_NS_BWD(8, true); else MMRE_NS_BWD(8, false);
+  } else {
+    hipLaunchKernelGGL(k_ns_backward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
+                       d_score, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
+  }
+#undef MMRE_NS_BWD
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
@@ -394,6 +1055,62 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_rows_backward, dim3((unsigned)((n_rows + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
                      d_grad_score, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel) {
+  (void)neg;
+  return 7 * (batch > 0 ? batch : 1) + (n_ent > 0 ? n_ent : 0) + (n_rel > 0 ? n_rel : 0) + 64;
+}
+
+extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int use_model_margin,
+                                        const float* d_ent, const float* d_ent_im, const float* d_rel,
+                                        const float* d_rel_im, int64_t n_ent, int64_t n_rel, int dim,
+                                        float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r,
+                                        int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
+                                        float regul_rate, float* d_score, float* d_loss, float* d_grad_ent,
+                                        float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work,
+                                        void* stream) {
+  NSArgs A;
+  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                   phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
+  if (rc) return rc;
+  if (!d_score || !d_loss || !d_work || !d_grad_ent || !d_grad_rel || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
+  if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
+  if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  const int nc = transe_fast_nc(A);
+  if (nc == 0 || neg > NSW * NSF_MAXJ) {  // generic: forward, then the backward with upstream gradient 1
+    rc = mmre_ns_forward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                         phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
+                         d_loss, d_work, stream);
+    if (rc) return rc;
+    return mmre_ns_backward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                            phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
+                            nullptr, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, stream);
+  }
+  float* part = d_work;
+  float* nrm_e = d_work + 7 * batch;
+  float* nrm_r = nrm_e + n_ent;
+  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n_ent + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, dim, nrm_e);
+  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n_rel + 3) / 4)), dim3(256), 0, st, d_rel, n_rel, dim, nrm_r);
+  const dim3 grid((unsigned)batch), blk(256);
+  const bool l2 = model == MMRE_TRANSE_L2;
+#define MMRE_NS_FUSED(NC_)                                                                                    \
+  do {                                                                                                        \
+    if (l2) hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, \
+                               d_grad_ent, d_grad_rel);                                                       \
+    else hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part,  \
+                            d_grad_ent, d_grad_rel);                                                          \
+  } while (0)
+  if (nc == 1) MMRE_NS_FUSED(1);
+  else if (nc == 2) MMRE_NS_FUSED(2);
+  else if (nc == 4) MMRE_NS_FUSED(4);
+  else MMRE_NS_FUSED(8);
+#undef MMRE_NS_FUSED
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_ns_reduce, dim3(1), dim3(256), 0, st, A, part, d_loss);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }

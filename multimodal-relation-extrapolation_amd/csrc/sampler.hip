@@ -6,7 +6,8 @@
 //    (next = next * 25214903917 + 11). Every positive consumes a FIXED number of draws
 //    (1 + 2*neg_rate in mode 0, 1 + neg_rate otherwise, + neg_rel_rate), so the state at
 //    the start of positive b is the thread seed advanced by (b - lef) * draws via an
-//    affine jump-ahead: one GPU thread per positive, same outputs as the pthreads.
+//    affine jump-ahead -- and so is the state before any negative's draws: one GPU thread per
+//    output row, same outputs as the pthreads.
 // 2. The repo's per-edge sampler (module/NegativeSampling.py:114-140, 321-375): per
 //    positive, Bernoulli(0.5) head/tail split of the neg_ent negatives, candidates drawn
 //    uniformly from the local node list [0, n_local) (NegativeSampling.py:210) and rejected
@@ -93,36 +94,37 @@ __device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64_t* __r
   return tmp + lef - ll + 1;
 }
 
-__global__ void k_sampler_openke(const int64_t* __restrict__ train_list, int64_t train_total,
-                                 const int64_t* __restrict__ head_hrt, const int64_t* __restrict__ tail_hrt,
-                                 const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
-                                 const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail,
-                                 const int64_t* __restrict__ rig_tail, const int64_t* __restrict__ lef_rel,
-                                 const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
-                                 const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel,
-                                 const uint64_t* __restrict__ seeds, int64_t work_threads, int64_t B, int64_t neg,
-                                 int64_t neg_rel, int64_t mode, int64_t* __restrict__ bh, int64_t* __restrict__ bt,
-                                 int64_t* __restrict__ br, float* __restrict__ by) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+// One GPU thread per output ROW (positive or negative): the state before any draw is the
+// pthread's seed advanced by an affine jump, so the rows of one positive -- a chain of up to
+// 1 + 2 neg dependent draws and binary searches in the reference -- are produced in parallel
+// (B (1 + neg + neg_rel) threads instead of B).
+__global__ __launch_bounds__(256) void k_sampler_openke(
+    const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
+    const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
+    const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
+    const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
+    const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* __restrict__ seeds,
+    int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, int64_t* __restrict__ bh,
+    int64_t* __restrict__ bt, int64_t* __restrict__ br, float* __restrict__ by) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B * (1 + neg + neg_rel)) return;
+  const int64_t b = row % B, j = row / B;  // j = 0: the positive; 1..neg: entity negatives; then relation ones
   // slice of the reference's pthread `id` that owns position b (Base.cpp:93-100)
-  int64_t id, lef;
-  if (B % work_threads == 0) {
-    const int64_t per = B / work_threads;
-    id = b / per;
-    lef = id * per;
-  } else {
-    const int64_t per = B / work_threads + 1;
-    id = b / per;
-    lef = id * per;
-  }
-  const int64_t draws = 1 + (mode == 0 ? 2 : 1) * neg + neg_rel;
-  uint64_t st = lcg_jump(seeds[id], (uint64_t)((b - lef) * draws));
-  const int64_t i = rand_max(&st, train_total);
+  const int64_t per = B % work_threads == 0 ? B / work_threads : B / work_threads + 1;
+  const int64_t id = b / per, lef = id * per;
+  const int64_t per_neg = mode == 0 ? 2 : 1;  // draws per entity negative: [prob draw,] corrupt draw
+  const int64_t draws = 1 + per_neg * neg + neg_rel;
+  const uint64_t base = (uint64_t)((b - lef) * draws);
+  uint64_t st = lcg_jump(seeds[id], base);
+  const int64_t i = rand_max(&st, train_total);  // Base.cpp:104
   const int64_t h = train_list[3 * i], r = train_list[3 * i + 1], t = train_list[3 * i + 2];
-  bh[b] = h; bt[b] = t; br[b] = r; by[b] = 1.0f;
-  int64_t last = B;
-  for (int64_t k = 0; k < neg; ++k) {
+  if (j == 0) {
+    bh[row] = h; bt[row] = t; br[row] = r; by[row] = 1.0f;
+    return;
+  }
+  if (j <= neg) {
+    const int64_t k = j - 1;
+    st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * k));
     bool replace_tail;
     if (mode == 0) {
       float prob = 500.0f;
@@ -132,18 +134,16 @@ __global__ void k_sampler_openke(const int64_t* __restrict__ train_list, int64_t
       replace_tail = mode != -1;
     }
     if (replace_tail) {  // corrupt_head returns a replacement TAIL (Base.cpp:116)
-      bh[b + last] = h; bt[b + last] = corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r); br[b + last] = r;
+      bh[row] = h; bt[row] = corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r); br[row] = r;
     } else {
-      bh[b + last] = corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r); bt[b + last] = t; br[b + last] = r;
+      bh[row] = corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r); bt[row] = t; br[row] = r;
     }
-    by[b + last] = -1.0f;
-    last += B;
+  } else {
+    const int64_t k = j - 1 - neg;
+    st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * neg + k));
+    bh[row] = h; bt[row] = t; br[row] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r);
   }
-  for (int64_t k = 0; k < neg_rel; ++k) {
-    bh[b + last] = h; bt[b + last] = t; br[b + last] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r);
-    by[b + last] = -1.0f;
-    last += B;
-  }
+  by[row] = -1.0f;
 }
 
 // ---------------------------------------------------------------- repo sampler --
@@ -233,7 +233,8 @@ extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_to
   if (mode < -1 || mode > 1) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const int threads = 256;
-  hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((batch_size + threads - 1) / threads)), dim3(threads), 0, st,
+  const int64_t rows = batch_size * (1 + neg_rate + neg_rel_rate);
+  hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((rows + threads - 1) / threads)), dim3(threads), 0, st,
                      d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
                      d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
                      work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_batch_h, d_batch_t, d_batch_r,

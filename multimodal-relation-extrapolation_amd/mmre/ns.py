@@ -34,12 +34,32 @@ def _scalar_args(spec, batch, neg, loss_margin, adv_t, regul_rate):
 
 
 class _FusedNS(torch.autograd.Function):
+    """Training (the tables need gradients): ONE mmre_ns_forward_backward call in the forward
+    emits the loss, the scores and the gradient tables for an upstream gradient of 1 (fused
+    launch for TransE); the backward scales them by the actual upstream gradient. Otherwise
+    mmre_ns_forward, with mmre_ns_backward as the backward."""
+
     @staticmethod
     def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate):
         dev = ent.device
         N = batch * (1 + neg)
         score = torch.empty(N, dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
+        ctx.mark_non_differentiable(score)
+        ctx.unit = None
+        if any(ctx.needs_input_grad[:4]):
+            E, R = int(ent.shape[0]), int(rel.shape[0])
+            work = torch.empty(int(lib().mmre_ns_fused_workspace(batch, neg, E, R)), dtype=torch.float32, device=dev)
+            ge, gr = torch.zeros_like(ent), torch.zeros_like(rel)
+            gei = torch.zeros_like(ent_im) if ent_im is not None else None
+            gri = torch.zeros_like(rel_im) if rel_im is not None else None
+            call("mmre_ns_forward_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
+                 int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), E, R, spec.dim,
+                 spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg, float(loss_margin), float(adv_t),
+                 float(regul_rate), ptr(score), ptr(loss), ptr(ge), ptr(gei), ptr(gr), ptr(gri), ptr(work),
+                 stream_ptr(dev))
+            ctx.unit = (ge, gr, gei, gri)
+            return loss[0], score
         work = torch.empty(int(lib().mmre_ns_workspace(batch, neg)), dtype=torch.float32, device=dev)
         call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
              ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
@@ -54,6 +74,11 @@ class _FusedNS(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_loss, g_score):
+        if ctx.unit is not None:  # gradients for upstream 1 were computed in the forward
+            gl = g_loss.reshape(()).to(torch.float32)
+            out = [None if x is None else x.mul_(gl) for x in ctx.unit]
+            ctx.unit = None
+            return (*out, None, None, None, None, None, None, None, None, None)
         ent, rel, ent_im, rel_im, h, t, r, score = ctx.saved_tensors
         spec, batch, neg, loss_margin, adv_t, regul_rate = ctx.cfg
         if not ctx.has_im:

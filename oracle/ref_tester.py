@@ -16,10 +16,12 @@ reference's own predictions in tests/golden/link_small.npz.
 
 Per query it also reads Base.so's rank deltas (l_rank / l_filter_rank / r_rank /
 r_filter_rank are float globals holding sums of exact integers below 2^24), so the GPU's
-per-query counts can be compared with the reference's one by one. After the timed loop it
-counts each sweep's near ties on the reference scores -- entities whose score lies within
-``tie_rel`` x max|score| of the truth's -- the only entities whose side of the strict `<`
-(Test.h:83, :147) a different float summation order can flip.
+per-query counts can be compared with the reference's one by one, and it returns the
+reference's score vectors (model.predict output of every sweep), so the caller can measure
+the GPU-vs-reference score error sweep by sweep and count the entities inside that error
+window around the truth -- the only ones whose side of the strict `<` (Test.h:83, :147) a
+different float summation order can flip. `near_ties` is a cruder, score-only screen
+(entities within ``tie_rel`` x max|score| of the truth).
 
 Usage (a child process of bench.py: Base.so is C++ with unguarded indexing):
     python oracle/ref_tester.py <workdir>
@@ -230,7 +232,8 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
     if not all(math.isfinite(float(m)) for m in metrics):
         raise RuntimeError("Base.so returned non-finite metrics")
     out = dict(counts=counts, q=q, metrics=metrics, near_ties=ties, elapsed=np.float64(elapsed),
-               threads=np.int64(torch.get_num_threads()), n_ent=np.int64(E), tie_rel=np.float64(tie_rel))
+               threads=np.int64(torch.get_num_threads()), n_ent=np.int64(E), tie_rel=np.float64(tie_rel),
+               scores=scores)
     np.savez(os.path.join(workdir, "result.npz"), **out)
     return out
 

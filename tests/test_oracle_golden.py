@@ -230,3 +230,24 @@ def test_ref_tester_near_ties():
     got = ref_tester.near_ties(s, np.array([0, 2]), 1e-4)
     # row 0: tol 2e-4 -> entities 1 and 3 are near; row 1: tol 5e-4 -> entity 0 is near
     np.testing.assert_array_equal(got, [2, 1])
+
+
+@pytest.mark.parametrize("name,norm,margin,adv,regul", [("transe", True, 5.0, None, 0.0),
+                                                         ("transe_nonorm", False, 3.0, None, 0.5),
+                                                         ("transe_adv", True, 5.0, 1.0, 0.0)])
+def test_ref_trainer_loss_is_the_reference(golden, name, norm, margin, adv, regul):
+    """oracle/ref_trainer.transe_ns_loss (bench --config ns cpu_baseline, float reference of the
+    fused loss) == the reference strategy's loss and gradients (golden strategy.npz)."""
+    import torch
+    import ref_trainer
+    g = golden("strategy")
+    ent = torch.from_numpy(g[f"{name}.ent_embeddings.weight"]).requires_grad_(True)
+    rel = torch.from_numpy(g[f"{name}.rel_embeddings.weight"]).requires_grad_(True)
+    h, t, r = (torch.from_numpy(g[f"{name}_{k}"]) for k in ("h", "t", "r"))
+    loss, score = ref_trainer.transe_ns_loss(ent, rel, h, t, r, int(g["B"]), margin, norm_flag=norm,
+                                             adv_temperature=adv, regul_rate=regul)
+    loss.backward()
+    np.testing.assert_array_equal(score.detach().numpy(), g[f"{name}_score"])
+    assert float(loss) == pytest.approx(float(g[f"{name}_loss"]), abs=1e-6)
+    np.testing.assert_allclose(ent.grad.numpy(), g[f"{name}.grad.ent_embeddings.weight"], atol=1e-7, rtol=1e-5)
+    np.testing.assert_allclose(rel.grad.numpy(), g[f"{name}.grad.rel_embeddings.weight"], atol=1e-7, rtol=1e-5)

@@ -45,12 +45,14 @@ def _oracle_counts(oracle_mod, w):
     ei = w["ent_im"].numpy() if "ent_im" in w else None
     ri = w["rel_im"].numpy() if "rel_im" in w else None
     hrt = oracle_mod.sorted_hrt(w["filter_h"], w["filter_r"], w["filter_t"])
-    out = []
+    out, scores = [], []
     for mode in ("head_batch", "tail_batch"):
         p = oracle_mod.link_predict(w["model"], mode, ent, rel, w["test_h"], w["test_r"], w["test_t"], ent_im=ei,
                                     rel_im=ri, **kw)
         out.append(oracle_mod.test_rank(mode, p, w["test_h"], w["test_r"], w["test_t"], hrt).T)
-    return np.concatenate(out, 1).astype(np.int32)   # (4, 2n): head block then tail block
+        scores.append(p)
+    # (4, 2n) counts: head block then tail block; the oracle's scores are the GPU's bit for bit
+    return np.concatenate(out, 1).astype(np.int32), scores
 
 
 @pytest.mark.parametrize("model", ["transe", "distmult", "complex", "rotate"])
@@ -58,11 +60,13 @@ def _oracle_counts(oracle_mod, w):
 def test_ref_leg_and_parity_block(oracle_mod, model, n_sample):
     import bench
     w = _workload(model)
-    counts = _oracle_counts(oracle_mod, w)
+    counts, sc = _oracle_counts(oracle_mod, w)
     ref = bench.ref_tester_leg(w, n_sample)
     assert ref is not None
     assert ref["counts"].shape == (2, n_sample, 2)
-    par = bench.parity_block(ref, counts, len(w["test_h"]), w)
+    par = bench.parity_block(ref, counts, len(w["test_h"]), w,
+                             gpu_scores=np.concatenate([sc[0][:n_sample], sc[1][:n_sample]]))
+    assert par["score_err_rel"] <= 1e-4
     assert par["queries_match"]
     # the oracle's canonical arithmetic differs from the reference's torch order only inside near ties
     assert par["unexplained_mismatches"] == 0, par
@@ -75,7 +79,7 @@ def test_ref_leg_and_parity_block(oracle_mod, model, n_sample):
 def test_parity_block_reports_a_planted_mismatch(oracle_mod):
     import bench
     w = _workload("distmult")
-    counts = _oracle_counts(oracle_mod, w)
+    counts, _ = _oracle_counts(oracle_mod, w)
     ref = bench.ref_tester_leg(w, 60)
     bad = counts.copy()
     bad[1, 3] += 5     # filtered head count of query 3
