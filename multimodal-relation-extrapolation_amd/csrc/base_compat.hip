@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -109,17 +110,39 @@ struct Device {
 };
 Device D;
 
-bool hip_ok(hipError_t e, const char* what) {
-  if (e != hipSuccess) {
-    fprintf(stderr, "libmmre_base: %s failed: %s\n", what, hipGetErrorString(e));
-    return false;
-  }
-  return true;
+// Errors never end the host process (Base.so's void API has no status return): a failure
+// throws BaseError up to the exported function, which latches it (code + message, printed
+// once to stderr) and returns; while an error is latched every other entry point returns at
+// once. mmre_base_last_error reads the latch, mmre_base_clear_error resets it.
+struct BaseError : std::runtime_error {
+  int code;
+  BaseError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+int g_err_code = 0;
+std::string g_err_msg;
+
+[[noreturn]] void fail(int code, const std::string& msg) { throw BaseError(code, msg); }
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) fail(MMRE_ERR_HIP_BASE + (int)e, std::string(what) + " failed: " + hipGetErrorString(e));
 }
-#define HIP_OR_DIE(x)                      \
-  do {                                     \
-    if (!hip_ok((x), #x)) std::abort();    \
-  } while (0)
+#define HIP_OR_DIE(x) hip_check((x), #x)
+
+template <class F>
+void guarded(F&& f) {
+  if (g_err_code) return;
+  try {
+    f();
+  } catch (const BaseError& e) {
+    g_err_code = e.code;
+    g_err_msg = e.what();
+    fprintf(stderr, "libmmre_base: %s\n", e.what());
+  } catch (const std::exception& e) {
+    g_err_code = MMRE_ERR_ARG;
+    g_err_msg = e.what();
+    fprintf(stderr, "libmmre_base: %s\n", e.what());
+  }
+}
 
 template <class T>
 T* upload(const std::vector<T>& v) {
@@ -275,14 +298,10 @@ __global__ __launch_bounds__(1024) void k_rank_scores(const float* __restrict__ 
 }
 
 void rank_call(const REAL* con, INT idx, bool tc, int side) {
-  if (idx < 0 || idx >= S.test_total) {
-    fprintf(stderr, "libmmre_base: test index %ld out of range [0, %ld)\n", (long)idx, (long)S.test_total);
-    std::abort();
-  }
-  if (tc && !S.have_types) {
-    fprintf(stderr, "libmmre_base: type_constrain requires importTypeFiles()\n");
-    std::abort();
-  }
+  if (idx < 0 || idx >= S.test_total)
+    fail(MMRE_ERR_ARG, "test index " + std::to_string((long)idx) + " out of range [0, " +
+                           std::to_string((long)S.test_total) + ")");
+  if (tc && !S.have_types) fail(MMRE_ERR_ARG, "type_constrain requires importTypeFiles()");
   test_device();
   const int64_t slot = (int64_t)S.calls.size();
   if (slot >= D.slot_cap) {  // grow the count array (rare: sized for one evaluation)
@@ -318,10 +337,7 @@ void rank_call(const REAL* con, INT idx, bool tc, int side) {
 // --------------------------------------------------------------- readers ----
 FILE* open_or_die(const std::string& p) {
   FILE* f = fopen(p.c_str(), "r");
-  if (!f) {
-    fprintf(stderr, "libmmre_base: cannot open %s\n", p.c_str());
-    std::abort();
-  }
+  if (!f) fail(MMRE_ERR_ARG, "cannot open " + p);
   return f;
 }
 
@@ -397,7 +413,7 @@ extern "C" void randReset() {
 }
 
 // -------------------------------------------------------------- Reader.h ----
-extern "C" void importTrainFiles() {
+static void importTrainFiles_impl() {
   printf("The toolkit is importing datasets.\n");
   S.rel_total = read_count(path_or(S.rel_file, "relation2id.txt"));
   S.ent_total = read_count(path_or(S.ent_file, "entity2id.txt"));
@@ -440,7 +456,7 @@ extern "C" void importTrainFiles() {
   D.train_ready = false;  // re-upload on the next sampling call
 }
 
-extern "C" void importTestFiles() {
+static void importTestFiles_impl() {
   S.rel_total = read_count(path_or(S.rel_file, "relation2id.txt"));
   S.ent_total = read_count(path_or(S.ent_file, "entity2id.txt"));
   INT n_test = 0, n_train = 0, n_valid = 0;
@@ -463,7 +479,7 @@ extern "C" void importTestFiles() {
   D.test_ready = false;
 }
 
-extern "C" void importTypeFiles() {
+static void importTypeFiles_impl() {
   FILE* f = open_or_die(S.in_path + "type_constrain.txt");
   long n = 0;
   if (fscanf(f, "%ld", &n) != 1) n = 0;
@@ -489,7 +505,7 @@ extern "C" void importTypeFiles() {
 }
 
 // -------------------------------------------------------------- Base.cpp ----
-extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y, INT batch_size, INT neg_rate,
+static void sampling_impl(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y, INT batch_size, INT neg_rate,
                          INT neg_rel_rate, INT mode, bool filter_flag, bool p, bool val_loss) {
   (void)filter_flag;  // accepted and ignored, as in Base.cpp:116/:119
   if (batch_size <= 0) return;
@@ -502,14 +518,8 @@ extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y
     }
     return;
   }
-  if (p && neg_rel_rate > 0) {
-    fprintf(stderr, "libmmre_base: sampling(p=true) relation corruption by kl_prob.txt is not supported\n");
-    std::abort();
-  }
-  if (S.seeds.size() != (size_t)S.work_threads) {
-    fprintf(stderr, "libmmre_base: call randReset() after setWorkThreads() before sampling\n");
-    std::abort();
-  }
+  if (p && neg_rel_rate > 0) fail(MMRE_ERR_ARG, "sampling(p=true) relation corruption by kl_prob.txt is not supported");
+  if (S.seeds.size() != (size_t)S.work_threads) fail(MMRE_ERR_ARG, "call randReset() after setWorkThreads() before sampling");
   train_device();
   const int64_t n = batch_size * (1 + neg_rate + neg_rel_rate);
   if (n > D.batch_cap) {
@@ -526,10 +536,7 @@ extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y
                                      D.d_rt, D.d_lr, D.d_rr, S.bern ? D.d_lm : nullptr, S.bern ? D.d_rm : nullptr,
                                      S.ent_total, S.rel_total, D.d_seeds, S.work_threads, batch_size, neg_rate,
                                      neg_rel_rate, mode, D.d_bh, D.d_bt, D.d_br, D.d_by, D.st);
-  if (rc != MMRE_OK) {
-    fprintf(stderr, "libmmre_base: mmre_sampler_openke failed (%d)\n", rc);
-    std::abort();
-  }
+  if (rc != MMRE_OK) fail(rc, "mmre_sampler_openke failed (" + std::to_string(rc) + ")");
   HIP_OR_DIE(hipMemcpyAsync(batch_h, D.d_bh, sizeof(int64_t) * n, hipMemcpyDeviceToHost, D.st));
   HIP_OR_DIE(hipMemcpyAsync(batch_t, D.d_bt, sizeof(int64_t) * n, hipMemcpyDeviceToHost, D.st));
   HIP_OR_DIE(hipMemcpyAsync(batch_r, D.d_br, sizeof(int64_t) * n, hipMemcpyDeviceToHost, D.st));
@@ -540,13 +547,13 @@ extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y
 }
 
 // ---------------------------------------------------------------- Test.h ----
-extern "C" void initTest() {
+static void initTest_impl() {
   S.last_head = S.last_tail = 0;
   if (D.test_ready) HIP_OR_DIE(hipStreamSynchronize(D.st));
   S.calls.clear();
 }
 
-extern "C" void getHeadBatch(INT* ph, INT* pt, INT* pr) {
+static void getHeadBatch_impl(INT* ph, INT* pt, INT* pr) {
   const Trip& q = S.test_list[(size_t)S.last_head];
   for (INT i = 0; i < S.ent_total; ++i) {
     ph[i] = i;
@@ -556,7 +563,7 @@ extern "C" void getHeadBatch(INT* ph, INT* pt, INT* pr) {
   S.last_head++;
 }
 
-extern "C" void getTailBatch(INT* ph, INT* pt, INT* pr) {
+static void getTailBatch_impl(INT* ph, INT* pt, INT* pr) {
   const Trip& q = S.test_list[(size_t)S.last_tail];
   for (INT i = 0; i < S.ent_total; ++i) {
     ph[i] = q.h;
@@ -566,10 +573,14 @@ extern "C" void getTailBatch(INT* ph, INT* pt, INT* pr) {
   S.last_tail++;
 }
 
-extern "C" void testHead(REAL* con, INT last_head, bool type_constrain) { rank_call(con, last_head, type_constrain, 0); }
-extern "C" void testTail(REAL* con, INT last_tail, bool type_constrain) { rank_call(con, last_tail, type_constrain, 1); }
+extern "C" void testHead(REAL* con, INT last_head, bool type_constrain) {
+  guarded([&] { rank_call(con, last_head, type_constrain, 0); });
+}
+extern "C" void testTail(REAL* con, INT last_tail, bool type_constrain) {
+  guarded([&] { rank_call(con, last_tail, type_constrain, 1); });
+}
 
-extern "C" void test_link_prediction(bool type_constrain) {
+static void test_link_prediction_impl(bool type_constrain) {
   const size_t n = S.calls.size();
   std::vector<int32_t> c(4 * n + 4);
   if (n) {
@@ -632,3 +643,50 @@ extern "C" REAL getTestLinkHit3(bool type_constrain) { return type_constrain ? S
 extern "C" REAL getTestLinkHit1(bool type_constrain) { return type_constrain ? S.hit1_tc : S.hit1; }
 extern "C" REAL getTestLinkMR(bool type_constrain) { return type_constrain ? S.mr_tc : S.mr; }
 extern "C" REAL getTestLinkMRR(bool type_constrain) { return type_constrain ? S.mrr_tc : S.mrr; }
+
+// --------------------------------------------------- exported entry points ----
+extern "C" void importTrainFiles() {
+  guarded([&] { importTrainFiles_impl(); });
+}
+
+extern "C" void importTestFiles() {
+  guarded([&] { importTestFiles_impl(); });
+}
+
+extern "C" void importTypeFiles() {
+  guarded([&] { importTypeFiles_impl(); });
+}
+
+extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y, INT batch_size, INT neg_rate, INT neg_rel_rate, INT mode, bool filter_flag, bool p, bool val_loss) {
+  guarded([&] { sampling_impl(batch_h, batch_t, batch_r, batch_y, batch_size, neg_rate, neg_rel_rate, mode, filter_flag, p, val_loss); });
+}
+
+extern "C" void initTest() {
+  guarded([&] { initTest_impl(); });
+}
+
+extern "C" void getHeadBatch(INT* ph, INT* pt, INT* pr) {
+  guarded([&] { getHeadBatch_impl(ph, pt, pr); });
+}
+
+extern "C" void getTailBatch(INT* ph, INT* pt, INT* pr) {
+  guarded([&] { getTailBatch_impl(ph, pt, pr); });
+}
+
+extern "C" void test_link_prediction(bool type_constrain) {
+  guarded([&] { test_link_prediction_impl(type_constrain); });
+}
+
+// ------------------------------------------------------------ error latch ----
+extern "C" int mmre_base_last_error(char* msg, int cap) {
+  if (msg && cap > 0) {
+    strncpy(msg, g_err_msg.c_str(), (size_t)cap - 1);
+    msg[cap - 1] = 0;
+  }
+  return g_err_code;
+}
+
+extern "C" void mmre_base_clear_error() {
+  g_err_code = 0;
+  g_err_msg.clear();
+}

@@ -31,6 +31,7 @@ SIGNATURES = {
     "test_link_prediction": (None, [_I]),
     "getTestLinkHit10": (_F, [_I]), "getTestLinkHit3": (_F, [_I]), "getTestLinkHit1": (_F, [_I]),
     "getTestLinkMR": (_F, [_I]), "getTestLinkMRR": (_F, [_I]),
+    "mmre_base_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]), "mmre_base_clear_error": (None, []),
 }
 
 _base = None
@@ -51,3 +52,18 @@ def load():
             fn.argtypes = args
         _base = L
     return _base
+
+
+def last_error():
+    """(code, message) of the latched error (0, '' when none)."""
+    buf = ctypes.create_string_buffer(512)
+    code = int(load().mmre_base_last_error(buf, len(buf)))
+    return code, buf.value.decode(errors="replace")
+
+
+def check():
+    """Raise MMREError for a latched error (and clear the latch)."""
+    code, msg = last_error()
+    if code:
+        load().mmre_base_clear_error()
+        raise MMREError(f"libmmre_base: {msg} (code {code})")

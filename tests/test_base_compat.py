@@ -24,7 +24,7 @@ def _base():
 def _declared():
     txt = open(os.path.join(REPO, "include", "mmre_base.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:void|int64_t|float)\s+(\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:void|int64_t|int|float)\s+(\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_exports_every_declared_symbol():
@@ -33,6 +33,33 @@ def test_exports_every_declared_symbol():
     assert len(names) >= 30
     for n in names:
         assert hasattr(L, n), n
+
+
+def test_errors_are_latched_not_fatal(tmp_path):
+    """Base.so crashes on a missing file or a bad index; libmmre_base latches the error,
+    returns, and refuses further work until it is cleared -- the host process lives on."""
+    from mmre import base
+    from mmre._lib import MMREError
+    L = _base()
+    L.mmre_base_clear_error()
+    L.setInPath((str(tmp_path) + "/nowhere/").encode())
+    L.importTrainFiles()
+    code, msg = base.last_error()
+    assert code == 1 and "cannot open" in msg
+    L.setInPath(SMALL.encode())
+    L.importTestFiles()                       # refused while latched: totals unchanged
+    with pytest.raises(MMREError):
+        base.check()
+    assert base.last_error()[0] == 0          # check() cleared the latch
+    L.importTestFiles()
+    n = L.getTestTotal()
+    assert n > 0
+    con = np.zeros(L.getEntityTotal(), np.float32)
+    L.testHead(con.ctypes.data, n + 5, 0)     # out of range: latched before any GPU work
+    code, msg = base.last_error()
+    assert code == 1 and "out of range" in msg
+    L.mmre_base_clear_error()
+    assert base.last_error() == (0, "")
 
 
 def test_readers_and_batches(golden):
