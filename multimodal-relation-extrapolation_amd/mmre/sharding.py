@@ -1,8 +1,9 @@
 """Relation-sharded multi-GPU evaluation.
 
-Whole test relations are assigned to ranks by LPT packing of their query counts, so every
-rank keeps Test.h's relation-major order (testList sorted by (r, h, t), Reader.h:227) for its
-queries and reuses its relations' rows. Entity and relation tables are replicated (11-60 MB at
+Test relations are assigned to ranks by LPT packing of their query counts (a relation larger
+than the per-rank share is first cut into contiguous query pieces), so every rank keeps
+Test.h's relation-major order (testList sorted by (r, h, t), Reader.h:227) for its queries
+and reuses its relations' rows. Entity and relation tables are replicated (11-60 MB at
 the ZS configs, far below 288 GB). After the local sweep, ONE all-gather of the per-rank int32
 rank-count lists (RCCL over xGMI; gloo on CPU in tests) lets every rank reduce the metrics in
 the reference's sequential order, so rank 0's metrics are bit-equal to the single-GPU run.
@@ -13,19 +14,34 @@ import numpy as np
 import torch
 
 
-def lpt_partition(rel_of_query: np.ndarray, world: int):
-    """Assign relations to `world` ranks, heaviest first onto the least-loaded rank.
-    Returns a list of boolean masks over queries (one per rank)."""
+def lpt_partition(rel_of_query: np.ndarray, world: int, split: bool = True):
+    """Assign the queries to `world` ranks by relation, heaviest relation first onto the
+    least-loaded rank (LPT). With split (SURVEY.md §8(e)'s fallback) no rank takes more than
+    the share ceil(Q / world): a relation that does not fit the least-loaded rank fills it with
+    a contiguous run of its queries (query order) and the rest moves on -- at most world - 1
+    cuts in all, and every rank's queries stay relation-major (Test.h's order). DB15K-ZS's
+    largest relation holds 18 % of the queries, which caps whole-relation LPT at 5.4x on 8
+    ranks. Deterministic (every rank computes the same partition). Returns one boolean mask
+    over the queries per rank."""
     rel_of_query = np.asarray(rel_of_query)
-    rels, counts = np.unique(rel_of_query, return_counts=True)
-    order = np.lexsort((rels, -counts))  # heaviest first, ties by relation id (deterministic)
+    Q = len(rel_of_query)
+    if Q == 0:
+        return [np.zeros(0, bool) for _ in range(world)]
+    share = -(-Q // world)
+    order_q = np.argsort(rel_of_query, kind="stable")
+    rels, starts, counts = np.unique(rel_of_query[order_q], return_index=True, return_counts=True)
+    order = np.lexsort((rels, -counts))  # heaviest first, ties by relation id
     load = np.zeros(world, np.int64)
-    owner = {}
+    own = np.zeros(Q, np.int64)
     for i in order:
-        k = int(np.argmin(load))
-        owner[int(rels[i])] = k
-        load[k] += counts[i]
-    own = np.array([owner[int(r)] for r in rel_of_query]) if len(rel_of_query) else np.zeros(0, int)
+        lo, left = int(starts[i]), int(counts[i])
+        while left > 0:
+            k = int(np.argmin(load))
+            take = left if not split else min(left, max(share - int(load[k]), 0) or left)
+            own[order_q[lo:lo + take]] = k
+            load[k] += take
+            lo += take
+            left -= take
     return [own == k for k in range(world)]
 
 
@@ -57,7 +73,12 @@ def gather_counts(local_counts: torch.Tensor, plan: ShardPlan, group=None):
     buf = torch.zeros((4, plan.pad), dtype=torch.int32, device=plan.device)
     buf[:, :local_counts.shape[1]] = local_counts
     out = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32, device=plan.device)
-    dist.all_gather_into_tensor(out, buf, group=group)  # rank-major concatenation along dim 0
+    if buf.is_cuda and dist.get_backend(group) == "gloo":  # gloo (tests): the exchange goes through host memory
+        host = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32)
+        dist.all_gather_into_tensor(host, buf.cpu(), group=group)
+        out.copy_(host)
+    else:
+        dist.all_gather_into_tensor(out, buf, group=group)  # rank-major concatenation along dim 0
     out = out.view(plan.world, 4, plan.pad)
     full = torch.empty((4, plan.n_total), dtype=torch.int32, device=plan.device)
     full[:, plan.dst] = out.permute(1, 0, 2).reshape(4, -1)[:, plan.cols]

@@ -169,7 +169,7 @@ def test_lpt_partition(world):
     from mmre.sharding import lpt_partition
     z = load_zs_test("FB15K-237-ZS")
     qr = np.concatenate([z["r"], z["r"]])
-    masks = lpt_partition(qr, world)
+    masks = lpt_partition(qr, world, split=False)
     assert np.array_equal(np.sum(masks, 0), np.ones(len(qr)))  # a partition
     for m in masks:  # whole relations per rank
         for r in np.unique(qr[m]):
@@ -178,6 +178,33 @@ def test_lpt_partition(world):
     # FB15K-237-ZS LPT ceilings 1.99 / 3.98 / 7.84 at 2 / 4 / 8 ranks
     ceiling = len(qr) / max(loads)
     assert ceiling >= {1: 1.0, 2: 1.98, 4: 3.9, 8: 7.5}[world]
+
+
+@pytest.mark.parametrize("dataset", ["FB15K-237-ZS", "DB15K-ZS"])
+@pytest.mark.parametrize("world", [2, 3, 8, 16])
+def test_lpt_partition_with_query_pieces(dataset, world):
+    """SURVEY §8(e) fallback: relations above the per-rank share are cut into contiguous
+    query pieces; DB15K-ZS's whole-relation ceiling at 8 ranks (5.41x) rises to > 7.5x, and
+    every rank's share of a relation is a run of consecutive queries of it (Test.h order)."""
+    from mmre.data import load_zs_test
+    from mmre.sharding import lpt_partition
+    z = load_zs_test(dataset)
+    qr = np.concatenate([z["r"], z["r"]])
+    masks = lpt_partition(qr, world)
+    assert np.array_equal(np.sum(masks, 0), np.ones(len(qr)))
+    ceiling = len(qr) / max(m.sum() for m in masks)
+    assert ceiling >= 0.93 * world
+    whole = len(qr) / max(m.sum() for m in lpt_partition(qr, world, split=False))
+    assert ceiling >= whole - 1e-9
+    for m in masks:
+        for r in np.unique(qr[m]):
+            idx = np.nonzero(qr == r)[0]          # the relation's queries in order
+            mine = np.nonzero(m[idx])[0]          # positions of this rank's among them
+            # pieces are contiguous in the relation's own order: few runs
+            runs = 1 + int(np.sum(np.diff(mine) > 1))
+            assert runs <= -(-len(idx) // -(-len(qr) // world)) + 1
+    if dataset == "DB15K-ZS" and world == 8:
+        assert whole < 5.5 and ceiling > 7.5
 
 
 def test_zs_datasets_shipped():

@@ -89,3 +89,60 @@ def test_sharded_counts_equal_single_rank(tmp_path, world, keep_rel):
                                            torch.from_numpy(np.r_[np.zeros(len(h), np.int8), np.ones(len(h), np.int8)]),
                                            None, None).numpy()
     assert np.array_equal(outs[0], single)
+
+
+# ------------------------------------------------------------------ GPU --
+def _gpu_worker(rank, world, port, res_path, dataset, model, dim):
+    """Each rank: the HIP sweep on cuda:0 through ShardedLinkEvaluation.launch/finish (counts
+    exchanged over gloo through host memory); rank 0 also runs the single-process evaluation
+    and the out-of-order ticket sequence."""
+    sys.path[:0] = [PKG, os.path.join(REPO, "oracle"), REPO]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmre.link import FilterIndex, ScoreSpec, evaluate_link_prediction, rotate_phase_denom
+    from mmre.sharding import ShardedLinkEvaluation
+    from mmre.workloads import zs_workload
+    dev = torch.device("cuda:0")
+    w = zs_workload(dataset, model, dim)
+    E = w["n_ent"]
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
+    pk = {"transe": 0, "distmult": 2, "complex": 2, "rotate": 3}[model]
+    spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
+                     ent_im=w["ent_im"].to(dev) if "ent_im" in w else None,
+                     rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=model == "transe",
+                     pred_kind=pk, margin=float(w.get("margin", 0.0)),
+                     phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
+    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+    a = ev.launch()
+    b = ev.launch()
+    mb, cb = ev.finish(b)        # out of order: b first, then a third launch while a is pending
+    c = ev.launch()
+    ma, ca = ev.finish(a)
+    mc, cc = ev.finish(c)
+    out = dict(counts_a=ca, counts_b=cb, counts_c=cc, n_local=np.array(int(ev.masks[rank].sum())))
+    if rank == 0:
+        m1, (h1, t1) = evaluate_link_prediction(spec, w["test_h"], w["test_r"], w["test_t"], index=index)
+        out["single"] = np.concatenate([h1, t1], 1)
+        out["metrics_equal"] = np.array(all(ma[g][k] == m1[g][k] for g in m1 for k in m1[g]))
+    np.savez(f"{res_path}_{rank}.npz", **out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dataset,model,dim,world", [("FB15K-237-ZS", "transe", 200, 2),
+                                                      ("DB15K-ZS", "complex", 200, 3)])
+def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world):
+    """The multi-rank path with the real HIP sweep at full size (C2; C3 with its largest
+    relation split across ranks): every rank's gathered counts -- for three overlapping
+    evaluations finished out of order -- and rank 0's metrics are bit-equal to one process."""
+    port = _free_port()
+    res = str(tmp_path / "hip")
+    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim), nprocs=world, join=True)
+    outs = [dict(np.load(f"{res}_{k}.npz")) for k in range(world)]
+    single = outs[0]["single"]
+    assert bool(outs[0]["metrics_equal"])
+    for o in outs:
+        for key in ("counts_a", "counts_b", "counts_c"):
+            assert np.array_equal(o[key], single), key
+    assert sum(int(o["n_local"]) for o in outs) == single.shape[1]
+    assert max(int(o["n_local"]) for o in outs) <= -(-single.shape[1] // world)
