@@ -793,8 +793,8 @@ def bench_m3ae(args, world, rank, dev, dist):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="test triples in the CPU-baseline / parity sample (0: per-config default)")

@@ -50,6 +50,42 @@ __device__ __forceinline__ float apply_pred(int kind, float m, float s) {
   }
 }
 
+// apply_pred with the kind fixed at compile time (sweep epilogues: no per-element branch)
+template <int K>
+struct PredK {
+  float m;
+  __device__ __forceinline__ float operator()(float s) const {
+    if constexpr (K == 0) return s;
+    else if constexpr (K == 1) return m - (m - s);
+    else if constexpr (K == 2) return -s;
+    else if constexpr (K == 3) return -(m - s);
+    else return m - s;
+  }
+};
+// ... and decoded once into uniform selects, for the other kinds. Same operations, bit-identical.
+struct PredFn {
+  float m;
+  bool use_m, twice;  // x = use_m ? m - s : s; x = twice ? m - x : x
+  uint32_t neg;       // sign-bit flip: exactly IEEE negation
+  __device__ __forceinline__ explicit PredFn(int kind, float margin)
+      : m(margin), use_m(kind == 1 || kind == 3 || kind >= 4), twice(kind == 1),
+        neg((kind == 2 || kind == 3) ? 0x80000000u : 0u) {}
+  __device__ __forceinline__ float operator()(float s) const {
+    float x = use_m ? m - s : s;
+    x = twice ? m - x : x;
+    return __uint_as_float(__float_as_uint(x) ^ neg);
+  }
+};
+// PredSel<K>: the compile-time kind K, or (K = -1) the run-time kind decoded into selects
+template <int K>
+struct PredSel : PredK<K> {
+  __device__ __forceinline__ PredSel(int, float margin) : PredK<K>{margin} {}
+};
+template <>
+struct PredSel<-1> : PredFn {
+  __device__ __forceinline__ PredSel(int kind, float margin) : PredFn(kind, margin) {}
+};
+
 // Canonical single-precision sincos: Cody-Waite reduction by pi/2 in fma form and
 // cephes minimax polynomials on [-pi/4, pi/4]. Same operation sequence as the CA
 // specification, so the RotatE rotation is reproducible bit-for-bit.

@@ -94,10 +94,16 @@ class ShardedLinkEvaluation:
     the int32 rank counts gives every rank the full count table; the Test.h metric reduction
     then runs in the reference's sequential query order, so rank 0's metrics are bit-identical
     to a single-GPU evaluation. `local_runner(qh, qr, qt, qm, filt)` -> (4, n_local) int32
-    device tensor is the per-rank sweep (defaults to mmre.link.LinkSweep)."""
+    device tensor is the per-rank sweep (defaults to mmre.link.LinkSweep).
+
+    graph=True (default LinkSweep runner on a GPU): the rank's local evaluation -- entity and
+    query prep, truth/filter kernels, sweep -- is captured once into a hipGraph and replayed,
+    so its ~6 launches cost one; what a rank pays whatever its share shrinks.
+    The all-gather and the D2H stay outside the graph. Timing events passed to counts() then
+    bracket the whole replay, not the sweep kernel alone."""
 
     def __init__(self, spec, test_h, test_r, test_t, index=None, type_constrain=False, group=None,
-                 device=None, local_runner=None):
+                 device=None, local_runner=None, graph=False):
         import torch.distributed as dist
         from .link import HEAD, TAIL
         self.group = group
@@ -126,6 +132,7 @@ class ShardedLinkEvaluation:
                                      "(type_constrain.txt, Reader.h:266-317)")
                 self.masks_tc = tuple(to(m) for m in tm)
         self.plan = ShardPlan(self.masks, dev) if self.world > 1 else None
+        self._default_runner = local_runner is None
         if local_runner is None:
             from .link import LinkSweep
             sw = LinkSweep(spec)
@@ -135,10 +142,30 @@ class ShardedLinkEvaluation:
                 return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs,
                               sweep_events=events)["counts"]
         self.local_runner = local_runner
+        self._graph_wanted = bool(graph) and dev.type == "cuda" and self._default_runner
+        self._graph = None
+
+    def _local(self, events=None):
+        if not self._graph_wanted:
+            return self.local_runner(*self.q, self.filt, self.masks_tc, events)
+        if self._graph is None:
+            # one eager run allocates every lazily sized buffer, then capture on a side stream
+            self.local_runner(*self.q, self.filt, self.masks_tc, None)
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_out = self.local_runner(*self.q, self.filt, self.masks_tc, None)
+            self._graph = g
+        if events is not None:
+            events[0].record()
+        self._graph.replay()
+        if events is not None:
+            events[1].record()
+        return self._graph_out
 
     def counts(self, events=None):
         """(4, 2n) int32 counts in global query order (head block, then tail block)."""
-        local = self.local_runner(*self.q, self.filt, self.masks_tc, events)
+        local = self._local(events)
         return gather_counts(local, self.plan, self.group) if self.world > 1 else local
 
     def launch(self, events=None):

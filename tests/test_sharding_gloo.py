@@ -92,7 +92,7 @@ def test_sharded_counts_equal_single_rank(tmp_path, world, keep_rel):
 
 
 # ------------------------------------------------------------------ GPU --
-def _gpu_worker(rank, world, port, res_path, dataset, model, dim):
+def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph):
     """Each rank: the HIP sweep on cuda:0 through ShardedLinkEvaluation.launch/finish (counts
     exchanged over gloo through host memory); rank 0 also runs the single-process evaluation
     and the out-of-order ticket sequence."""
@@ -112,7 +112,7 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim):
                      rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=model == "transe",
                      pred_kind=pk, margin=float(w.get("margin", 0.0)),
                      phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
-    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev, graph=graph)
     a = ev.launch()
     b = ev.launch()
     mb, cb = ev.finish(b)        # out of order: b first, then a third launch while a is pending
@@ -129,15 +129,17 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dataset,model,dim,world", [("FB15K-237-ZS", "transe", 200, 2),
-                                                      ("DB15K-ZS", "complex", 200, 3)])
-def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world):
+@pytest.mark.parametrize("dataset,model,dim,world,graph", [("FB15K-237-ZS", "transe", 200, 2, False),
+                                                            ("FB15K-237-ZS", "transe", 200, 2, True),
+                                                            ("DB15K-ZS", "complex", 200, 3, True)])
+def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph):
     """The multi-rank path with the real HIP sweep at full size (C2; C3 with its largest
-    relation split across ranks): every rank's gathered counts -- for three overlapping
-    evaluations finished out of order -- and rank 0's metrics are bit-equal to one process."""
+    relation split across ranks), eager and with each rank's local evaluation replayed from a
+    hipGraph: every rank's gathered counts -- for three overlapping evaluations finished out of
+    order -- and rank 0's metrics are bit-equal to one process."""
     port = _free_port()
     res = str(tmp_path / "hip")
-    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim), nprocs=world, join=True)
+    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph), nprocs=world, join=True)
     outs = [dict(np.load(f"{res}_{k}.npz")) for k in range(world)]
     single = outs[0]["single"]
     assert bool(outs[0]["metrics_equal"])
