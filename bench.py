@@ -77,8 +77,8 @@ def valu_ops_per_triple(model, dim):
     return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 16.75 * dim}.get(model)
 
 
-KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false>", "rotate": "k_sweep_valu<2, false, false>",
-                "distmult": "k_sweep_mfma<false, false>", "complex": "k_sweep_mfma<false, false>"}
+KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
+                "distmult": "k_sweep_mfma<false, false, 2", "complex": "k_sweep_mfma<false, false, 2"}
 
 
 def pmc_traffic(config: str, model: str):

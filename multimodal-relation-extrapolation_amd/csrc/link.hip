@@ -17,6 +17,8 @@
 //   k_sweep_mfma      DistMult/ComplEx: v_mfma_f32_32x32x2_f32, register-counter epilogue
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "mmre_common.h"
 
 namespace mmre {
@@ -820,9 +822,10 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
           int c = 0, cc = 0;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const int64_t e = ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
+            // 32-bit ids (int32 by check_link_args); bitwise &: no per-pair branch
+            const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
             const float v = pred(op_final<OP>(acc[i][j]));
-            const bool better = (v < th) && (e != tr) && (e < n_ent);
+            const bool better = (v < th) & (e != tr) & (e < n_ent);
             c += better;
             if constexpr (TC) {
               const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
@@ -887,192 +890,19 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 // score is bit-identical to the threshold (same canonical chain), so `< thr` rejects it.
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-template <bool TC, bool STORE, int PK>
+template <bool TC, bool STORE, int PK, int KS>
 __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
     int64_t q_pad, int64_t n_query, int ktot, int n_et, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
     const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
     int32_t* __restrict__ counts, float* __restrict__ scores) {
-  constexpr int KS = KS_MFMA;
+  static_assert(KS == 16 || KS == 32, "stage of 16 or 32 K rows");
   __shared__ float sq[2][KS][TQ];
   __shared__ float se[2][KS][TE];
   __shared__ int32_t s_rel[TC ? TQ : 1];
   __shared__ int8_t s_mode[TC ? TQ : 1];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const PredSel<PK> pred(pred_kind, margin);
-  const int wq = wave >> 1, we = wave & 1;
-  const int lrow = lane >> 5, lcol = lane & 31;
-  const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
-  const int per_grp = gridDim.x / n_groups;
-  const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et);
-  const int u0 = (int)((int64_t)gmem * um.count / per_grp);
-  const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
-  if (u0 >= u1) return;  // uniform over the workgroup
-  const int nkc = ktot / KS;  // planes are padded to whole stages (plane_rows)
-
-  // rows of this lane: ql(bi, r) = wq*64 + bi*32 + (r&3) + 8*(r>>2) + 4*lrow
-  float th[2][16];
-  int cnt[2][16], cnt_tc[TC ? 2 : 1][TC ? 16 : 1];
-  auto row_of = [&](int bi, int r) { return wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lrow; };
-  auto load_rows = [&](int qtile) {
-    const int64_t q0 = (int64_t)qtile * TQ;
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t q = q0 + row_of(bi, r);
-        th[bi][r] = q < n_query ? thr[q] : -INFINITY;  // -inf: nothing beats a padded row
-        cnt[bi][r] = 0;
-        if constexpr (TC) cnt_tc[bi][r] = 0;
-      }
-    if constexpr (TC) {
-      __syncthreads();  // previous tile's s_rel/s_mode readers are done
-      if (tid < TQ) {
-        const int64_t q = q0 + tid;
-        s_rel[tid] = q < n_query ? (int32_t)qr[q] : 0;
-        s_mode[tid] = q < n_query ? qmode[q] : 0;
-      }
-    }
-  };
-  auto flush_rows = [&](int qtile) {
-    const int64_t q0 = (int64_t)qtile * TQ;
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int c = cnt[bi][r];
-#pragma unroll
-        for (int sh = 1; sh < 32; sh <<= 1) c += __shfl_xor(c, sh);  // the 32 column lanes
-        int cc = 0;
-        if constexpr (TC) {
-          cc = cnt_tc[bi][r];
-#pragma unroll
-          for (int sh = 1; sh < 32; sh <<= 1) cc += __shfl_xor(cc, sh);
-        }
-        const int64_t q = q0 + row_of(bi, r);
-        if (lcol == 0 && q < n_query) {
-          if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
-          if constexpr (TC) {
-            if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
-          }
-        }
-      }
-  };
-
-  const int srow = tid >> 5, sc4 = tid & 31;  // rows srow + 8 i of the stage
-  float4 rq0, rq1, re0, re1;  // named scalars, not an array: kept in VGPRs
-  int ld_unit = u0, ld_kc = 0, ld_qt, ld_et;
-  um.at(u0, ld_qt, ld_et);
-  auto gload = [&]() {
-    const int k = ld_kc * KS + srow;
-    const float* qp = q_km + (int64_t)k * q_pad + (int64_t)ld_qt * TQ + sc4 * 4;
-    const float* ep = ent_km + (int64_t)k * e_pad + (int64_t)ld_et * TE + sc4 * 4;
-    rq0 = *reinterpret_cast<const float4*>(qp);
-    rq1 = *reinterpret_cast<const float4*>(qp + 8 * q_pad);
-    re0 = *reinterpret_cast<const float4*>(ep);
-    re1 = *reinterpret_cast<const float4*>(ep + 8 * e_pad);
-    if (++ld_kc == nkc) {
-      ld_kc = 0;
-      if (++ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
-    }
-  };
-  auto swrite = [&](int buf) {
-    *reinterpret_cast<float4*>(&sq[buf][srow][sc4 * 4]) = rq0;
-    *reinterpret_cast<float4*>(&sq[buf][srow + 8][sc4 * 4]) = rq1;
-    *reinterpret_cast<float4*>(&se[buf][srow][sc4 * 4]) = re0;
-    *reinterpret_cast<float4*>(&se[buf][srow + 8][sc4 * 4]) = re1;
-  };
-
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
-
-  int cur_qt, cur_et;
-  um.at(u0, cur_qt, cur_et);
-  load_rows(cur_qt);
-  gload();
-  swrite(0);
-  __syncthreads();
-
-  int buf = 0;
-  for (int unit = u0; unit < u1; ++unit) {
-    for (int kc = 0; kc < nkc; ++kc) {
-      const bool more = ld_unit < u1;
-      if (more) gload();
-#pragma unroll
-      for (int kp2 = 0; kp2 < KS; kp2 += 2) {
-        const float a0 = sq[buf][kp2 + lrow][wq * 64 + lcol];
-        const float a1 = sq[buf][kp2 + lrow][wq * 64 + 32 + lcol];
-        const float b0 = se[buf][kp2 + lrow][we * 64 + lcol];
-        const float b1 = se[buf][kp2 + lrow][we * 64 + 32 + lcol];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-      }
-      if (kc == nkc - 1) {  // unit finished: rank epilogue
-        const int64_t q0 = (int64_t)cur_qt * TQ;
-        const int64_t ebase = (int64_t)cur_et * TE + we * 64;
-#pragma unroll
-        for (int bj = 0; bj < 2; ++bj) {
-          const int64_t e = ebase + bj * 32 + lcol;
-          const bool ev = e < n_ent;
-#pragma unroll
-          for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float v = pred(acc[bi][bj][r]);
-              const bool better = ev && (v < th[bi][r]);
-              cnt[bi][r] += better;
-              if constexpr (TC) {
-                const int ql = row_of(bi, r);
-                const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e);
-              }
-              if constexpr (STORE) {
-                const int64_t q = q0 + row_of(bi, r);
-                if (q < n_query && ev) scores[q * n_ent + e] = v;
-              }
-              acc[bi][bj][r] = 0.0f;
-            }
-        }
-        const bool last = unit + 1 >= u1;
-        int next_qt = cur_qt, next_et = cur_et;
-        if (!last) um.at(unit + 1, next_qt, next_et);
-        if (last || next_qt != cur_qt) {  // uniform: leave this query tile
-          flush_rows(cur_qt);
-          if (!last) load_rows(next_qt);
-        }
-        cur_qt = next_qt;
-        cur_et = next_et;
-      }
-      if (more) swrite(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
-    }
-  }
-}
-
-template <bool TC, bool STORE, int PK>
-__global__ __launch_bounds__(NT, 2) void k_sweep_mfma_v3(
-    const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
-    int64_t q_pad, int64_t n_query, int ktot, int n_et, int n_groups, int pred_kind, float margin,
-    const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
-    const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
-    int32_t* __restrict__ counts, float* __restrict__ scores) {
-  constexpr int KS = KS_MFMA;
-  __shared__ float sq[2][KS][TQ];
-  __shared__ float se[2][KS][TE];
-  __shared__ int32_t s_rel[TC ? TQ : 1];
-  __shared__ int8_t s_mode[TC ? TQ : 1];
-  __shared__ float s_th[2][TQ];
+  __shared__ __attribute__((aligned(16))) float s_th[2][TQ];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1142,7 +972,7 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma_v3(
   };
 
   const int srow = tid >> 5, sc4 = tid & 31;  // rows srow + 8 i of the stage
-  float4 rq0, rq1, re0, re1;  // named scalars, not an array: kept in VGPRs
+  float4 rq0, rq1, re0, re1, rq2, rq3, re2, re3;  // named scalars, not an array: kept in VGPRs
   int ld_unit = u0, ld_kc = 0, ld_qt, ld_et;
   um.at(u0, ld_qt, ld_et);
   auto gload = [&]() {
@@ -1153,6 +983,12 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma_v3(
     rq1 = *reinterpret_cast<const float4*>(qp + 8 * q_pad);
     re0 = *reinterpret_cast<const float4*>(ep);
     re1 = *reinterpret_cast<const float4*>(ep + 8 * e_pad);
+    if constexpr (KS == 32) {
+      rq2 = *reinterpret_cast<const float4*>(qp + 16 * q_pad);
+      rq3 = *reinterpret_cast<const float4*>(qp + 24 * q_pad);
+      re2 = *reinterpret_cast<const float4*>(ep + 16 * e_pad);
+      re3 = *reinterpret_cast<const float4*>(ep + 24 * e_pad);
+    }
     if (++ld_kc == nkc) {
       ld_kc = 0;
       if (++ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
@@ -1163,6 +999,12 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma_v3(
     *reinterpret_cast<float4*>(&sq[buf][srow + 8][sc4 * 4]) = rq1;
     *reinterpret_cast<float4*>(&se[buf][srow][sc4 * 4]) = re0;
     *reinterpret_cast<float4*>(&se[buf][srow + 8][sc4 * 4]) = re1;
+    if constexpr (KS == 32) {
+      *reinterpret_cast<float4*>(&sq[buf][srow + 16][sc4 * 4]) = rq2;
+      *reinterpret_cast<float4*>(&sq[buf][srow + 24][sc4 * 4]) = rq3;
+      *reinterpret_cast<float4*>(&se[buf][srow + 16][sc4 * 4]) = re2;
+      *reinterpret_cast<float4*>(&se[buf][srow + 24][sc4 * 4]) = re3;
+    }
   };
 
   floatx16 acc[2][2];
@@ -1185,50 +1027,65 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma_v3(
     for (int kc = 0; kc < nkc; ++kc) {
       const bool more = ld_unit < u1;
       if (more) gload();
-      // every operand of the stage read up front (16 ds_read2), then 32 MFMAs back to back
-      float opa[KS / 2][2], opb[KS / 2][2];
-#pragma unroll
-      for (int p = 0; p < KS / 2; ++p) {
-        opa[p][0] = sq[buf][2 * p + lrow][wq * 64 + lcol];
-        opa[p][1] = sq[buf][2 * p + lrow][wq * 64 + 32 + lcol];
-        opb[p][0] = se[buf][2 * p + lrow][we * 64 + lcol];
-        opb[p][1] = se[buf][2 * p + lrow][we * 64 + 32 + lcol];
-      }
+      // the next stage's loads stay at the top of this one: hipcc otherwise sinks them to
+      // their use at the stage's end and every stage waits a full L2 / MALL latency
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int p = 0; p < KS / 2; ++p) {
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(opa[p][0], opb[p][0], acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(opa[p][0], opb[p][1], acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(opa[p][1], opb[p][0], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(opa[p][1], opb[p][1], acc[1][1], 0, 0, 0);
+      for (int kp2 = 0; kp2 < KS; kp2 += 2) {
+        const float a0 = sq[buf][kp2 + lrow][wq * 64 + lcol];
+        const float a1 = sq[buf][kp2 + lrow][wq * 64 + 32 + lcol];
+        const float b0 = se[buf][kp2 + lrow][we * 64 + lcol];
+        const float b1 = se[buf][kp2 + lrow][we * 64 + 32 + lcol];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);
       if (kc == nkc - 1) {  // unit finished: rank epilogue
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE + we * 64;
+        // the lane's 32 row thresholds, 8 LDS reads issued together (a read per compare
+        // serialised 64 LDS latencies per unit); rows row_of(bi, 4i) .. + 3 are contiguous
+        float tv[2][16];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r4 = 0; r4 < 16; r4 += 4) {
+            const float4 t4 = *reinterpret_cast<const float4*>(&s_th[tpar][row_of(bi, r4)]);
+            tv[bi][r4] = t4.x;
+            tv[bi][r4 + 1] = t4.y;
+            tv[bi][r4 + 2] = t4.z;
+            tv[bi][r4 + 3] = t4.w;
+          }
 #pragma unroll
         for (int bj = 0; bj < 2; ++bj) {
           const int64_t e = ebase + bj * 32 + lcol;
-          const bool ev = e < n_ent;
+          if (e < n_ent) {  // one exec mask per column block (lanes diverge in the last tile only)
 #pragma unroll
-          for (int bi = 0; bi < 2; ++bi)
+            for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const float v = pred(acc[bi][bj][r]);
-              const bool better = ev && (v < s_th[tpar][row_of(bi, r)]);
-              cnt[bi][r] += better;
-              if constexpr (TC) {
-                const int ql = row_of(bi, r);
-                const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e);
+              for (int r = 0; r < 16; ++r) {
+                const float v = pred(acc[bi][bj][r]);
+                const bool better = v < tv[bi][r];
+                cnt[bi][r] += better;
+                if constexpr (TC) {
+                  const int ql = row_of(bi, r);
+                  const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                  cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e);
+                }
+                if constexpr (STORE) {
+                  const int64_t q = q0 + row_of(bi, r);
+                  if (q < n_query) scores[q * n_ent + e] = v;
+                }
               }
-              if constexpr (STORE) {
-                const int64_t q = q0 + row_of(bi, r);
-                if (q < n_query && ev) scores[q * n_ent + e] = v;
-              }
-              acc[bi][bj][r] = 0.0f;
-            }
+          }
         }
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.0f;
         const bool last = unit + 1 >= u1;
         int next_qt = cur_qt, next_et = cur_et;
         if (!last) um.at(unit + 1, next_qt, next_et);
@@ -1242,217 +1099,6 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma_v3(
       if (more) swrite(buf ^ 1);
       __syncthreads();
       buf ^= 1;
-    }
-  }
-}
-
-// ------------------------------------------------- MFMA sweep, LDS-DMA pipeline ---
-// Same units, tiles, MFMA chain and epilogue as k_sweep_mfma, but everything the loop reads
-// from memory goes global -> LDS by global_load_lds (no VGPR staging, no register wait):
-// the k-major planes into a ring of three 16-row stages, two stages in flight, and each
-// unit's 128 thresholds into a ring of three rows, issued with the unit's first stage. The
-// wait for stage t is a counted `s_waitcnt vmcnt(4)` that leaves stage t + 1's loads of the
-// wave outstanding across the barrier (raw s_barrier: __syncthreads would drain them). A
-// plain global load anywhere in the loop would make the compiler drain every load in flight
-// at its use (vmcnt counts in order), hence the thresholds through LDS too.
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-constexpr int MRING = 3;
-
-// The 32 thresholds of a lane's rows (row_of(bi, 4i) .. + 3 = p[32 bi + 8 i ..]) by LDS reads
-// the compiler cannot see: a plain ds_read of a row that global_load_lds fills makes hipcc
-// wait for every LDS-DMA load in flight (vmcnt(0)), here two stages of the ring. The row was
-// made visible by the counted wait + barrier of the unit's first stage.
-__device__ __forceinline__ void lds_thresholds(const float* p, float4 (&t)[2][4]) {
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
-  asm volatile(
-      "ds_read_b128 %0, %8\n ds_read_b128 %1, %8 offset:32\n ds_read_b128 %2, %8 offset:64\n"
-      " ds_read_b128 %3, %8 offset:96\n ds_read_b128 %4, %8 offset:128\n ds_read_b128 %5, %8 offset:160\n"
-      " ds_read_b128 %6, %8 offset:192\n ds_read_b128 %7, %8 offset:224\n s_waitcnt lgkmcnt(0)"
-      : "=&v"(t[0][0]), "=&v"(t[0][1]), "=&v"(t[0][2]), "=&v"(t[0][3]), "=&v"(t[1][0]), "=&v"(t[1][1]),
-        "=&v"(t[1][2]), "=&v"(t[1][3])
-      : "v"(a));
-}
-
-template <bool TC, bool STORE, int PK>
-__global__ __launch_bounds__(NT, 2) void k_sweep_mfma_glds(
-    const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
-    int64_t q_pad, int64_t n_query, int ktot, int n_et, int n_groups, int pred_kind, float margin,
-    const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
-    const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
-    int32_t* __restrict__ counts, float* __restrict__ scores) {
-  constexpr int KS = KS_MFMA;
-  // ONE __shared__ object: beside a second one hipcc (ROCm 7.2) waits vmcnt(0) before the
-  // first ds_read of every stage, draining the in-flight loads (cdna_hip_programming.md §5)
-  constexpr int SQF = MRING * KS * TQ, SEF = MRING * KS * TE, STF = MRING * TQ;
-  __shared__ __attribute__((aligned(16))) float smem[SQF + SEF + STF + (TC ? TQ + TQ / 4 : 0)];
-  float(*sq)[KS][TQ] = reinterpret_cast<float(*)[KS][TQ]>(smem);
-  float(*se)[KS][TE] = reinterpret_cast<float(*)[KS][TE]>(smem + SQF);
-  float(*s_th)[TQ] = reinterpret_cast<float(*)[TQ]>(smem + SQF + SEF);
-  int32_t* s_rel = reinterpret_cast<int32_t*>(smem + SQF + SEF + STF);
-  int8_t* s_mode = reinterpret_cast<int8_t*>(smem + SQF + SEF + STF + TQ);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const PredSel<PK> pred(pred_kind, margin);
-  const int wq = wave >> 1, we = wave & 1;
-  const int lrow = lane >> 5, lcol = lane & 31;
-  const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
-  const int per_grp = gridDim.x / n_groups;
-  const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et);
-  const int u0 = (int)((int64_t)gmem * um.count / per_grp);
-  const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
-  if (u0 >= u1) return;  // uniform over the workgroup
-  const int nkc = ktot / KS;
-  const int n_stage = (u1 - u0) * nkc;
-
-  int cnt[2][16], cnt_tc[TC ? 2 : 1][TC ? 16 : 1];
-  auto row_of = [&](int bi, int r) { return wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lrow; };
-  auto reset_rows = [&](int qtile) {
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        cnt[bi][r] = 0;
-        if constexpr (TC) cnt_tc[bi][r] = 0;
-      }
-    if constexpr (TC) {
-      __syncthreads();
-      if (tid < TQ) {
-        const int64_t q = (int64_t)qtile * TQ + tid;
-        s_rel[tid] = q < n_query ? (int32_t)qr[q] : 0;
-        s_mode[tid] = q < n_query ? qmode[q] : 0;
-      }
-      __syncthreads();
-    }
-  };
-  auto flush_rows = [&](int qtile) {
-    const int64_t q0 = (int64_t)qtile * TQ;
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int c = cnt[bi][r];
-#pragma unroll
-        for (int sh = 1; sh < 32; sh <<= 1) c += __shfl_xor(c, sh);
-        int cc = 0;
-        if constexpr (TC) {
-          cc = cnt_tc[bi][r];
-#pragma unroll
-          for (int sh = 1; sh < 32; sh <<= 1) cc += __shfl_xor(cc, sh);
-        }
-        const int64_t q = q0 + row_of(bi, r);
-        if (lcol == 0 && q < n_query) {
-          if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
-          if constexpr (TC) {
-            if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
-          }
-        }
-      }
-  };
-
-  // stage t of this workgroup -> LDS slot t % MRING. Wave w fills rows 4w .. 4w + 3 of both
-  // operands: two 2-row (1 KB) instructions each; lane l covers row + (l >> 5), floats 4 (l & 31).
-  // A unit's first stage also brings its thresholds: waves 0 and 1, 64 queries each, 4 B per
-  // lane, lanes past n_query masked off (the epilogue masks those rows).
-  auto issue = [&](int t) {
-    const int ul = t / nkc, kc = t - ul * nkc;
-    int qt, et;
-    um.at(u0 + ul, qt, et);
-    const int slot = t % MRING;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = 4 * wave + 2 * i;
-      const int64_t k = (int64_t)kc * KS + row + lrow;
-      const float* qp = q_km + k * q_pad + (int64_t)qt * TQ + lcol * 4;
-      const float* ep = ent_km + k * e_pad + (int64_t)et * TE + lcol * 4;
-      __builtin_amdgcn_global_load_lds(qp, (lds_ptr_t)&sq[slot][row][0], 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(ep, (lds_ptr_t)&se[slot][row][0], 16, 0, 0);
-    }
-    if (kc == 0 && wave < 2) {
-      const int64_t q = (int64_t)qt * TQ + wave * 64 + lane;
-      if (q < n_query) __builtin_amdgcn_global_load_lds(thr + q, (lds_ptr_t)&s_th[ul % MRING][wave * 64], 4, 0, 0);
-    }
-  };
-
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
-
-  int cur_qt, cur_et;
-  um.at(u0, cur_qt, cur_et);
-  reset_rows(cur_qt);
-  issue(0);
-  if (n_stage > 1) issue(1);
-  for (int t = 0; t < n_stage; ++t) {
-    // stage t landed (the wave's own loads: at most the 4-5 of stage t + 1 stay outstanding),
-    // then every wave's part of stage t is visible and every wave is done reading slot
-    // (t + 2) % 3 and threshold row (unit + 2) % 3
-    if (t + 1 < n_stage) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + 2 < n_stage) issue(t + 2);
-    const int slot = t % MRING;
-#pragma unroll
-    for (int kp2 = 0; kp2 < KS; kp2 += 2) {
-      const float a0 = sq[slot][kp2 + lrow][wq * 64 + lcol];
-      const float a1 = sq[slot][kp2 + lrow][wq * 64 + 32 + lcol];
-      const float b0 = se[slot][kp2 + lrow][we * 64 + lcol];
-      const float b1 = se[slot][kp2 + lrow][we * 64 + 32 + lcol];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (t % nkc == nkc - 1) {  // unit finished: rank epilogue
-      const int ul = t / nkc;
-      const int64_t q0 = (int64_t)cur_qt * TQ;
-      const int64_t ebase = (int64_t)cur_et * TE + we * 64;
-      const int64_t qv = n_query - q0;  // rows < qv are real queries
-      const float* th = s_th[ul % MRING];
-      float4 t4[2][4];  // rows row_of(bi, 4i) .. + 3
-      lds_thresholds(th + row_of(0, 0), t4);
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-        for (int r4 = 0; r4 < 16; r4 += 4) {
-          const int ql0 = row_of(bi, r4); // rows ql0 .. ql0 + 3
-          const float4 tq4 = t4[bi][r4 / 4];
-          const float tv[4] = {tq4.x, tq4.y, tq4.z, tq4.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = r4 + j;
-            const bool rv = ql0 + j < qv;
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj) {
-              const int64_t e = ebase + bj * 32 + lcol;
-              const float v = pred(acc[bi][bj][r]);
-              const bool better = rv && e < n_ent && (v < tv[j]);
-              cnt[bi][r] += better;
-              if constexpr (TC) {
-                const uint32_t* tm = s_mode[ql0 + j] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql0 + j], e);
-              }
-              if constexpr (STORE) {
-                if (rv && e < n_ent) scores[(q0 + ql0 + j) * n_ent + e] = v;
-              }
-              acc[bi][bj][r] = 0.0f;
-            }
-          }
-        }
-      const bool last = ul + 1 >= u1 - u0;
-      int next_qt = cur_qt, next_et = cur_et;
-      if (!last) um.at(u0 + ul + 1, next_qt, next_et);
-      if (last || next_qt != cur_qt) {  // uniform: leave this query tile
-        flush_rows(cur_qt);
-        if (!last) reset_rows(next_qt);
-      }
-      cur_qt = next_qt;
-      cur_et = next_et;
     }
   }
 }
@@ -1597,7 +1243,7 @@ static int check_link_args(int model, int pred_kind, const float* d_ent_km, int6
   if (!d_ent_km || !d_q_km || !d_q_true || !d_counts || !d_truth || !d_qmode || !d_qr) return MMRE_ERR_ARG;
   if (n_query <= 0 || n_ent <= 0 || e_pad < n_ent || e_pad % TE || q_pad < n_query || q_pad % TQ) return MMRE_ERR_ARG;
   if ((d_type_head == nullptr) != (d_type_tail == nullptr)) return MMRE_ERR_ARG;
-  if (n_ent >= (int64_t)INT32_MAX) return MMRE_ERR_SHAPE;
+  if (n_ent > (int64_t)INT32_MAX - 256) return MMRE_ERR_SHAPE;  // padded ids stay int32
   return MMRE_OK;
 }
 
@@ -1704,14 +1350,21 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
   const int n_et = (int)(e_pad / TE);
   // persistent XCD-grouped grid as for the VALU sweep, 2 workgroups per resident slot (MI355X,
   // KCM = 16: C3 1.20 / 1.24 / 1.22 / 1.24 ms and C5 36.5 / 36.5 / 36.5 / 36.6 ms at 1/2/3/4x)
-  static const int mfma_impl = [] {  /* MMRE_MFMA_IMPL=glds|v3: other MFMA kernels (A/B) */
-    const char* e = getenv("MMRE_MFMA_IMPL");
-    return !e ? 0 : e[0] == 'g' ? 1 : e[0] == 'v' ? 2 : 0;
-  }();
+  // K stages of 32 rows when the planes hold a whole number of them (C3 ComplEx 2 x 208, C5
+  // DistMult 256), else 16: half the per-stage staging and barriers per MFMA
+  // (scripts/probes/mfma_stage.hip: 0.79 -> 0.86 of the f32 MFMA peak with L2-resident data)
+  static const char* ks_env = getenv("MMRE_MFMA_STAGE"); /* experiments: 16 forces 16-row stages */
+  const bool ks32 = ktot % 32 == 0 && !(ks_env && atoi(ks_env) == 16);
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
 #define MMRE_MFMA_K(KERNEL)                                                                                       \
   do {                                                                                                            \
-    int g = 2 * resident_groups((const void*)KERNEL, NT); /* flat 1-4x on C3/C5 */                              \
+    /* 16 units per workgroup, between 2 and 8 x the resident slots: short ranges let the      */                \
+    /* dispatcher balance CUs of different speed (C5 1,024 / 4,096 groups: 35.1 / 34.3 ms) while */                \
+    /* the few-unit C3 keeps ranges long enough to amortise each group's first stage (C3: 1,024 */                \
+    /* groups 1.12 ms, 4,096 1.17 ms)                                                           */                \
+    const int res = resident_groups((const void*)KERNEL, NT);                                                     \
+    const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                           \
+    int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>(2LL * res, units / 16)) & ~7;                     \
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                              \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL(KERNEL, dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,       \
@@ -1720,14 +1373,15 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
   } while (0)
 #define MMRE_MFMA(TCV, STV, PKV)                                                                           \
   do {                                                                                                 \
-    if (mfma_impl == 1) MMRE_MFMA_K((k_sweep_mfma_glds<TCV, STV, PKV>));                               \
-    else if (mfma_impl == 2) MMRE_MFMA_K((k_sweep_mfma_v3<TCV, STV, PKV>));                            \
-    else MMRE_MFMA_K((k_sweep_mfma<TCV, STV, PKV>));                                                   \
+    if (ks32) MMRE_MFMA_K((k_sweep_mfma<TCV, STV, PKV, 32>));                                          \
+    else MMRE_MFMA_K((k_sweep_mfma<TCV, STV, PKV, 16>));                                               \
   } while (0)
-  // run-time prediction kind (decoded into selects): compiled in (PredK<2>), the MFMA kernels
-  // spill ~100 SGPRs and run 1.5 % slower on C5
+  // DistMult / ComplEx predict -s: compiled into the plain sweep's epilogue (one compare with a
+  // negated operand per pair); other kinds and the TC / STORE variants decode it at run time
   if (tc) { if (store) MMRE_MFMA(true, true, -1); else MMRE_MFMA(true, false, -1); }
-  else { if (store) MMRE_MFMA(false, true, -1); else MMRE_MFMA(false, false, -1); }
+  else if (store) MMRE_MFMA(false, true, -1);
+  else if (pred_kind == 2) MMRE_MFMA(false, false, 2);
+  else MMRE_MFMA(false, false, -1);
 #undef MMRE_MFMA
 #undef MMRE_MFMA_K
   MMRE_CHECK_LAUNCH();

@@ -8,6 +8,6 @@ for c in ${@:-c2 c3 c5}; do
   for rep in 1 2; do
     MMRE_LIB=$other TAG=other timeout -k 10 200 python scripts/ab_sweep.py $c 10 2>&1 | grep sweep || exit 1
     TAG=new timeout -k 10 200 python scripts/ab_sweep.py $c 10 2>&1 | grep sweep || exit 1
-    [ $c != c2 ] && [ $c != c4 ] && { MMRE_MFMA_IMPL=v3 TAG=new_v3 timeout -k 10 200 python scripts/ab_sweep.py $c 10 2>&1 | grep sweep || exit 1; }
+    [ $c != c2 ] && [ $c != c4 ] && { MMRE_MFMA_STAGE=16 TAG=new_ks16 timeout -k 10 200 python scripts/ab_sweep.py $c 10 2>&1 | grep sweep || exit 1; }
   done
 done

@@ -33,7 +33,8 @@ __global__ __launch_bounds__(256, OCC) void k(const float* __restrict__ src, flo
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
   float ra0 = lane * 1e-3f, ra1 = ra0 + 1.0f, rb0 = ra0 * 0.5f, rb1 = ra0 + 2.0f;
   const int srow = tid >> 5, sc4 = tid & 31;
-  auto src_row = [&](int s) { return ((int64_t)blockIdx.x * 7 + s * KS) % (src_rows - KS); };
+  // big sources: each stage reads a different far-apart slice (HBM streaming, as C5's table)
+  auto src_row = [&](int s) { return ((int64_t)blockIdx.x * 7919 + (int64_t)s * KS * 61) % (src_rows - KS); };
   // V4: wave w fills rows (KS/4) w .. of both operands, 2 rows (1 KB) per instruction
   auto issue = [&](int s) {
     const int slot = s % 3;
@@ -111,10 +112,11 @@ int main() {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   float* out;
   (void)hipMalloc(&out, 1024 * sizeof(float));
-  const int64_t src_rows = 1 << 13;  // 16 MB source: L2 / Infinity-Cache resident
+  int64_t src_rows = 1 << 13;  // 16 MB source: L2 / Infinity-Cache resident
+  const int64_t big_rows = (int64_t)1 << 20;  // 2 GB source: HBM
   float* src;
-  (void)hipMalloc(&src, src_rows * 512 * sizeof(float));
-  (void)hipMemset(src, 0, src_rows * 512 * sizeof(float));
+  (void)hipMalloc(&src, big_rows * 512 * sizeof(float));
+  (void)hipMemset(src, 0, big_rows * 512 * sizeof(float));
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -132,22 +134,19 @@ int main() {
       if (ms < best) best = ms;
     }
     const double flops = (double)blocks * 4 * stages * (ks / 2) * 4 * (32.0 * 32 * 2 * 2);
-    printf("%-40s KS %2d  %d/CU  %8.3f ms  %7.1f TF  %.3f of 157.3\n", name, ks, per_cu, best, flops / best / 1e9,
+    printf("%-40s %s KS %2d  %d/CU  %8.3f ms  %7.1f TF  %.3f of 157.3\n", name, src_rows > 100000 ? "HBM" : "L2 ", ks, per_cu, best, flops / best / 1e9,
            flops / best / 1e9 / 157.3);
   };
   run(k<0, 16, 2>, "V0 register operands", 2, 16);
   run(k<1, 16, 2>, "V1 + LDS operand reads", 2, 16);
   run(k<2, 16, 2>, "V2 + barrier per stage", 2, 16);
-  run(k<3, 16, 2>, "V3 + global->LDS staging (early)", 2, 16);
-  run(k<4, 16, 2>, "V4 glds ring, 2 stages in flight", 2, 16);
-  run(k<2, 32, 2>, "V2 + barrier per stage", 2, 32);
-  run(k<3, 32, 2>, "V3 + global->LDS staging (early)", 2, 32);
-  run(k<4, 32, 2>, "V4 glds ring, 2 stages in flight", 2, 32);
-  run(k<2, 16, 3>, "V2 + barrier per stage", 3, 16);
-  run(k<3, 16, 3>, "V3 + global->LDS staging (early)", 3, 16);
-  run(k<4, 16, 3>, "V4 glds ring, 2 stages in flight", 3, 16);
-  run(k<3, 32, 3>, "V3 + global->LDS staging (early)", 3, 32);
-  run(k<4, 32, 3>, "V4 glds ring, 2 stages in flight", 3, 32);
+  for (int big = 0; big < 2; ++big) {
+    src_rows = big ? big_rows : (1 << 13);
+    run(k<3, 16, 2>, "V3 + global->LDS staging (early)", 2, 16);
+    run(k<4, 16, 2>, "V4 glds ring, 2 stages in flight", 2, 16);
+    run(k<3, 32, 2>, "V3 + global->LDS staging (early)", 2, 32);
+    run(k<4, 16, 3>, "V4 glds ring, 2 stages in flight", 3, 16);
+  }
   (void)hipFree(src);
   (void)hipFree(out);
   return 0;
