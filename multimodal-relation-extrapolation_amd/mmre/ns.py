@@ -40,7 +40,7 @@ class _FusedNS(torch.autograd.Function):
     mmre_ns_forward, with mmre_ns_backward as the backward."""
 
     @staticmethod
-    def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate):
+    def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate, events):
         dev = ent.device
         N = batch * (1 + neg)
         score = torch.empty(N, dtype=torch.float32, device=dev)
@@ -53,11 +53,15 @@ class _FusedNS(torch.autograd.Function):
             ge, gr = torch.zeros_like(ent), torch.zeros_like(rel)
             gei = torch.zeros_like(ent_im) if ent_im is not None else None
             gri = torch.zeros_like(rel_im) if rel_im is not None else None
+            if events is not None:
+                events[0].record()
             call("mmre_ns_forward_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
                  int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), E, R, spec.dim,
                  spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg, float(loss_margin), float(adv_t),
                  float(regul_rate), ptr(score), ptr(loss), ptr(ge), ptr(gei), ptr(gr), ptr(gri), ptr(work),
                  stream_ptr(dev))
+            if events is not None:
+                events[1].record()
             ctx.unit = (ge, gr, gei, gri)
             return loss[0], score
         work = torch.empty(int(lib().mmre_ns_workspace(batch, neg)), dtype=torch.float32, device=dev)
@@ -78,7 +82,7 @@ class _FusedNS(torch.autograd.Function):
             gl = g_loss.reshape(()).to(torch.float32)
             out = [None if x is None else x.mul_(gl) for x in ctx.unit]
             ctx.unit = None
-            return (*out, None, None, None, None, None, None, None, None, None)
+            return (*out, None, None, None, None, None, None, None, None, None, None)
         ent, rel, ent_im, rel_im, h, t, r, score = ctx.saved_tensors
         spec, batch, neg, loss_margin, adv_t, regul_rate = ctx.cfg
         if not ctx.has_im:
@@ -93,19 +97,22 @@ class _FusedNS(torch.autograd.Function):
              ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
              batch, neg, float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei),
              ptr(gr), ptr(gri), None, stream_ptr(dev))
-        return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None
+        return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None
 
 
 def fused_ns_loss(spec: NSSpec, ent, rel, h, t, r, batch: int, neg: int, loss_margin: float,
-                  adv_temperature: float | None = None, regul_rate: float = 0.0, ent_im=None, rel_im=None):
-    """Returns (loss scalar tensor, scores (B*(1+k),)). Differentiable w.r.t. the tables."""
+                  adv_temperature: float | None = None, regul_rate: float = 0.0, ent_im=None, rel_im=None,
+                  events=None):
+    """Returns (loss scalar tensor, scores (B*(1+k),)). Differentiable w.r.t. the tables.
+    events: optional (start, end) torch.cuda.Event pair recorded around the fused
+    forward + gradient call alone (training mode), for kernel timing."""
     require_cuda(ent, rel, h, t, r, ent_im, rel_im)
     h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
     if ent.dtype != torch.float32 or rel.dtype != torch.float32:
         raise TypeError("fused_ns_loss: float32 tables")
     return _FusedNS.apply(ent.contiguous(), rel.contiguous(), None if ent_im is None else ent_im.contiguous(),
                           None if rel_im is None else rel_im.contiguous(), h, t, r, spec, int(batch), int(neg),
-                          float(loss_margin), float(adv_temperature or 0.0), float(regul_rate))
+                          float(loss_margin), float(adv_temperature or 0.0), float(regul_rate), events)
 
 
 class _ScoreRows(torch.autograd.Function):
