@@ -837,7 +837,7 @@ def main():
     if args.config == "m3ae":
         return bench_m3ae(args, world, rank, dev, dist)
     if cfg["dataset"] == "synthetic-1M":
-        w = synthetic_large()
+        w = synthetic_large(generator_device=dev)
     else:
         w = zs_workload(cfg["dataset"], cfg["model"], cfg["dim"], n_test=cfg.get("n_test"))
     w["norm_flag"] = cfg["norm"]
@@ -923,8 +923,9 @@ def main():
                     "the measured HBM traffic is in traffic / hbm_measured_GBs"})
         data = {"c1": "synthetic TransE tables trained on the FB15K-237-ZS test triples",
                 "c2": "synthetic TransE tables trained on the FB15K-237-ZS test triples",
-                "c5": "synthetic 1M-entity DistMult tables (OpenKE xavier init, seed 0) and 4,096 random test "
-                      "triples (= the filter set)"}.get(args.config, f"synthetic {model} tables (OpenKE init, seed 0)")
+                "c5": "synthetic 1M-entity DistMult entity table (OpenKE xavier init, seed 0); relation table = the "
+                      "zsl_module generator (random-init UnifiedModel SN layers + LayerNormalization, HIP) over "
+                      "synthetic 384-d text CLS rows + noise; 4,096 random test triples (= the filter set)"}.get(args.config, f"synthetic {model} tables (OpenKE init, seed 0)")
         if args.config != "c5":
             data += (f" ({args.train_steps} steps of this build's HIP trainer: bit-exact OpenKE sampler + fused margin"
                      f" loss, SGD 1.0, margin 5, neg 25)" if "trained" in w else "") + \

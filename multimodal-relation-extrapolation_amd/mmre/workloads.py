@@ -57,12 +57,29 @@ def zs_workload(dataset: str = "FB15K-237-ZS", model: str = "transe", dim: int =
     return w
 
 
-def synthetic_large(n_ent=1_000_000, n_rel=235, dim=256, n_query=8192, seed=0):
-    """C5: synthetic |E| = 1M DistMult d=256 with 8,192 random queries."""
+def synthetic_large(n_ent=1_000_000, n_rel=235, dim=256, n_query=8192, seed=0, generator_device=None):
+    """C5: synthetic |E| = 1M DistMult d=256 with 8,192 random queries.
+
+    generator_device (a GPU): the relation table is instead the zsl_module generator's output,
+    as BASELINE configs[4] describes ("text features through zsl_module generator"): one
+    synthetic 384-d text CLS row per relation + a noise row (15-d, N(0,1)) through
+    UnifiedModel's generate_fc_layer / des_rel_map_layer1 / des_rel_map_layer2 / layer_norm
+    (mmre.generator.RelationGenerator, random init, eval mode: model.py:679-686) on the HIP
+    generator kernels. w["rel_source"] records which."""
     gen = torch.Generator().manual_seed(seed)
     rng = np.random.default_rng(seed + 1)
     w = dict(dataset="synthetic-1M", model="distmult", dim=dim, n_ent=n_ent, n_rel=n_rel,
-             ent=xavier(n_ent, dim, gen), rel=xavier(n_rel, dim, gen))
+             ent=xavier(n_ent, dim, gen), rel=xavier(n_rel, dim, gen), rel_source="xavier")
+    if generator_device is not None:
+        from .generator import RelationGenerator
+        dev = torch.device(generator_device)
+        torch.manual_seed(seed + 2)
+        g = RelationGenerator(reduced_dim=384, noise_dim=15, emb_dim=dim).to(dev).eval()
+        cls = torch.randn((n_rel, 384), generator=gen).to(dev)
+        noise = torch.randn((n_rel, 15), generator=gen).to(dev)
+        with torch.no_grad():
+            w["rel"] = g.generate(cls, noise).float().cpu()
+        w["rel_source"] = "generator"
     h = rng.integers(0, n_ent, n_query // 2)
     r = rng.integers(0, n_rel, n_query // 2)
     t = rng.integers(0, n_ent, n_query // 2)

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="time one rank's share of a W-way relation-sharded step (no collective)")
+    ap.add_argument("--graph", action="store_true", help="--emulate-world: replay each rank's local evaluation "
+                    "from a hipGraph")
     a = ap.parse_args()
     if a.emulate_world:
         return emulate(a)
@@ -102,10 +104,22 @@ def emulate(a):
             torch.cuda.current_stream().synchronize()
         for _ in range(3):
             step()
+        if a.graph:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                gc = sw.run(*q, filt=filt, buffers=bufs)["counts"]
+
+            def step():
+                g.replay()
+                host.copy_(gc, non_blocking=True)
+                torch.cuda.current_stream().synchronize()
+            for _ in range(3):
+                step()
         ms = timeit(step, a.reps)
         worst = max(worst, ms)
         print(f"rank {k}: {int(m.sum())} sweeps, step {ms:.3f} ms, sweep kernel {ev[0].elapsed_time(ev[1]):.3f} ms")
-    print(f"world {a.emulate_world}: slowest rank {worst:.3f} ms (+ all-gather + metric reduction)")
+    print(f"world {a.emulate_world}{' (graph)' if a.graph else ''}: slowest rank {worst:.3f} ms "
+          f"(+ all-gather + metric reduction)")
 
 
 if __name__ == "__main__":

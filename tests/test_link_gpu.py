@@ -305,7 +305,7 @@ def test_full_size_configs(oracle_mod, config):
     from mmre.link import FilterIndex
     from mmre.workloads import synthetic_large, zs_workload
     if config == "c5":
-        w = synthetic_large()
+        w = synthetic_large(generator_device="cuda:0")  # relation rows from the HIP generator
     else:
         w = zs_workload(*{"c3": ("DB15K-ZS", "complex", 200), "c4": ("FB15K-237-ZS", "rotate", 512)}[config])
     model, E, R = w["model"], int(w["n_ent"]), int(w["n_rel"])
