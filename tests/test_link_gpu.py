@@ -336,3 +336,38 @@ def test_full_size_configs(oracle_mod, config):
         assert np.array_equal(c[:, s].T[:, :2], o_c[:, :2])
         truth_ids = qh[s] if mode_id == 0 else qt[s]
         assert np.array_equal(out["truth"][s], o_pred[np.arange(len(s)), truth_ids])
+
+
+def test_c1_config_full_oracle(oracle_mod):
+    """BASELINE configs[0] (C1): FB15K-237-ZS TransE d=100 on the first 1,000 test triples in
+    Test.h order (the reference's OpenKE Tester path, Tester.py:70-91), tables trained by this
+    build's trainer so ranks are not degenerate, evaluated as bench.py --config c1 does
+    (ShardedLinkEvaluation: filter groups, pipelined launch/finish): every one of the 2,000
+    sweeps' raw / filtered counts equal the oracle's, and so the Test.h metrics."""
+    from mmre.link import FilterIndex, link_metrics
+    from mmre.sharding import ShardedLinkEvaluation
+    from mmre.workloads import train_transe, zs_workload
+    w = zs_workload("FB15K-237-ZS", "transe", 100, n_test=1000)
+    w["norm_flag"] = True
+    train_transe(w, "cuda:0", steps=100)
+    E, R, n = int(w["n_ent"]), int(w["n_rel"]), len(w["test_h"])
+    assert n == 1000
+    ent, rel = w["ent"].numpy(), w["rel"].numpy()
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, R)
+    ev = ShardedLinkEvaluation(_spec_from("transe", ent, rel, norm=True, dim=100), w["test_h"], w["test_r"],
+                               w["test_t"], index=index, device="cuda:0")
+    metrics, counts = ev.finish(ev.launch())
+    h, r, t = (np.asarray(w[k], np.int64) for k in ("test_h", "test_r", "test_t"))
+    hrt = oracle_mod.sorted_hrt(np.asarray(w["filter_h"], np.int64), np.asarray(w["filter_r"], np.int64),
+                                np.asarray(w["filter_t"], np.int64))
+    oc = []
+    for mode in ("head_batch", "tail_batch"):
+        o_pred = oracle_mod.link_predict("transe", mode, ent, rel, h, r, t, norm_flag=True)
+        oc.append(oracle_mod.test_rank(mode, o_pred, h, r, t, hrt)[:, :2].T)
+    o_counts = np.concatenate(oc, 1)
+    assert np.array_equal(counts[:2], o_counts)
+    z = np.zeros((2, n), np.int32)
+    o_metrics = link_metrics(np.concatenate([o_counts[:, :n], z]).astype(np.int32),
+                             np.concatenate([o_counts[:, n:], z]).astype(np.int32))
+    assert metrics["filter"] == o_metrics["filter"] and metrics["raw"] == o_metrics["raw"]
+    assert metrics["filter"]["hit10"] > 0.5      # trained tables: truths rank near the top
