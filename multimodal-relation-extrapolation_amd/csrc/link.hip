@@ -34,9 +34,12 @@ constexpr int NT = 256;   // threads per workgroup
 // add exact zeros to the fma chain; a 32-row stage measured slower: C3 1.27 vs 1.18 ms, C5
 // 37.9 vs 36.6 ms at 248 VGPRs); TransE/RotatE to the VALU sweep's 8.
 constexpr int KS_MFMA = 16;
-__host__ __device__ inline bool mfma_model(int model) { return model == MMRE_DISTMULT || model == MMRE_COMPLEX; }
-inline int plane_rows(int model, int dim) { return (int)round_up(dim, mfma_model(model) ? KS_MFMA : KC); }
 __host__ __device__ inline int n_planes(int model) { return (model == MMRE_COMPLEX || model == MMRE_ROTATE) ? 2 : 1; }
+__host__ __device__ inline bool mfma_model(int model) { return model == MMRE_DISTMULT || model == MMRE_COMPLEX; }
+// MFMA planes: K = n_planes x plane_rows a multiple of 16 (ComplEx d = 200: 2 x 200, no padding)
+inline int plane_rows(int model, int dim) {
+  return (int)round_up(dim, !mfma_model(model) ? KC : KS_MFMA / n_planes(model));
+}
 
 // ------------------------------------------------------------------ prep ----
 // Both prep kernels stage a block of rows through LDS (row stride kt+1: odd, so the
@@ -915,7 +918,10 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
   const int u0 = (int)((int64_t)gmem * um.count / per_grp);
   const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
   if (u0 >= u1) return;  // uniform over the workgroup
-  const int nkc = ktot / KS;  // planes are padded to whole stages (plane_rows)
+  // stages of KS rows; with KS = 32 and K = 32 n + 16 (plane_rows: K is a multiple of 16) the
+  // unit's last stage holds 16 rows (a uniform branch skips its upper half)
+  const int nkc = (ktot + KS - 1) / KS;
+  const bool half_tail = KS == 32 && (ktot % 32) != 0;
 
   // rows of this lane: ql(bi, r) = wq*64 + bi*32 + (r&3) + 8*(r>>2) + 4*lrow
   int tpar = 0;  // s_th slot of the current query tile
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     rq1 = *reinterpret_cast<const float4*>(qp + 8 * q_pad);
     re0 = *reinterpret_cast<const float4*>(ep);
     re1 = *reinterpret_cast<const float4*>(ep + 8 * e_pad);
-    if constexpr (KS == 32) {
+    if (KS == 32 && !(half_tail && ld_kc == nkc - 1)) {  // rows past K are never read
       rq2 = *reinterpret_cast<const float4*>(qp + 16 * q_pad);
       rq3 = *reinterpret_cast<const float4*>(qp + 24 * q_pad);
       re2 = *reinterpret_cast<const float4*>(ep + 16 * e_pad);
@@ -1030,17 +1036,21 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
       // the next stage's loads stay at the top of this one: hipcc otherwise sinks them to
       // their use at the stage's end and every stage waits a full L2 / MALL latency
       __builtin_amdgcn_sched_barrier(0);
+      auto mfma_rows = [&](int k0) {  // 16 K rows = 8 k pairs from stage row k0
 #pragma unroll
-      for (int kp2 = 0; kp2 < KS; kp2 += 2) {
-        const float a0 = sq[buf][kp2 + lrow][wq * 64 + lcol];
-        const float a1 = sq[buf][kp2 + lrow][wq * 64 + 32 + lcol];
-        const float b0 = se[buf][kp2 + lrow][we * 64 + lcol];
-        const float b1 = se[buf][kp2 + lrow][we * 64 + 32 + lcol];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-      }
+        for (int kp2 = 0; kp2 < 16; kp2 += 2) {
+          const float a0 = sq[buf][k0 + kp2 + lrow][wq * 64 + lcol];
+          const float a1 = sq[buf][k0 + kp2 + lrow][wq * 64 + 32 + lcol];
+          const float b0 = se[buf][k0 + kp2 + lrow][we * 64 + lcol];
+          const float b1 = se[buf][k0 + kp2 + lrow][we * 64 + 32 + lcol];
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+      };
+      mfma_rows(0);
+      if (KS == 32 && !(half_tail && kc == nkc - 1)) mfma_rows(16);
       if (kc == nkc - 1) {  // unit finished: rank epilogue
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE + we * 64;
@@ -1350,11 +1360,11 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
   const int n_et = (int)(e_pad / TE);
   // persistent XCD-grouped grid as for the VALU sweep, 2 workgroups per resident slot (MI355X,
   // KCM = 16: C3 1.20 / 1.24 / 1.22 / 1.24 ms and C5 36.5 / 36.5 / 36.5 / 36.6 ms at 1/2/3/4x)
-  // K stages of 32 rows when the planes hold a whole number of them (C3 ComplEx 2 x 208, C5
-  // DistMult 256), else 16: half the per-stage staging and barriers per MFMA
-  // (scripts/probes/mfma_stage.hip: 0.79 -> 0.86 of the f32 MFMA peak with L2-resident data)
+  // K stages of 32 rows (a unit's last one 16 when K = 32 n + 16: C3 ComplEx 2 x 200): half the
+  // per-stage staging and barriers per MFMA of 16-row stages (scripts/probes/mfma_stage.hip:
+  // 0.79 -> 0.86 of the f32 MFMA peak, L2-resident or HBM-streamed alike)
   static const char* ks_env = getenv("MMRE_MFMA_STAGE"); /* experiments: 16 forces 16-row stages */
-  const bool ks32 = ktot % 32 == 0 && !(ks_env && atoi(ks_env) == 16);
+  const bool ks32 = !(ks_env && atoi(ks_env) == 16);
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
 #define MMRE_MFMA_K(KERNEL)                                                                                       \
   do {                                                                                                            \
