@@ -809,10 +809,13 @@ def main():
                     help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
     ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", default="relation", choices=["relation", "entity"],
+                    help="N > 1 link configs: split the queries (relation-sharded, one all-gather; default) or "
+                         "the entity table (every query against 1/N of the entities, one all-reduce)")
     args = ap.parse_args()
 
     from mmre.link import FilterIndex, ScoreSpec, rotate_phase_denom
-    from mmre.sharding import ShardedLinkEvaluation
+    from mmre.sharding import EntityShardedLinkEvaluation, ShardedLinkEvaluation
     from mmre.workloads import synthetic_large, train_transe, zs_workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -858,8 +861,14 @@ def main():
                      rel_im=w.get("rel_im").to(dev) if "rel_im" in w else None, norm_flag=cfg["norm"],
                      pred_kind=pk, margin=float(w.get("margin", 0.0)),
                      phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
-    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
-    n_local = int(ev.masks[rank].sum())
+    if args.shard == "entity":
+        ev = EntityShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+        n_local = 2 * n if ev.entity_range[1] > ev.entity_range[0] else 0
+        e_local = ev.entity_range[1] - ev.entity_range[0]
+    else:
+        ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+        n_local = int(ev.masks[rank].sum())
+        e_local = E
 
     def steps(k, evs=None):
         # evaluation i + 1 is enqueued before the host reduces evaluation i's metrics, so that
@@ -897,7 +906,7 @@ def main():
     value = total_triples * args.steps / elapsed
     if rank == 0:
         bpt = bytes_per_triple(model, dim)
-        triples_launch = n_local * E
+        triples_launch = n_local * e_local
         tps = triples_launch / (sweep_ms * 1e-3) if sweep_ms > 0 else 0.0
         traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
         if model in ("distmult", "complex"):
@@ -935,7 +944,10 @@ def main():
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
                "config": {"workload": cfg["workload"], "n_entities": E, "dim": dim, "n_sweeps": 2 * n,
-                          "parallelism": f"relation-sharded x{world} (LPT), RCCL all-gather of rank counts"},
+                          "parallelism": (f"entity-sharded x{world} (1/N of the entity tiles per rank), RCCL all-reduce "
+                                          f"of the count table" if args.shard == "entity" else
+                                          f"query-sharded x{world} (relation-major LPT with relation splits), RCCL "
+                                          f"all-gather of rank counts")},
                "roofline": roof,
                "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
                            "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],

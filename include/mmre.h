@@ -131,6 +131,18 @@ int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_k
                     const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
                     const float* d_truth, float* d_scores, void* stream);
 
+/* The same sweep over the entity slice [e_begin, e_end) only (e_begin a multiple of 128), for
+ * entity-sharded evaluation (the alternative for huge E): each rank sweeps every
+ * query against its slice after a truth pass whose filter lists hold only the slice's entities
+ * (mmre_link_truth[_grouped] with restricted lists), so summing d_counts over the ranks
+ * (one all-reduce of int32) gives exactly the whole-table counts. Replaces the per-query
+ * testHead/testTail scan of Test.h:65-192 for the slice. No score rows. */
+int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
+                          int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km,
+                          const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query,
+                          int64_t q_pad, int dim, const uint32_t* d_type_head, const uint32_t* d_type_tail,
+                          int32_t* d_counts, const float* d_truth, void* stream);
+
 /* Test.h:232-327 test_link_prediction + getTestLink* (Test.h:356-390), host side,
  * with the reference's float accumulation order (P14). Counts: int32, column c of
  * query i at counts[c*stride + i] (c = raw, filt, raw_tc, filt_tc).

@@ -653,7 +653,7 @@ struct UnitMap {
 template <int OP, bool TC, bool STORE, int PK>
 __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
-    int64_t q_pad, int64_t n_query, int kp, int n_et, int n_groups, int pred_kind, float margin,
+    int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,
     const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
     const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
@@ -828,11 +828,11 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
             // 32-bit ids (int32 by check_link_args); bitwise &: no per-pair branch
             const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
             const float v = pred(op_final<OP>(acc[i][j]));
-            const bool better = (v < th) & (e != tr) & (e < n_ent);
+            const bool better = (v < th) & (e + e_base != tr) & (e < n_ent);
             c += better;
             if constexpr (TC) {
               const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-              cc += better && type_bit(m, type_words, s_rel[slot][ql], e);
+              cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
             }
             if constexpr (STORE) {
               if (q0 + ql < n_query && e < n_ent) scores[(q0 + ql) * n_ent + e] = v;
@@ -896,7 +896,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 template <bool TC, bool STORE, int PK, int KS>
 __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
-    int64_t q_pad, int64_t n_query, int ktot, int n_et, int n_groups, int pred_kind, float margin,
+    int64_t q_pad, int64_t n_query, int ktot, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
     const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
     int32_t* __restrict__ counts, float* __restrict__ scores) {
@@ -1081,7 +1081,7 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
                 if constexpr (TC) {
                   const int ql = row_of(bi, r);
                   const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                  cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e);
+                  cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e + e_base);
                 }
                 if constexpr (STORE) {
                   const int64_t q = q0 + row_of(bi, r);
@@ -1128,11 +1128,10 @@ static int resident_groups(const void* kernel, int threads) {
 }
 
 template <int OP, bool TCV, bool STV, int PK>
-static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, int64_t n_ent, const float* q_km,
-                            int64_t q_pad, int64_t n_query, int kp, int pk, float m, const float* thr,
-                            const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, const uint32_t* th,
-                            const uint32_t* tt, int64_t tw, int32_t* counts, float* scores) {
-  const int n_et = (int)(e_pad / TE);
+static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, int64_t n_ent, int n_et, int e_base,
+                            const float* q_km, int64_t q_pad, int64_t n_query, int kp, int pk, float m,
+                            const float* thr, const int32_t* qtrue, const int64_t* qr, const int8_t* qmode,
+                            const uint32_t* th, const uint32_t* tt, int64_t tw, int32_t* counts, float* scores) {
   // 16 workgroups per resident slot: short per-workgroup ranges let the dispatcher balance
   // CUs that run at different speeds (C2 on MI355X: 1,024 groups 4.0 ms, 8,192 3.43 ms,
   // 16,384 3.30 ms, 30,528 (one unit each) 3.36 ms).
@@ -1152,16 +1151,16 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   else if (gmode && gmode[0] >= '1' && gmode[0] <= '9') g = atoi(gmode);
   const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;
   hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad, n_ent, q_km,
-                     q_pad, n_query, kp, n_et, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores);
+                     q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores);
 }
 
 template <int OP>
 static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km, int64_t e_pad, int64_t n_ent,
-                       const float* q_km, int64_t q_pad, int64_t n_query, int kp, int pk, float m, const float* thr,
+                       int n_et, int e_base, const float* q_km, int64_t q_pad, int64_t n_query, int kp, int pk, float m, const float* thr,
                        const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, const uint32_t* th,
                        const uint32_t* tt, int64_t tw, int32_t* counts, float* scores) {
 #define MMRE_LV1(TCV, STV, PKV) \
-  launch_valu_one<OP, TCV, STV, PKV>(st, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores)
+  launch_valu_one<OP, TCV, STV, PKV>(st, ent_km, e_pad, n_ent, n_et, e_base, q_km, q_pad, n_query, kp, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores)
   // the model's usual prediction kind is compiled into the epilogue of the plain sweep
   constexpr int fast = (OP == 2) ? 3 : 0;  // RotatE -(m - s), TransE s
   if (tc && store) MMRE_LV1(true, true, -1);
@@ -1334,22 +1333,30 @@ extern "C" int mmre_link_truth(int model, int pred_kind, float margin, const flo
 #undef MMRE_TF
 }
 
-extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
-                               int64_t e_pad, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
-                               const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
-                               const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
-                               const float* d_truth, float* d_scores, void* stream) {
+// The sweep over entities [e_begin, e_end) of the table (e_begin a multiple of TE): the kernels
+// see the slice (pointer offset by e_begin columns, row stride e_pad, n_ent_local ids) and add
+// e_begin back wherever an absolute id matters (truth exclusion, type-constraint bits).
+static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent, int64_t e_pad,
+                      int64_t e_begin, int64_t e_end, const float* d_q_km, const int32_t* d_q_true,
+                      const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
+                      const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
+                      const float* d_truth, float* d_scores, hipStream_t st) {
   int rc = check_link_args(model, pred_kind, d_ent_km, n_ent, e_pad, d_q_km, d_q_true, d_qr, d_qmode, n_query, q_pad,
                            d_type_head, d_type_tail, d_counts, d_truth);
   if (rc) return rc;
-  hipStream_t st = (hipStream_t)stream;
+  if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
+  if (d_scores && (e_begin != 0 || e_end != n_ent)) return MMRE_ERR_ARG;  // score rows are whole-table
+  const int64_t tw = (n_ent + 31) / 32;  // type bitsets span the whole table
+  const int e_base = (int)e_begin;
+  d_ent_km += e_begin;
+  n_ent = e_end - e_begin;
+  const int n_et = (int)((n_ent + TE - 1) / TE);
   const int kp = plane_rows(model, dim);
-  const int64_t tw = (n_ent + 31) / 32;
   const bool tc = d_type_head != nullptr;
   const bool store = d_scores != nullptr;
   const int op = op_of_model(model);
   if (op <= 2) {
-#define MMRE_LV(OPV) launch_valu<OPV>(tc, store, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad, n_query, kp, pred_kind, \
+#define MMRE_LV(OPV) launch_valu<OPV>(tc, store, st, d_ent_km, e_pad, n_ent, n_et, e_base, d_q_km, q_pad, n_query, kp, pred_kind, \
                                       margin, d_truth, d_q_true, d_qr, d_qmode, d_type_head, d_type_tail, tw, d_counts, d_scores)
     if (op == 0) return MMRE_LV(0);
     if (op == 1) return MMRE_LV(1);
@@ -1357,7 +1364,6 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
 #undef MMRE_LV
   }
   const int ktot = n_planes(model) * kp;
-  const int n_et = (int)(e_pad / TE);
   // persistent XCD-grouped grid as for the VALU sweep, 2 workgroups per resident slot (MI355X,
   // KCM = 16: C3 1.20 / 1.24 / 1.22 / 1.24 ms and C5 36.5 / 36.5 / 36.5 / 36.6 ms at 1/2/3/4x)
   // K stages of 32 rows (a unit's last one 16 when K = 32 n + 16: C3 ComplEx 2 x 200): half the
@@ -1378,7 +1384,7 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                              \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL(KERNEL, dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,       \
-                       n_query, ktot, n_et, ng, pred_kind, margin, d_truth, d_qr, d_qmode, d_type_head,          \
+                       n_query, ktot, n_et, e_base, ng, pred_kind, margin, d_truth, d_qr, d_qmode, d_type_head,  \
                        d_type_tail, tw, d_counts, d_scores);                                                      \
   } while (0)
 #define MMRE_MFMA(TCV, STV, PKV)                                                                           \
@@ -1396,4 +1402,24 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
 #undef MMRE_MFMA_K
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
+}
+
+extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
+                               int64_t e_pad, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
+                               const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
+                               const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
+                               const float* d_truth, float* d_scores, void* stream) {
+  if (n_ent <= 0) return MMRE_ERR_ARG;
+  return sweep_impl(model, pred_kind, margin, d_ent_km, n_ent, e_pad, 0, n_ent, d_q_km, d_q_true, d_qr, d_qmode,
+                    n_query, q_pad, dim, d_type_head, d_type_tail, d_counts, d_truth, d_scores, (hipStream_t)stream);
+}
+
+extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
+                                     int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km,
+                                     const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
+                                     int64_t n_query, int64_t q_pad, int dim, const uint32_t* d_type_head,
+                                     const uint32_t* d_type_tail, int32_t* d_counts, const float* d_truth,
+                                     void* stream) {
+  return sweep_impl(model, pred_kind, margin, d_ent_km, n_ent, e_pad, e_begin, e_end, d_q_km, d_q_true, d_qr, d_qmode,
+                    n_query, q_pad, dim, d_type_head, d_type_tail, d_counts, d_truth, nullptr, (hipStream_t)stream);
 }

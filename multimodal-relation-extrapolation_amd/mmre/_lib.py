@@ -29,6 +29,7 @@ SIGNATURES = {
     "mmre_link_truth_grouped": (I32, [I32, I32, F32, P, I64, P, P, P, P, I64, I32, P, P, I64, P, P, P, I64, P, P, P,
                                       P, P, P]),
     "mmre_link_sweep": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P]),
+    "mmre_link_sweep_range": (I32, [I32, I32, F32, P, I64, I64, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P]),
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
     "mmre_glibc_rand": (I32, [I64, I64, P]),
     "mmre_sampler_advance": (I32, [P, I64, I64, I64, I64, I64]),

@@ -99,13 +99,15 @@ class FilterIndex:
             ids[dst] = gids
         return off, ids
 
-    def groups(self, qh, qr, qt, qmode, max_group: int = 64):
+    def groups(self, qh, qr, qt, qmode, max_group: int = 64, entity_range=None):
         """Filter groups: queries with the same (mode, r, anchor) share their known-entity
         list (Test.h:85 `_find` looks up (r, t) for head_batch, (h, r) for tail_batch).
         Groups larger than `max_group` queries are split (one wave of the count kernel per
         group). Returns (grp_qoff int64 [G+1], grp_q int32 [Q], off int64 [G+1], ids int32,
         entry_q int32): the query partition, one CSR list per group and, per listed entity,
-        the group member whose query vector scores it -- for mmre_link_truth_grouped."""
+        the group member whose query vector scores it -- for mmre_link_truth_grouped.
+        entity_range (e0, e1): keep only listed entities in [e0, e1) -- the filter correction of
+        a rank that sweeps that slice of the table (entity-sharded evaluation)."""
         qh, qr, qt, qmode = (np.asarray(x, np.int64) for x in (qh, qr, qt, qmode))
         anchor = np.where(qmode == HEAD, qt, qh)
         key = (qmode * self.n_rel + qr) * self.n_ent + anchor
@@ -123,6 +125,11 @@ class FilterIndex:
         first = grp_q[grp_qoff[:-1]]
         off, ids = self.filters(qh[first], qr[first], qt[first], qmode[first])
         entry_q = np.repeat(first, np.diff(off)).astype(np.int32)
+        if entity_range is not None:
+            e0, e1 = entity_range
+            keep = (ids >= e0) & (ids < e1)
+            kept = np.concatenate([[0], np.cumsum(keep, dtype=np.int64)])[off]  # new CSR offsets
+            off, ids, entry_q = kept, ids[keep], entry_q[keep]
         return grp_qoff, grp_q, off, ids, entry_q
 
     def type_masks(self):
@@ -180,12 +187,15 @@ class LinkSweep:
                     truth=torch.empty(n_query, dtype=torch.float32, device=dev), q_pad=q_pad)
 
     def run(self, qh, qr, qt, qmode, filt=None, type_masks=None, return_scores=False, buffers=None,
-            prepare=True, sweep_events=None, q_rows=True):
+            prepare=True, sweep_events=None, q_rows=True, entity_range=None):
         """qh/qr/qt int64 and qmode int8 device tensors. filt: per-query CSR (off int64, ids int32)
         or filter groups (grp_qoff, grp_q, off, ids, entry_q), see FilterIndex.groups.
         sweep_events: optional (start, end) torch.cuda.Event pair recorded around the sweep kernel alone
         (on the stream the kernels are launched on). q_rows=False: no row-major query copy (the
         per-query truth/filter kernel then gathers the query vectors from the k-major plane).
+        entity_range (e0, e1), e0 a multiple of 128: sweep only those entities (filt restricted
+        to them: FilterIndex.groups(..., entity_range)); summing counts over a partition of the
+        table gives the whole-table counts (mmre_link_sweep_range).
         Returns dict(counts=(4, Q) int32 [raw, filt, raw_tc, filt_tc], truth=(Q,), scores=(Q, E)|None)."""
         s = self.spec
         n = int(qh.shape[0])
@@ -228,9 +238,16 @@ class LinkSweep:
                  b["q_pad"], s.dim, ptr(off), ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
         if sweep_events is not None:
             sweep_events[0].record()
-        call("mmre_link_sweep", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
-             self.e_pad, ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(th),
-             ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(scores), st)
+        if entity_range is not None:
+            if return_scores:
+                raise ValueError("entity_range sweeps keep no score rows")
+            call("mmre_link_sweep_range", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km),
+                 self.n_ent, self.e_pad, int(entity_range[0]), int(entity_range[1]), ptr(b["q_km"]), ptr(b["q_true"]),
+                 ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
+        else:
+            call("mmre_link_sweep", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
+                 self.e_pad, ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(th),
+                 ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(scores), st)
         if sweep_events is not None:
             sweep_events[1].record()
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)

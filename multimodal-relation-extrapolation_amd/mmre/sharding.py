@@ -213,3 +213,89 @@ class ShardedLinkEvaluation:
     def run(self, events=None, copy_counts=True):
         """(metrics, counts (4, 2n) int32) of one evaluation, synchronously."""
         return self.finish(self.launch(events), copy_counts)
+
+
+def entity_slices(n_ent: int, world: int, tile: int = 128):
+    """Contiguous entity slices [e0, e1) per rank, cut at multiples of the sweep's entity tile:
+    rank k owns tiles [k T / W, (k + 1) T / W) of the T = ceil(E / tile) tiles."""
+    n_t = -(-int(n_ent) // tile)
+    out = []
+    for k in range(world):
+        t0, t1 = k * n_t // world, (k + 1) * n_t // world
+        out.append((t0 * tile, min(t1 * tile, int(n_ent))))
+    return out
+
+
+def reduce_counts(counts: torch.Tensor, group=None):
+    """Sum each rank's (4, Q) int32 counts over the group in place: ONE all-reduce (RCCL under
+    'nccl'; through host memory under 'gloo'). Integer sums are exact, so the result is the
+    whole-table count table bit for bit."""
+    import torch.distributed as dist
+    if counts.is_cuda and dist.get_backend(group) == "gloo":
+        host = counts.cpu()
+        dist.all_reduce(host, group=group)
+        counts.copy_(host)
+    else:
+        dist.all_reduce(counts, group=group)
+    return counts
+
+
+class EntityShardedLinkEvaluation(ShardedLinkEvaluation):
+    """Entity-sharded filtered link prediction (the alternative for huge E): every
+    rank sweeps ALL queries against its contiguous 1/world of the entity tiles (the table itself
+    stays replicated for the truth scores), with filter lists restricted to its slice, and one
+    all-reduce (sum) of the int32 count table gives every rank the whole-table counts; the
+    Test.h reduction then runs in the reference's order, bit-identical to one GPU. Same
+    launch / finish / run API as ShardedLinkEvaluation. Per-rank work is E / world per query
+    whatever the relation mix; the price is the truth pass and query prep of every query on
+    every rank, and an all-reduce of 4 x Q int32 instead of an all-gather of each rank's share."""
+
+    def __init__(self, spec, test_h, test_r, test_t, index=None, type_constrain=False, group=None, device=None):
+        import torch.distributed as dist
+        from .link import HEAD, TAIL, LinkSweep
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        th, tr, tt = (np.asarray(x, np.int64) for x in (test_h, test_r, test_t))
+        self.n = len(th)
+        qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
+        qm = np.concatenate([np.full(self.n, HEAD, np.int8), np.full(self.n, TAIL, np.int8)])
+        dev = torch.device(device) if device is not None else spec.ent.device
+        self.device = dev
+        n_ent = int(spec.ent.shape[0])
+        self.slices = entity_slices(n_ent, self.world)
+        self.entity_range = self.slices[self.rank]
+        self.masks = [np.ones(2 * self.n, bool) for _ in range(self.world)]  # every rank: every query
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        self.q = [to(qh), to(qr), to(qt), to(qm)]
+        self.filt = None
+        self.masks_tc = None
+        if index is not None:
+            self.filt = tuple(to(a) for a in index.groups(qh, qr, qt, qm, entity_range=self.entity_range))
+            if type_constrain:
+                tm = index.type_masks()
+                if tm is None:
+                    raise ValueError("type_constrain=True needs the FilterIndex's type constraints "
+                                     "(type_constrain.txt, Reader.h:266-317)")
+                self.masks_tc = tuple(to(m) for m in tm)
+        self.plan = None
+        self._default_runner = False
+        self._graph_wanted = False
+        self._graph = None
+        sw = LinkSweep(spec)
+        bufs = sw.alloc_queries(2 * self.n)
+        e0, e1 = self.entity_range
+
+        def local_runner(qh_, qr_, qt_, qm_, filt, masks_tc, events=None):
+            if e1 <= e0:  # more ranks than entity tiles: this rank's slice is empty
+                if events is not None:
+                    events[0].record()
+                    events[1].record()
+                return torch.zeros((4, 2 * self.n), dtype=torch.int32, device=dev)
+            return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs, sweep_events=events,
+                          entity_range=(e0, e1))["counts"]
+        self.local_runner = local_runner
+
+    def counts(self, events=None):
+        local = self.local_runner(*self.q, self.filt, self.masks_tc, events)
+        return reduce_counts(local, self.group) if self.world > 1 else local

@@ -214,3 +214,31 @@ def test_zs_datasets_shipped():
     assert len(np.unique(z["r"])) == 29
     z = load_zs_test("DB15K-ZS")
     assert len(z["h"]) == 5653 and int(z["n_ent"]) == 12741 and int(z["n_rel"]) == 157
+
+
+def test_entity_slices_and_restricted_filter_lists():
+    """Entity sharding's host side: slices cut at whole 128-entity tiles cover the table once,
+    and filter lists restricted to each slice partition the whole list of every group (same
+    scoring member per entry)."""
+    from mmre.link import FilterIndex
+    from mmre.sharding import entity_slices
+    for E, W in ((14541, 8), (300, 4), (100, 3), (129, 2)):
+        sl = entity_slices(E, W)
+        assert sl[0][0] == 0 and sl[-1][1] == E
+        assert all(a % 128 == 0 and a <= b for a, b in sl)
+        assert all(sl[k][1] == sl[k + 1][0] for k in range(W - 1))
+    rng = np.random.default_rng(0)
+    E, R = 500, 7
+    h, r, t = rng.integers(0, E, 3000), rng.integers(0, R, 3000), rng.integers(0, E, 3000)
+    ix = FilterIndex(h, r, t, E, R)
+    qm = np.r_[np.zeros(100, np.int8), np.ones(100, np.int8)]
+    full = ix.groups(h[:200], r[:200], t[:200], qm)
+    parts = [ix.groups(h[:200], r[:200], t[:200], qm, entity_range=s) for s in entity_slices(E, 3)]
+    for g in range(len(full[0]) - 1):
+        whole = full[3][full[2][g]:full[2][g + 1]]
+        got = np.concatenate([p[3][p[2][g]:p[2][g + 1]] for p in parts])
+        assert sorted(got.tolist()) == sorted(whole.tolist())
+        for p, (e0, e1) in zip(parts, entity_slices(E, 3)):
+            ids = p[3][p[2][g]:p[2][g + 1]]
+            assert np.all((ids >= e0) & (ids < e1))
+            assert np.all(p[4][p[2][g]:p[2][g + 1]] == full[0][g] * 0 + full[1][full[0][g]])

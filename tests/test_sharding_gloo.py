@@ -148,3 +148,53 @@ def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, wor
             assert np.array_equal(o[key], single), key
     assert sum(int(o["n_local"]) for o in outs) == single.shape[1]
     assert max(int(o["n_local"]) for o in outs) <= -(-single.shape[1] // world)
+
+
+def _entity_worker(rank, world, port, res_path, dataset, model, dim):
+    """Each rank: the HIP sweep of ALL queries against its entity slice on cuda:0, counts summed
+    over gloo (host memory); rank 0 also runs the single-process evaluation."""
+    sys.path[:0] = [PKG, os.path.join(REPO, "oracle"), REPO]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mmre.link import FilterIndex, ScoreSpec, evaluate_link_prediction
+    from mmre.sharding import EntityShardedLinkEvaluation
+    from mmre.workloads import zs_workload
+    dev = torch.device("cuda:0")
+    w = zs_workload(dataset, model, dim)
+    E = w["n_ent"]
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
+    pk = {"transe": 0, "distmult": 2, "complex": 2}[model]
+    spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
+                     ent_im=w["ent_im"].to(dev) if "ent_im" in w else None,
+                     rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=model == "transe",
+                     pred_kind=pk, margin=0.0)
+    ev = EntityShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+    a = ev.launch()
+    b = ev.launch()
+    mb, cb = ev.finish(b)
+    ma, ca = ev.finish(a)
+    out = dict(counts_a=ca, counts_b=cb, e0=np.array(ev.entity_range[0]), e1=np.array(ev.entity_range[1]))
+    if rank == 0:
+        m1, (h1, t1) = evaluate_link_prediction(spec, w["test_h"], w["test_r"], w["test_t"], index=index)
+        out["single"] = np.concatenate([h1, t1], 1)
+        out["metrics_equal"] = np.array(all(ma[g][k] == m1[g][k] for g in m1 for k in m1[g]))
+    np.savez(f"{res_path}_{rank}.npz", **out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dataset,model,dim,world", [("FB15K-237-ZS", "transe", 200, 2),
+                                                      ("DB15K-ZS", "complex", 200, 3)])
+def test_entity_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world):
+    """SURVEY 8(e)'s alternative for huge E: each rank sweeps every query against a contiguous
+    slice of the entity tiles (VALU TransE and MFMA ComplEx kernels), counts summed by one
+    all-reduce: every rank's counts and rank 0's metrics are bit-equal to one process."""
+    port = _free_port()
+    res = str(tmp_path / "ent")
+    mp.spawn(_entity_worker, args=(world, port, res, dataset, model, dim), nprocs=world, join=True)
+    outs = [dict(np.load(f"{res}_{k}.npz")) for k in range(world)]
+    single = outs[0]["single"]
+    assert bool(outs[0]["metrics_equal"])
+    for o in outs:
+        assert np.array_equal(o["counts_a"], single) and np.array_equal(o["counts_b"], single)
+    assert outs[0]["e0"] == 0 and all(outs[k]["e1"] == outs[k + 1]["e0"] for k in range(world - 1))
