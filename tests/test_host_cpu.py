@@ -35,7 +35,7 @@ def test_product_binding_loads_without_gpu():
     assert L.mmre_link_pad(1) == 128 and L.mmre_link_pad(129) == 256
     # VALU models pad d to 8 rows per plane, the MFMA models (DistMult/ComplEx) to 16 (one K stage)
     assert L.mmre_link_k(0, 200) == 200 and L.mmre_link_k(4, 13) == 32
-    assert L.mmre_link_k(2, 200) == 208 and L.mmre_link_k(3, 200) == 416
+    assert L.mmre_link_k(2, 200) == 208 and L.mmre_link_k(3, 200) == 400  # MFMA K: a multiple of 16
 
 
 def test_metrics_host_matches_reference(golden):
