@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="time one rank's share of a W-way relation-sharded step (no collective)")
+    ap.add_argument("--entity", action="store_true", help="--emulate-world: entity-sharded ranks (all queries "
+                    "against 1/W of the entity tiles) instead of query-sharded")
     ap.add_argument("--graph", action="store_true", help="--emulate-world: replay each rank's local evaluation "
                     "from a hipGraph")
     a = ap.parse_args()
@@ -87,19 +89,24 @@ def emulate(a):
     n = len(th)
     qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
     qm = np.concatenate([np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)])
+    from mmre.sharding import entity_slices
     masks = lpt_partition(qr, a.emulate_world)
+    slices = entity_slices(w["n_ent"], a.emulate_world)
+    if a.entity:
+        masks = [np.ones(2 * n, bool)] * a.emulate_world
     to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
     worst = 0.0
     for k, m in enumerate(masks):
+        er = slices[k] if a.entity else None
         q = [to(x[m]) for x in (qh, qr, qt, qm)]
-        filt = tuple(to(x) for x in index.groups(qh[m], qr[m], qt[m], qm[m]))
+        filt = tuple(to(x) for x in index.groups(qh[m], qr[m], qt[m], qm[m], entity_range=er))
         sw = LinkSweep(spec)
         bufs = sw.alloc_queries(int(m.sum()))
         host = torch.empty((4, int(m.sum())), dtype=torch.int32, pin_memory=True)
         ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
 
         def step():
-            c = sw.run(*q, filt=filt, buffers=bufs, sweep_events=ev)["counts"]
+            c = sw.run(*q, filt=filt, buffers=bufs, sweep_events=ev, entity_range=er)["counts"]
             host.copy_(c, non_blocking=True)
             torch.cuda.current_stream().synchronize()
         for _ in range(3):
@@ -107,7 +114,7 @@ def emulate(a):
         if a.graph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                gc = sw.run(*q, filt=filt, buffers=bufs)["counts"]
+                gc = sw.run(*q, filt=filt, buffers=bufs, entity_range=er)["counts"]
 
             def step():
                 g.replay()
@@ -118,7 +125,8 @@ def emulate(a):
         ms = timeit(step, a.reps)
         worst = max(worst, ms)
         print(f"rank {k}: {int(m.sum())} sweeps, step {ms:.3f} ms, sweep kernel {ev[0].elapsed_time(ev[1]):.3f} ms")
-    print(f"world {a.emulate_world}{' (graph)' if a.graph else ''}: slowest rank {worst:.3f} ms "
+    print(f"world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "
+          f"slowest rank {worst:.3f} ms "
           f"(+ all-gather + metric reduction)")
 
 
