@@ -759,22 +759,37 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
           float4 y0 = se[buf][NPL - 1][kk][te], y1 = se[buf][NPL - 1][kk][16 + te];
           const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
           const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
-          // two phases per row of 8: independent elements sit between each v_rsq_f32 and its
-          // use (no trans-use hazard padding)
+          // software pipeline across rows: row i + 1's v and v_rsq_f32 are issued before row i's
+          // uses, so every rsq result is consumed a whole row later (C4 83.6 -> 81.2 ms; the 16
+          // extra VGPRs cost a few dwords of scratch at 168)
+          float v[8], y[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float dr = qa[0] - xv[j], di = qb[0] - yv[j];
+            v[j] = dr * dr + di * di;
+            y[j] = __builtin_amdgcn_rsqf(v[j]);
+          }
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            float v[8], y[8];
+            float vn[8], yn[8];
+            if (i + 1 < 8) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float dr = qa[i] - xv[j], di = qb[i] - yv[j];
-              v[j] = dr * dr + di * di;
-              y[j] = __builtin_amdgcn_rsqf(v[j]);
+              for (int j = 0; j < 8; ++j) {
+                const float dr = qa[i + 1] - xv[j], di = qb[i + 1] - yv[j];
+                vn[j] = dr * dr + di * di;
+                yn[j] = __builtin_amdgcn_rsqf(vn[j]);
+              }
             }
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
               lo = min(lo, min(__float_as_uint(v[j]), __float_as_uint(v[j + 1])));  // v >= 0: bit order
               acc[i][j] = acc[i][j] + rot_mag(v[j], y[j]);
               acc[i][j + 1] = acc[i][j + 1] + rot_mag(v[j + 1], y[j + 1]);
+            }
+            if (i + 1 < 8) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) { v[j] = vn[j]; y[j] = yn[j]; }
             }
           }
         } else {
