@@ -429,20 +429,49 @@ def bench_ns(args, world, rank, dev, dist):
         opt.step()
         return loss
 
-    for i in range(args.warmup):
-        step(i)
+    # warmup on a side stream (lazy autograd / optimizer state), then -- unless --ns-eager -- the
+    # whole training step (sampler batch + device seed advance, fused loss and gradients, the
+    # autograd backward, SGD) captured once into a hipGraph and replayed: the step's ~12 launches
+    # cost one, and nothing waits for the host (the sampler keeps its LCG states in HBM)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for i in range(args.warmup):
+            step(i)
+    torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize()
+    graph = None
+    if not args.ns_eager:
+        opt.zero_grad(set_to_none=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_b = smp.sample(B, k, out=bufs[0])
+            g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k, margin)
+            g_loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(5)) for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = step(i, evs[i])
+        if graph is not None:
+            graph.replay()
+        else:
+            loss = step(i, evs[i])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if graph is not None:  # the fused call and the step's parts timed on eager steps after the timed region
+        loss = g_loss.detach().clone()
+        del g_loss, g_b, graph  # drop the captured autograd graph before eager backward passes
+        graph = True
+        evs = evs[:20]
+        for i in range(len(evs)):
+            step(i, evs[i])
+        torch.cuda.synchronize()
     fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     bwd_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     fused_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
@@ -466,7 +495,8 @@ def bench_ns(args, world, rank, dev, dist):
                "data": "synthetic TransE tables (OpenKE xavier init, seed 0); training triples = 272,115 synthetic "
                        "+ the FB15K-237-ZS test triples",
                "config": {"workload": CONFIGS["ns"]["workload"], "batch": B, "neg_ent": k, "rows_per_step": n_rows,
-                          "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}"},
+                          "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}",
+                          "launch": "hipGraph replay of the whole step" if graph else "eager"},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": ATOMIC_PEAK_GBS,
                             "unit": "GB/s of f32 atomic adds (memory-side atomic rate, MI355X_MICROARCH.md)",
                             "frac": ach / ATOMIC_PEAK_GBS, "traffic": None,
@@ -808,6 +838,7 @@ def main():
     ap.add_argument("--train-steps", type=int, default=300,
                     help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
     ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
+    ap.add_argument("--ns-eager", action="store_true", help="--config ns: launch each step eagerly (no hipGraph)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", default="relation", choices=["relation", "entity"],
                     help="N > 1 link configs: split the queries (relation-sharded, one all-gather; default) or "

@@ -163,6 +163,10 @@ int64_t mmre_sampler_draws_per_positive(int64_t neg_rate, int64_t neg_rel_rate, 
 /* Advance host-side per-thread LCG states by one sampling() call. */
 int mmre_sampler_advance(uint64_t* h_seeds, int64_t work_threads, int64_t batch_size, int64_t neg_rate,
                          int64_t neg_rel_rate, int64_t mode);
+/* The same advance applied to device-resident states on a stream, so a training loop keeps
+ * the seeds in HBM (no host copy per batch; the sequence can be captured in a hipGraph). */
+int mmre_sampler_advance_device(uint64_t* d_seeds, int64_t work_threads, int64_t batch_size, int64_t neg_rate,
+                                int64_t neg_rel_rate, int64_t mode, void* stream);
 /* One sampling() call on the GPU. Index arrays are the Reader.h:53-160 train
  * index (int64 rows (h, r, t); head_hrt sorted (h,r,t), tail_hrt (t,r,h),
  * rel_hrt (h,t,r); lef/rig per entity). d_left_mean/d_right_mean NULL = bern off.

@@ -211,9 +211,38 @@ __global__ void k_sampler_repo(const int64_t* __restrict__ eh, const int64_t* __
   }
 }
 
+// The per-pthread LCG states after one sampling call, on the device (mmre_sampler_advance's
+// arithmetic): thread id's state jumps by (its positives) x (draws per positive), its
+// positives being Base.cpp:161-197's [lef, rig) split of the batch.
+__global__ void k_sampler_advance(uint64_t* seeds, int64_t work_threads, int64_t batch_size, int64_t per) {
+  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (id >= work_threads) return;
+  int64_t lef, rig;
+  if (batch_size % work_threads == 0) {
+    lef = id * (batch_size / work_threads);
+    rig = (id + 1) * (batch_size / work_threads);
+  } else {
+    lef = id * (batch_size / work_threads + 1);
+    rig = (id + 1) * (batch_size / work_threads + 1);
+    if (rig > batch_size) rig = batch_size;
+  }
+  const int64_t cnt = rig > lef ? rig - lef : 0;
+  seeds[id] = lcg_jump(seeds[id], (uint64_t)(cnt * per));
+}
+
 }  // namespace mmre
 
 using namespace mmre;
+
+extern "C" int mmre_sampler_advance_device(uint64_t* d_seeds, int64_t work_threads, int64_t batch_size,
+                                           int64_t neg_rate, int64_t neg_rel_rate, int64_t mode, void* stream) {
+  if (!d_seeds || work_threads <= 0 || batch_size <= 0 || neg_rate < 0 || neg_rel_rate < 0) return MMRE_ERR_ARG;
+  const int64_t per = mmre_sampler_draws_per_positive(neg_rate, neg_rel_rate, mode);
+  hipLaunchKernelGGL(k_sampler_advance, dim3((unsigned)((work_threads + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     d_seeds, work_threads, batch_size, per);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
 
 extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
                                    const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,

@@ -33,6 +33,7 @@ SIGNATURES = {
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
     "mmre_glibc_rand": (I32, [I64, I64, P]),
     "mmre_sampler_advance": (I32, [P, I64, I64, I64, I64, I64]),
+    "mmre_sampler_advance_device": (I32, [P, I64, I64, I64, I64, I64, P]),
     "mmre_sampler_draws_per_positive": (I64, [I64, I64, I64]),
     "mmre_sampler_openke": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64, I64,
                                   P, P, P, P, P]),

@@ -29,6 +29,7 @@ class OpenKESampler:
         self.device = torch.device(device)
         self.work_threads = int(work_threads)
         self.bern = bool(bern)
+        self._seeds_dev = torch.empty(self.work_threads, dtype=torch.int64, device=self.device)
         self.seeds = (np.asarray(seeds, np.uint64).copy() if seeds is not None
                       else glibc_seeds(self.work_threads, seed_skip))
         self.train_total = int(train_total if train_total is not None else index.train_total)
@@ -37,7 +38,16 @@ class OpenKESampler:
         self._d = {k: to(getattr(ix, k)) for k in ("train_list", "head_hrt", "tail_hrt", "rel_hrt", "lef_head",
                                                    "rig_head", "lef_tail", "rig_tail", "lef_rel", "rig_rel",
                                                    "left_mean", "right_mean")}
-        self._seeds_dev = torch.empty(self.work_threads, dtype=torch.int64, device=self.device)
+
+    @property
+    def seeds(self) -> np.ndarray:
+        """The per-pthread LCG states (Random.h next_random[]), host mirror of the device copy."""
+        return self._seeds
+
+    @seeds.setter
+    def seeds(self, value):
+        self._seeds = np.asarray(value, np.uint64).copy()
+        self._seeds_dev.copy_(torch.from_numpy(self._seeds.view(np.int64)))
 
     def sample(self, batch_size: int, neg_ent: int = 1, neg_rel: int = 0, mode: int = 0, out=None):
         B = int(batch_size)
@@ -48,7 +58,6 @@ class OpenKESampler:
                        batch_t=torch.empty(n, dtype=torch.int64, device=dev),
                        batch_r=torch.empty(n, dtype=torch.int64, device=dev),
                        batch_y=torch.empty(n, dtype=torch.float32, device=dev))
-        self._seeds_dev.copy_(torch.from_numpy(self.seeds.view(np.int64)), non_blocking=False)
         d = self._d
         call("mmre_sampler_openke", ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]), ptr(d["tail_hrt"]),
              ptr(d["rel_hrt"]), ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]), ptr(d["rig_tail"]),
@@ -56,8 +65,11 @@ class OpenKESampler:
              ptr(d["right_mean"]) if self.bern else None, self.index.n_ent, self.index.n_rel,
              ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel), int(mode),
              ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]), ptr(out["batch_y"]), stream_ptr(dev))
-        # the per-thread LCG states advance by a fixed number of draws per positive
-        call("mmre_sampler_advance", self.seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, B,
+        # the per-thread LCG states advance by a fixed number of draws per positive: on the device,
+        # behind the sampling kernel on the same stream (no host copy per batch), and on the mirror
+        call("mmre_sampler_advance_device", ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel),
+             int(mode), stream_ptr(dev))
+        call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, B,
              int(neg_ent), int(neg_rel), int(mode))
         return out
 

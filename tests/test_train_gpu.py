@@ -30,6 +30,8 @@ def test_openke_sampler_bit_exact(golden, ds):
             assert np.array_equal(got, g[f"{name}_step{step}"]), (name, step)
             assert np.array_equal(out["batch_y"].cpu().numpy(), g[f"{name}_y{step}"])
         assert np.array_equal(s.seeds, g[f"{name}_seeds_end"])
+        # the device-resident states (advanced on the stream) equal Base.cpp's after 3 batches too
+        assert np.array_equal(s._seeds_dev.cpu().numpy().view(np.uint64), g[f"{name}_seeds_end"])
 
 
 def test_openke_sampler_full_size_properties():
