@@ -898,14 +898,17 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 // ------------------------------------------------------------ MFMA sweep ---
 // DistMult / ComplEx: S = Q (queries x K) . E^T (K x entities) with the f32-input MFMA
 // v_mfma_f32_32x32x2_f32 (exact f32, a k-ordered fma chain: the canonical order).
-// Work units and the XCD-grouped persistent split are the VALU sweep's: (query tile of
-// 128) x (entity tile of 128), query-tile major within each XCD group's 1/8 of the table.
-// 4 waves as 2 (q) x 2 (e); each wave 64 x 64 = 2 x 2 blocks of 32 x 32 accumulators.
-// Epilogue: each lane holds 32 query rows x 1 entity column of the 64 x 64 block; it
-// compares against the rows' thresholds (kept in registers for the whole query tile) and
-// bumps per-row register counters; the counters are reduced across the 32 column lanes
-// only when the workgroup leaves the query tile. The truth needs no exclusion test: its
-// score is bit-identical to the threshold (same canonical chain), so `< thr` rejects it.
+// Work units and the XCD-grouped split are the VALU sweep's (UnitMap): (query tile of 128) x
+// (entity tile of 128). 4 waves as 2 (q) x 2 (e); each wave 64 x 64 = 2 x 2 blocks of 32 x 32
+// accumulators. K goes through double-buffered LDS stages of KS rows, register-staged, the
+// next stage's global loads issued at the top of the current one (scripts/probes/
+// mfma_stage.hip: with two 256-thread workgroups per CU this beats LDS-DMA rings and a single
+// 256 x 128 workgroup). Epilogue: each lane holds 32 query rows x 1 entity column of the
+// 64 x 64 block; it reads the rows' thresholds from LDS (8 b128 reads, once per unit),
+// compares and bumps per-row register counters; the counters are reduced across the 32
+// column lanes only when the workgroup leaves the query tile. The truth needs no exclusion
+// test: its score is bit-identical to the threshold (same canonical chain), so `< thr`
+// rejects it.
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 template <bool TC, bool STORE, int PK, int KS>

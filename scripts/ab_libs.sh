@@ -1,6 +1,6 @@
 #!/bin/bash
-# Interleaved A/B of the sweep kernels on one box: the in-tree library (register-staged MFMA
-# kernel, and MMRE_MFMA_IMPL=glds) against another build (MMRE_LIB), alternating runs.
+# Interleaved A/B of the sweep kernels on one box: the in-tree library (default, and 16-row MFMA
+# K stages via MMRE_MFMA_STAGE=16) against another build (MMRE_LIB), alternating runs.
 # usage: scripts/ab_libs.sh <other.so> [configs...]
 other=$1; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
