@@ -359,7 +359,7 @@ def bench_zsl(args, world, rank, dev, dist):
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=_coll_dev(dist, dev))
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     total = int(off[-1])
@@ -476,7 +476,7 @@ def bench_ns(args, world, rank, dev, dist):
     bwd_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     fused_ms = float(np.mean([e[3].elapsed_time(e[4]) for e in evs]))
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=_coll_dev(dist, dev))
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if rank == 0:
@@ -776,7 +776,7 @@ def bench_m3ae(args, world, rank, dev, dist):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=_coll_dev(dist, dev))
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     # roofline: the dominant kernel, fc1 (+GELU) of a block over the packed rows, timed alone
@@ -827,6 +827,11 @@ def bench_m3ae(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def _coll_dev(dist, dev):
+    """Device for a small collective operand: the GPU under RCCL, the host under gloo."""
+    return dev if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -854,12 +859,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # MMRE_BENCH_GLOO=1 rehearses the N > 1 path on a one-GPU box: every rank on cuda:0, gloo
+    # collectives through host tensors (the driver's multi-GPU runs use RCCL, one rank per GPU)
+    rehearse = world > 1 and os.environ.get("MMRE_BENCH_GLOO") == "1"
+    dev_index = 0 if rehearse else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     cfg = CONFIGS[args.config]
     if args.config == "zsl":
@@ -880,7 +892,7 @@ def main():
         train_transe(w, dev, steps=args.train_steps)
         if dist:  # every rank evaluates rank 0's tables (float atomics make training run-dependent)
             for k in ("ent", "rel"):
-                t = w[k].to(dev)
+                t = w[k].to(_coll_dev(dist, dev))
                 dist.broadcast(t, 0)
                 w[k] = t.cpu()
     E = w["n_ent"]
@@ -928,7 +940,7 @@ def main():
     elapsed = time.perf_counter() - t0
     sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if n_local else 0.0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=_coll_dev(dist, dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     _, counts = ev.run()  # one more evaluation outside the timed region: the counts the parity check reads
@@ -970,14 +982,15 @@ def main():
             data += (f" ({args.train_steps} steps of this build's HIP trainer: bit-exact OpenKE sampler + fused margin"
                      f" loss, SGD 1.0, margin 5, neg 25)" if "trained" in w else "") + \
                 f" over the real {w['dataset']} test triples; filter set = all test triples + 272,115 synthetic train"
+        coll = "RCCL" if not dist or dist.get_backend() == "nccl" else "gloo rehearsal (every rank on cuda:0)"
         out = {"metric": METRIC if args.config == "c2" else f"scored triples/sec, {cfg['workload']}",
                "value": value, "unit": "scored triples/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
                "config": {"workload": cfg["workload"], "n_entities": E, "dim": dim, "n_sweeps": 2 * n,
-                          "parallelism": (f"entity-sharded x{world} (1/N of the entity tiles per rank), RCCL all-reduce "
+                          "parallelism": (f"entity-sharded x{world} (1/N of the entity tiles per rank), {coll} all-reduce "
                                           f"of the count table" if args.shard == "entity" else
-                                          f"query-sharded x{world} (relation-major LPT with relation splits), RCCL "
+                                          f"query-sharded x{world} (relation-major LPT with relation splits), {coll} "
                                           f"all-gather of rank counts")},
                "roofline": roof,
                "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
@@ -986,6 +999,19 @@ def main():
                "parity": None}
         if "trained" in w:
             out["config"]["tables"] = w["trained"]
+        if world > 1:
+            # the sharded evaluation's gathered counts vs one-GPU evaluation of every query on
+            # rank 0 (itself checked against the reference Base.so at N = 1): bit-equal counts
+            # mean bit-equal hit@k at this GPU count
+            from mmre.link import evaluate_link_prediction
+            m1, (h1, t1) = evaluate_link_prediction(spec, w["test_h"], w["test_r"], w["test_t"], index=index)
+            single = np.concatenate([h1, t1], 1)
+            out["parity"] = {"source": f"{args.shard}-sharded x{world} gathered counts vs a one-GPU evaluation of all "
+                                       f"{2 * n} sweeps on rank 0",
+                             "sweeps": 2 * n, "counts_bit_equal": bool(np.array_equal(np.asarray(counts), single)),
+                             "mismatched_sweeps": int((np.asarray(counts)[:2] != single[:2]).any(0).sum()),
+                             "metrics_bit_equal": all(metrics[g][k] == m1[g][k] for g in ("filter", "raw")
+                                                      for k in m1[g])}
         if world == 1 and not args.no_cpu_baseline:
             ref = ref_tester_leg(w, args.cpu_sample or REF_SAMPLE[args.config])
             if ref is not None:
