@@ -382,7 +382,7 @@ def bench_zsl(args, world, rank, dev, dist):
                "metrics": m}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_zsl(w)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_with_build(out)), flush=True)
     if dist:
         dist.destroy_process_group()
 
@@ -511,7 +511,7 @@ def bench_ns(args, world, rank, dev, dist):
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_with_build(out)), flush=True)
     if dist:
         dist.destroy_process_group()
 
@@ -641,7 +641,7 @@ def bench_gan(args, world, rank, dev, dist):
            "eager_ms_per_step": eager_ms, "last_losses_G": [float(x) for x in out.cpu()]}
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_gan(w, centroids.cpu(), n_lab)
-    print(json.dumps(res), flush=True)
+    print(json.dumps(_with_build(res)), flush=True)
 
 
 def cpu_baseline_gan(w, centroids, n_lab, iters=3):
@@ -822,9 +822,16 @@ def bench_m3ae(args, world, rank, dev, dist):
                                     "never computed"}}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline_m3ae(enc, gen, w)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_with_build(out)), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def _with_build(out):
+    """Name the binary that produced the line (path, size, sha256 prefix of libmmre_hip.so)."""
+    from mmre._lib import lib_identity
+    out["build"] = lib_identity()
+    return out
 
 
 def _coll_dev(dist, dev):
@@ -1018,7 +1025,7 @@ def main():
                 out["cpu_baseline"] = cpu_baseline_block(ref, w)
                 gs = sample_scores(spec, w, int(ref["n"]), dev)
                 out["parity"] = parity_block(ref, counts, n, w, gpu_scores=gs)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(_with_build(out)), flush=True)
     if dist:
         dist.destroy_process_group()
 

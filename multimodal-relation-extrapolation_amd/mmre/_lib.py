@@ -107,6 +107,16 @@ def lib():
     return _lib
 
 
+def lib_identity() -> dict:
+    """Which binary the process runs: path, size and sha256 prefix of libmmre_hip.so (the bench
+    records it, so a result names the exact build that produced it)."""
+    import hashlib
+    with open(LIB_PATH, "rb") as f:
+        blob = f.read()
+    return {"path": os.path.relpath(LIB_PATH, os.path.dirname(os.path.dirname(os.path.dirname(LIB_PATH)))),
+            "bytes": len(blob), "sha256": hashlib.sha256(blob).hexdigest()[:16]}
+
+
 def check(rc: int, what: str = "") -> None:
     if rc != 0:
         if rc >= 1000:
