@@ -221,9 +221,10 @@ int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model
                      float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
 
 /* Forward + gradient in one pass, for training: everything mmre_ns_forward computes, plus
- * d(loss)/d(tables) for an upstream gradient of 1, ACCUMULATED into the (caller-zeroed)
- * dense gradient tables; the caller scales them by the actual upstream gradient. TransE
- * (L1 / L2, dim <= 512, neg <= 32) runs one fused launch over a norm pre-pass; other models
+ * d(loss)/d(tables) for an upstream gradient of 1 WRITTEN to the dense gradient tables (the
+ * call zeroes them first: no caller fill needed); the caller scales them by the actual
+ * upstream gradient. TransE (L1 / L2, dim <= 512, neg <= 32) runs a pre-pass (row norms,
+ * gradient rows zeroed), the fused kernel and the fixed-order loss reduction; other models
  * run the forward and the backward above. Replaces strategy NegativeSampling.forward +
  * loss.backward() (NegativeSampling.py:23-32, Trainer.py:43-54) for one batch.
  * d_work: >= mmre_ns_fused_workspace(B, k, n_ent, n_rel) floats. */

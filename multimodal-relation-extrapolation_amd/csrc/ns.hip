@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void k_ns_forward(NSArgs A, float* __restrict_
 }
 
 // Fixed-order reduction of the per-positive partials (bit-reproducible loss).
-__global__ __launch_bounds__(256) void k_ns_reduce(NSArgs A, const float* __restrict__ part, float* __restrict__ loss) {
+__device__ void ns_reduce_block(const NSArgs& A, const float* part, float* loss) {
   __shared__ double red[7][256];
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int64_t b = threadIdx.x; b < A.B; b += blockDim.x)
@@ -268,6 +268,10 @@ __global__ __launch_bounds__(256) void k_ns_reduce(NSArgs A, const float* __rest
     }
     loss[0] = (float)l;
   }
+}
+
+__global__ __launch_bounds__(256) void k_ns_reduce(NSArgs A, const float* __restrict__ part, float* __restrict__ loss) {
+  ns_reduce_block(A, part, loss);
 }
 
 __global__ __launch_bounds__(256) void k_ns_backward(NSArgs A, const float* __restrict__ score,
@@ -558,6 +562,12 @@ __device__ __forceinline__ void neg_backward(const NSArgs& A, const RowCtx<NC>& 
                                              float reg_ent, float reg_rel, float* gent, float* grel, Vec<NC>& Gh,
                                              Vec<NC>& Gr, Vec<NC>& Gt, float& oh, float& orr, float& ot) {
   const int d = A.dim;
+  if (g == 0.0f && reg_ent == 0.0f && reg_rel == 0.0f) {  // inactive hinge, no regularization: nothing to add
+    oh += R.own_h ? 1.0f : 0.0f;
+    orr += R.own_r ? 1.0f : 0.0f;
+    ot += R.own_t ? 1.0f : 0.0f;
+    return;
+  }
   Vec<NC> gx;
   row_gx<NC, L2>(gx, A, R, g, lane);
   if (R.own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; }
@@ -687,16 +697,29 @@ __global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const floa
 // ---------------------------------------------------------------------------------------
 constexpr int NSF_MAXJ = 8;
 
-__global__ __launch_bounds__(256) void k_row_norms(const float* __restrict__ tab, int64_t n, int d,
-                                                   float* __restrict__ out) {
+// Pre-pass of the fused launch, one wave per row over the entity rows then the relation
+// rows: the row's L2 norm, and the row of the gradient table zeroed (the fused kernel's
+// atomics accumulate into it, so the tables need no separate fill).
+// (A last-workgroup loss reduction inside the fused kernel was tried instead of k_ns_reduce:
+// its per-workgroup device-scope fence writes back the XCD's L2 each time, 0.12 -> 0.19 ms.)
+__global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
+                                                    const float* __restrict__ rel, int64_t n_rel, int d,
+                                                    float* __restrict__ nrm_e, float* __restrict__ nrm_r,
+                                                    float* __restrict__ gent, float* __restrict__ grel) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n) return;
-  const float* p = tab + row * d;
+  if (row >= n_ent + n_rel) return;
+  const bool is_ent = row < n_ent;
+  const int64_t i0 = (is_ent ? row : row - n_ent) * d;
+  const float* p = (is_ent ? ent : rel) + i0;
+  float* g = (is_ent ? gent : grel) + i0;
   float s = 0.0f;
-  for (int i = lane; i < d; i += kWave) s += p[i] * p[i];
+  for (int i = lane; i < d; i += kWave) {
+    s += p[i] * p[i];
+    g[i] = 0.0f;
+  }
   s = wave_sum(s);
-  if (lane == 0) out[row] = sqrtf(s);
+  if (lane == 0) (is_ent ? nrm_e : nrm_r)[is_ent ? row : row - n_ent] = sqrtf(s);
 }
 
 __device__ __forceinline__ int64_t readlane64(int64_t v, int src) {
@@ -886,6 +909,12 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
       neg_backward<NC, L2>(A, R, row, g, lane, reg, reg, gent, grel, Gh, Gr, Gt, oh, orr, ot);
       continue;
     }
+    if (g == 0.0f && reg == 0.0f) {  // inactive hinge, no regularization: no gradient, no atomics
+      oh += code[u] != 0 ? 1.0f : 0.0f;
+      orr += code[u] != 2 ? 1.0f : 0.0f;
+      ot += code[u] != 1 ? 1.0f : 0.0f;
+      continue;
+    }
     const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
     if (code[u] != 3) vnorm(cn, C[u], cc);
     fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]);
@@ -913,20 +942,21 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   }
   if (lane == 0) { s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot; }
   __syncthreads();
-  if (w != 0) return;
-  for (int i = 0; i < NSW - 1; ++i) {
+  if (w == 0) {
+    for (int i = 0; i < NSW - 1; ++i) {
 #pragma unroll
-    for (int q = 0; q < NC; ++q) {
-      Gh.v[q] += s_acc[i][0][q * kWave + lane];
-      Gr.v[q] += s_acc[i][1][q * kWave + lane];
-      Gt.v[q] += s_acc[i][2][q * kWave + lane];
+      for (int q = 0; q < NC; ++q) {
+        Gh.v[q] += s_acc[i][0][q * kWave + lane];
+        Gr.v[q] += s_acc[i][1][q * kWave + lane];
+        Gt.v[q] += s_acc[i][2][q * kWave + lane];
+      }
     }
+    float kh = 0.f, kr = 0.f, kt = 0.f;
+    for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
+    scatter_row(gent, ph, d, lane, Ph, P.sh, Gh, nf, reg * kh);
+    scatter_row(grel, pr, d, lane, Pr, P.sr, Gr, nf, reg * kr);
+    scatter_row(gent, pt, d, lane, Pt, P.st, Gt, nf, reg * kt);
   }
-  float kh = 0.f, kr = 0.f, kt = 0.f;
-  for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
-  scatter_row(gent, ph, d, lane, Ph, P.sh, Gh, nf, reg * kh);
-  scatter_row(grel, pr, d, lane, Pr, P.sr, Gr, nf, reg * kr);
-  scatter_row(gent, pt, d, lane, Pt, P.st, Gt, nf, reg * kt);
 }
 
 // which TransE fast-path instance fits: elements per lane (0: none, generic path)
@@ -1060,7 +1090,7 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
 }
 
 extern "C" int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel) {
-  (void)neg;
+  (void)neg;  // partials, entity norms, relation norms (+ slack)
   return 7 * (batch > 0 ? batch : 1) + (n_ent > 0 ? n_ent : 0) + (n_rel > 0 ? n_rel : 0) + 64;
 }
 
@@ -1082,6 +1112,13 @@ extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_ma
   hipStream_t st = (hipStream_t)stream;
   const int nc = transe_fast_nc(A);
   if (nc == 0 || neg > NSW * NSF_MAXJ) {  // generic: forward, then the backward with upstream gradient 1
+    const int64_t ew = model == MMRE_ROTATE ? 2 * (int64_t)dim : dim;
+    MMRE_CHECK(hipMemsetAsync(d_grad_ent, 0, (size_t)(n_ent * ew) * sizeof(float), st));
+    MMRE_CHECK(hipMemsetAsync(d_grad_rel, 0, (size_t)(n_rel * dim) * sizeof(float), st));
+    if (model == MMRE_COMPLEX) {
+      MMRE_CHECK(hipMemsetAsync(d_grad_ent_im, 0, (size_t)(n_ent * dim) * sizeof(float), st));
+      MMRE_CHECK(hipMemsetAsync(d_grad_rel_im, 0, (size_t)(n_rel * dim) * sizeof(float), st));
+    }
     rc = mmre_ns_forward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                          phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
                          d_loss, d_work, stream);
@@ -1093,8 +1130,10 @@ extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_ma
   float* part = d_work;
   float* nrm_e = d_work + 7 * batch;
   float* nrm_r = nrm_e + n_ent;
-  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n_ent + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, dim, nrm_e);
-  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n_rel + 3) / 4)), dim3(256), 0, st, d_rel, n_rel, dim, nrm_r);
+  // the pre-pass (norms, gradient rows zeroed), the fused kernel, the fixed-order loss reduction
+  hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
+                     n_rel, dim, nrm_e, nrm_r, d_grad_ent, d_grad_rel);
+  MMRE_CHECK_LAUNCH();
   const dim3 grid((unsigned)batch), blk(256);
   const bool l2 = model == MMRE_TRANSE_L2;
 #define MMRE_NS_FUSED(NC_)                                                                                    \

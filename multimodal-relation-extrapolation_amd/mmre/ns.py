@@ -4,7 +4,8 @@ forward  = model(data) in 'normal' mode for B*(1+k) rows -> MarginLoss (optional
            self-adversarial) + regul_rate * regularization, one launch + one fixed-order
            reduction (OpenKE strategy/NegativeSampling.py:23-32, MarginLoss.py:24-28,
            TransE.py:92-102; repo module/NegativeSampling.py:204-229).
-backward = d(loss)/d(embedding tables) scattered into dense gradient tables (float atomics).
+backward = d(loss)/d(embedding tables) scattered into dense gradient tables (float atomics;
+           all-zero row gradients, e.g. inactive hinges without regularization, issue none).
 """
 from __future__ import annotations
 
@@ -50,9 +51,9 @@ class _FusedNS(torch.autograd.Function):
         if any(ctx.needs_input_grad[:4]):
             E, R = int(ent.shape[0]), int(rel.shape[0])
             work = torch.empty(int(lib().mmre_ns_fused_workspace(batch, neg, E, R)), dtype=torch.float32, device=dev)
-            ge, gr = torch.zeros_like(ent), torch.zeros_like(rel)
-            gei = torch.zeros_like(ent_im) if ent_im is not None else None
-            gri = torch.zeros_like(rel_im) if rel_im is not None else None
+            ge, gr = torch.empty_like(ent), torch.empty_like(rel)  # written (zeroed) by the call
+            gei = torch.empty_like(ent_im) if ent_im is not None else None
+            gri = torch.empty_like(rel_im) if rel_im is not None else None
             if events is not None:
                 events[0].record()
             call("mmre_ns_forward_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
