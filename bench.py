@@ -500,7 +500,7 @@ def bench_ns(args, world, rank, dev, dist):
                "roofline": {"bound": "hbm", "achieved": ach, "peak": ATOMIC_PEAK_GBS,
                             "unit": "GB/s of f32 atomic adds (memory-side atomic rate, MI355X_MICROARCH.md)",
                             "frac": ach / ATOMIC_PEAK_GBS, "traffic": None,
-                            "kernel": "mmre_ns_forward_backward: k_row_norms + k_ns_transe_fused<4, false> + "
+                            "kernel": "mmre_ns_forward_backward: k_ns_prepass + k_ns_transe_fused<4, false> + "
                                       "k_ns_reduce (events around the one C-ABI call)",
                             "kernel_ms": fused_ms, "atomic_bytes": atomic_bytes,
                             "algorithmic_bytes": fwd_bytes + atomic_bytes,
