@@ -220,15 +220,31 @@ int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model
                      const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
                      float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
 
-/* Forward + gradient in one pass, for training: everything mmre_ns_forward computes, plus
- * d(loss)/d(tables) for an upstream gradient of 1 WRITTEN to the dense gradient tables (the
- * call zeroes them first: no caller fill needed); the caller scales them by the actual
- * upstream gradient. TransE (L1 / L2, dim <= 512, neg <= 32) runs a pre-pass (row norms,
- * gradient rows zeroed), the fused kernel and the fixed-order loss reduction; other models
- * run the forward and the backward above. Replaces strategy NegativeSampling.forward +
- * loss.backward() (NegativeSampling.py:23-32, Trainer.py:43-54) for one batch.
- * d_work: >= mmre_ns_fused_workspace(B, k, n_ent, n_rel) floats. */
-int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel);
+/* Training: forward, loss and d(loss)/d(tables). mmre_ns_fused_forward computes everything
+ * mmre_ns_forward computes and keeps what the gradient needs in d_work; mmre_ns_fused_grad
+ * then WRITES every row of the dense gradient tables (no caller fill): d(loss)/d(table) *
+ * d_grad_loss[0] (NULL: 1). mmre_ns_forward_backward is the two in sequence with an upstream
+ * gradient of 1. TransE (L1 / L2, dim <= 512, neg <= 32): a norm pre-pass, the fused kernel
+ * (each row read once, the gradient contributions written to slots and counted per table
+ * row), the fixed-order loss reduction, and the slots bucketed by table row; the gradient is
+ * one wave per table row summing its bucket in batch order -- no float atomics,
+ * bit-reproducible. Other
+ * models run the forward above and, in mmre_ns_fused_grad, zero the tables and run the
+ * backward above. Replaces strategy NegativeSampling.forward + loss.backward()
+ * (NegativeSampling.py:23-32, Trainer.py:43-54) for one batch. d_work: >=
+ * mmre_ns_fused_workspace(B, k, n_ent, n_rel, dim) floats, kept between the two calls. */
+int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel, int dim);
+int mmre_ns_fused_forward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
+                          const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent,
+                          int64_t n_rel, int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,
+                          const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
+                          float regul_rate, float* d_score, float* d_loss, float* d_work, void* stream);
+int mmre_ns_fused_grad(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
+                       const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent, int64_t n_rel,
+                       int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r,
+                       int64_t batch, int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
+                       const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
+                       float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
 int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
                              const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent,
                              int64_t n_rel, int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,

@@ -237,13 +237,16 @@ __global__ __launch_bounds__(256) void k_ns_forward(NSArgs A, float* __restrict_
   }
 }
 
-// Fixed-order reduction of the per-positive partials (bit-reproducible loss).
+// Fixed-order reduction of the per-positive partials (bit-reproducible loss) by threads
+// 0..255 of the workgroup (every thread of it must call: it synchronises).
 __device__ void ns_reduce_block(const NSArgs& A, const float* part, float* loss) {
   __shared__ double red[7][256];
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int64_t b = threadIdx.x; b < A.B; b += blockDim.x)
+  const bool mine = threadIdx.x < 256;
+  for (int64_t b = threadIdx.x; mine && b < A.B; b += 256)
     for (int i = 0; i < 7; ++i) acc[i] += part[b * 7 + i];
-  for (int i = 0; i < 7; ++i) red[i][threadIdx.x] = acc[i];
+  if (mine)
+    for (int i = 0; i < 7; ++i) red[i][threadIdx.x] = acc[i];
   __syncthreads();
   for (int s = 128; s >= 1; s >>= 1) {
     if ((int)threadIdx.x < s)
@@ -686,38 +689,110 @@ __global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const floa
 }
 
 // ---------------------------------------------------------------------------------------
-// Fused forward + gradient (TransE fast path, K <= NSW * NSF_MAXJ). The margin loss's
-// d(loss)/d(score) of every row depends only on its own positive's scores (hinge indicator,
-// self-adversarial softmax over the positive's negatives), so the workgroup that scores a
-// positive can also emit its gradients, per unit upstream gradient: the rows are read ONCE
-// (kept in registers between the scoring and the gradient pass), the row norms come from a
-// pre-pass (one scalar per entity / relation instead of a wave reduction per row), and the
-// gradient atomics of one positive overlap the gathers of the others in the same launch.
-// The caller scales the gradient tables by the upstream gradient in the backward.
+// Fused forward + row-owner gradient (TransE fast path, K <= NSW * NSF_MAXJ).
+// The margin loss's d(loss)/d(score) of every row depends only on its own positive's scores
+// (hinge indicator, self-adversarial softmax over the positive's negatives), so the
+// workgroup that scores a positive also forms its gradient, in the normalised space, per unit
+// upstream gradient: the rows are read ONCE (kept in registers between the scoring and the
+// gradient pass) and the row norms come from a pre-pass. A negative shares the positive's
+// relation and one of its entities (Base.cpp:111-124), so what it adds to the positive's own
+// three rows is summed in registers across the negatives; per negative one row is left, the
+// corrupted one.
+// No float atomics anywhere: k_ns_transe_fused writes every contribution to a SLOT (its
+// values + the table row it belongs to) and counts the slots per table row; k_ns_scan_reduce turns
+// the counts into bucket offsets and k_ns_place drops each slot id into its row's bucket
+// (integer atomics: the bucket's CONTENT is fixed, its order is not); k_ns_row_owner -- one
+// wave per table row -- takes its bucket's slots in increasing slot id (batch order, the same
+// every run), sums them, maps the sum through the row's normalisation, adds the
+// regularization term, scales by the upstream gradient and writes the row, every row
+// (untouched ones as zeros): no fills, no scaling pass, bit-reproducible gradient tables.
+// Slots of positive b start at b (3 + 3K): slot q < 3 is the positive's h / r / t (row 3b + q
+// of `shared` holds its signed sum), slot 3 + 3j + q is negative j's h / r / t when that row
+// is not shared with the positive (record bK + j of `rec` holds the negative's gx; a t slot
+// takes -gx). Keys: entity id, n_ent + relation id, or the sentinel n_ent + n_rel.
+// For L1 TransE a negative's gx is g sign(x) elementwise, so its record is |g| and two bit
+// planes (x > 0, x < 0) -- 2 + 4 NC words instead of d floats (72 B instead of 800 at d 200);
+// the row-owner pass rebuilds the same floats (|g| times +-1 is exact). L2 stores gx.
 // ---------------------------------------------------------------------------------------
 constexpr int NSF_MAXJ = 8;
 
+struct NSSlots {        // the row-owner gradient's workspace
+  float* shared;        // 3 B rows of dim floats: the positives' own rows
+  float* rec;           // K B records of a negative's gx (ns_rec_words)
+  float* mult;          // per slot: occurrences of its row in the batch (regularization)
+  uint32_t* keys;       // per slot: table row
+  int32_t* counts;      // per table row: its slots (zeroed by the pre-pass)
+  uint32_t sentinel;    // n_ent + n_rel: no slot
+};
+
+// words per negative record: gx itself (L2), or |g| + pad + NC (x > 0, x < 0) 64-bit masks (L1)
+__host__ __device__ constexpr int ns_rec_words(int nc, bool l2, int d) { return l2 ? d : 2 + 4 * nc; }
+
+template <int NC>
+__device__ __forceinline__ void vstore(float* row, const Vec<NC>& v, int d, int lane) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = lane + c * kWave;
+    if (i < d) row[i] = v.v[c];
+  }
+}
+
+// negative record idx <- gx = g sign(x) (L1: |g| and the sign planes of gx) or gx (L2)
+template <int NC, bool L2>
+__device__ __forceinline__ void store_rec(float* rec, int64_t idx, const Vec<NC>& gx, float g, int d, int lane) {
+  if constexpr (L2) {
+    vstore(rec + idx * d, gx, d, lane);
+  } else {
+    float* r = rec + idx * ns_rec_words(NC, false, d);
+    uint64_t val = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {  // wave-uniform masks; lane 2c / 2c + 1 stores plane c's pair
+      const uint64_t pm = __ballot(gx.v[c] > 0.0f), nm = __ballot(gx.v[c] < 0.0f);
+      if (lane == 2 * c) val = pm;
+      if (lane == 2 * c + 1) val = nm;
+    }
+    if (lane < 2 * NC) reinterpret_cast<uint64_t*>(r + 2)[lane] = val;
+    if (lane == 0) { r[0] = fabsf(g); r[1] = 0.0f; }
+  }
+}
+
+// a slot's contribution row: a shared sum row, or a negative's record decoded
+template <int NC, bool L2>
+__device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ shared, const float* __restrict__ rec,
+                                          int64_t idx, bool neg, int d, int lane) {
+  if (!neg) {
+    vload(v, shared + idx * d, d, lane);
+  } else if constexpr (L2) {
+    vload(v, rec + idx * d, d, lane);
+  } else {
+    const float* r = rec + idx * ns_rec_words(NC, false, d);
+    const float mag = r[0];
+    const uint64_t* m = reinterpret_cast<const uint64_t*>(r + 2);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int sg = (int)((m[2 * c] >> lane) & 1ull) - (int)((m[2 * c + 1] >> lane) & 1ull);
+      v.v[c] = mag * (float)sg;
+    }
+  }
+}
+
 // Pre-pass of the fused launch, one wave per row over the entity rows then the relation
-// rows: the row's L2 norm, and the row of the gradient table zeroed (the fused kernel's
-// atomics accumulate into it, so the tables need no separate fill).
+// rows: the row's L2 norm (one scalar per row instead of a wave reduction per use), and the
+// row's slot count / placement cursor zeroed.
 // (A last-workgroup loss reduction inside the fused kernel was tried instead of k_ns_reduce:
 // its per-workgroup device-scope fence writes back the XCD's L2 each time, 0.12 -> 0.19 ms.)
 __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
                                                     const float* __restrict__ rel, int64_t n_rel, int d,
                                                     float* __restrict__ nrm_e, float* __restrict__ nrm_r,
-                                                    float* __restrict__ gent, float* __restrict__ grel) {
+                                                    int32_t* __restrict__ counts, int32_t* __restrict__ cursor) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;
+  if (lane == 0) { counts[row] = 0; cursor[row] = 0; }  // the row's slot bucket, for this call
   const bool is_ent = row < n_ent;
-  const int64_t i0 = (is_ent ? row : row - n_ent) * d;
-  const float* p = (is_ent ? ent : rel) + i0;
-  float* g = (is_ent ? gent : grel) + i0;
+  const float* p = (is_ent ? ent : rel) + (is_ent ? row : row - n_ent) * d;
   float s = 0.0f;
-  for (int i = lane; i < d; i += kWave) {
-    s += p[i] * p[i];
-    g[i] = 0.0f;
-  }
+  for (int i = lane; i < d; i += kWave) s += p[i] * p[i];
   s = wave_sum(s);
   if (lane == 0) (is_ent ? nrm_e : nrm_r)[is_ent ? row : row - n_ent] = sqrtf(s);
 }
@@ -754,7 +829,7 @@ __device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Ve
 template <int NC, bool L2>
 __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
                                                          const float* __restrict__ nrm_r, float* __restrict__ score,
-                                                         float* __restrict__ part, float* gent, float* grel) {
+                                                         float* __restrict__ part, NSSlots S, int64_t n_ent) {
   __shared__ float s_n[NSW * NSF_MAXJ];
   __shared__ float s_c[NSW * NSF_MAXJ];
   __shared__ float s_gp;
@@ -878,10 +953,11 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     }
   }
   __syncthreads();
-  // gradient pass (upstream gradient 1)
+  // gradient pass (upstream gradient 1): contributions into slots
   const double N = (double)A.B * (1.0 + (double)A.K);
   const float reg = A.regul_rate != 0.0f ? (float)(A.regul_rate * 2.0 / (3.0 * N * d)) : 0.0f;
   const float sgn = A.use_model_margin ? -1.0f : 1.0f;
+  const int64_t sb = b * (3 + 3 * A.K);     // this positive's first slot
   Vec<NC> Gh, Gr, Gt, gx;
 #pragma unroll
   for (int q = 0; q < NC; ++q) Gh.v[q] = Gr.v[q] = Gt.v[q] = 0.0f;
@@ -902,34 +978,44 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     if (u >= nj) continue;
     const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
     const float g = -sgn * s_c[j];
-    if (code[u] == 4) {
+    uint32_t kq0 = S.sentinel, kq1 = S.sentinel, kq2 = S.sentinel;  // this negative's h / r / t slots
+    if (code[u] == 4) {  // shares fewer than two rows: every row it does not share gets a slot
       RowCtx<NC> R;
       row_ctx_load(R, A, row, ph, pr, pt, P, lane);
       row_ctx_norms(R, P);
-      neg_backward<NC, L2>(A, R, row, g, lane, reg, reg, gent, grel, Gh, Gr, Gt, oh, orr, ot);
-      continue;
-    }
-    if (g == 0.0f && reg == 0.0f) {  // inactive hinge, no regularization: no gradient, no atomics
+      if (g == 0.0f && reg == 0.0f) {
+        oh += R.own_h ? 1.0f : 0.0f;
+        orr += R.own_r ? 1.0f : 0.0f;
+        ot += R.own_t ? 1.0f : 0.0f;
+      } else {
+        row_gx<NC, L2>(gx, A, R, g, lane);
+        if (R.own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)A.h[row];
+        if (R.own_r) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + A.r[row]);
+        if (R.own_t) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)A.t[row];
+        store_rec<NC, L2>(S.rec, b * A.K + j, gx, g, d, lane);
+      }
+    } else if (g == 0.0f && reg == 0.0f) {  // inactive hinge, no regularization: adds nothing
       oh += code[u] != 0 ? 1.0f : 0.0f;
       orr += code[u] != 2 ? 1.0f : 0.0f;
       ot += code[u] != 1 ? 1.0f : 0.0f;
-      continue;
+    } else {
+      const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
+      if (code[u] != 3) vnorm(cn, C[u], cc);
+      fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]);
+      const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
+#pragma unroll
+      for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
+      if (code[u] != 0) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)readlane64(my_h, u);
+      if (code[u] != 2) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + readlane64(my_r, u));
+      if (code[u] != 1) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)readlane64(my_t, u);
+      if (code[u] != 3) store_rec<NC, L2>(S.rec, b * A.K + j, gx, L2 ? 0.0f : gs, d, lane);
     }
-    const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
-    if (code[u] != 3) vnorm(cn, C[u], cc);
-    fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]);
-    const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
-#pragma unroll
-    for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
-    if (code[u] != 0) { vadd(Gh, gx, 1.0f); oh += 1.0f; }
-    if (code[u] != 2) { vadd(Gr, gx, 1.0f); orr += 1.0f; }
-    if (code[u] != 1) { vadd(Gt, gx, -1.0f); ot += 1.0f; }
-    if (code[u] == 0) scatter_row(gent, readlane64(my_h, u), d, lane, C[u], cnr[u] * cnr[u], gx, nf, reg);
-    else if (code[u] == 2) scatter_row(grel, readlane64(my_r, u), d, lane, C[u], cnr[u] * cnr[u], gx, nf, reg);
-    else if (code[u] == 1) {
-#pragma unroll
-      for (int q = 0; q < NC; ++q) gx.v[q] = -gx.v[q];
-      scatter_row(gent, readlane64(my_t, u), d, lane, C[u], cnr[u] * cnr[u], gx, nf, reg);
+    if (lane < 3) {
+      const int64_t sl = sb + 3 + 3 * j + lane;
+      const uint32_t key = lane == 0 ? kq0 : (lane == 1 ? kq1 : kq2);
+      S.keys[sl] = key;
+      S.mult[sl] = 1.0f;
+      if (key != S.sentinel) atomicAdd(&S.counts[key], 1);
     }
   }
   if (w > 0) {
@@ -942,7 +1028,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   }
   if (lane == 0) { s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot; }
   __syncthreads();
-  if (w == 0) {
+  if (w == 0) {  // the positive's own rows: one signed sum each, in the fixed wave order
     for (int i = 0; i < NSW - 1; ++i) {
 #pragma unroll
       for (int q = 0; q < NC; ++q) {
@@ -953,9 +1039,208 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     }
     float kh = 0.f, kr = 0.f, kt = 0.f;
     for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
-    scatter_row(gent, ph, d, lane, Ph, P.sh, Gh, nf, reg * kh);
-    scatter_row(grel, pr, d, lane, Pr, P.sr, Gr, nf, reg * kr);
-    scatter_row(gent, pt, d, lane, Pt, P.st, Gt, nf, reg * kt);
+    vstore(S.shared + (3 * b + 0) * d, Gh, d, lane);
+    vstore(S.shared + (3 * b + 1) * d, Gr, d, lane);
+    vstore(S.shared + (3 * b + 2) * d, Gt, d, lane);
+    if (lane < 3) {
+      const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
+      S.keys[sb + lane] = key;
+      S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
+      atomicAdd(&S.counts[key], 1);
+    }
+  }
+}
+
+// One 1,024-thread workgroup after the fused kernel: the fixed-order loss reduction
+// (ns_reduce_block, the arithmetic of k_ns_reduce, on the first 256 threads) and the exclusive
+// scan of the per-row slot counts into bucket offsets (offs[n] = all slots), over coalesced
+// 4,096-count tiles: four counts per thread, wave scans by shuffles, the 16 wave totals in LDS.
+__global__ __launch_bounds__(1024) void k_ns_scan_reduce(NSArgs A, const float* __restrict__ part,
+                                                         float* __restrict__ loss, const int32_t* __restrict__ counts,
+                                                         int64_t n, int32_t* __restrict__ offs) {
+  __shared__ int32_t s_w[16];
+  __shared__ int32_t s_carry;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  ns_reduce_block(A, part, loss);
+  if (t == 0) s_carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 4096) {
+    const int64_t i = base + 4 * (int64_t)t;
+    int32_t c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = i + q < n ? counts[i + q] : 0;
+    const int32_t tot = c[0] + c[1] + c[2] + c[3];
+    int32_t inc = tot;  // inclusive scan of the thread totals within the wave
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const int32_t v = __shfl_up(inc, sh);
+      if (lane >= sh) inc += v;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    int32_t before = s_carry;
+    for (int k = 0; k < wv; ++k) before += s_w[k];
+    int32_t run = before + inc - tot;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (i + q < n) offs[i + q] = run;
+      run += c[q];
+    }
+    __syncthreads();
+    if (t == 1023) s_carry = run;  // the last thread's running total = the tile's end
+    __syncthreads();
+  }
+  if (t == 0) offs[n] = s_carry;
+}
+
+// Each slot's id into its row's bucket (position within the bucket by arrival: the owner
+// restores the batch order).
+__global__ __launch_bounds__(256) void k_ns_place(const uint32_t* __restrict__ keys, int64_t n_slots,
+                                                  uint32_t sentinel, const int32_t* __restrict__ offs,
+                                                  int32_t* __restrict__ cursor, int32_t* __restrict__ sslot) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_slots) return;
+  const uint32_t k = keys[i];
+  if (k == sentinel) return;
+  sslot[offs[k] + atomicAdd(&cursor[k], 1)] = (int32_t)i;
+}
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) v = min(v, __shfl_xor(v, s));
+  return v;
+}
+
+__device__ __forceinline__ int64_t readlane64u(int64_t v, int src) {  // src wave-uniform
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, src);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), src);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// One wave per table row (entities, then relations): the row's slots (a contiguous run of
+// the sorted keys) summed in batch order, d(loss)/d(raw row) = (dy - y (y . dy)) / |v| with
+// y = v / max(|v|, eps) when the model normalises (dy / eps below eps), + reg * (occurrences)
+// * v, times the upstream gradient; written to every row of the gradient table.
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ ent, const float* __restrict__ rel,
+                                                      int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
+                                                      const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
+                                                      const float* __restrict__ shared, const float* __restrict__ rec,
+                                                      const float* __restrict__ mult,
+                                                      const int32_t* __restrict__ offs,
+                                                      const int32_t* __restrict__ sslot, int64_t K,
+                                                      const float* __restrict__ grad_loss, float* __restrict__ gent,
+                                                      float* __restrict__ grel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_ent + n_rel) return;  // wave-uniform
+  const bool is_ent = row < n_ent;
+  const int64_t id = is_ent ? row : row - n_ent;
+  float* o = (is_ent ? gent : grel) + id * d;
+  const int64_t i0 = offs[row], i1 = offs[row + 1];
+  if (i0 == i1) {  // not in the batch: zero gradient
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + c * kWave;
+      if (i < d) o[i] = 0.0f;
+    }
+    return;
+  }
+  const int64_t spp = 3 + 3 * K;
+  Vec<NC> dy;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) dy.v[c] = 0.0f;
+  float cnt = 0.0f;
+  // the bucket's slots in increasing slot id (batch order), 64 at a time: lane u gets the
+  // u-th. A bucket of <= 64 (nearly all rows) is ranked in registers: lane l's rank = how many
+  // of the bucket's ids are smaller, and a ds_permute sends each id to the lane of its rank.
+  // A larger bucket (a hub row) selects its next 64 by repeated wave minima over the bucket.
+  const int64_t c = i1 - i0;
+  int prev = -1;
+  for (int64_t c0 = 0; c0 < c; c0 += kWave) {
+    const int n = (int)((c - c0) < kWave ? (c - c0) : kWave);
+    int ordered = 0;
+    if (c <= kWave) {
+      const int mine = lane < c ? sslot[i0 + lane] : INT_MAX;
+      int rank = 0;
+      for (int m = 0; m < n; ++m) rank += __builtin_amdgcn_readlane(mine, m) < mine;
+      ordered = __builtin_amdgcn_ds_permute((lane < n ? rank : lane) * 4, mine);
+    } else {
+      for (int u = 0; u < n; ++u) {
+        int v = INT_MAX;
+        for (int64_t e = i0 + lane; e < i1; e += kWave) {
+          const int sv = sslot[e];
+          if (sv > prev && sv < v) v = sv;
+        }
+        v = wave_min_i32(v);
+        if (lane == u) ordered = v;
+        prev = v;
+      }
+    }
+    int64_t src = 0;  // shared row index, or -(record index + 1) for a negative's record
+    float sg = 0.0f, m = 0.0f;
+    if (lane < n) {  // lane u decodes its slot: where its contribution lives, and its sign
+      const int64_t sl = ordered;
+      const int64_t b = sl / spp, t = sl - b * spp;
+      if (t < 3) { src = 3 * b + t; sg = 1.0f; }
+      else { const int64_t jq = t - 3; src = -(b * K + jq / 3) - 1; sg = jq % 3 == 2 ? -1.0f : 1.0f; }
+      m = mult[sl];
+    }
+    cnt += wave_sum(m);  // integer-valued: exact in any order
+    int u = 0;
+    for (; u + 4 <= n; u += 4) {  // four slots in flight, added in slot order
+      Vec<NC> v0, v1, v2, v3;
+      const int64_t s0 = readlane64u(src, u), s1 = readlane64u(src, u + 1);
+      const int64_t s2 = readlane64u(src, u + 2), s3 = readlane64u(src, u + 3);
+      load_slot<NC, L2>(v0, shared, rec, s0 < 0 ? -s0 - 1 : s0, s0 < 0, d, lane);
+      load_slot<NC, L2>(v1, shared, rec, s1 < 0 ? -s1 - 1 : s1, s1 < 0, d, lane);
+      load_slot<NC, L2>(v2, shared, rec, s2 < 0 ? -s2 - 1 : s2, s2 < 0, d, lane);
+      load_slot<NC, L2>(v3, shared, rec, s3 < 0 ? -s3 - 1 : s3, s3 < 0, d, lane);
+      const float g0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sg), u));
+      const float g1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sg), u + 1));
+      const float g2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sg), u + 2));
+      const float g3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sg), u + 3));
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        dy.v[c] += g0 * v0.v[c];
+        dy.v[c] += g1 * v1.v[c];
+        dy.v[c] += g2 * v2.v[c];
+        dy.v[c] += g3 * v3.v[c];
+      }
+    }
+    for (; u < n; ++u) {
+      Vec<NC> v0;
+      const int64_t s0 = readlane64u(src, u);
+      load_slot<NC, L2>(v0, shared, rec, s0 < 0 ? -s0 - 1 : s0, s0 < 0, d, lane);
+      const float g0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sg), u));
+#pragma unroll
+      for (int c = 0; c < NC; ++c) dy.v[c] += g0 * v0.v[c];
+    }
+  }
+  Vec<NC> v;
+  vload(v, (is_ent ? ent : rel) + id * d, d, lane);
+  const float G = grad_loss ? grad_loss[0] : 1.0f;
+  const float rr = reg * cnt;
+  if (norm_flag) {
+    const float nv = (is_ent ? nrm_e : nrm_r)[id];
+    const float cv = fmaxf(nv, 1e-12f);
+    float dot = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) dot += (v.v[c] / cv) * dy.v[c];
+    dot = wave_sum(dot);
+    const float scale = nv > 1e-12f ? 1.0f / nv : 1.0f / 1e-12f;
+    const float proj = nv > 1e-12f ? dot : 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + c * kWave;
+      if (i < d) o[i] = ((dy.v[c] - (v.v[c] / cv) * proj) * scale + rr * v.v[c]) * G;
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + c * kWave;
+      if (i < d) o[i] = (dy.v[c] + rr * v.v[c]) * G;
+    }
   }
 }
 
@@ -1089,9 +1374,145 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
   return MMRE_OK;
 }
 
-extern "C" int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel) {
-  (void)neg;  // partials, entity norms, relation norms (+ slack)
-  return 7 * (batch > 0 ? batch : 1) + (n_ent > 0 ? n_ent : 0) + (n_rel > 0 ? n_rel : 0) + 64;
+// Workspace of the fused path, in 4-byte words, 256-B aligned pieces: loss partials, row
+// norms, the slot contributions / occurrences / keys, the per-row slot counts, placement
+// cursors and bucket offsets, the bucketed slot ids.
+struct FusedWs {
+  int64_t part, nrm_e, nrm_r, shared, rec, mult, keys, counts, cursor, offs, sslot, total, slots;
+  uint32_t sentinel;
+};
+
+static int64_t al64(int64_t x) { return (x + 63) & ~(int64_t)63; }
+
+static void fused_ws(int64_t B, int64_t K, int64_t E, int64_t R, int d, FusedWs& w) {
+  w.slots = (3 + 3 * K) * B;
+  w.sentinel = (uint32_t)(E + R);
+  int64_t o = 0;
+  w.part = o;    o = al64(o + 7 * B);
+  w.nrm_e = o;   o = al64(o + E);
+  w.nrm_r = o;   o = al64(o + R);
+  w.shared = o;  o = al64(o + 3 * B * d);
+  w.rec = o;     o = al64(o + K * B * (d > ns_rec_words(8, false, d) ? d : ns_rec_words(8, false, d)));
+  w.mult = o;    o = al64(o + w.slots);
+  w.keys = o;    o = al64(o + w.slots);
+  w.counts = o;  o = al64(o + E + R);
+  w.cursor = o;  o = al64(o + E + R);
+  w.offs = o;    o = al64(o + E + R + 1);
+  w.sslot = o;   o = al64(o + w.slots);
+  w.total = o;
+}
+
+extern "C" int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel, int dim) {
+  FusedWs w;
+  fused_ws(batch > 0 ? batch : 1, neg > 0 ? neg : 0, n_ent > 0 ? n_ent : 0, n_rel > 0 ? n_rel : 0, dim > 0 ? dim : 1,
+           w);
+  return w.total > 7 * batch ? w.total : 7 * batch;
+}
+
+static bool fused_fast(const NSArgs& A) { return transe_fast_nc(A) != 0 && A.K <= NSW * NSF_MAXJ; }
+
+extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margin, int use_model_margin,
+                                     const float* d_ent, const float* d_ent_im, const float* d_rel,
+                                     const float* d_rel_im, int64_t n_ent, int64_t n_rel, int dim, float phase_denom,
+                                     const int64_t* d_h, const int64_t* d_t, const int64_t* d_r, int64_t batch,
+                                     int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
+                                     float* d_score, float* d_loss, float* d_work, void* stream) {
+  NSArgs A;
+  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                   phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
+  if (rc) return rc;
+  if (!d_score || !d_loss || !d_work || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
+  if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
+  if (!fused_fast(A))  // other models: the plain forward; mmre_ns_fused_grad runs their backward
+    return mmre_ns_forward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                           phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
+                           d_loss, d_work, stream);
+  hipStream_t st = (hipStream_t)stream;
+  FusedWs w;
+  fused_ws(batch, neg, n_ent, n_rel, dim, w);
+  float* part = d_work + w.part;
+  float* nrm_e = d_work + w.nrm_e;
+  float* nrm_r = d_work + w.nrm_r;
+  int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
+  int32_t* cursor = reinterpret_cast<int32_t*>(d_work + w.cursor);
+  int32_t* offs = reinterpret_cast<int32_t*>(d_work + w.offs);
+  NSSlots S{d_work + w.shared, d_work + w.rec, d_work + w.mult, reinterpret_cast<uint32_t*>(d_work + w.keys), counts,
+            w.sentinel};
+  hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
+                     n_rel, dim, nrm_e, nrm_r, counts, cursor);
+  MMRE_CHECK_LAUNCH();
+  const dim3 grid((unsigned)batch), blk(256);
+  const bool l2 = model == MMRE_TRANSE_L2;
+  const int nc = transe_fast_nc(A);
+#define MMRE_NS_FUSED(NC_)                                                                                    \
+  do {                                                                                                        \
+    if (l2) hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, \
+                               S, n_ent);                                                                     \
+    else hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part,  \
+                            S, n_ent);                                                                        \
+  } while (0)
+  if (nc == 1) MMRE_NS_FUSED(1);
+  else if (nc == 2) MMRE_NS_FUSED(2);
+  else if (nc == 4) MMRE_NS_FUSED(4);
+  else MMRE_NS_FUSED(8);
+#undef MMRE_NS_FUSED
+  MMRE_CHECK_LAUNCH();
+  // the loss, and the slot buckets per table row: offsets, then every slot id into its bucket
+  hipLaunchKernelGGL(k_ns_scan_reduce, dim3(1), dim3(1024), 0, st, A, part, d_loss, counts, n_ent + n_rel, offs);
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_ns_place, dim3((unsigned)((w.slots + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t*>(S.keys), w.slots, w.sentinel, offs, cursor,
+                     reinterpret_cast<int32_t*>(d_work + w.sslot));
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_ns_fused_grad(int model, int norm_flag, float model_margin, int use_model_margin,
+                                  const float* d_ent, const float* d_ent_im, const float* d_rel, const float* d_rel_im,
+                                  int64_t n_ent, int64_t n_rel, int dim, float phase_denom, const int64_t* d_h,
+                                  const int64_t* d_t, const int64_t* d_r, int64_t batch, int64_t neg,
+                                  float loss_margin, float adv_temperature, float regul_rate, const float* d_score,
+                                  const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im, float* d_grad_rel,
+                                  float* d_grad_rel_im, float* d_work, void* stream) {
+  NSArgs A;
+  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                   phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
+  if (rc) return rc;
+  if (!d_score || !d_work || !d_grad_ent || !d_grad_rel || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
+  if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
+  if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  if (!fused_fast(A)) {  // other models: zeroed tables, then the atomic backward
+    const int64_t ew = model == MMRE_ROTATE ? 2 * (int64_t)dim : dim;
+    MMRE_CHECK(hipMemsetAsync(d_grad_ent, 0, (size_t)(n_ent * ew) * sizeof(float), st));
+    MMRE_CHECK(hipMemsetAsync(d_grad_rel, 0, (size_t)(n_rel * dim) * sizeof(float), st));
+    if (model == MMRE_COMPLEX) {
+      MMRE_CHECK(hipMemsetAsync(d_grad_ent_im, 0, (size_t)(n_ent * dim) * sizeof(float), st));
+      MMRE_CHECK(hipMemsetAsync(d_grad_rel_im, 0, (size_t)(n_rel * dim) * sizeof(float), st));
+    }
+    return mmre_ns_backward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                            phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
+                            d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, stream);
+  }
+  FusedWs w;
+  fused_ws(batch, neg, n_ent, n_rel, dim, w);
+  const double N = (double)batch * (1.0 + (double)neg);
+  const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
+  const dim3 grid((unsigned)((n_ent + n_rel + 3) / 4)), blk(256);
+#define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
+  hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), grid, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
+                     d_work + w.nrm_e, d_work + w.nrm_r, d_work + w.shared, d_work + w.rec, d_work + w.mult,          \
+                     reinterpret_cast<const int32_t*>(d_work + w.offs),                                               \
+                     reinterpret_cast<const int32_t*>(d_work + w.sslot), neg, d_grad_loss, d_grad_ent, d_grad_rel)
+  const int nc = transe_fast_nc(A);
+  const bool l2 = model == MMRE_TRANSE_L2;
+  if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }
+  else if (nc == 2) { if (l2) MMRE_NS_OWNER(2, true); else MMRE_NS_OWNER(2, false); }
+  else if (nc == 4) { if (l2) MMRE_NS_OWNER(4, true); else MMRE_NS_OWNER(4, false); }
+  else { if (l2) MMRE_NS_OWNER(8, true); else MMRE_NS_OWNER(8, false); }
+#undef MMRE_NS_OWNER
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
 }
 
 extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int use_model_margin,
@@ -1102,54 +1523,12 @@ extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_ma
                                         float regul_rate, float* d_score, float* d_loss, float* d_grad_ent,
                                         float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work,
                                         void* stream) {
-  NSArgs A;
-  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
-                   phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
+  int rc = mmre_ns_fused_forward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im,
+                                 n_ent, n_rel, dim, phase_denom, d_h, d_t, d_r, batch, neg, loss_margin,
+                                 adv_temperature, regul_rate, d_score, d_loss, d_work, stream);
   if (rc) return rc;
-  if (!d_score || !d_loss || !d_work || !d_grad_ent || !d_grad_rel || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
-  if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
-  if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
-  hipStream_t st = (hipStream_t)stream;
-  const int nc = transe_fast_nc(A);
-  if (nc == 0 || neg > NSW * NSF_MAXJ) {  // generic: forward, then the backward with upstream gradient 1
-    const int64_t ew = model == MMRE_ROTATE ? 2 * (int64_t)dim : dim;
-    MMRE_CHECK(hipMemsetAsync(d_grad_ent, 0, (size_t)(n_ent * ew) * sizeof(float), st));
-    MMRE_CHECK(hipMemsetAsync(d_grad_rel, 0, (size_t)(n_rel * dim) * sizeof(float), st));
-    if (model == MMRE_COMPLEX) {
-      MMRE_CHECK(hipMemsetAsync(d_grad_ent_im, 0, (size_t)(n_ent * dim) * sizeof(float), st));
-      MMRE_CHECK(hipMemsetAsync(d_grad_rel_im, 0, (size_t)(n_rel * dim) * sizeof(float), st));
-    }
-    rc = mmre_ns_forward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
-                         phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
-                         d_loss, d_work, stream);
-    if (rc) return rc;
-    return mmre_ns_backward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
-                            phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
-                            nullptr, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, stream);
-  }
-  float* part = d_work;
-  float* nrm_e = d_work + 7 * batch;
-  float* nrm_r = nrm_e + n_ent;
-  // the pre-pass (norms, gradient rows zeroed), the fused kernel, the fixed-order loss reduction
-  hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
-                     n_rel, dim, nrm_e, nrm_r, d_grad_ent, d_grad_rel);
-  MMRE_CHECK_LAUNCH();
-  const dim3 grid((unsigned)batch), blk(256);
-  const bool l2 = model == MMRE_TRANSE_L2;
-#define MMRE_NS_FUSED(NC_)                                                                                    \
-  do {                                                                                                        \
-    if (l2) hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, \
-                               d_grad_ent, d_grad_rel);                                                       \
-    else hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part,  \
-                            d_grad_ent, d_grad_rel);                                                          \
-  } while (0)
-  if (nc == 1) MMRE_NS_FUSED(1);
-  else if (nc == 2) MMRE_NS_FUSED(2);
-  else if (nc == 4) MMRE_NS_FUSED(4);
-  else MMRE_NS_FUSED(8);
-#undef MMRE_NS_FUSED
-  MMRE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_ns_reduce, dim3(1), dim3(256), 0, st, A, part, d_loss);
-  MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  return mmre_ns_fused_grad(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, n_ent,
+                            n_rel, dim, phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature,
+                            regul_rate, d_score, nullptr, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work,
+                            stream);
 }

@@ -44,7 +44,11 @@ SIGNATURES = {
                               P]),
     "mmre_ns_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
                                P, P, P, P, P]),
-    "mmre_ns_fused_workspace": (I64, [I64, I64, I64, I64]),
+    "mmre_ns_fused_workspace": (I64, [I64, I64, I64, I64, I32]),
+    "mmre_ns_fused_forward": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
+                                    F32, P, P, P, P]),
+    "mmre_ns_fused_grad": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32, F32,
+                                 P, P, P, P, P, P, P, P]),
     "mmre_ns_forward_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
                                        F32, P, P, P, P, P, P, P, P]),
     "mmre_score_rows_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, P, P, P, P, P, P]),

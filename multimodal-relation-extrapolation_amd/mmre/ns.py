@@ -4,8 +4,9 @@ forward  = model(data) in 'normal' mode for B*(1+k) rows -> MarginLoss (optional
            self-adversarial) + regul_rate * regularization, one launch + one fixed-order
            reduction (OpenKE strategy/NegativeSampling.py:23-32, MarginLoss.py:24-28,
            TransE.py:92-102; repo module/NegativeSampling.py:204-229).
-backward = d(loss)/d(embedding tables) scattered into dense gradient tables (float atomics;
-           all-zero row gradients, e.g. inactive hinges without regularization, issue none).
+backward = d(loss)/d(embedding tables) into dense gradient tables: for TransE one wave per table
+           row sums the row's contributions in batch order (no float atomics, bit-reproducible);
+           other models scatter with float atomics.
 """
 from __future__ import annotations
 
@@ -35,10 +36,11 @@ def _scalar_args(spec, batch, neg, loss_margin, adv_t, regul_rate):
 
 
 class _FusedNS(torch.autograd.Function):
-    """Training (the tables need gradients): ONE mmre_ns_forward_backward call in the forward
-    emits the loss, the scores and the gradient tables for an upstream gradient of 1 (fused
-    launch for TransE); the backward scales them by the actual upstream gradient. Otherwise
-    mmre_ns_forward, with mmre_ns_backward as the backward."""
+    """Training (the tables need gradients): mmre_ns_fused_forward in the forward (loss,
+    scores, and the gradient's slot contributions kept in the workspace), mmre_ns_fused_grad
+    in the backward (every row of the gradient tables written, scaled by the upstream
+    gradient; for TransE a row-owner pass with no float atomics). Otherwise mmre_ns_forward,
+    with mmre_ns_backward as the backward."""
 
     @staticmethod
     def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate, events):
@@ -47,49 +49,57 @@ class _FusedNS(torch.autograd.Function):
         score = torch.empty(N, dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(score)
-        ctx.unit = None
-        if any(ctx.needs_input_grad[:4]):
-            E, R = int(ent.shape[0]), int(rel.shape[0])
-            work = torch.empty(int(lib().mmre_ns_fused_workspace(batch, neg, E, R)), dtype=torch.float32, device=dev)
-            ge, gr = torch.empty_like(ent), torch.empty_like(rel)  # written (zeroed) by the call
-            gei = torch.empty_like(ent_im) if ent_im is not None else None
-            gri = torch.empty_like(rel_im) if rel_im is not None else None
-            if events is not None:
-                events[0].record()
-            call("mmre_ns_forward_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
-                 int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), E, R, spec.dim,
-                 spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg, float(loss_margin), float(adv_t),
-                 float(regul_rate), ptr(score), ptr(loss), ptr(ge), ptr(gei), ptr(gr), ptr(gri), ptr(work),
-                 stream_ptr(dev))
-            if events is not None:
-                events[1].record()
-            ctx.unit = (ge, gr, gei, gri)
-            return loss[0], score
-        work = torch.empty(int(lib().mmre_ns_workspace(batch, neg)), dtype=torch.float32, device=dev)
-        call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
-             ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
-             batch, neg, float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(loss), ptr(work),
-             stream_ptr(dev))
-        ctx.save_for_backward(ent, rel, ent_im if ent_im is not None else ent, rel_im if rel_im is not None else rel,
-                              h, t, r, score)
+        ctx.fused = any(ctx.needs_input_grad[:4])
         ctx.has_im = ent_im is not None
         ctx.cfg = (spec, batch, neg, loss_margin, adv_t, regul_rate)
-        ctx.mark_non_differentiable(score)
+        if ctx.fused:
+            E, R = int(ent.shape[0]), int(rel.shape[0])
+            work = torch.empty(int(lib().mmre_ns_fused_workspace(batch, neg, E, R, spec.dim)), dtype=torch.float32,
+                               device=dev)
+            if events is not None:
+                events[0].record()
+            call("mmre_ns_fused_forward", spec.model_id, int(spec.norm_flag), spec.model_margin,
+                 int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), E, R, spec.dim,
+                 spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg, float(loss_margin), float(adv_t),
+                 float(regul_rate), ptr(score), ptr(loss), ptr(work), stream_ptr(dev))
+            if events is not None:
+                events[1].record()
+            ctx.work = work
+            ctx.events = events
+        else:
+            work = torch.empty(int(lib().mmre_ns_workspace(batch, neg)), dtype=torch.float32, device=dev)
+            call("mmre_ns_forward", spec.model_id, int(spec.norm_flag), spec.model_margin,
+                 int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim,
+                 spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg, float(loss_margin), float(adv_t),
+                 float(regul_rate), ptr(score), ptr(loss), ptr(work), stream_ptr(dev))
+        ctx.save_for_backward(ent, rel, ent_im if ent_im is not None else ent, rel_im if rel_im is not None else rel,
+                              h, t, r, score)
         return loss[0], score
 
     @staticmethod
     def backward(ctx, g_loss, g_score):
-        if ctx.unit is not None:  # gradients for upstream 1 were computed in the forward
-            gl = g_loss.reshape(()).to(torch.float32)
-            out = [None if x is None else x.mul_(gl) for x in ctx.unit]
-            ctx.unit = None
-            return (*out, None, None, None, None, None, None, None, None, None, None)
         ent, rel, ent_im, rel_im, h, t, r, score = ctx.saved_tensors
         spec, batch, neg, loss_margin, adv_t, regul_rate = ctx.cfg
         if not ctx.has_im:
             ent_im = rel_im = None
         dev = ent.device
         gl = g_loss.reshape(1).to(torch.float32).contiguous()
+        if ctx.fused:  # every row written by the call: no fills
+            ge, gr = torch.empty_like(ent), torch.empty_like(rel)
+            gei = torch.empty_like(ent_im) if ent_im is not None else None
+            gri = torch.empty_like(rel_im) if rel_im is not None else None
+            ev = ctx.events
+            if ev is not None and len(ev) > 2:
+                ev[2].record()
+            call("mmre_ns_fused_grad", spec.model_id, int(spec.norm_flag), spec.model_margin,
+                 int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), int(ent.shape[0]),
+                 int(rel.shape[0]), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg,
+                 float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei),
+                 ptr(gr), ptr(gri), ptr(ctx.work), stream_ptr(dev))
+            if ev is not None and len(ev) > 2:
+                ev[3].record()
+            ctx.work = ctx.events = None
+            return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None
         ge = torch.zeros_like(ent)
         gr = torch.zeros_like(rel)
         gei = torch.zeros_like(ent_im) if ent_im is not None else None
@@ -105,8 +115,9 @@ def fused_ns_loss(spec: NSSpec, ent, rel, h, t, r, batch: int, neg: int, loss_ma
                   adv_temperature: float | None = None, regul_rate: float = 0.0, ent_im=None, rel_im=None,
                   events=None):
     """Returns (loss scalar tensor, scores (B*(1+k),)). Differentiable w.r.t. the tables.
-    events: optional (start, end) torch.cuda.Event pair recorded around the fused
-    forward + gradient call alone (training mode), for kernel timing."""
+    events: optional torch.cuda.Events recorded around the C-ABI calls alone (training mode), for
+    kernel timing: (start, end) of mmre_ns_fused_forward, and with four, (start, end) of the
+    backward's mmre_ns_fused_grad."""
     require_cuda(ent, rel, h, t, r, ent_im, rel_im)
     h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
     if ent.dtype != torch.float32 or rel.dtype != torch.float32:

@@ -74,3 +74,60 @@ def test_fused_ns_at_c2_shape_matches_reference(c2_training, neg, margin, adv, r
     touched[h.numpy()] = True
     touched[t.numpy()] = True
     assert not ent.grad.cpu().numpy()[~touched].any()
+
+
+def _c2_batch(c2_training, neg, skip=1):
+    from mmre.sampler import OpenKESampler
+    w, idx = c2_training
+    smp = OpenKESampler(idx, DEV, bern=True)
+    for _ in range(skip):
+        smp.sample(2721, neg)
+    return smp.sample(2721, neg)
+
+
+@pytest.mark.parametrize("regul", [0.0, 0.5])
+def test_fused_ns_gradients_are_bit_reproducible(c2_training, regul):
+    """The TransE gradient has no float atomics (slots sorted by table row, one wave per row
+    summing them in batch order): the same batch gives bit-identical gradient tables, run to
+    run, and an upstream gradient G scales them exactly (the row-owner pass multiplies once)."""
+    from mmre.ns import NSSpec, fused_ns_loss
+    w, _ = c2_training
+    b = _c2_batch(c2_training, 25)
+    spec = NSSpec("transe", 200, norm_flag=True)
+    grads = []
+    for scale in (1.0, 1.0, 2.5):
+        ent = w["ent"].to(DEV).requires_grad_(True)
+        rel = w["rel"].to(DEV).requires_grad_(True)
+        loss, _ = fused_ns_loss(spec, ent, rel, b["batch_h"], b["batch_t"], b["batch_r"], 2721, 25, 5.0, None, regul)
+        (loss * scale).backward()
+        grads.append((ent.grad.clone(), rel.grad.clone()))
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    assert torch.equal(grads[2][0], grads[0][0] * 2.5) and torch.equal(grads[2][1], grads[0][1] * 2.5)
+
+
+def test_one_shot_abi_equals_autograd_pair(c2_training):
+    """mmre_ns_forward_backward (forward + gradient, upstream 1, tables written without a fill)
+    gives the autograd pair's loss, scores and gradients bit for bit."""
+    from mmre._lib import call, lib, ptr, stream_ptr
+    from mmre.ns import NSSpec, fused_ns_loss
+    w, _ = c2_training
+    b = _c2_batch(c2_training, 10, skip=2)
+    B, k, d = 2721, 10, 200
+    E, R = int(w["n_ent"]), int(w["n_rel"])
+    ent = w["ent"].to(DEV).requires_grad_(True)
+    rel = w["rel"].to(DEV).requires_grad_(True)
+    loss, score = fused_ns_loss(NSSpec("transe", d, norm_flag=True), ent, rel, b["batch_h"], b["batch_t"],
+                                b["batch_r"], B, k, 3.0, None, 0.5)
+    loss.backward()
+    e0, r0 = ent.detach(), rel.detach()
+    work = torch.empty(int(lib().mmre_ns_fused_workspace(B, k, E, R, d)), dtype=torch.float32, device=DEV)
+    s1 = torch.empty(B * (1 + k), dtype=torch.float32, device=DEV)
+    l1 = torch.empty(1, dtype=torch.float32, device=DEV)
+    ge = torch.full_like(e0, float("nan"))  # poisoned: every row must be written
+    gr = torch.full_like(r0, float("nan"))
+    call("mmre_ns_forward_backward", 0, 1, 0.0, 0, ptr(e0), None, ptr(r0), None, E, R, d, 0.0, ptr(b["batch_h"]),
+         ptr(b["batch_t"]), ptr(b["batch_r"]), B, k, 3.0, 0.0, 0.5, ptr(s1), ptr(l1), ptr(ge), None, ptr(gr), None,
+         ptr(work), stream_ptr(DEV))
+    torch.cuda.synchronize()
+    assert torch.equal(l1[0], loss.detach()) and torch.equal(s1, score)
+    assert torch.equal(ge, ent.grad) and torch.equal(gr, rel.grad)
