@@ -503,7 +503,7 @@ def bench_ns(args, world, rank, dev, dist):
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": None,
                             "kernel": "mmre_ns_fused_forward (k_ns_prepass + k_ns_transe_fused<4, false> + "
-                                      "k_ns_scan_reduce (loss + bucket offsets) + k_ns_place) + mmre_ns_fused_grad "
+                                      "k_ns_scan (bucket offsets) + k_ns_place (+ the loss)) + mmre_ns_fused_grad "
                                       "(k_ns_row_owner<4, false>): events around the two C-ABI calls",
                             "kernel_ms": fused_ms, "fused_forward_ms": fused_fwd_ms, "fused_grad_ms": fused_grad_ms,
                             "algorithmic_bytes": fwd_bytes + grad_bytes, "slot_bytes": slot_bytes,

@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const floa
 // three rows is summed in registers across the negatives; per negative one row is left, the
 // corrupted one.
 // No float atomics anywhere: k_ns_transe_fused writes every contribution to a SLOT (its
-// values + the table row it belongs to) and counts the slots per table row; k_ns_scan_reduce turns
+// values + the table row it belongs to) and counts the slots per table row; k_ns_scan turns
 // the counts into bucket offsets and k_ns_place drops each slot id into its row's bucket
 // (integer atomics: the bucket's CONTENT is fixed, its order is not); k_ns_row_owner -- one
 // wave per table row -- takes its bucket's slots in increasing slot id (batch order, the same
@@ -1051,17 +1051,14 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   }
 }
 
-// One 1,024-thread workgroup after the fused kernel: the fixed-order loss reduction
-// (ns_reduce_block, the arithmetic of k_ns_reduce, on the first 256 threads) and the exclusive
-// scan of the per-row slot counts into bucket offsets (offs[n] = all slots), over coalesced
-// 4,096-count tiles: four counts per thread, wave scans by shuffles, the 16 wave totals in LDS.
-__global__ __launch_bounds__(1024) void k_ns_scan_reduce(NSArgs A, const float* __restrict__ part,
-                                                         float* __restrict__ loss, const int32_t* __restrict__ counts,
-                                                         int64_t n, int32_t* __restrict__ offs) {
+// Exclusive scan of the per-row slot counts into bucket offsets (offs[n] = all slots), one
+// 1,024-thread workgroup over coalesced 4,096-count tiles: four counts per thread, wave scans
+// by shuffles, the 16 wave totals in LDS.
+__global__ __launch_bounds__(1024) void k_ns_scan(const int32_t* __restrict__ counts, int64_t n,
+                                                  int32_t* __restrict__ offs) {
   __shared__ int32_t s_w[16];
   __shared__ int32_t s_carry;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  ns_reduce_block(A, part, loss);
   if (t == 0) s_carry = 0;
   __syncthreads();
   for (int64_t base = 0; base < n; base += 4096) {
@@ -1094,10 +1091,13 @@ __global__ __launch_bounds__(1024) void k_ns_scan_reduce(NSArgs A, const float* 
 }
 
 // Each slot's id into its row's bucket (position within the bucket by arrival: the owner
-// restores the batch order).
-__global__ __launch_bounds__(256) void k_ns_place(const uint32_t* __restrict__ keys, int64_t n_slots,
+// restores the batch order); workgroup 0 also reduces the loss (ns_reduce_block, the fixed
+// order and arithmetic of k_ns_reduce).
+__global__ __launch_bounds__(256) void k_ns_place(NSArgs A, const float* __restrict__ part, float* __restrict__ loss,
+                                                  const uint32_t* __restrict__ keys, int64_t n_slots,
                                                   uint32_t sentinel, const int32_t* __restrict__ offs,
                                                   int32_t* __restrict__ cursor, int32_t* __restrict__ sslot) {
+  if (blockIdx.x == 0) ns_reduce_block(A, part, loss);  // uniform per workgroup
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_slots) return;
   const uint32_t k = keys[i];
@@ -1138,6 +1138,10 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
   const int64_t id = is_ent ? row : row - n_ent;
   float* o = (is_ent ? gent : grel) + id * d;
   const int64_t i0 = offs[row], i1 = offs[row + 1];
+  // the row itself and its norm, in flight while the bucket is ordered and summed
+  Vec<NC> v;
+  vload(v, (is_ent ? ent : rel) + id * d, d, lane);
+  const float nv = (is_ent ? nrm_e : nrm_r)[id];
   if (i0 == i1) {  // not in the batch: zero gradient
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -1217,12 +1221,9 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
       for (int c = 0; c < NC; ++c) dy.v[c] += g0 * v0.v[c];
     }
   }
-  Vec<NC> v;
-  vload(v, (is_ent ? ent : rel) + id * d, d, lane);
   const float G = grad_loss ? grad_loss[0] : 1.0f;
   const float rr = reg * cnt;
   if (norm_flag) {
-    const float nv = (is_ent ? nrm_e : nrm_r)[id];
     const float cv = fmaxf(nv, 1e-12f);
     float dot = 0.0f;
 #pragma unroll
@@ -1457,10 +1458,10 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   else MMRE_NS_FUSED(8);
 #undef MMRE_NS_FUSED
   MMRE_CHECK_LAUNCH();
-  // the loss, and the slot buckets per table row: offsets, then every slot id into its bucket
-  hipLaunchKernelGGL(k_ns_scan_reduce, dim3(1), dim3(1024), 0, st, A, part, d_loss, counts, n_ent + n_rel, offs);
+  // the slot buckets per table row: offsets, then every slot id into its bucket (+ the loss)
+  hipLaunchKernelGGL(k_ns_scan, dim3(1), dim3(1024), 0, st, counts, n_ent + n_rel, offs);
   MMRE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_ns_place, dim3((unsigned)((w.slots + 255) / 256)), dim3(256), 0, st,
+  hipLaunchKernelGGL(k_ns_place, dim3((unsigned)((w.slots + 255) / 256)), dim3(256), 0, st, A, part, d_loss,
                      reinterpret_cast<const uint32_t*>(S.keys), w.slots, w.sentinel, offs, cursor,
                      reinterpret_cast<int32_t*>(d_work + w.sslot));
   MMRE_CHECK_LAUNCH();
