@@ -797,9 +797,11 @@ __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ en
   if (lane == 0) (is_ent ? nrm_e : nrm_r)[is_ent ? row : row - n_ent] = sqrtf(s);
 }
 
-__device__ __forceinline__ int64_t readlane64(int64_t v, int src) {
-  const int lo = __shfl((int)(uint32_t)(uint64_t)v, src), hi = __shfl((int)((uint64_t)v >> 32), src);
-  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+// lane src's 64-bit value as a wave-uniform (scalar) value; src must be wave-uniform
+__device__ __forceinline__ int64_t readlane64u(int64_t v, int src) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, src);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), src);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 template <int NC>
@@ -862,7 +864,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     code[u] = 3;
     cnr[u] = 0.0f;
     if (u < nj) {
-      const int64_t h = readlane64(my_h, u), t = readlane64(my_t, u), r = readlane64(my_r, u);
+      const int64_t h = readlane64u(my_h, u), t = readlane64u(my_t, u), r = readlane64u(my_r, u);
       const bool oh = h == ph, ot = t == pt, orr = r == pr;
       if (orr && ot && !oh) { code[u] = 0; vload(C[u], A.ent + h * d, d, lane); cnr[u] = nrm_e[h]; }
       else if (orr && oh && !ot) { code[u] = 1; vload(C[u], A.ent + t * d, d, lane); cnr[u] = nrm_e[t]; }
@@ -872,18 +874,23 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   }
   const float ch = nf ? fmaxf(nph, 1e-12f) : 1.0f, cr = nf ? fmaxf(npr, 1e-12f) : 1.0f;
   const float ct = nf ? fmaxf(npt, 1e-12f) : 1.0f;
-  Vec<NC> hn, rn, tn, x, cn;
+  Vec<NC> hn, rn, tn, x;
   vnorm(hn, Ph, ch); vnorm(rn, Pr, cr); vnorm(tn, Pt, ct);
   float p_raw = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
   if (L2) p_raw = sqrtf(p_raw);
   const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
-  RowCtx<NC> P;  // for the generic-row helpers
-  P.h = Ph; P.r = Pr; P.t = Pt; P.sh = nph * nph; P.sr = npr * npr; P.st = npt * npt;
-  P.own_h = P.own_r = P.own_t = true;
+  const float psh = nph * nph, psr = npr * npr, pst = npt * npt;
+  // the positive's raw rows for the generic-row helpers (a negative sharing fewer than two
+  // rows: not an OpenKE batch), re-read there so that they hold no registers on the fast path
+  auto pos_ctx = [&](RowCtx<NC>& P) {
+    vload(P.h, A.ent + ph * d, d, lane); vload(P.r, A.rel + pr * d, d, lane); vload(P.t, A.ent + pt * d, d, lane);
+    P.sh = psh; P.sr = psr; P.st = pst;
+    P.own_h = P.own_r = P.own_t = true;
+  };
   float qh = 0.f, qt = 0.f, qr = 0.f;
   if (w == 0) {
     if (lane == 0) score[b] = p;
-    qh = P.sh; qt = P.st; qr = P.sr;
+    qh = psh; qt = pst; qr = psr;
   }
   float sraw[NSF_MAXJ];
 #pragma unroll
@@ -893,22 +900,23 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
     float n;
     if (code[u] == 4) {
-      RowCtx<NC> R;
+      RowCtx<NC> P, R;
+      pos_ctx(P);
       row_ctx_load(R, A, row, ph, pr, pt, P, lane);
       row_ctx_norms(R, P);
       n = row_fwd<NC, L2>(A, R, lane);
       qh += R.sh; qt += R.st; qr += R.sr;
     } else {
       const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
-      if (code[u] != 3) vnorm(cn, C[u], cc);
-      float sv = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]));
+      if (code[u] != 3) vnorm(C[u], C[u], cc);  // normalised in place: the gradient pass reuses it
+      float sv = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
       if (L2) sv = sqrtf(sv);
       sraw[u] = sv;
       n = A.use_model_margin ? A.model_margin - sv : sv;
       const float sq = cnr[u] * cnr[u];
-      qh += code[u] == 0 ? sq : P.sh;
-      qt += code[u] == 1 ? sq : P.st;
-      qr += code[u] == 2 ? sq : P.sr;
+      qh += code[u] == 0 ? sq : psh;
+      qt += code[u] == 1 ? sq : pst;
+      qr += code[u] == 2 ? sq : psr;
     }
     if (lane == 0) { score[row] = n; s_n[j] = n; }
   }
@@ -980,7 +988,8 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     const float g = -sgn * s_c[j];
     uint32_t kq0 = S.sentinel, kq1 = S.sentinel, kq2 = S.sentinel;  // this negative's h / r / t slots
     if (code[u] == 4) {  // shares fewer than two rows: every row it does not share gets a slot
-      RowCtx<NC> R;
+      RowCtx<NC> P, R;
+      pos_ctx(P);
       row_ctx_load(R, A, row, ph, pr, pt, P, lane);
       row_ctx_norms(R, P);
       if (g == 0.0f && reg == 0.0f) {
@@ -999,15 +1008,13 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
       orr += code[u] != 2 ? 1.0f : 0.0f;
       ot += code[u] != 1 ? 1.0f : 0.0f;
     } else {
-      const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
-      if (code[u] != 3) vnorm(cn, C[u], cc);
-      fused_x<NC, L2>(x, hn, rn, tn, cn, code[u]);
+      fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]);  // C[u] normalised by the forward
       const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
 #pragma unroll
       for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
-      if (code[u] != 0) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)readlane64(my_h, u);
-      if (code[u] != 2) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + readlane64(my_r, u));
-      if (code[u] != 1) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)readlane64(my_t, u);
+      if (code[u] != 0) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)readlane64u(my_h, u);
+      if (code[u] != 2) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + readlane64u(my_r, u));
+      if (code[u] != 1) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)readlane64u(my_t, u);
       if (code[u] != 3) store_rec<NC, L2>(S.rec, b * A.K + j, gx, L2 ? 0.0f : gs, d, lane);
     }
     if (lane < 3) {
@@ -1111,11 +1118,6 @@ __device__ __forceinline__ int wave_min_i32(int v) {
   return v;
 }
 
-__device__ __forceinline__ int64_t readlane64u(int64_t v, int src) {  // src wave-uniform
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, src);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), src);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
 
 // One wave per table row (entities, then relations): the row's slots (a contiguous run of
 // the sorted keys) summed in batch order, d(loss)/d(raw row) = (dy - y (y . dy)) / |v| with
