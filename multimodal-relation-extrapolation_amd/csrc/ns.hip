@@ -784,7 +784,9 @@ __device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ 
 __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
                                                     const float* __restrict__ rel, int64_t n_rel, int d,
                                                     float* __restrict__ nrm_e, float* __restrict__ nrm_r,
-                                                    int32_t* __restrict__ counts, int32_t* __restrict__ cursor) {
+                                                    int32_t* __restrict__ counts, int32_t* __restrict__ cursor,
+                                                    int32_t* __restrict__ defer) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) defer[0] = 0;  // no deferred positives yet
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;
@@ -828,10 +830,59 @@ __device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Ve
   return acc;
 }
 
-template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
-                                                         const float* __restrict__ nrm_r, float* __restrict__ score,
-                                                         float* __restrict__ part, NSSlots S, int64_t n_ent) {
+// Row `row` (wave-uniform) of a [*, d] table through a buffer resource sized to the row: the
+// padding lanes (element >= d) read 0 and their stores are dropped by the hardware range check,
+// so the fast path has no per-element bounds branches.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* table, int64_t row, int d) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(table + row * d), (short)0, d * 4, 0x00020000);
+}
+
+template <int NC>
+__device__ __forceinline__ void vload_row(Vec<NC>& o, const float* table, int64_t row, int d, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(table, row, d);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) o.v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (lane + c * kWave) * 4, 0, 0));
+}
+
+template <int NC>
+__device__ __forceinline__ void vstore_row(float* table, int64_t row, const Vec<NC>& v, int d, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(table, row, d);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.v[c]), rs, (lane + c * kWave) * 4, 0, 0);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the wave as a wave-uniform value, without LDS: DPP butterflies inside each row of 16
+// lanes (quad xor 1, quad xor 2, half-row mirror, row mirror: every lane ends with its row's
+// sum; IEEE addition is commutative, so mirrored pairs agree bit for bit), then the four row
+// sums in a fixed order. All 64 lanes must be active.
+__device__ __forceinline__ float wave_sum_u(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+// One positive's workgroup. GEN = false (k_ns_transe_fused, every positive): the OpenKE batch
+// shape, each negative sharing two of the positive's rows; a positive with any other negative
+// is appended to the `defer` list untouched, before anything is written. GEN = true
+// (k_ns_transe_fused_generic, the deferred positives only): also the generic-row path. The
+// split keeps the generic path's registers out of the fast instance (122 -> ~90 VGPRs).
+template <int NC, bool L2, bool GEN>
+__device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __restrict__ nrm_e,
+                                              const float* __restrict__ nrm_r, float* __restrict__ score,
+                                              float* __restrict__ part, const NSSlots& S, int64_t n_ent, int64_t b,
+                                              int32_t* __restrict__ defer) {
+  __shared__ int s_gen[NSW];
   __shared__ float s_n[NSW * NSF_MAXJ];
   __shared__ float s_c[NSW * NSF_MAXJ];
   __shared__ float s_gp;
@@ -839,7 +890,6 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   __shared__ float s_acc[NSW - 1][3][NC * kWave];
   __shared__ float s_occ[NSW][3];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t b = blockIdx.x;
   const int d = A.dim;
   const int nf = A.norm_flag;
   const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
@@ -851,9 +901,9 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     my_h = A.h[row]; my_t = A.t[row]; my_r = A.r[row];
   }
   Vec<NC> Ph, Pr, Pt;
-  vload(Ph, A.ent + ph * d, d, lane);
-  vload(Pr, A.rel + pr * d, d, lane);
-  vload(Pt, A.ent + pt * d, d, lane);
+  vload_row(Ph, A.ent, ph, d, lane);
+  vload_row(Pr, A.rel, pr, d, lane);
+  vload_row(Pt, A.ent, pt, d, lane);
   const float nph = nrm_e[ph], npr = nrm_r[pr], npt = nrm_e[pt];
   // issue every corrupted-row load of the wave before any arithmetic
   Vec<NC> C[NSF_MAXJ];
@@ -866,17 +916,31 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     if (u < nj) {
       const int64_t h = readlane64u(my_h, u), t = readlane64u(my_t, u), r = readlane64u(my_r, u);
       const bool oh = h == ph, ot = t == pt, orr = r == pr;
-      if (orr && ot && !oh) { code[u] = 0; vload(C[u], A.ent + h * d, d, lane); cnr[u] = nrm_e[h]; }
-      else if (orr && oh && !ot) { code[u] = 1; vload(C[u], A.ent + t * d, d, lane); cnr[u] = nrm_e[t]; }
-      else if (oh && ot && !orr) { code[u] = 2; vload(C[u], A.rel + r * d, d, lane); cnr[u] = nrm_r[r]; }
+      if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], A.ent, h, d, lane); cnr[u] = nrm_e[h]; }
+      else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], A.ent, t, d, lane); cnr[u] = nrm_e[t]; }
+      else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], A.rel, r, d, lane); cnr[u] = nrm_r[r]; }
       else if (!(oh && ot && orr)) code[u] = 4;  // shares less than two rows: generic path
+    }
+  }
+  if constexpr (!GEN) {  // any generic row in this positive: defer it whole to the generic instance
+    bool gen = false;
+#pragma unroll
+    for (int u = 0; u < NSF_MAXJ; ++u) gen |= code[u] == 4;
+    if (lane == 0) s_gen[w] = gen;
+    __syncthreads();
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NSW; ++i) any |= s_gen[i] != 0;
+    if (any) {
+      if (threadIdx.x == 0) defer[1 + atomicAdd(defer, 1)] = (int32_t)b;
+      return;
     }
   }
   const float ch = nf ? fmaxf(nph, 1e-12f) : 1.0f, cr = nf ? fmaxf(npr, 1e-12f) : 1.0f;
   const float ct = nf ? fmaxf(npt, 1e-12f) : 1.0f;
   Vec<NC> hn, rn, tn, x;
   vnorm(hn, Ph, ch); vnorm(rn, Pr, cr); vnorm(tn, Pt, ct);
-  float p_raw = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
+  float p_raw = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
   if (L2) p_raw = sqrtf(p_raw);
   const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
   const float psh = nph * nph, psr = npr * npr, pst = npt * npt;
@@ -899,7 +963,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     if (u >= nj) continue;
     const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
     float n;
-    if (code[u] == 4) {
+    if (GEN && code[u] == 4) {
       RowCtx<NC> P, R;
       pos_ctx(P);
       row_ctx_load(R, A, row, ph, pr, pt, P, lane);
@@ -909,7 +973,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     } else {
       const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
       if (code[u] != 3) vnorm(C[u], C[u], cc);  // normalised in place: the gradient pass reuses it
-      float sv = wave_sum(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
+      float sv = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
       if (L2) sv = sqrtf(sv);
       sraw[u] = sv;
       n = A.use_model_margin ? A.model_margin - sv : sv;
@@ -973,7 +1037,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   if (w == 0) {
     const float g = sgn * s_gp;
     p_raw = fused_x<NC, L2>(x, hn, rn, tn, hn, 3);  // x of the positive again (registers)
-    const float gs = L2 ? (p_raw > 0.0f ? g / sqrtf(wave_sum(p_raw)) : 0.0f) : g;
+    const float gs = L2 ? (p_raw > 0.0f ? g / sqrtf(wave_sum_u(p_raw)) : 0.0f) : g;
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
       const float gv = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
@@ -987,7 +1051,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
     const float g = -sgn * s_c[j];
     uint32_t kq0 = S.sentinel, kq1 = S.sentinel, kq2 = S.sentinel;  // this negative's h / r / t slots
-    if (code[u] == 4) {  // shares fewer than two rows: every row it does not share gets a slot
+    if (GEN && code[u] == 4) {  // shares fewer than two rows: every row it does not share gets a slot
       RowCtx<NC> P, R;
       pos_ctx(P);
       row_ctx_load(R, A, row, ph, pr, pt, P, lane);
@@ -1046,15 +1110,37 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
     }
     float kh = 0.f, kr = 0.f, kt = 0.f;
     for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
-    vstore(S.shared + (3 * b + 0) * d, Gh, d, lane);
-    vstore(S.shared + (3 * b + 1) * d, Gr, d, lane);
-    vstore(S.shared + (3 * b + 2) * d, Gt, d, lane);
+    vstore_row(S.shared, 3 * b + 0, Gh, d, lane);
+    vstore_row(S.shared, 3 * b + 1, Gr, d, lane);
+    vstore_row(S.shared, 3 * b + 2, Gt, d, lane);
     if (lane < 3) {
       const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
       S.keys[sb + lane] = key;
       S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
       atomicAdd(&S.counts[key], 1);
     }
+  }
+}
+
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
+                                                         const float* __restrict__ nrm_r, float* __restrict__ score,
+                                                         float* __restrict__ part, NSSlots S, int64_t n_ent,
+                                                         int32_t* __restrict__ defer) {
+  ns_fused_body<NC, L2, false>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, defer);
+}
+
+// the deferred positives (defer[0] of them, ids from defer[1]); nothing to do for OpenKE batches
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_transe_fused_generic(NSArgs A, const float* __restrict__ nrm_e,
+                                                                 const float* __restrict__ nrm_r,
+                                                                 float* __restrict__ score, float* __restrict__ part,
+                                                                 NSSlots S, int64_t n_ent,
+                                                                 const int32_t* __restrict__ defer) {
+  const int n = defer[0];
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    ns_fused_body<NC, L2, true>(A, nrm_e, nrm_r, score, part, S, n_ent, defer[1 + i], nullptr);
+    __syncthreads();  // the body's LDS is reused by the next deferred positive
   }
 }
 
@@ -1381,7 +1467,7 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
 // norms, the slot contributions / occurrences / keys, the per-row slot counts, placement
 // cursors and bucket offsets, the bucketed slot ids.
 struct FusedWs {
-  int64_t part, nrm_e, nrm_r, shared, rec, mult, keys, counts, cursor, offs, sslot, total, slots;
+  int64_t part, nrm_e, nrm_r, shared, rec, mult, keys, counts, cursor, offs, sslot, defer, total, slots;
   uint32_t sentinel;
 };
 
@@ -1402,6 +1488,7 @@ static void fused_ws(int64_t B, int64_t K, int64_t E, int64_t R, int d, FusedWs&
   w.cursor = o;  o = al64(o + E + R);
   w.offs = o;    o = al64(o + E + R + 1);
   w.sslot = o;   o = al64(o + w.slots);
+  w.defer = o;   o = al64(o + B + 1);
   w.total = o;
 }
 
@@ -1439,20 +1526,29 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
   int32_t* cursor = reinterpret_cast<int32_t*>(d_work + w.cursor);
   int32_t* offs = reinterpret_cast<int32_t*>(d_work + w.offs);
+  int32_t* defer = reinterpret_cast<int32_t*>(d_work + w.defer);
   NSSlots S{d_work + w.shared, d_work + w.rec, d_work + w.mult, reinterpret_cast<uint32_t*>(d_work + w.keys), counts,
             w.sentinel};
   hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
-                     n_rel, dim, nrm_e, nrm_r, counts, cursor);
+                     n_rel, dim, nrm_e, nrm_r, counts, cursor, defer);
   MMRE_CHECK_LAUNCH();
   const dim3 grid((unsigned)batch), blk(256);
   const bool l2 = model == MMRE_TRANSE_L2;
   const int nc = transe_fast_nc(A);
-#define MMRE_NS_FUSED(NC_)                                                                                    \
-  do {                                                                                                        \
-    if (l2) hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, \
-                               S, n_ent);                                                                     \
-    else hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part,  \
-                            S, n_ent);                                                                        \
+  const dim3 ggrid((unsigned)(batch < 128 ? batch : 128));
+#define MMRE_NS_FUSED(NC_)                                                                                       \
+  do {                                                                                                           \
+    if (l2) {                                                                                                    \
+      hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,   \
+                         n_ent, defer);                                                                          \
+      hipLaunchKernelGGL((k_ns_transe_fused_generic<NC_, true>), ggrid, blk, 0, st, A, nrm_e, nrm_r, d_score,    \
+                         part, S, n_ent, defer);                                                                 \
+    } else {                                                                                                     \
+      hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,  \
+                         n_ent, defer);                                                                          \
+      hipLaunchKernelGGL((k_ns_transe_fused_generic<NC_, false>), ggrid, blk, 0, st, A, nrm_e, nrm_r, d_score,   \
+                         part, S, n_ent, defer);                                                                 \
+    }                                                                                                            \
   } while (0)
   if (nc == 1) MMRE_NS_FUSED(1);
   else if (nc == 2) MMRE_NS_FUSED(2);

@@ -131,3 +131,56 @@ def test_one_shot_abi_equals_autograd_pair(c2_training):
     torch.cuda.synchronize()
     assert torch.equal(l1[0], loss.detach()) and torch.equal(s1, score)
     assert torch.equal(ge, ent.grad) and torch.equal(gr, rel.grad)
+
+
+@pytest.mark.parametrize("frac,p_norm,adv", [(0.05, 1, None), (0.05, 2, 1.0), (1.0, 1, None)])
+def test_fused_ns_deferred_generic_rows(c2_training, frac, p_norm, adv):
+    """Batches that are not OpenKE-shaped: negatives replaced by random (h, r, t) rows (sharing
+    fewer than two rows with their positive), by a relation corruption, or by the positive
+    itself. The fast fused instance defers every positive holding such a row to the generic
+    instance (k_ns_transe_fused_generic); frac = 1.0 defers all 2,721 of them, more than the
+    generic grid. Loss, scores and gradients vs the float64 reference op sequence; the
+    gradient tables stay bit-reproducible."""
+    import ref_trainer
+    from mmre.ns import NSSpec, fused_ns_loss
+    w, _ = c2_training
+    B, k, d = 2721, 25, 200
+    E, R = int(w["n_ent"]), int(w["n_rel"])
+    b = _c2_batch(c2_training, k)
+    h, t, r = (b[x].clone() for x in ("batch_h", "batch_t", "batch_r"))
+    g = torch.Generator().manual_seed(7)
+    pos = torch.nonzero(torch.rand(B, generator=g) < frac).flatten()
+    for i, j in enumerate(torch.randint(0, k, (len(pos),), generator=g).tolist()):
+        row = int(pos[i]) + (j + 1) * B
+        kind = i % 3
+        if kind == 0:    # random row: the generic path
+            h[row] = int(torch.randint(0, E, (1,), generator=g))
+            t[row] = int(torch.randint(0, E, (1,), generator=g))
+            r[row] = int(torch.randint(0, R, (1,), generator=g))
+        elif kind == 1:  # relation corruption (shares h and t)
+            h[row], t[row] = h[int(pos[i])], t[int(pos[i])]
+            r[row] = (r[int(pos[i])] + 1) % R
+        else:            # a copy of the positive
+            h[row], t[row], r[row] = h[int(pos[i])], t[int(pos[i])], r[int(pos[i])]
+    grads = []
+    for _ in range(2):
+        ent = w["ent"].to(DEV).requires_grad_(True)
+        rel = w["rel"].to(DEV).requires_grad_(True)
+        loss, score = fused_ns_loss(NSSpec("transe" if p_norm == 1 else "transe_l2", d, norm_flag=True), ent, rel, h, t, r, B, k,
+                                    5.0, adv, 0.0)
+        loss.backward()
+        grads.append((ent.grad.clone(), rel.grad.clone()))
+    torch.cuda.synchronize()
+    assert torch.equal(grads[0][0], grads[1][0]) and torch.equal(grads[0][1], grads[1][1])
+    hc, tc, rc = h.cpu(), t.cpu(), r.cpu()
+    e64 = w["ent"].double().requires_grad_(True)
+    r64 = w["rel"].double().requires_grad_(True)
+    ref_loss, ref_score = ref_trainer.transe_ns_loss(e64, r64, hc, tc, rc, B, 5.0, norm_flag=True, p_norm=p_norm,
+                                                     adv_temperature=adv)
+    ref_loss.backward()
+    rs = ref_score.detach().numpy()
+    assert np.abs(score.detach().cpu().numpy() - rs).max() <= 1e-4 * max(1.0, np.abs(rs).max())
+    assert abs(float(loss) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    for got, want in ((grads[0][0], e64.grad), (grads[0][1], r64.grad)):
+        gw, gg = want.numpy(), got.cpu().double().numpy()
+        assert np.linalg.norm(gg - gw) <= 1e-3 * np.linalg.norm(gw)
