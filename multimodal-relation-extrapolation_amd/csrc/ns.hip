@@ -721,6 +721,7 @@ struct NSSlots {        // the row-owner gradient's workspace
   float* rec;           // K B records of a negative's gx (ns_rec_words)
   float* mult;          // per slot: occurrences of its row in the batch (regularization)
   uint32_t* keys;       // per slot: table row
+  int32_t* pos;         // per slot: its place in the row's bucket (arrival order of the count)
   int32_t* counts;      // per table row: its slots (zeroed by the pre-pass)
   uint32_t sentinel;    // n_ent + n_rel: no slot
 };
@@ -778,19 +779,18 @@ __device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ 
 
 // Pre-pass of the fused launch, one wave per row over the entity rows then the relation
 // rows: the row's L2 norm (one scalar per row instead of a wave reduction per use), and the
-// row's slot count / placement cursor zeroed.
+// row's slot count zeroed (and the deferred-positive count).
 // (A last-workgroup loss reduction inside the fused kernel was tried instead of k_ns_reduce:
 // its per-workgroup device-scope fence writes back the XCD's L2 each time, 0.12 -> 0.19 ms.)
 __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
                                                     const float* __restrict__ rel, int64_t n_rel, int d,
                                                     float* __restrict__ nrm_e, float* __restrict__ nrm_r,
-                                                    int32_t* __restrict__ counts, int32_t* __restrict__ cursor,
-                                                    int32_t* __restrict__ defer) {
+                                                    int32_t* __restrict__ counts, int32_t* __restrict__ defer) {
   if (blockIdx.x == 0 && threadIdx.x == 0) defer[0] = 0;  // no deferred positives yet
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;
-  if (lane == 0) { counts[row] = 0; cursor[row] = 0; }  // the row's slot bucket, for this call
+  if (lane == 0) counts[row] = 0;  // the row's slot bucket, for this call
   const bool is_ent = row < n_ent;
   const float* p = (is_ent ? ent : rel) + (is_ent ? row : row - n_ent) * d;
   float s = 0.0f;
@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       const uint32_t key = lane == 0 ? kq0 : (lane == 1 ? kq1 : kq2);
       S.keys[sl] = key;
       S.mult[sl] = 1.0f;
-      if (key != S.sentinel) atomicAdd(&S.counts[key], 1);
+      if (key != S.sentinel) S.pos[sl] = atomicAdd(&S.counts[key], 1);
     }
   }
   if (w > 0) {
@@ -1117,7 +1117,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
       S.keys[sb + lane] = key;
       S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
-      atomicAdd(&S.counts[key], 1);
+      S.pos[sb + lane] = atomicAdd(&S.counts[key], 1);
     }
   }
 }
@@ -1145,21 +1145,32 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused_generic(NSArgs A, const
 }
 
 // Exclusive scan of the per-row slot counts into bucket offsets (offs[n] = all slots), one
-// 1,024-thread workgroup over coalesced 4,096-count tiles: four counts per thread, wave scans
-// by shuffles, the 16 wave totals in LDS.
+// 1,024-thread workgroup over tiles of 16,384 counts (one tile up to 16 k table rows): each
+// thread loads its 16 consecutive counts with four 16-B loads before any arithmetic (one
+// memory round trip per tile), wave scans of the thread totals by shuffles, the 16 wave totals
+// in LDS.
 __global__ __launch_bounds__(1024) void k_ns_scan(const int32_t* __restrict__ counts, int64_t n,
                                                   int32_t* __restrict__ offs) {
+  constexpr int PT = 16;
   __shared__ int32_t s_w[16];
-  __shared__ int32_t s_carry;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t == 0) s_carry = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += 4096) {
-    const int64_t i = base + 4 * (int64_t)t;
-    int32_t c[4];
+  int32_t carry = 0;
+  for (int64_t base = 0; base < n; base += 1024 * PT) {
+    const int64_t i = base + (int64_t)PT * t;
+    int32_t c[PT];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = i + q < n ? counts[i + q] : 0;
-    const int32_t tot = c[0] + c[1] + c[2] + c[3];
+    for (int q = 0; q < PT; q += 4) {
+      if (i + q + 3 < n) {
+        const int4 v = *reinterpret_cast<const int4*>(counts + i + q);
+        c[q] = v.x; c[q + 1] = v.y; c[q + 2] = v.z; c[q + 3] = v.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) c[q + e] = i + q + e < n ? counts[i + q + e] : 0;
+      }
+    }
+    int32_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < PT; ++q) tot += c[q];
     int32_t inc = tot;  // inclusive scan of the thread totals within the wave
 #pragma unroll
     for (int sh = 1; sh < 64; sh <<= 1) {
@@ -1168,34 +1179,39 @@ __global__ __launch_bounds__(1024) void k_ns_scan(const int32_t* __restrict__ co
     }
     if (lane == 63) s_w[wv] = inc;
     __syncthreads();
-    int32_t before = s_carry;
-    for (int k = 0; k < wv; ++k) before += s_w[k];
+    int32_t before = carry, all = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int32_t x = s_w[k];
+      before += k < wv ? x : 0;
+      all += x;
+    }
     int32_t run = before + inc - tot;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < PT; ++q) {
       if (i + q < n) offs[i + q] = run;
       run += c[q];
     }
-    __syncthreads();
-    if (t == 1023) s_carry = run;  // the last thread's running total = the tile's end
-    __syncthreads();
+    carry += all;
+    __syncthreads();  // s_w is rewritten by the next tile
   }
-  if (t == 0) offs[n] = s_carry;
+  if (t == 0) offs[n] = carry;
 }
 
-// Each slot's id into its row's bucket (position within the bucket by arrival: the owner
-// restores the batch order); workgroup 0 also reduces the loss (ns_reduce_block, the fixed
-// order and arithmetic of k_ns_reduce).
+// Each slot's id into its row's bucket, at the place its count's atomic returned in the
+// fused kernel (arrival order: the owner restores the batch order): a plain scatter.
+// Workgroup 0 also reduces the loss (ns_reduce_block, the fixed order and arithmetic of
+// k_ns_reduce).
 __global__ __launch_bounds__(256) void k_ns_place(NSArgs A, const float* __restrict__ part, float* __restrict__ loss,
-                                                  const uint32_t* __restrict__ keys, int64_t n_slots,
-                                                  uint32_t sentinel, const int32_t* __restrict__ offs,
-                                                  int32_t* __restrict__ cursor, int32_t* __restrict__ sslot) {
+                                                  const uint32_t* __restrict__ keys, const int32_t* __restrict__ pos,
+                                                  int64_t n_slots, uint32_t sentinel,
+                                                  const int32_t* __restrict__ offs, int32_t* __restrict__ sslot) {
   if (blockIdx.x == 0) ns_reduce_block(A, part, loss);  // uniform per workgroup
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_slots) return;
   const uint32_t k = keys[i];
   if (k == sentinel) return;
-  sslot[offs[k] + atomicAdd(&cursor[k], 1)] = (int32_t)i;
+  sslot[offs[k] + pos[i]] = (int32_t)i;
 }
 
 __device__ __forceinline__ int wave_min_i32(int v) {
@@ -1464,10 +1480,10 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
 }
 
 // Workspace of the fused path, in 4-byte words, 256-B aligned pieces: loss partials, row
-// norms, the slot contributions / occurrences / keys, the per-row slot counts, placement
-// cursors and bucket offsets, the bucketed slot ids.
+// norms, the slot contributions / occurrences / keys / bucket places, the per-row slot
+// counts, bucket offsets, the bucketed slot ids, the deferred positives.
 struct FusedWs {
-  int64_t part, nrm_e, nrm_r, shared, rec, mult, keys, counts, cursor, offs, sslot, defer, total, slots;
+  int64_t part, nrm_e, nrm_r, shared, rec, mult, keys, pos, counts, offs, sslot, defer, total, slots;
   uint32_t sentinel;
 };
 
@@ -1484,8 +1500,8 @@ static void fused_ws(int64_t B, int64_t K, int64_t E, int64_t R, int d, FusedWs&
   w.rec = o;     o = al64(o + K * B * (d > ns_rec_words(8, false, d) ? d : ns_rec_words(8, false, d)));
   w.mult = o;    o = al64(o + w.slots);
   w.keys = o;    o = al64(o + w.slots);
+  w.pos = o;     o = al64(o + w.slots);
   w.counts = o;  o = al64(o + E + R);
-  w.cursor = o;  o = al64(o + E + R);
   w.offs = o;    o = al64(o + E + R + 1);
   w.sslot = o;   o = al64(o + w.slots);
   w.defer = o;   o = al64(o + B + 1);
@@ -1524,13 +1540,12 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   float* nrm_e = d_work + w.nrm_e;
   float* nrm_r = d_work + w.nrm_r;
   int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
-  int32_t* cursor = reinterpret_cast<int32_t*>(d_work + w.cursor);
   int32_t* offs = reinterpret_cast<int32_t*>(d_work + w.offs);
   int32_t* defer = reinterpret_cast<int32_t*>(d_work + w.defer);
-  NSSlots S{d_work + w.shared, d_work + w.rec, d_work + w.mult, reinterpret_cast<uint32_t*>(d_work + w.keys), counts,
-            w.sentinel};
+  NSSlots S{d_work + w.shared, d_work + w.rec, d_work + w.mult, reinterpret_cast<uint32_t*>(d_work + w.keys),
+            reinterpret_cast<int32_t*>(d_work + w.pos), counts, w.sentinel};
   hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
-                     n_rel, dim, nrm_e, nrm_r, counts, cursor, defer);
+                     n_rel, dim, nrm_e, nrm_r, counts, defer);
   MMRE_CHECK_LAUNCH();
   const dim3 grid((unsigned)batch), blk(256);
   const bool l2 = model == MMRE_TRANSE_L2;
@@ -1560,7 +1575,7 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   hipLaunchKernelGGL(k_ns_scan, dim3(1), dim3(1024), 0, st, counts, n_ent + n_rel, offs);
   MMRE_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_ns_place, dim3((unsigned)((w.slots + 255) / 256)), dim3(256), 0, st, A, part, d_loss,
-                     reinterpret_cast<const uint32_t*>(S.keys), w.slots, w.sentinel, offs, cursor,
+                     reinterpret_cast<const uint32_t*>(S.keys), S.pos, w.slots, w.sentinel, offs,
                      reinterpret_cast<int32_t*>(d_work + w.sslot));
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;

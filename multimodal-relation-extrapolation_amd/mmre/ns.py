@@ -49,6 +49,7 @@ class _FusedNS(torch.autograd.Function):
         score = torch.empty(N, dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
         ctx.mark_non_differentiable(score)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the (non-differentiable) scores
         ctx.fused = any(ctx.needs_input_grad[:4])
         ctx.has_im = ent_im is not None
         ctx.cfg = (spec, batch, neg, loss_margin, adv_t, regul_rate)
@@ -78,6 +79,8 @@ class _FusedNS(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_loss, g_score):
+        if g_loss is None:
+            return (None,) * 14
         ent, rel, ent_im, rel_im, h, t, r, score = ctx.saved_tensors
         spec, batch, neg, loss_margin, adv_t, regul_rate = ctx.cfg
         if not ctx.has_im:
