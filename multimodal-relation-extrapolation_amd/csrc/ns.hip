@@ -357,6 +357,27 @@ __device__ __forceinline__ void vload(Vec<NC>& o, const float* row, int d, int l
   }
 }
 
+// Row `row` (wave-uniform) of a [*, d] table through a buffer resource sized to the row: the
+// padding lanes (element >= d) read 0 and their stores are dropped by the hardware range check,
+// so the fast path has no per-element bounds branches.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* table, int64_t row, int d) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(table + row * d), (short)0, d * 4, 0x00020000);
+}
+
+template <int NC>
+__device__ __forceinline__ void vload_row(Vec<NC>& o, const float* table, int64_t row, int d, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(table, row, d);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) o.v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (lane + c * kWave) * 4, 0, 0));
+}
+
+template <int NC>
+__device__ __forceinline__ void vstore_row(float* table, int64_t row, const Vec<NC>& v, int d, int lane) {
+  const __amdgpu_buffer_rsrc_t rs = row_rsrc(table, row, d);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.v[c]), rs, (lane + c * kWave) * 4, 0, 0);
+}
+
 template <int NC>
 __device__ __forceinline__ float vsq(const Vec<NC>& a) {
   float s = 0.0f;
@@ -762,9 +783,9 @@ template <int NC, bool L2>
 __device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ shared, const float* __restrict__ rec,
                                           int64_t idx, bool neg, int d, int lane) {
   if (!neg) {
-    vload(v, shared + idx * d, d, lane);
+    vload_row(v, shared, idx, d, lane);
   } else if constexpr (L2) {
-    vload(v, rec + idx * d, d, lane);
+    vload_row(v, rec, idx, d, lane);
   } else {
     const float* r = rec + idx * ns_rec_words(NC, false, d);
     const float mag = r[0];
@@ -828,27 +849,6 @@ __device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Ve
     acc += L2 ? e * e : fabsf(e);
   }
   return acc;
-}
-
-// Row `row` (wave-uniform) of a [*, d] table through a buffer resource sized to the row: the
-// padding lanes (element >= d) read 0 and their stores are dropped by the hardware range check,
-// so the fast path has no per-element bounds branches.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const float* table, int64_t row, int d) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(table + row * d), (short)0, d * 4, 0x00020000);
-}
-
-template <int NC>
-__device__ __forceinline__ void vload_row(Vec<NC>& o, const float* table, int64_t row, int d, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = row_rsrc(table, row, d);
-#pragma unroll
-  for (int c = 0; c < NC; ++c) o.v[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (lane + c * kWave) * 4, 0, 0));
-}
-
-template <int NC>
-__device__ __forceinline__ void vstore_row(float* table, int64_t row, const Vec<NC>& v, int d, int lane) {
-  const __amdgpu_buffer_rsrc_t rs = row_rsrc(table, row, d);
-#pragma unroll
-  for (int c = 0; c < NC; ++c) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v.v[c]), rs, (lane + c * kWave) * 4, 0, 0);
 }
 
 template <int CTRL>
@@ -1244,14 +1244,13 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
   const int64_t i0 = offs[row], i1 = offs[row + 1];
   // the row itself and its norm, in flight while the bucket is ordered and summed
   Vec<NC> v;
-  vload(v, (is_ent ? ent : rel) + id * d, d, lane);
+  vload_row(v, is_ent ? ent : rel, id, d, lane);
   const float nv = (is_ent ? nrm_e : nrm_r)[id];
   if (i0 == i1) {  // not in the batch: zero gradient
+    Vec<NC> z;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + c * kWave;
-      if (i < d) o[i] = 0.0f;
-    }
+    for (int c = 0; c < NC; ++c) z.v[c] = 0.0f;
+    vstore_row(o, 0, z, d, lane);
     return;
   }
   const int64_t spp = 3 + 3 * K;
@@ -1336,16 +1335,12 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
     const float scale = nv > 1e-12f ? 1.0f / nv : 1.0f / 1e-12f;
     const float proj = nv > 1e-12f ? dot : 0.0f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + c * kWave;
-      if (i < d) o[i] = ((dy.v[c] - (v.v[c] / cv) * proj) * scale + rr * v.v[c]) * G;
-    }
+    for (int c = 0; c < NC; ++c) dy.v[c] = ((dy.v[c] - (v.v[c] / cv) * proj) * scale + rr * v.v[c]) * G;
+    vstore_row(o, 0, dy, d, lane);
   } else {
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + c * kWave;
-      if (i < d) o[i] = (dy.v[c] + rr * v.v[c]) * G;
-    }
+    for (int c = 0; c < NC; ++c) dy.v[c] = (dy.v[c] + rr * v.v[c]) * G;
+    vstore_row(o, 0, dy, d, lane);
   }
 }
 

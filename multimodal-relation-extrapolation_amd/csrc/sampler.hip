@@ -37,17 +37,31 @@ __device__ uint64_t lcg_jump(uint64_t x, uint64_t n) {
   return A * x + C;
 }
 
+// The block [ll, rr] of rows whose column `kc` equals `key` inside the sorted range
+// [lef0, rig0] (Corrupt.h's two binary searches, same midpoints and results) -- the lower and
+// upper searches advance together, so their dependent loads are issued in pairs and the chain
+// is as long as one search.
+__device__ __forceinline__ void key_block(const int64_t* __restrict__ T, int kc, int64_t lef0, int64_t rig0,
+                                          int64_t key, int64_t& ll, int64_t& rr) {
+  int64_t al = lef0 - 1, ar = rig0, bl = lef0, br = rig0 + 1;
+  while (al + 1 < ar || bl + 1 < br) {
+    const bool ga = al + 1 < ar, gb = bl + 1 < br;
+    const int64_t ma = (al + ar) >> 1, mb = (bl + br) >> 1;
+    const int64_t va = ga ? T[3 * ma + kc] : 0, vb = gb ? T[3 * mb + kc] : 0;
+    if (ga) { if (va >= key) ar = ma; else al = ma; }
+    if (gb) { if (vb <= key) bl = mb; else br = mb; }
+  }
+  ll = ar;
+  rr = bl;
+}
+
 // corrupt_head (Corrupt.h:7-43): uniform entity not among the known TAILS of (h, r),
 // found by skipping the sorted tails of the (h, r) block of trainHead.
 __device__ int64_t corrupt_head(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_head,
                                 const int64_t* __restrict__ rig_head, int64_t n_ent, uint64_t* st, int64_t h,
                                 int64_t r) {
-  int64_t lef = lef_head[h] - 1, rig = rig_head[h], mid, ll, rr;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] >= r) rig = mid; else lef = mid; }
-  ll = rig;
-  lef = lef_head[h]; rig = rig_head[h] + 1;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] <= r) lef = mid; else rig = mid; }
-  rr = lef;
+  int64_t lef, rig, mid, ll, rr;
+  key_block(T, 1, lef_head[h], rig_head[h], r, ll, rr);
   const int64_t tmp = rand_max(st, n_ent - (rr - ll + 1));
   if (tmp < T[3 * ll + 2]) return tmp;
   if (tmp > T[3 * rr + 2] - rr + ll - 1) return tmp + rr - ll + 1;
@@ -61,12 +75,8 @@ __device__ int64_t corrupt_head(const int64_t* __restrict__ T, const int64_t* __
 __device__ int64_t corrupt_tail(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_tail,
                                 const int64_t* __restrict__ rig_tail, int64_t n_ent, uint64_t* st, int64_t t,
                                 int64_t r) {
-  int64_t lef = lef_tail[t] - 1, rig = rig_tail[t], mid, ll, rr;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] >= r) rig = mid; else lef = mid; }
-  ll = rig;
-  lef = lef_tail[t]; rig = rig_tail[t] + 1;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] <= r) lef = mid; else rig = mid; }
-  rr = lef;
+  int64_t lef, rig, mid, ll, rr;
+  key_block(T, 1, lef_tail[t], rig_tail[t], r, ll, rr);
   const int64_t tmp = rand_max(st, n_ent - (rr - ll + 1));
   if (tmp < T[3 * ll + 0]) return tmp;
   if (tmp > T[3 * rr + 0] - rr + ll - 1) return tmp + rr - ll + 1;
@@ -80,12 +90,8 @@ __device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64_t* __r
                                const int64_t* __restrict__ rig_rel, int64_t n_rel, uint64_t* st, int64_t h, int64_t t,
                                int64_t r) {
   (void)r;
-  int64_t lef = lef_rel[h] - 1, rig = rig_rel[h], mid, ll, rr;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] >= t) rig = mid; else lef = mid; }
-  ll = rig;
-  lef = lef_rel[h]; rig = rig_rel[h] + 1;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] <= t) lef = mid; else rig = mid; }
-  rr = lef;
+  int64_t lef, rig, mid, ll, rr;
+  key_block(T, 2, lef_rel[h], rig_rel[h], t, ll, rr);
   const int64_t tmp = rand_max(st, n_rel - (rr - ll + 1));
   if (tmp < T[3 * ll + 1]) return tmp;
   if (tmp > T[3 * rr + 1] - rr + ll - 1) return tmp + rr - ll + 1;
