@@ -902,23 +902,29 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 // (entity tile of 128). 4 waves as 2 (q) x 2 (e); each wave 64 x 64 = 2 x 2 blocks of 32 x 32
 // accumulators. K goes through double-buffered LDS stages of KS rows, register-staged, the
 // next stage's global loads issued at the top of the current one (scripts/probes/
-// mfma_stage.hip: with two 256-thread workgroups per CU this beats LDS-DMA rings and a single
-// 256 x 128 workgroup). Epilogue: each lane holds 32 query rows x 1 entity column of the
-// 64 x 64 block; it reads the rows' thresholds from LDS (8 b128 reads, once per unit),
-// compares and bumps per-row register counters; the counters are reduced across the 32
-// column lanes only when the workgroup leaves the query tile. The truth needs no exclusion
+// mfma_stage.hip: this beats LDS-DMA rings and a single 256 x 128 workgroup). The plain
+// sweep runs KS = 16 at four 256-thread workgroups per CU (33 KB LDS, 112 VGPRs); the type-
+// constrained / score-storing variants KS = 32 at two. Epilogue: each lane holds 32 query rows
+// x 1 entity column of the 64 x 64 block and reads the rows' thresholds from LDS (b128 reads,
+// once per unit). KS = 16: each row's 64 compares are counted by two ballots into a counter
+// held by the lane of that row (one register for the wave's 64 rows); KS = 32: per-lane
+// register counters for its 32 rows, reduced across the 32 column lanes. Either way the
+// counts reach HBM only when the workgroup leaves the query tile. The truth needs no exclusion
 // test: its score is bit-identical to the threshold (same canonical chain), so `< thr`
 // rejects it.
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 template <bool TC, bool STORE, int PK, int KS>
-__global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
+__global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep_mfma(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
     int64_t q_pad, int64_t n_query, int ktot, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
     const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
     int32_t* __restrict__ counts, float* __restrict__ scores) {
   static_assert(KS == 16 || KS == 32, "stage of 16 or 32 K rows");
+  // 16-row stages (33 KB of LDS) run 4 workgroups per CU: the row counters then live one row
+  // per lane (ballot counts), which frees the 32 registers of per-lane row counters
+  constexpr bool BAL = KS == 16;
   __shared__ float sq[2][KS][TQ];
   __shared__ float se[2][KS][TE];
   __shared__ int32_t s_rel[TC ? TQ : 1];
@@ -943,7 +949,11 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
 
   // rows of this lane: ql(bi, r) = wq*64 + bi*32 + (r&3) + 8*(r>>2) + 4*lrow
   int tpar = 0;  // s_th slot of the current query tile
-  int cnt[2][16], cnt_tc[TC ? 2 : 1][TC ? 16 : 1];
+  // per-row counters of the current query tile. BAL: one row per lane, lane L holds wave row L
+  // (tile row wq * 64 + L), each row's 64 compares counted by two ballots; else each lane
+  // counts its own column of its 32 rows, reduced over the 32 column lanes at the flush
+  int cntv = 0, cntv_tc = 0;
+  int cnt[BAL ? 1 : 2][BAL ? 1 : 16], cnt_tc[TC && !BAL ? 2 : 1][TC && !BAL ? 16 : 1];
   auto row_of = [&](int bi, int r) { return wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lrow; };
   auto load_rows = [&](int qtile) {
     const int64_t q0 = (int64_t)qtile * TQ;
@@ -954,13 +964,17 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
       const int64_t q = q0 + tid;
       s_th[tpar][tid] = q < n_query ? thr[q] : -INFINITY;  // -inf: nothing beats a padded row
     }
+    cntv = 0;
+    cntv_tc = 0;
+    if constexpr (!BAL) {
 #pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        cnt[bi][r] = 0;
-        if constexpr (TC) cnt_tc[bi][r] = 0;
-      }
+        for (int r = 0; r < 16; ++r) {
+          cnt[bi][r] = 0;
+          if constexpr (TC) cnt_tc[bi][r] = 0;
+        }
+    }
     if constexpr (TC) {
       __syncthreads();  // previous tile's s_rel/s_mode readers are done
       if (tid < TQ) {
@@ -971,28 +985,38 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
     }
   };
   auto flush_rows = [&](int qtile) {
-    const int64_t q0 = (int64_t)qtile * TQ;
-#pragma unroll
-    for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        int c = cnt[bi][r];
-#pragma unroll
-        for (int sh = 1; sh < 32; sh <<= 1) c += __shfl_xor(c, sh);  // the 32 column lanes
-        int cc = 0;
+    if constexpr (BAL) {  // each lane its row's count (both column waves add)
+      const int64_t q = (int64_t)qtile * TQ + wq * 64 + lane;
+      if (q < n_query) {
+        if (cntv) { atomicAdd(&counts[q], cntv); atomicAdd(&counts[n_query + q], cntv); }
         if constexpr (TC) {
-          cc = cnt_tc[bi][r];
-#pragma unroll
-          for (int sh = 1; sh < 32; sh <<= 1) cc += __shfl_xor(cc, sh);
-        }
-        const int64_t q = q0 + row_of(bi, r);
-        if (lcol == 0 && q < n_query) {
-          if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
-          if constexpr (TC) {
-            if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
-          }
+          if (cntv_tc) { atomicAdd(&counts[2 * n_query + q], cntv_tc); atomicAdd(&counts[3 * n_query + q], cntv_tc); }
         }
       }
+    } else {
+      const int64_t q0 = (int64_t)qtile * TQ;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int c = cnt[bi][r];
+#pragma unroll
+          for (int sh = 1; sh < 32; sh <<= 1) c += __shfl_xor(c, sh);  // the 32 column lanes
+          int cc = 0;
+          if constexpr (TC) {
+            cc = cnt_tc[bi][r];
+#pragma unroll
+            for (int sh = 1; sh < 32; sh <<= 1) cc += __shfl_xor(cc, sh);
+          }
+          const int64_t q = q0 + row_of(bi, r);
+          if (lcol == 0 && q < n_query) {
+            if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
+            if constexpr (TC) {
+              if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
+            }
+          }
+        }
+    }
   };
 
   const int srow = tid >> 5, sc4 = tid & 31;  // rows srow + 8 i of the stage
@@ -1072,40 +1096,84 @@ __global__ __launch_bounds__(NT, 2) void k_sweep_mfma(
       if (kc == nkc - 1) {  // unit finished: rank epilogue
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE + we * 64;
-        // the lane's 32 row thresholds, 8 LDS reads issued together (a read per compare
-        // serialised 64 LDS latencies per unit); rows row_of(bi, 4i) .. + 3 are contiguous
-        float tv[2][16];
+        const int64_t e0 = ebase + lcol, e1 = ebase + 32 + lcol;
+        const bool ev0 = e0 < n_ent, ev1 = e1 < n_ent;
+        if constexpr (BAL) {
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+          for (int bi = 0; bi < 2; ++bi) {
+            float tv[16];  // the lane's 16 row thresholds of block bi: 4 LDS reads issued together
 #pragma unroll
-          for (int r4 = 0; r4 < 16; r4 += 4) {
-            const float4 t4 = *reinterpret_cast<const float4*>(&s_th[tpar][row_of(bi, r4)]);
-            tv[bi][r4] = t4.x;
-            tv[bi][r4 + 1] = t4.y;
-            tv[bi][r4 + 2] = t4.z;
-            tv[bi][r4 + 3] = t4.w;
-          }
+            for (int r4 = 0; r4 < 16; r4 += 4) {
+              const float4 t4 = *reinterpret_cast<const float4*>(&s_th[tpar][row_of(bi, r4)]);
+              tv[r4] = t4.x;
+              tv[r4 + 1] = t4.y;
+              tv[r4 + 2] = t4.z;
+              tv[r4 + 3] = t4.w;
+            }
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj) {
-          const int64_t e = ebase + bj * 32 + lcol;
-          if (e < n_ent) {  // one exec mask per column block (lanes diverge in the last tile only)
-#pragma unroll
-            for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                const float v = pred(acc[bi][bj][r]);
-                const bool better = v < tv[bi][r];
-                cnt[bi][r] += better;
-                if constexpr (TC) {
-                  const int ql = row_of(bi, r);
-                  const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                  cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e + e_base);
-                }
-                if constexpr (STORE) {
-                  const int64_t q = q0 + row_of(bi, r);
-                  if (q < n_query) scores[q * n_ent + e] = v;
+            for (int r = 0; r < 16; ++r) {
+              // row (bi, r) of lane half lrow is wave row L0 + 4 lrow; its 64 compares (2 column
+              // blocks x 32 lanes) are counted by two ballots
+              const float v0 = pred(acc[bi][0][r]), v1 = pred(acc[bi][1][r]);
+              const bool b0 = ev0 && v0 < tv[r], b1 = ev1 && v1 < tv[r];
+              const uint64_t m0 = __ballot(b0), m1 = __ballot(b1);
+              const int L0 = bi * 32 + (r & 3) + 8 * (r >> 2);
+              const int c_lo = __popcll(m0 & 0xffffffffull) + __popcll(m1 & 0xffffffffull);
+              const int c_hi = __popcll(m0 >> 32) + __popcll(m1 >> 32);
+              cntv += lane == L0 ? c_lo : (lane == L0 + 4 ? c_hi : 0);
+              if constexpr (TC) {
+                const int ql = row_of(bi, r);
+                const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                const uint64_t t0 = __ballot(b0 && type_bit(tm, type_words, s_rel[ql], e0 + e_base));
+                const uint64_t t1 = __ballot(b1 && type_bit(tm, type_words, s_rel[ql], e1 + e_base));
+                cntv_tc += lane == L0 ? __popcll(t0 & 0xffffffffull) + __popcll(t1 & 0xffffffffull)
+                                      : (lane == L0 + 4 ? __popcll(t0 >> 32) + __popcll(t1 >> 32) : 0);
+              }
+              if constexpr (STORE) {
+                const int64_t q = q0 + row_of(bi, r);
+                if (q < n_query) {
+                  if (ev0) scores[q * n_ent + e0] = v0;
+                  if (ev1) scores[q * n_ent + e1] = v1;
                 }
               }
+            }
+          }
+        } else {
+          // the lane's 32 row thresholds, 8 LDS reads issued together (a read per compare
+          // serialised 64 LDS latencies per unit); rows row_of(bi, 4i) .. + 3 are contiguous
+          float tv[2][16];
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r4 = 0; r4 < 16; r4 += 4) {
+              const float4 t4 = *reinterpret_cast<const float4*>(&s_th[tpar][row_of(bi, r4)]);
+              tv[bi][r4] = t4.x;
+              tv[bi][r4 + 1] = t4.y;
+              tv[bi][r4 + 2] = t4.z;
+              tv[bi][r4 + 3] = t4.w;
+            }
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj) {
+            const int64_t e = bj ? e1 : e0;
+            if (bj ? ev1 : ev0) {  // one exec mask per column block (lanes diverge in the last tile only)
+#pragma unroll
+              for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                  const float v = pred(acc[bi][bj][r]);
+                  const bool better = v < tv[bi][r];
+                  cnt[bi][r] += better;
+                  if constexpr (TC) {
+                    const int ql = row_of(bi, r);
+                    const uint32_t* tm = s_mode[ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                    cnt_tc[bi][r] += better && type_bit(tm, type_words, s_rel[ql], e + e_base);
+                  }
+                  if constexpr (STORE) {
+                    const int64_t q = q0 + row_of(bi, r);
+                    if (q < n_query) scores[q * n_ent + e] = v;
+                  }
+                }
+            }
           }
         }
 #pragma unroll
@@ -1387,18 +1455,24 @@ static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent
   // K stages of 32 rows (a unit's last one 16 when K = 32 n + 16: C3 ComplEx 2 x 200): half the
   // per-stage staging and barriers per MFMA of 16-row stages (scripts/probes/mfma_stage.hip:
   // 0.79 -> 0.86 of the f32 MFMA peak, L2-resident or HBM-streamed alike)
-  static const char* ks_env = getenv("MMRE_MFMA_STAGE"); /* experiments: 16 forces 16-row stages */
-  const bool ks32 = !(ks_env && atoi(ks_env) == 16);
+  // The plain sweep (no type constraint, no score store) runs 16-row stages at 4 workgroups
+  // per CU (33 KB of LDS, 112 VGPRs with the ballot row counters): C3 1.03 -> 0.97 ms, C5
+  // 33.7 -> 33.0 ms against 32-row stages at 2 per CU; the TC / STORE variants keep 32-row
+  // stages (their extra registers would spill at 4 per CU).
+  static const char* ks_env = getenv("MMRE_MFMA_STAGE"); /* experiments: 16 / 32 force the stage */
+  const int ks_force = ks_env ? atoi(ks_env) : 0;
+  const bool ks32 = ks_force == 32 || (ks_force != 16 && (tc || store));
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
 #define MMRE_MFMA_K(KERNEL)                                                                                       \
   do {                                                                                                            \
-    /* 16 units per workgroup, between 2 and 8 x the resident slots: short ranges let the      */                \
-    /* dispatcher balance CUs of different speed (C5 1,024 / 4,096 groups: 35.1 / 34.3 ms) while */                \
-    /* the few-unit C3 keeps ranges long enough to amortise each group's first stage (C3: 1,024 */                \
-    /* groups 1.12 ms, 4,096 1.17 ms)                                                           */                \
+    /* 16 units per workgroup, between 1 (2 with 32-row stages) and 8 x the resident slots:    */                \
+    /* short ranges let the dispatcher balance CUs of different speed (C5 1,024 / 4,096 groups:  */                \
+    /* 35.1 / 34.3 ms) while the few-unit C3 keeps ranges long enough to amortise each group's   */                \
+    /* first stage (16-row stages at 4 / CU, C3: 1,024 groups 0.97 ms, 2,048 1.04, 4,096 1.02)   */                \
     const int res = resident_groups((const void*)KERNEL, NT);                                                     \
     const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                           \
-    int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>(2LL * res, units / 16)) & ~7;                     \
+    const int64_t lo = ks32 ? 2LL * res : (int64_t)res;                                                           \
+    int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>(lo, units / 16)) & ~7;                            \
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                              \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL(KERNEL, dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,       \
