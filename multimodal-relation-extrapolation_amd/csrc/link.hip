@@ -262,7 +262,7 @@ __device__ __forceinline__ float op_step(float acc, float qa, float qb, float x,
     return acc + d * d;
   } else if constexpr (OP == 2) {
     float dr = qa - x, di = qb - y;
-    return acc + sqrtf(dr * dr + di * di);
+    return acc + sqrtf(__builtin_fmaf(di, di, dr * dr));
   } else {
     return __builtin_fmaf(x, qa, acc);
   }
@@ -272,7 +272,7 @@ __device__ __forceinline__ float op_final(float acc) {
   if constexpr (OP == 1) return sqrtf(acc);
   else return acc;
 }
-// RotatE's |(dr, di)| = sqrt(v), v = dr*dr + di*di, correctly rounded, for the sweep's inner
+// RotatE's |(dr, di)| = sqrt(v), v = fma(di, di, dr*dr), correctly rounded, for the sweep's inner
 // loop, in full-rate f32 arithmetic only: y = v_rsq_f32(v), s = v*y, h = y/2, then one
 // Newton step s + (v - s*s)*h in fma form. Checked exhaustively on MI355X against IEEE
 // sqrtf over every float input (scripts/probes/sqrt_candidates.hip): exact for all
@@ -766,7 +766,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float dr = qa[0] - xv[j], di = qb[0] - yv[j];
-            v[j] = dr * dr + di * di;
+            v[j] = __builtin_fmaf(di, di, dr * dr);
             y[j] = __builtin_amdgcn_rsqf(v[j]);
           }
 #pragma unroll
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 const float dr = qa[i + 1] - xv[j], di = qb[i + 1] - yv[j];
-                vn[j] = dr * dr + di * di;
+                vn[j] = __builtin_fmaf(di, di, dr * dr);
                 yn[j] = __builtin_amdgcn_rsqf(vn[j]);
               }
             }

@@ -17,7 +17,7 @@
  *   TransE  L2 : s = 0; for k: x = q_k - e_k; s = s + x*x;  s = sqrtf(s)
  *   DistMult   : s = 0; for k: s = fmaf(e_k, q_k, s)
  *   ComplEx    : s = 0; for k: s = fmaf(re_k, qa_k, s); for k: s = fmaf(im_k, qb_k, s)
- *   RotatE     : s = 0; for k: dr = qa_k - x_k; di = qb_k - y_k; s = s + sqrtf(dr*dr + di*di)
+ *   RotatE     : s = 0; for k: dr = qa_k - x_k; di = qb_k - y_k; s = s + sqrtf(fmaf(di, di, dr*dr))
  * Query vectors (element-wise, same rounding as the reference's torch ops):
  *   TransE  head: q = -(r - t)   tail: q = h + r          (TransE.py:71-74)
  *   DistMult head: q = r * t     tail: q = h * r          (DistMult.py:37-42)
@@ -166,7 +166,7 @@ static float score_one(int model, const float *ent, const float *ent_im, const f
         const float *row = ent + e * 2 * d;
         for (int k = 0; k < d; ++k) {
             float dr = qa[k] - row[k], di = qb[k] - row[d + k];
-            s = s + sqrtf(dr * dr + di * di);
+            s = s + sqrtf(fmaf(di, di, dr * dr));
         }
     }
     return s;
