@@ -857,6 +857,8 @@ def main():
     ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
     ap.add_argument("--ns-eager", action="store_true", help="--config ns: launch each step eagerly (no hipGraph)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="link configs: launch each rank's local evaluation eagerly (default: one hipGraph replay)")
     ap.add_argument("--shard", default="relation", choices=["relation", "entity"],
                     help="N > 1 link configs: split the queries (relation-sharded, one all-gather; default) or "
                          "the entity table (every query against 1/N of the entities, one all-reduce)")
@@ -923,7 +925,10 @@ def main():
         n_local = 2 * n if ev.entity_range[1] > ev.entity_range[0] else 0
         e_local = ev.entity_range[1] - ev.entity_range[0]
     else:
-        ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+        # the rank's local evaluation (entity / query prep, truth and filter kernels, sweep)
+        # replayed from one hipGraph; kernel_ms comes from an eager twin after the timed region
+        ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev,
+                                   graph=not args.eager)
         n_local = int(ev.masks[rank].sum())
         e_local = E
 
@@ -942,7 +947,9 @@ def main():
 
     steps(args.warmup)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    graphed = getattr(ev, "_graph_wanted", False)
+    evs = None if graphed else [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                                for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -952,6 +959,15 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if graphed and n_local:  # the sweep kernel alone: events on the launch stream of eager evaluations
+        from mmre.link import LinkSweep
+        sw = LinkSweep(spec)
+        bufs = sw.alloc_queries(len(ev.q_host[0]))
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for e2 in evs:
+            sw.run(*ev.q, filt=ev.filt, type_masks=ev.masks_tc, buffers=bufs, sweep_events=e2)
+        torch.cuda.synchronize()
+        del sw, bufs
     sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if n_local else 0.0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=_coll_dev(dist, dev))
@@ -1005,7 +1021,8 @@ def main():
                           "parallelism": (f"entity-sharded x{world} (1/N of the entity tiles per rank), {coll} all-reduce "
                                           f"of the count table" if args.shard == "entity" else
                                           f"query-sharded x{world} (relation-major LPT with relation splits), {coll} "
-                                          f"all-gather of rank counts")},
+                                          f"all-gather of rank counts"),
+                          "launch": "hipGraph replay of each rank's local evaluation" if graphed else "eager"},
                "roofline": roof,
                "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
                            "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
