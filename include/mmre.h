@@ -181,6 +181,25 @@ int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const 
                         int64_t mode, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
                         float* d_batch_y, void* stream);
 
+/* The (h, r) block of head_hrt and the (t, r) block of tail_hrt of every train row i, with
+ * their first / last tail / head: int32 d_blocks[n_train][8] = (ll, rr, tail[ll], tail[rr],
+ * ll', rr', head[ll'], head[rr']). What corrupt_head / corrupt_tail (Corrupt.h:7-81) look up
+ * before their draw, built once per train index (n_train = rows of d_train_list). */
+int mmre_sampler_blocks(const int64_t* d_train_list, int64_t n_train, const int64_t* d_head_hrt,
+                        const int64_t* d_tail_hrt, const int64_t* d_lef_head, const int64_t* d_rig_head,
+                        const int64_t* d_lef_tail, const int64_t* d_rig_tail, int32_t* d_blocks, void* stream);
+/* mmre_sampler_openke reading the kept (entity, relation)'s block from d_blocks for train
+ * rows i < n_blocks (bit-identical batches: the same blocks, found without the two binary
+ * searches per negative); d_blocks NULL / n_blocks 0 is mmre_sampler_openke itself. */
+int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
+                                int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                                int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
+                                int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, void* stream);
+
 /* The repo's per-edge filtered sampler (module/NegativeSampling.py:114-140,
  * 321-375): per positive edge b (local ids d_eh/d_et, relation d_er), neg
  * negatives split head/tail by Bernoulli(0.5); candidates uniform over the local

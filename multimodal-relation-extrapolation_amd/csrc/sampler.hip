@@ -55,19 +55,27 @@ __device__ __forceinline__ void key_block(const int64_t* __restrict__ T, int kc,
   rr = bl;
 }
 
+// The draw and the final skip of Corrupt.h's corruption, given the block [ll, rr] of rows of T
+// sharing the kept (entity, relation) and its first / last value `tll` / `trr` in column col:
+// a uniform id among the n - (rr - ll + 1) ids not in the block.
+__device__ int64_t corrupt_in_block(const int64_t* __restrict__ T, int col, int64_t n, uint64_t* st, int64_t ll,
+                                    int64_t rr, int64_t tll, int64_t trr) {
+  const int64_t tmp = rand_max(st, n - (rr - ll + 1));
+  if (tmp < tll) return tmp;
+  if (tmp > trr - rr + ll - 1) return tmp + rr - ll + 1;
+  int64_t lef = ll, rig = rr + 1, mid;
+  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + col] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
+  return tmp + lef - ll + 1;
+}
+
 // corrupt_head (Corrupt.h:7-43): uniform entity not among the known TAILS of (h, r),
 // found by skipping the sorted tails of the (h, r) block of trainHead.
 __device__ int64_t corrupt_head(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_head,
                                 const int64_t* __restrict__ rig_head, int64_t n_ent, uint64_t* st, int64_t h,
                                 int64_t r) {
-  int64_t lef, rig, mid, ll, rr;
+  int64_t ll, rr;
   key_block(T, 1, lef_head[h], rig_head[h], r, ll, rr);
-  const int64_t tmp = rand_max(st, n_ent - (rr - ll + 1));
-  if (tmp < T[3 * ll + 2]) return tmp;
-  if (tmp > T[3 * rr + 2] - rr + ll - 1) return tmp + rr - ll + 1;
-  lef = ll; rig = rr + 1;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
-  return tmp + lef - ll + 1;
+  return corrupt_in_block(T, 2, n_ent, st, ll, rr, T[3 * ll + 2], T[3 * rr + 2]);
 }
 
 // corrupt_tail (Corrupt.h:45-81): uniform entity not among the known HEADS of (t, r);
@@ -75,14 +83,31 @@ __device__ int64_t corrupt_head(const int64_t* __restrict__ T, const int64_t* __
 __device__ int64_t corrupt_tail(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_tail,
                                 const int64_t* __restrict__ rig_tail, int64_t n_ent, uint64_t* st, int64_t t,
                                 int64_t r) {
-  int64_t lef, rig, mid, ll, rr;
+  int64_t ll, rr;
   key_block(T, 1, lef_tail[t], rig_tail[t], r, ll, rr);
-  const int64_t tmp = rand_max(st, n_ent - (rr - ll + 1));
-  if (tmp < T[3 * ll + 0]) return tmp;
-  if (tmp > T[3 * rr + 0] - rr + ll - 1) return tmp + rr - ll + 1;
-  lef = ll; rig = rr + 1;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 0] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
-  return tmp + lef - ll + 1;
+  return corrupt_in_block(T, 0, n_ent, st, ll, rr, T[3 * ll + 0], T[3 * rr + 0]);
+}
+
+// Per train row i (h, r, t): the (h, r) block of head_hrt with its first / last tail and the
+// (t, r) block of tail_hrt with its first / last head -- what corrupt_head / corrupt_tail find
+// before their draw -- as int32 [i][8]. Built once per train index, it shortens a sampled
+// row's chain of dependent loads to seeds -> train row -> its blocks (-> rarely the skip).
+__global__ __launch_bounds__(256) void k_sampler_blocks(const int64_t* __restrict__ train_list, int64_t n,
+                                                        const int64_t* __restrict__ head_hrt,
+                                                        const int64_t* __restrict__ tail_hrt,
+                                                        const int64_t* __restrict__ lef_head,
+                                                        const int64_t* __restrict__ rig_head,
+                                                        const int64_t* __restrict__ lef_tail,
+                                                        const int64_t* __restrict__ rig_tail, int32_t* __restrict__ blk) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t h = train_list[3 * i], r = train_list[3 * i + 1], t = train_list[3 * i + 2];
+  int64_t ll, rr, tl, tr;
+  key_block(head_hrt, 1, lef_head[h], rig_head[h], r, ll, rr);
+  key_block(tail_hrt, 1, lef_tail[t], rig_tail[t], r, tl, tr);
+  int4* o = reinterpret_cast<int4*>(blk + 8 * i);
+  o[0] = make_int4((int)ll, (int)rr, (int)head_hrt[3 * ll + 2], (int)head_hrt[3 * rr + 2]);
+  o[1] = make_int4((int)tl, (int)tr, (int)tail_hrt[3 * tl + 0], (int)tail_hrt[3 * tr + 0]);
 }
 
 // corrupt_rel with p == false (Corrupt.h:85-162); T rows (h, r, t) sorted by (h, t, r).
@@ -110,8 +135,9 @@ __global__ __launch_bounds__(256) void k_sampler_openke(
     const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
     const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
     const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* __restrict__ seeds,
-    int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, int64_t* __restrict__ bh,
-    int64_t* __restrict__ bt, int64_t* __restrict__ br, float* __restrict__ by) {
+    int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk,
+    int64_t n_blk, int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br,
+    float* __restrict__ by) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= B * (1 + neg + neg_rel)) return;
   const int64_t b = row % B, j = row / B;  // j = 0: the positive; 1..neg: entity negatives; then relation ones
@@ -139,10 +165,18 @@ __global__ __launch_bounds__(256) void k_sampler_openke(
     } else {
       replace_tail = mode != -1;
     }
+    // the kept (entity, relation)'s block: from the per-train-row table when there is one
+    const bool pre = i < n_blk;
+    int4 kb = make_int4(0, 0, 0, 0);
+    if (pre) kb = reinterpret_cast<const int4*>(blk + 8 * i)[replace_tail ? 0 : 1];
     if (replace_tail) {  // corrupt_head returns a replacement TAIL (Base.cpp:116)
-      bh[row] = h; bt[row] = corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r); br[row] = r;
+      bh[row] = h; br[row] = r;
+      bt[row] = pre ? corrupt_in_block(head_hrt, 2, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
+                    : corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r);
     } else {
-      bh[row] = corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r); bt[row] = t; br[row] = r;
+      bt[row] = t; br[row] = r;
+      bh[row] = pre ? corrupt_in_block(tail_hrt, 0, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
+                    : corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r);
     }
   } else {
     const int64_t k = j - 1 - neg;
@@ -250,14 +284,14 @@ extern "C" int mmre_sampler_advance_device(uint64_t* d_seeds, int64_t work_threa
   return MMRE_OK;
 }
 
-extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+extern "C" int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
                                    const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
                                    const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
                                    const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
                                    const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
                                    int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
-                                   int64_t mode, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
-                                   float* d_batch_y, void* stream) {
+                                   int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
+                                   int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, void* stream) {
   if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
       !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y)
     return MMRE_ERR_ARG;
@@ -266,14 +300,45 @@ extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_to
   if (train_total <= 0 || n_ent <= 1 || work_threads <= 0 || batch_size <= 0 || neg_rate < 0 || neg_rel_rate < 0)
     return MMRE_ERR_ARG;
   if (mode < -1 || mode > 1) return MMRE_ERR_ARG;
+  if (n_blocks < 0 || (n_blocks > 0 && !d_blocks)) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const int threads = 256;
   const int64_t rows = batch_size * (1 + neg_rate + neg_rel_rate);
   hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((rows + threads - 1) / threads)), dim3(threads), 0, st,
                      d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
                      d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
-                     work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_batch_h, d_batch_t, d_batch_r,
-                     d_batch_y);
+                     work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
+                     d_batch_t, d_batch_r, d_batch_y);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                   const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
+                                   int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                                   int64_t mode, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
+                                   float* d_batch_y, void* stream) {
+  return mmre_sampler_openke_blocked(d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head,
+                                     d_rig_head, d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean,
+                                     d_right_mean, n_ent, n_rel, d_seeds, work_threads, batch_size, neg_rate,
+                                     neg_rel_rate, mode, nullptr, 0, d_batch_h, d_batch_t, d_batch_r, d_batch_y,
+                                     stream);
+}
+
+extern "C" int mmre_sampler_blocks(const int64_t* d_train_list, int64_t n_train, const int64_t* d_head_hrt,
+                                   const int64_t* d_tail_hrt, const int64_t* d_lef_head, const int64_t* d_rig_head,
+                                   const int64_t* d_lef_tail, const int64_t* d_rig_tail, int32_t* d_blocks,
+                                   void* stream) {
+  if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
+      !d_blocks || n_train <= 0)
+    return MMRE_ERR_ARG;
+  if (n_train > INT32_MAX) return MMRE_ERR_SHAPE;  // int32 block rows
+  hipLaunchKernelGGL(k_sampler_blocks, dim3((unsigned)((n_train + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_train_list, n_train, d_head_hrt, d_tail_hrt, d_lef_head, d_rig_head, d_lef_tail, d_rig_tail,
+                     d_blocks);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }

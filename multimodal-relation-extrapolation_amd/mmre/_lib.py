@@ -37,6 +37,9 @@ SIGNATURES = {
     "mmre_sampler_draws_per_positive": (I64, [I64, I64, I64]),
     "mmre_sampler_openke": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64, I64,
                                   P, P, P, P, P]),
+    "mmre_sampler_blocks": (I32, [P, I64, P, P, P, P, P, P, P, P]),
+    "mmre_sampler_openke_blocked": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64,
+                                          I64, P, I64, P, P, P, P, P]),
     "mmre_sampler_repo": (I32, [P, P, P, I64, I64, I64, P, I64, P, P, P, I64, P, P, P, I64, ctypes.c_uint64, I32,
                                 P, P, P, P]),
     "mmre_ns_workspace": (I64, [I64, I64]),

@@ -38,6 +38,14 @@ class OpenKESampler:
         self._d = {k: to(getattr(ix, k)) for k in ("train_list", "head_hrt", "tail_hrt", "rel_hrt", "lef_head",
                                                    "rig_head", "lef_tail", "rig_tail", "lef_rel", "rig_rel",
                                                    "left_mean", "right_mean")}
+        # each train row's (h, r) / (t, r) blocks, looked up once here instead of by two binary
+        # searches per sampled negative (mmre_sampler_blocks)
+        d = self._d
+        self._n_blocks = int(ix.train_list.shape[0])
+        self._blocks = torch.empty((self._n_blocks, 8), dtype=torch.int32, device=self.device)
+        call("mmre_sampler_blocks", ptr(d["train_list"]), self._n_blocks, ptr(d["head_hrt"]), ptr(d["tail_hrt"]),
+             ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]), ptr(d["rig_tail"]), ptr(self._blocks),
+             stream_ptr(self.device))
 
     @property
     def seeds(self) -> np.ndarray:
@@ -59,12 +67,13 @@ class OpenKESampler:
                        batch_r=torch.empty(n, dtype=torch.int64, device=dev),
                        batch_y=torch.empty(n, dtype=torch.float32, device=dev))
         d = self._d
-        call("mmre_sampler_openke", ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]), ptr(d["tail_hrt"]),
-             ptr(d["rel_hrt"]), ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]), ptr(d["rig_tail"]),
-             ptr(d["lef_rel"]), ptr(d["rig_rel"]), ptr(d["left_mean"]) if self.bern else None,
+        call("mmre_sampler_openke_blocked", ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]),
+             ptr(d["tail_hrt"]), ptr(d["rel_hrt"]), ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]),
+             ptr(d["rig_tail"]), ptr(d["lef_rel"]), ptr(d["rig_rel"]), ptr(d["left_mean"]) if self.bern else None,
              ptr(d["right_mean"]) if self.bern else None, self.index.n_ent, self.index.n_rel,
              ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel), int(mode),
-             ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]), ptr(out["batch_y"]), stream_ptr(dev))
+             ptr(self._blocks), self._n_blocks, ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]),
+             ptr(out["batch_y"]), stream_ptr(dev))
         # the per-thread LCG states advance by a fixed number of draws per positive: on the device,
         # behind the sampling kernel on the same stream (no host copy per batch), and on the mirror
         call("mmre_sampler_advance_device", ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel),
