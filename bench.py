@@ -406,7 +406,8 @@ def bench_ns(args, world, rank, dev, dist):
     ent = w["ent"].to(dev).requires_grad_(True)
     rel = w["rel"].to(dev).requires_grad_(True)
     spec = NSSpec("transe", d, norm_flag=True)
-    opt = torch.optim.SGD([ent, rel], lr=1.0)
+    from mmre.optim import SGD
+    opt = SGD([ent, rel], lr=1.0)  # OpenKE Trainer's optimizer: one HIP launch per step
     n_rows = B * (1 + k)
     bufs = [dict(batch_h=torch.empty(n_rows, dtype=torch.int64, device=dev),
                  batch_t=torch.empty(n_rows, dtype=torch.int64, device=dev),

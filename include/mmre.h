@@ -214,6 +214,13 @@ int mmre_sampler_repo(const int64_t* d_eh, const int64_t* d_et, const int64_t* d
                       const int64_t* d_tf_off, const int64_t* d_tf_vals, int64_t tf_n, uint64_t seed,
                       int filter_flag, int64_t* d_out_h, int64_t* d_out_t, int64_t* d_out_r, void* stream);
 
+/* Plain SGD step p <- p - lr * g (one fma per element) over `count` <= 8 float32 tensors in
+ * one launch; params[t] / grads[t] 16-B aligned, numel[t] elements each. Replaces the
+ * reference optimizer's step (optim.SGD without momentum / weight decay, OpenKE
+ * Trainer.py:82-86) after the fused gradient. */
+int mmre_sgd_step(float* const* params, const float* const* grads, const int64_t* numel, int count, float lr,
+                  void* stream);
+
 /* ====================================================================== *
  *  Negative-sampling margin loss, fused (OpenKE strategy/NegativeSampling *
  *  .py:23-32 + loss/MarginLoss.py:24-28 + model forward/regularization;   *

@@ -42,6 +42,7 @@ SIGNATURES = {
                                           I64, P, I64, P, P, P, P, P]),
     "mmre_sampler_repo": (I32, [P, P, P, I64, I64, I64, P, I64, P, P, P, I64, P, P, P, I64, ctypes.c_uint64, I32,
                                 P, P, P, P]),
+    "mmre_sgd_step": (I32, [P, P, P, I32, F32, P]),
     "mmre_ns_workspace": (I64, [I64, I64]),
     "mmre_ns_forward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
                               P]),

@@ -108,7 +108,8 @@ def train_transe(w, device, steps: int = 300, batch: int = 2721, neg: int = 25, 
     ent = w["ent"].to(dev).clone().requires_grad_(True)
     rel = w["rel"].to(dev).clone().requires_grad_(True)
     spec = NSSpec("transe", w["dim"], norm_flag=bool(w.get("norm_flag", True)))
-    opt = torch.optim.SGD([ent, rel], lr=lr)
+    from .optim import SGD
+    opt = SGD([ent, rel], lr=lr)
     loss = None
     for _ in range(int(steps)):
         b = smp.sample(batch, neg)

@@ -53,7 +53,8 @@ class Trainer(object):
             return optim.Adadelta(p, lr=self.alpha, weight_decay=self.weight_decay)
         if m == "adam":
             return optim.Adam(p, lr=self.alpha, weight_decay=self.weight_decay)
-        return optim.SGD(p, lr=self.alpha, weight_decay=self.weight_decay)
+        from mmre.optim import SGD  # plain SGD: one HIP launch over the tables (torch's step otherwise)
+        return SGD(p, lr=self.alpha, weight_decay=self.weight_decay)
 
     def run(self):
         if self.use_gpu:

@@ -151,3 +151,34 @@ def test_repo_negative_sampling_loss(golden):
     torch.cuda.synchronize()
     assert abs(loss.item() - float(g["struct_loss"])) < 1e-4 * max(1, abs(float(g["struct_loss"])))
     assert np.allclose(score.cpu().numpy(), g["score"], rtol=1e-4, atol=1e-4)
+
+
+def test_hip_sgd_step_matches_torch():
+    """mmre.optim.SGD: the plain step is one HIP launch (mmre_sgd_step) over up to 8 tensors
+    per launch, float4 streams with a scalar tail; p - lr g within one rounding of torch's
+    (the fma vs torch's separate multiply-add); momentum / weight decay run torch's own step."""
+    from mmre.optim import SGD
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    shapes = [(14208, 200), (235, 200), (7,), (1, 5), (1031,)] + [(33, 3)] * 6   # 11 tensors: 2 launches
+    ref = [torch.randn(s, generator=g).to(dev) for s in shapes]
+    mine = [r.clone() for r in ref]
+    grads = [torch.randn(s, generator=g).to(dev) for s in shapes]
+    for ps in (ref, mine):
+        for p, gr in zip(ps, grads):
+            p.grad = gr.clone()
+    torch.optim.SGD(ref, lr=0.37).step()
+    SGD(mine, lr=0.37).step()
+    torch.cuda.synchronize()
+    for a, b in zip(ref, mine):
+        assert torch.allclose(a, b, rtol=2e-7, atol=1e-7), (a - b).abs().max()
+    # options the kernel does not cover: torch's own step, bit for bit
+    ref2 = [r.clone() for r in ref]
+    mine2 = [r.clone() for r in ref]
+    for ps in (ref2, mine2):
+        for p, gr in zip(ps, grads):
+            p.grad = gr.clone()
+    torch.optim.SGD(ref2, lr=0.1, momentum=0.9, weight_decay=0.01).step()
+    SGD(mine2, lr=0.1, momentum=0.9, weight_decay=0.01).step()
+    for a, b in zip(ref2, mine2):
+        assert torch.equal(a, b)
