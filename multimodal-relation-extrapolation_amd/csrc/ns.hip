@@ -874,7 +874,7 @@ __device__ __forceinline__ float wave_sum_u(float v) {
 
 // One positive's workgroup. GEN = false (k_ns_transe_fused, every positive): the OpenKE batch
 // shape, each negative sharing two of the positive's rows; a positive with any other negative
-// is appended to the `defer` list untouched, before anything is written. GEN = true
+// is appended to the `defer` list after the forward (only its scores written, all rewritten). GEN = true
 // (k_ns_transe_fused_generic, the deferred positives only): also the generic-row path. The
 // split keeps the generic path's registers out of the fast instance (122 -> ~90 VGPRs).
 template <int NC, bool L2, bool GEN>
@@ -922,19 +922,11 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       else if (!(oh && ot && orr)) code[u] = 4;  // shares less than two rows: generic path
     }
   }
-  if constexpr (!GEN) {  // any generic row in this positive: defer it whole to the generic instance
+  if constexpr (!GEN) {  // a generic row in this wave: the positive is deferred after the forward barrier
     bool gen = false;
 #pragma unroll
     for (int u = 0; u < NSF_MAXJ; ++u) gen |= code[u] == 4;
     if (lane == 0) s_gen[w] = gen;
-    __syncthreads();
-    bool any = false;
-#pragma unroll
-    for (int i = 0; i < NSW; ++i) any |= s_gen[i] != 0;
-    if (any) {
-      if (threadIdx.x == 0) defer[1 + atomicAdd(defer, 1)] = (int32_t)b;
-      return;
-    }
   }
   const float ch = nf ? fmaxf(nph, 1e-12f) : 1.0f, cr = nf ? fmaxf(npr, 1e-12f) : 1.0f;
   const float ct = nf ? fmaxf(npt, 1e-12f) : 1.0f;
@@ -986,6 +978,18 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   }
   if (lane == 0) { s_sq[w][0] = qh; s_sq[w][1] = qt; s_sq[w][2] = qr; }
   __syncthreads();
+  if constexpr (!GEN) {
+    // any generic row in this positive: hand it whole to the generic instance. Nothing but its
+    // scores was written (those of its generic rows are meaningless here), and the generic
+    // instance, which runs after this kernel, rewrites every score of the positive.
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NSW; ++i) any |= s_gen[i] != 0;
+    if (any) {
+      if (threadIdx.x == 0) defer[1 + atomicAdd(defer, 1)] = (int32_t)b;
+      return;
+    }
+  }
   if (w == 0) {  // loss partial and d(loss)/d(forward score) of every row, per unit upstream gradient
     const float m = A.loss_margin;
     const bool have = lane < A.K;
