@@ -541,7 +541,9 @@ def bench_ns(args, world, rank, dev, dist):
                             "step_forward_ms": fwd_ms, "step_backward_ms": bwd_ms,
                             "note": "no float atomics: the gradient contributions are bucketed by table row and "
                                     "one wave per table row summing them in batch order (bit-reproducible); the "
-                                    "rest of the step is the sampler and SGD"},
+                                    "rest of the step is the sampler and SGD. The fused call is a chain of six "
+                                    "short kernels over ~74 MB of gathers (9 us at the HBM peak): latency-bound, "
+                                    "its largest kernel k_ns_transe_fused ~45 us (profiles/r2/ns_kernel_stats.csv)"},
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
