@@ -617,8 +617,11 @@ __global__ __launch_bounds__(64) void k_filter_count(const int64_t* __restrict__
 // units +-1, so no XCD runs a whole extra round of units (C3: 100 entity tiles = 8 x 12 + 4;
 // whole-tile groups of 12 and 13 left the 13-tile XCDs 10 units per workgroup against 8.7).
 struct UnitMap {
-  int m, r, ex0, el0, n_main, lo0, count;
-  __device__ __forceinline__ UnitMap(int grp, int n_groups, int n_qt, int n_et) {
+  int m, r, ex0, el0, n_main, lo0, count, nq;
+  bool emajor;  // entity-tile-major order inside the group (consecutive units share an entity tile)
+  __device__ __forceinline__ UnitMap(int grp, int n_groups, int n_qt, int n_et, bool emajor_ = false) {
+    nq = n_qt;
+    emajor = emajor_;
     m = n_et / n_groups;
     r = n_et - m * n_groups;
     ex0 = grp * m;
@@ -631,8 +634,13 @@ struct UnitMap {
   // unit i (< count) of the group -> (query tile, entity tile)
   __device__ __forceinline__ void at(int i, int& qt, int& et) const {
     if (i < n_main) {
-      qt = i / m;
-      et = ex0 + i % m;
+      if (emajor) {
+        qt = i % nq;
+        et = ex0 + i / nq;
+      } else {
+        qt = i / m;
+        et = ex0 + i % m;
+      }
     } else {
       const int j = lo0 + (i - n_main);
       qt = j / r;
@@ -920,7 +928,7 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
     int64_t q_pad, int64_t n_query, int ktot, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
     const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
-    int32_t* __restrict__ counts, float* __restrict__ scores) {
+    int32_t* __restrict__ counts, float* __restrict__ scores, int emajor) {
   static_assert(KS == 16 || KS == 32, "stage of 16 or 32 K rows");
   // 16-row stages (33 KB of LDS) run 4 workgroups per CU: the row counters then live one row
   // per lane (ballot counts), which frees the 32 registers of per-lane row counters
@@ -938,7 +946,7 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
   const int lrow = lane >> 5, lcol = lane & 31;
   const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
   const int per_grp = gridDim.x / n_groups;
-  const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et);
+  const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et, emajor != 0);
   const int u0 = (int)((int64_t)gmem * um.count / per_grp);
   const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
   if (u0 >= u1) return;  // uniform over the workgroup
@@ -1463,6 +1471,14 @@ static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent
   const int ks_force = ks_env ? atoi(ks_env) : 0;
   const bool ks32 = ks_force == 32 || (ks_force != 16 && (tc || store));
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
+  // Units entity-tile-major inside each XCD group when the entity planes outgrow the caches
+  // (> 64 MB; the 256 MB MALL also holds the query planes): a workgroup's consecutive units then
+  // share its entity tile (L2-resident) and sweep the query tiles, which stay MALL-resident, so
+  // the table streams from HBM about once instead of once per query tile (C5, a 1 GB table:
+  // 35.8 -> 34.5 ms on one box, 60 -> ~1 GB of entity reads per launch); C3's 20 MB planes keep
+  // the query-major order (0.979 vs 0.982 ms).
+  static const char* order_env = getenv("MMRE_MFMA_EMAJOR"); /* experiments: 0 / 1 force the order */
+  const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
 #define MMRE_MFMA_K(KERNEL)                                                                                       \
   do {                                                                                                            \
     /* 16 units per workgroup, between 1 (2 with 32-row stages) and 8 x the resident slots:    */                \
@@ -1477,7 +1493,7 @@ static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL(KERNEL, dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,       \
                        n_query, ktot, n_et, e_base, ng, pred_kind, margin, d_truth, d_qr, d_qmode, d_type_head,  \
-                       d_type_tail, tw, d_counts, d_scores);                                                      \
+                       d_type_tail, tw, d_counts, d_scores, emajor);                                              \
   } while (0)
 #define MMRE_MFMA(TCV, STV, PKV)                                                                           \
   do {                                                                                                 \
