@@ -72,9 +72,10 @@ def bytes_per_triple(model, dim):
 
 def valu_ops_per_triple(model, dim):
     """VALU issue slots per scored triple in the sweep's inner loop: TransE L1
-    sub + add; RotatE 2 sub, 4 mul, 2 add, 2 fma, 3/4 of a min for the tiny-input check, and
-    v_rsq_f32 at quarter rate = 4 slots (measured, scripts/probes/trans_rate.hip)."""
-    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 16.75 * dim}.get(model)
+    sub + add; RotatE 15.75: the round-1 count of 16.75 (12 f32 ops, 3/4 of a min for the
+    tiny-input check, v_rsq_f32 at quarter rate = 4 slots, measured by
+    scripts/probes/trans_rate.hip) less the add that v = fma(di, di, dr*dr) folds away."""
+    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 15.75 * dim}.get(model)
 
 
 KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
