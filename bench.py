@@ -72,10 +72,11 @@ def bytes_per_triple(model, dim):
 
 def valu_ops_per_triple(model, dim):
     """VALU issue slots per scored triple in the sweep's inner loop: TransE L1
-    sub + add; RotatE 15.75: the round-1 count of 16.75 (12 f32 ops, 3/4 of a min for the
+    sub + add; RotatE 15.5: the round-1 count of 16.75 (12 f32 ops, 3/4 of a min for the
     tiny-input check, v_rsq_f32 at quarter rate = 4 slots, measured by
-    scripts/probes/trans_rate.hip) less the add that v = fma(di, di, dr*dr) folds away."""
-    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 15.75 * dim}.get(model)
+    scripts/probes/trans_rate.hip) less the add that v = fma(di, di, dr*dr) folds away and
+    a quarter min (the check is one v_min3 per two elements)."""
+    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 15.5 * dim}.get(model)
 
 
 KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",

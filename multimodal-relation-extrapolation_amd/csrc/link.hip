@@ -791,7 +791,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
-              lo = min(lo, min(__float_as_uint(v[j]), __float_as_uint(v[j + 1])));  // v >= 0: bit order
+              lo = min(min(lo, __float_as_uint(v[j])), __float_as_uint(v[j + 1]));  // v >= 0: bit order; one v_min3
               acc[i][j] = acc[i][j] + rot_mag(v[j], y[j]);
               acc[i][j + 1] = acc[i][j + 1] + rot_mag(v[j + 1], y[j + 1]);
             }
