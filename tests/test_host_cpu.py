@@ -242,3 +242,24 @@ def test_entity_slices_and_restricted_filter_lists():
             ids = p[3][p[2][g]:p[2][g + 1]]
             assert np.all((ids >= e0) & (ids < e1))
             assert np.all(p[4][p[2][g]:p[2][g + 1]] == full[0][g] * 0 + full[1][full[0][g]])
+
+
+def test_sgd_routes_only_plain_cuda_steps_to_hip():
+    """mmre.optim.SGD is torch.optim.SGD wherever the HIP step does not apply (host tensors,
+    momentum, weight decay): bit-identical to torch there; the eligibility test itself."""
+    import torch
+    from mmre.optim import SGD
+    g = torch.Generator().manual_seed(0)
+    for kw in ({}, {"momentum": 0.9}, {"weight_decay": 0.01}, {"momentum": 0.5, "nesterov": True}):
+        a = [torch.randn(37, 5, generator=g), torch.randn(11, generator=g)]
+        b = [x.clone() for x in a]
+        for ps in (a, b):
+            for p in ps:
+                p.grad = torch.ones_like(p) * 0.25
+        torch.optim.SGD(a, lr=0.3, **kw).step()
+        SGD(b, lr=0.3, **kw).step()
+        assert all(torch.equal(x, y) for x, y in zip(a, b)), kw
+    opt = SGD([torch.zeros(3, requires_grad=True)], lr=0.1)
+    assert opt._plain(opt.param_groups[0])
+    assert not opt._plain(dict(opt.param_groups[0], momentum=0.9))
+    assert not opt._plain(dict(opt.param_groups[0], weight_decay=1e-4))
