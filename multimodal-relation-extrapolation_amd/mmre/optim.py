@@ -21,7 +21,8 @@ class SGD(torch.optim.SGD):
     def _eligible(self, group, ps) -> bool:
         return self._plain(group) and all(
             p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and not p.grad.is_sparse
-            and p.grad.dtype == torch.float32 and p.grad.is_contiguous() for p in ps)
+            and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
+            and p.data_ptr() % 16 == 0 and p.grad.data_ptr() % 16 == 0 for p in ps)  # float4 streams
 
     @torch.no_grad()
     def step(self, closure=None):
