@@ -799,13 +799,15 @@ __device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ 
 }
 
 // Pre-pass of the fused launch, one wave per row over the entity rows then the relation
-// rows: the row's L2 norm (one scalar per row instead of a wave reduction per use), and the
-// row's slot count zeroed (and the deferred-positive count).
+// rows: the row's L2 norm (one scalar per row instead of a wave reduction per use), with
+// norm_flag the normalised row itself, x / max(|x|, eps) (the fused kernel's operands, so it
+// divides nothing), and the row's slot count zeroed (and the deferred-positive count).
 // (A last-workgroup loss reduction inside the fused kernel was tried instead of k_ns_reduce:
 // its per-workgroup device-scope fence writes back the XCD's L2 each time, 0.12 -> 0.19 ms.)
 __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
                                                     const float* __restrict__ rel, int64_t n_rel, int d,
                                                     float* __restrict__ nrm_e, float* __restrict__ nrm_r,
+                                                    float* __restrict__ ent_n, float* __restrict__ rel_n,
                                                     int32_t* __restrict__ counts, int32_t* __restrict__ defer) {
   if (blockIdx.x == 0 && threadIdx.x == 0) defer[0] = 0;  // no deferred positives yet
   const int lane = threadIdx.x & 63;
@@ -814,10 +816,38 @@ __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ en
   if (lane == 0) counts[row] = 0;  // the row's slot bucket, for this call
   const bool is_ent = row < n_ent;
   const float* p = (is_ent ? ent : rel) + (is_ent ? row : row - n_ent) * d;
+  float* o = ent_n ? (is_ent ? ent_n : rel_n) + (is_ent ? row : row - n_ent) * d : nullptr;
   float s = 0.0f;
+  if (d <= 8 * kWave) {  // the fused path's rows (d <= 512): read once into registers
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int i = lane + c * kWave;
+      v[c] = i < d ? p[i] : 0.0f;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) s += v[c] * v[c];  // same order as the strided loop below
+    s = wave_sum(s);
+    const float nr = sqrtf(s);
+    if (lane == 0) (is_ent ? nrm_e : nrm_r)[is_ent ? row : row - n_ent] = nr;
+    if (o) {
+      const float cn = fmaxf(nr, 1e-12f);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int i = lane + c * kWave;
+        if (i < d) o[i] = v[c] / cn;
+      }
+    }
+    return;
+  }
   for (int i = lane; i < d; i += kWave) s += p[i] * p[i];
   s = wave_sum(s);
-  if (lane == 0) (is_ent ? nrm_e : nrm_r)[is_ent ? row : row - n_ent] = sqrtf(s);
+  const float nr = sqrtf(s);
+  if (lane == 0) (is_ent ? nrm_e : nrm_r)[is_ent ? row : row - n_ent] = nr;
+  if (o) {
+    const float cn = fmaxf(nr, 1e-12f);
+    for (int i = lane; i < d; i += kWave) o[i] = p[i] / cn;
+  }
 }
 
 // lane src's 64-bit value as a wave-uniform (scalar) value; src must be wave-uniform
@@ -881,7 +911,8 @@ template <int NC, bool L2, bool GEN>
 __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __restrict__ nrm_e,
                                               const float* __restrict__ nrm_r, float* __restrict__ score,
                                               float* __restrict__ part, const NSSlots& S, int64_t n_ent, int64_t b,
-                                              int32_t* __restrict__ defer) {
+                                              int32_t* __restrict__ defer, const float* __restrict__ ent_n,
+                                              const float* __restrict__ rel_n) {
   __shared__ int s_gen[NSW];
   __shared__ float s_n[NSW * NSF_MAXJ];
   __shared__ float s_c[NSW * NSF_MAXJ];
@@ -891,7 +922,6 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   __shared__ float s_occ[NSW][3];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d = A.dim;
-  const int nf = A.norm_flag;
   const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
   // this wave's negatives j = w + NSW u, u < nj; lane u holds negative u's row ids
   const int nj = w < A.K ? (int)((A.K - w + NSW - 1) / NSW) : 0;
@@ -900,10 +930,11 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     const int64_t row = b + (w + NSW * (int64_t)lane + 1) * A.B;
     my_h = A.h[row]; my_t = A.t[row]; my_r = A.r[row];
   }
-  Vec<NC> Ph, Pr, Pt;
-  vload_row(Ph, A.ent, ph, d, lane);
-  vload_row(Pr, A.rel, pr, d, lane);
-  vload_row(Pt, A.ent, pt, d, lane);
+  // the rows as the model uses them: normalised by the pre-pass (norm_flag), else the tables
+  Vec<NC> hn, rn, tn;
+  vload_row(hn, ent_n, ph, d, lane);
+  vload_row(rn, rel_n, pr, d, lane);
+  vload_row(tn, ent_n, pt, d, lane);
   const float nph = nrm_e[ph], npr = nrm_r[pr], npt = nrm_e[pt];
   // issue every corrupted-row load of the wave before any arithmetic
   Vec<NC> C[NSF_MAXJ];
@@ -916,9 +947,9 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     if (u < nj) {
       const int64_t h = readlane64u(my_h, u), t = readlane64u(my_t, u), r = readlane64u(my_r, u);
       const bool oh = h == ph, ot = t == pt, orr = r == pr;
-      if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], A.ent, h, d, lane); cnr[u] = nrm_e[h]; }
-      else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], A.ent, t, d, lane); cnr[u] = nrm_e[t]; }
-      else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], A.rel, r, d, lane); cnr[u] = nrm_r[r]; }
+      if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], ent_n, h, d, lane); cnr[u] = nrm_e[h]; }
+      else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], ent_n, t, d, lane); cnr[u] = nrm_e[t]; }
+      else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], rel_n, r, d, lane); cnr[u] = nrm_r[r]; }
       else if (!(oh && ot && orr)) code[u] = 4;  // shares less than two rows: generic path
     }
   }
@@ -928,10 +959,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     for (int u = 0; u < NSF_MAXJ; ++u) gen |= code[u] == 4;
     if (lane == 0) s_gen[w] = gen;
   }
-  const float ch = nf ? fmaxf(nph, 1e-12f) : 1.0f, cr = nf ? fmaxf(npr, 1e-12f) : 1.0f;
-  const float ct = nf ? fmaxf(npt, 1e-12f) : 1.0f;
-  Vec<NC> hn, rn, tn, x;
-  vnorm(hn, Ph, ch); vnorm(rn, Pr, cr); vnorm(tn, Pt, ct);
+  Vec<NC> x;
   float p_raw = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
   if (L2) p_raw = sqrtf(p_raw);
   const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
@@ -963,8 +991,6 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       n = row_fwd<NC, L2>(A, R, lane);
       qh += R.sh; qt += R.st; qr += R.sr;
     } else {
-      const float cc = nf ? fmaxf(cnr[u], 1e-12f) : 1.0f;
-      if (code[u] != 3) vnorm(C[u], C[u], cc);  // normalised in place: the gradient pass reuses it
       float sv = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
       if (L2) sv = sqrtf(sv);
       sraw[u] = sv;
@@ -1130,8 +1156,9 @@ template <int NC, bool L2>
 __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
                                                          const float* __restrict__ nrm_r, float* __restrict__ score,
                                                          float* __restrict__ part, NSSlots S, int64_t n_ent,
-                                                         int32_t* __restrict__ defer) {
-  ns_fused_body<NC, L2, false>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, defer);
+                                                         int32_t* __restrict__ defer, const float* __restrict__ ent_n,
+                                                         const float* __restrict__ rel_n) {
+  ns_fused_body<NC, L2, false>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, defer, ent_n, rel_n);
 }
 
 // the deferred positives (defer[0] of them, ids from defer[1]); nothing to do for OpenKE batches
@@ -1140,10 +1167,12 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused_generic(NSArgs A, const
                                                                  const float* __restrict__ nrm_r,
                                                                  float* __restrict__ score, float* __restrict__ part,
                                                                  NSSlots S, int64_t n_ent,
-                                                                 const int32_t* __restrict__ defer) {
+                                                                 const int32_t* __restrict__ defer,
+                                                                 const float* __restrict__ ent_n,
+                                                                 const float* __restrict__ rel_n) {
   const int n = defer[0];
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
-    ns_fused_body<NC, L2, true>(A, nrm_e, nrm_r, score, part, S, n_ent, defer[1 + i], nullptr);
+    ns_fused_body<NC, L2, true>(A, nrm_e, nrm_r, score, part, S, n_ent, defer[1 + i], nullptr, ent_n, rel_n);
     __syncthreads();  // the body's LDS is reused by the next deferred positive
   }
 }
@@ -1482,7 +1511,7 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
 // norms, the slot contributions / occurrences / keys / bucket places, the per-row slot
 // counts, bucket offsets, the bucketed slot ids, the deferred positives.
 struct FusedWs {
-  int64_t part, nrm_e, nrm_r, shared, rec, mult, keys, pos, counts, offs, sslot, defer, total, slots;
+  int64_t part, nrm_e, nrm_r, ent_n, rel_n, shared, rec, mult, keys, pos, counts, offs, sslot, defer, total, slots;
   uint32_t sentinel;
 };
 
@@ -1495,6 +1524,8 @@ static void fused_ws(int64_t B, int64_t K, int64_t E, int64_t R, int d, FusedWs&
   w.part = o;    o = al64(o + 7 * B);
   w.nrm_e = o;   o = al64(o + E);
   w.nrm_r = o;   o = al64(o + R);
+  w.ent_n = o;   o = al64(o + E * d);
+  w.rel_n = o;   o = al64(o + R * d);
   w.shared = o;  o = al64(o + 3 * B * d);
   w.rec = o;     o = al64(o + K * B * (d > ns_rec_words(8, false, d) ? d : ns_rec_words(8, false, d)));
   w.mult = o;    o = al64(o + w.slots);
@@ -1543,8 +1574,13 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   int32_t* defer = reinterpret_cast<int32_t*>(d_work + w.defer);
   NSSlots S{d_work + w.shared, d_work + w.rec, d_work + w.mult, reinterpret_cast<uint32_t*>(d_work + w.keys),
             reinterpret_cast<int32_t*>(d_work + w.pos), counts, w.sentinel};
+  // norm_flag: the fused kernel reads the rows normalised by the pre-pass; else the tables
+  float* ent_n = norm_flag ? d_work + w.ent_n : nullptr;
+  float* rel_n = norm_flag ? d_work + w.rel_n : nullptr;
   hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
-                     n_rel, dim, nrm_e, nrm_r, counts, defer);
+                     n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, counts, defer);
+  const float* ent_u = norm_flag ? ent_n : d_ent;
+  const float* rel_u = norm_flag ? rel_n : d_rel;
   MMRE_CHECK_LAUNCH();
   const dim3 grid((unsigned)batch), blk(256);
   const bool l2 = model == MMRE_TRANSE_L2;
@@ -1554,14 +1590,14 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   do {                                                                                                           \
     if (l2) {                                                                                                    \
       hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,   \
-                         n_ent, defer);                                                                          \
+                         n_ent, defer, ent_u, rel_u);                                                                          \
       hipLaunchKernelGGL((k_ns_transe_fused_generic<NC_, true>), ggrid, blk, 0, st, A, nrm_e, nrm_r, d_score,    \
-                         part, S, n_ent, defer);                                                                 \
+                         part, S, n_ent, defer, ent_u, rel_u);                                                   \
     } else {                                                                                                     \
       hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,  \
-                         n_ent, defer);                                                                          \
+                         n_ent, defer, ent_u, rel_u);                                                                          \
       hipLaunchKernelGGL((k_ns_transe_fused_generic<NC_, false>), ggrid, blk, 0, st, A, nrm_e, nrm_r, d_score,   \
-                         part, S, n_ent, defer);                                                                 \
+                         part, S, n_ent, defer, ent_u, rel_u);                                                   \
     }                                                                                                            \
   } while (0)
   if (nc == 1) MMRE_NS_FUSED(1);
