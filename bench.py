@@ -545,7 +545,7 @@ def bench_ns(args, world, rank, dev, dist):
                                     "one wave per table row summing them in batch order (bit-reproducible); the "
                                     "rest of the step is the sampler and SGD. The fused call is a chain of six "
                                     "short kernels over ~74 MB of gathers (9 us at the HBM peak): latency-bound, "
-                                    "its largest kernel k_ns_transe_fused ~45 us (profiles/r2/ns_kernel_stats.csv)"},
+                                    "its largest kernel k_ns_transe_fused ~39 us (profiles/r2/ns_kernel_stats.csv)"},
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
