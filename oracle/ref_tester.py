@@ -27,7 +27,11 @@ Usage (a child process of bench.py: Base.so is C++ with unguarded indexing):
     python oracle/ref_tester.py <workdir>
 <workdir> holds the OpenKE files (entity2id / relation2id / train2id / valid2id / test2id),
 tables.npz (ent, rel[, ent_im, rel_im]) and meta.json (model, dim, norm_flag, margin,
-epsilon, threads); the result goes to <workdir>/result.npz.
+epsilon, threads[, summary, near_rel]); the result goes to <workdir>/result.npz. With
+``summary`` the score vectors are not kept (C5's would be 8 MB per sweep): per sweep it keeps
+the truth's reference score, max|s| and every other entity whose reference score lies within
+near_rel x max|s| of the truth's (ids + scores, CSR) -- the only entities whose side of the
+strict `<` a different summation order can flip (tests/golden/make_ref_parity.py).
 """
 from __future__ import annotations
 
@@ -172,6 +176,45 @@ def near_ties(scores, truth, tie_rel):
     return close.sum(1)
 
 
+def prepare_workdir(workdir: str, w: dict, th, tr, tt, **meta_extra):
+    """Write the OpenKE directory + tables + meta a Tester run over the sample (th, tr, tt)
+    needs: test2id = the sample; train2id = the workload's filter set minus one copy of each
+    sampled triple, so Base.so filters with exactly the triples the GPU evaluation filters
+    with; one valid triple, a copy of a sampled test triple (already in the filter set):
+    Reader.h:255-256 reads validList[0] unguarded, so an empty valid2id.txt crashes Base.so
+    intermittently."""
+    th, tr, tt = (np.asarray(x, np.int64) for x in (th, tr, tt))
+    fh, fr, ft = (np.asarray(w[k], np.int64) for k in ("filter_h", "filter_r", "filter_t"))
+    keep = np.ones(len(fh), bool)
+    key = (fh * w["n_rel"] + fr) * w["n_ent"] + ft
+    skey = (th * w["n_rel"] + tr) * w["n_ent"] + tt
+    pos = {}
+    for i, k in enumerate(key.tolist()):
+        pos.setdefault(k, i)
+    for k in skey.tolist():
+        if k in pos:
+            keep[pos.pop(k)] = False
+    trn = np.stack([fh[keep], ft[keep], fr[keep]], 1)
+    tst = np.stack([th, tt, tr], 1)
+    for name, arr in (("train2id.txt", trn), ("valid2id.txt", tst[:1]), ("test2id.txt", tst)):
+        with open(os.path.join(workdir, name), "w") as f:
+            f.write(f"{len(arr)}\n")
+            np.savetxt(f, arr, fmt="%d")
+    for name, cnt in (("entity2id.txt", w["n_ent"]), ("relation2id.txt", w["n_rel"])):
+        with open(os.path.join(workdir, name), "w") as f:
+            f.write(f"{cnt}\n")
+    as_np = lambda v: v.numpy() if hasattr(v, "numpy") else np.asarray(v)
+    tables = {"ent": as_np(w["ent"]), "rel": as_np(w["rel"])}
+    if "ent_im" in w:
+        tables.update(ent_im=as_np(w["ent_im"]), rel_im=as_np(w["rel_im"]))
+    np.savez(os.path.join(workdir, "tables.npz"), **tables)
+    meta = dict(model=w["model"], dim=w["dim"], norm_flag=bool(w.get("norm_flag", False)),
+                margin=w.get("margin"), epsilon=w.get("epsilon"))
+    meta.update(meta_extra)
+    with open(os.path.join(workdir, "meta.json"), "w") as f:
+        json.dump(meta, f)
+
+
 def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
     import torch
     with open(os.path.join(workdir, "meta.json")) as f:
@@ -203,8 +246,27 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
     ph, pt, pr = (np.zeros(E, np.int64) for _ in range(3))
     counts = np.zeros((2, n, 2), np.int64)       # [head|tail][query][raw, filt]
     q = np.zeros((n, 3), np.int64)               # (h, r, t) as Base.so's testList holds them
-    scores = np.zeros((2, n, E), np.float32)
+    summary = bool(meta.get("summary", False))
+    near_rel = float(meta.get("near_rel", 1e-5))
+    scores = None if summary else np.zeros((2, n, E), np.float32)
+    truth_s = np.zeros((2, n), np.float32)
+    smax = np.zeros((2, n), np.float32)
+    near_ids, near_cnt = [], np.zeros((2, n), np.int64)
+
+    def keep(side, idx, s, truth):
+        truth_s[side, idx] = s[truth]
+        smax[side, idx] = np.max(np.abs(s))
+        if scores is not None:
+            scores[side, idx] = s
+        else:
+            tol = near_rel * float(smax[side, idx])
+            j = np.flatnonzero(np.abs(s.astype(np.float64) - float(s[truth])) <= tol)
+            j = j[j != truth]
+            near_ids.append((side, idx, j.astype(np.int32), s[j]))
+            near_cnt[side, idx] = len(j)
+
     keys = (("l_rank", "l_filter_rank"), ("r_rank", "r_filter_rank"))
+    t_keep = 0.0
     t0 = time.perf_counter()
     with stdout_to_stderr():
         for idx in range(n):
@@ -215,7 +277,7 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             lib.testHead(s.ctypes.data, idx, 0)
             counts[0, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[0], before)]
             q[idx, 1], q[idx, 2] = pr[0], pt[0]
-            scores[0, idx] = s
+            head_s = s
             lib.getTailBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
             s = np.ascontiguousarray(predict(torch.from_numpy(ph[:1]), torch.from_numpy(pt),
                                              torch.from_numpy(pr[:1]), "tail_batch"), np.float32)
@@ -223,17 +285,30 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             lib.testTail(s.ctypes.data, idx, 0)
             counts[1, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[1], before)]
             q[idx, 0] = ph[0]
-            scores[1, idx] = s
+            k0 = time.perf_counter()
+            keep(0, idx, head_s, int(q[idx, 0]))   # the head sweep's truth is the tail batch's anchor
+            keep(1, idx, s, int(q[idx, 2]))
+            t_keep += time.perf_counter() - k0
         lib.test_link_prediction(0)
-        elapsed = time.perf_counter() - t0
+        elapsed = time.perf_counter() - t0 - t_keep
         metrics = np.array([lib.getTestLinkMRR(0), lib.getTestLinkMR(0), lib.getTestLinkHit10(0),
                             lib.getTestLinkHit3(0), lib.getTestLinkHit1(0)], np.float32)
-    ties = np.stack([near_ties(scores[0], q[:, 0], tie_rel), near_ties(scores[1], q[:, 2], tie_rel)])
     if not all(math.isfinite(float(m)) for m in metrics):
         raise RuntimeError("Base.so returned non-finite metrics")
-    out = dict(counts=counts, q=q, metrics=metrics, near_ties=ties, elapsed=np.float64(elapsed),
+    out = dict(counts=counts, q=q, metrics=metrics, elapsed=np.float64(elapsed),
                threads=np.int64(torch.get_num_threads()), n_ent=np.int64(E), tie_rel=np.float64(tie_rel),
-               scores=scores)
+               truth_scores=truth_s, score_absmax=smax)
+    if scores is not None:
+        out["scores"] = scores
+        out["near_ties"] = np.stack([near_ties(scores[0], q[:, 0], tie_rel), near_ties(scores[1], q[:, 2], tie_rel)])
+    else:
+        # near lists in sweep order [head sweeps 0..n-1 | tail sweeps 0..n-1]
+        near_ids.sort(key=lambda x: (x[0], x[1]))
+        out["near_off"] = np.r_[0, np.cumsum(near_cnt.reshape(-1))].astype(np.int64)
+        out["near_ids"] = (np.concatenate([x[2] for x in near_ids]) if near_ids else np.zeros(0, np.int32))
+        out["near_scores"] = (np.concatenate([x[3] for x in near_ids]) if near_ids else np.zeros(0, np.float32))
+        out["near_rel"] = np.float64(near_rel)
+        out["near_ties"] = near_cnt
     np.savez(os.path.join(workdir, "result.npz"), **out)
     return out
 
