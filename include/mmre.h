@@ -387,6 +387,34 @@ int mmre_extractor_targets(const float* d_vecs, int64_t n_sets, int n_samples, i
 int mmre_rank_desc(const float* d_scores, const int64_t* d_off, int64_t n_query, int32_t* d_rank, void* stream);
 
 /* ====================================================================== *
+ *  ZSL Extractor in TRAINING mode (dropout active): pretrain_Extractor    *
+ *  (module/zsl_module.py:289-348) and the GAN loop's Extractor calls      *
+ *  while it is in training mode (:371-383, :430-440). The frozen          *
+ *  symbol_emb side of the forward; the linears run on mmre_gemm_f32.      *
+ * ====================================================================== */
+
+/* Per row r of (d_pairs[r] = (e1, e2) symbol ids, neighbour lists d_conn_left/right[r]
+ * (max_nb, 2), column 1 = neighbour symbol; the get_meta layout, :265-287):
+ *   d_nsum_left[r]  = sum_s dropout(emb[conn_left[r][s][1]])     (neighbor_encoder :47-59
+ *   d_nsum_right[r] = sum_s dropout(emb[conn_right[r][s][1]])     before gcn_w, whose linear
+ *                                                                 part is applied to the sum)
+ *   d_e1[r], d_e2[r] = dropout_e(emb[e1]), dropout_e(emb[e2])    (entity_encoder :61-67)
+ * all (n_rows, dim). Dropout p (0 <= p < 1): kept values x * (1 / (1 - p)); the masks are a
+ * counter hash of d_rng_state[0] (seed) and d_rng_state[1] (offset) on device, or -- when
+ * d_mask_nb_left / d_mask_nb_right (n_rows, max_nb, dim) and d_mask_ent (n_rows, 2, dim) are
+ * all given -- those 0/1 bytes. max_nb <= 64. */
+int mmre_extractor_train_inputs(int dim, const float* d_sym_emb, const int64_t* d_pairs, const int64_t* d_conn_left,
+                                const int64_t* d_conn_right, int max_nb, int64_t n_rows, float p,
+                                const uint64_t* d_rng_state, const uint8_t* d_mask_nb_left,
+                                const uint8_t* d_mask_nb_right, const uint8_t* d_mask_ent, float* d_nsum_left,
+                                float* d_nsum_right, float* d_e1, float* d_e2, void* stream);
+/* Elementwise dropout (nn.Dropout in training mode, e.g. SupportEncoder :257): d_y = keep ?
+ * d_x * (1 / (1 - p)) : 0, the keep bytes to d_mask if non-NULL; draws from d_rng_state with
+ * dropout stream `stream_id` (distinct streams of one step draw independent masks). */
+int mmre_dropout(const float* d_x, float* d_y, uint8_t* d_mask, int64_t n, float p, const uint64_t* d_rng_state,
+                 int stream_id, void* stream);
+
+/* ====================================================================== *
  *  Frozen M3AE text encoder: the producer of the generator's CLS input.   *
  *  Replaces MaskedMultimodalAutoencoder.forward_representation(image=None,*
  *  text, text_padding_mask, deterministic=True) (module/model.py:323-356) *

@@ -72,6 +72,8 @@ SIGNATURES = {
     "mmre_extractor_encode": (I32, [I32, P, F32, P, P, P, P, I64, P, P, I32, P, P, P]),
     "mmre_extractor_targets": (I32, [P, I64, I32, I32, I32, P, P]),
     "mmre_rank_desc": (I32, [P, P, I64, P, P]),
+    "mmre_extractor_train_inputs": (I32, [I32, P, P, P, P, I32, I64, F32, P, P, P, P, P, P, P, P, P]),
+    "mmre_dropout": (I32, [P, P, P, I64, F32, P, I32, P]),
     "mmre_m3ae_max_len": (I32, []),
     "mmre_m3ae_plan_size": (I64, [I64]),
     "mmre_m3ae_plan": (I32, [P, P, I64, I64, I32, I64, P, P]),

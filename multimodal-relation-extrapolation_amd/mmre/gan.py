@@ -39,11 +39,14 @@ class ZSLGANStep:
     tables give the Extractor vectors of (head, tail) entity-id pairs)."""
 
     def __init__(self, generator, discriminator, cls_table, centroids, ranker, lr_G=1e-4, lr_D=1e-4,
-                 pretrain_margin=5.0, gan_batch_rela=2, gp_lambda=10.0):
+                 pretrain_margin=5.0, gan_batch_rela=2, gp_lambda=10.0, vecs_fn=None):
         self.G, self.D = generator, discriminator
         self.cls_table, self.centroids, self.ranker = cls_table, centroids, ranker
         self.margin, self.gan_batch_rela, self.gp_lambda = float(pretrain_margin), int(gan_batch_rela), gp_lambda
         self.n_labels = int(centroids.shape[0])
+        # vecs_fn(heads, tails): Extractor vectors of a training-mode Extractor (dropout,
+        # mmre.extractor_train.PretrainStep.vectors); None: the frozen eval-mode tables
+        self.vecs_fn = vecs_fn
         dev = cls_table.device
         self.optim_D = torch.optim.Adam([p for p in self.D.parameters() if p.requires_grad], lr=lr_D,
                                         betas=(0.5, 0.9), capturable=True)
@@ -56,6 +59,8 @@ class ZSLGANStep:
 
     # ---------------------------------------------------------------- pieces
     def extractor_vecs(self, heads, tails):
+        if self.vecs_fn is not None:
+            return self.vecs_fn(heads, tails)
         r = self.ranker
         g, _ = encode(r.pack, r.dim, r.ln_eps, r.left, heads, r.right, tails, want_g=True, want_score=False)
         return g

@@ -87,7 +87,20 @@ class Extractor(nn.Module):
 
     def forward(self, query, support, query_meta=None, support_meta=None):
         """query (B, 2), support (few, 2) symbol ids; metas from ZSLGraph.get_meta.
-        Returns (query_g (B, d), matching_scores = query_g . mean(support_g) squeezed)."""
+        Returns (query_g (B, d), matching_scores = query_g . mean(support_g) squeezed).
+        Training mode: differentiable, dropout masks drawn per call (one launch chain over the
+        support and query rows together)."""
+        if self.training:
+            from mmre.extractor_train import DropoutRNG, train_forward
+            if getattr(self, "_rng", None) is None or self._rng.state.device != query.device:
+                self._rng = DropoutRNG(torch.initial_seed(), query.device)
+            S = int(support.shape[0])
+            pairs = torch.cat((support, query))
+            meta = tuple(torch.cat((a, b)) for a, b in zip(support_meta, query_meta))
+            g = train_forward(self, pairs, meta, rng=self._rng)
+            self._rng.advance()
+            query_g = g[S:]
+            return query_g, torch.matmul(query_g, g[:S].mean(0, keepdim=True).t()).squeeze()
         support_g, _ = self.encode_pairs(support, support_meta)
         s_mean = targets(support_g.unsqueeze(0), normalize=False)  # (1, d) = mean over support rows
         query_g, scores = self.encode_pairs(query, query_meta, targets_=s_mean, normalize=False)
@@ -409,18 +422,54 @@ class ZSLmodule(nn.Module):
         return self.graph.get_meta(left, right, device=self.device)
 
     # ---------------------------------------------------------------- training
-    def pretrain_Extractor(self):
-        print("##EXTRACTOR PRETRAINING (zsl_module.py:289-348) is outside this build's path: "
-              "the Extractor keeps its current weights")
+    def _pretrain_step(self):
+        """optim_E (Adam, lr_E) persists across train() calls, as the reference's (:183-186)."""
+        if getattr(self, "_pstep", None) is None:
+            from mmre.extractor_train import PretrainStep
+            dev = self.device
+            g = self.graph
+            self._pstep = PretrainStep(self.Extractor, torch.as_tensor(g.ent_sym, device=dev),
+                                       torch.as_tensor(g.connections, device=dev),
+                                       torch.as_tensor(g.e1_degrees, dtype=torch.float32, device=dev),
+                                       lr=self.lr_E, margin=self.pretrain_margin, seed=torch.initial_seed())
+        return self._pstep
+
+    def pretrain_Extractor(self, rng=None):
+        """:289-348: pretrain_times + 1 steps over Extractor_generate batches (utils.py:548-613),
+        margin loss relu(pretrain_margin - (query - false)).mean(), Adam; prints the reference's
+        'Step: ...' line every pretrain_loss_every steps; then save_pretrain. Each step is one
+        hipGraph replay (mmre.extractor_train.PretrainStep). rng: the batch generator's
+        random.Random (the reference's module-level random is unseeded)."""
+        import random
+        from collections import deque
+        from mmre.extractor_train import extractor_generate
+        step = self._pretrain_step()
+        losses = deque([], 100)
+        batches = extractor_generate(self.train_tasks, self.rel2candidates, self.e1rel_e2, self.ent2id,
+                                     self.pretrain_batch_size, self.pretrain_few, self.pretrain_subepoch,
+                                     rng if rng is not None else random.Random())
+        dev = self.device
+        i = 0
+        for data in batches:
+            i += 1
+            loss = step.replay({k: torch.as_tensor(v, device=dev) for k, v in data.items()})
+            losses.append(float(loss))
+            if i % self.pretrain_loss_every == 0:
+                print("Step: %d, Feature Extractor Pretraining loss: %.2f" % (i, np.mean(losses)))
+            if i > self.pretrain_times:
+                break
+        self.pretrain_losses = list(losses)
+        self.save_pretrain()
 
     def _ranker(self):
         self.Extractor.eval()
         return ZSLRanker(self.Extractor, self.graph.ent_sym, self.graph.connections, self.graph.e1_degrees,
                          device=self.device)
 
-    def _centroids(self, ranker):
+    def _centroids(self, ranker, vecs_fn=None):
         """centroid_matrix (:353-383): the mean Extractor vector of every train relation's pairs
-        (centroid_generate, utils.py:615-623), row rela2label[relation]; one encode launch."""
+        (centroid_generate, utils.py:615-623), row rela2label[relation]; one encode launch
+        (vecs_fn: the training-mode Extractor's vectors instead, dropout included)."""
         heads, tails, labels = [], [], []
         for rel, triples in self.train_tasks.items():
             heads += [self.ent2id[t[0]] for t in triples]
@@ -428,8 +477,11 @@ class ZSLmodule(nn.Module):
             labels += [self.rela2label[rel]] * len(triples)
         dev = self.device
         h, t, lab = (torch.as_tensor(x, dtype=torch.int64, device=dev) for x in (heads, tails, labels))
-        g, _ = encode(ranker.pack, ranker.dim, ranker.ln_eps, ranker.left, h, ranker.right, t, want_g=True,
-                      want_score=False)
+        if vecs_fn is not None:
+            g = vecs_fn(h, t)
+        else:
+            g, _ = encode(ranker.pack, ranker.dim, ranker.ln_eps, ranker.left, h, ranker.right, t, want_g=True,
+                          want_score=False)
         sums = torch.zeros((len(self.train_tasks), self.emb_dim), dtype=torch.float32, device=dev)
         sums.index_add_(0, lab, g)
         cnt = torch.bincount(lab, minlength=len(self.train_tasks)).clamp(min=1).to(torch.float32)
@@ -442,6 +494,7 @@ class ZSLmodule(nn.Module):
         import random
         from mmre.gan import ZSLGANStep
         print("\n##START ADVERSARIAL TRAINING...")
+        extractor_training = self.Extractor.training
         self.pretrain_Extractor()
         grad_list = ["generate_fc_layer.weight_orig", "generate_fc_layer.bias", "des_rel_map_layer1.weight_orig",
                      "des_rel_map_layer1.bias", "des_rel_map_layer2.weight_orig", "des_rel_map_layer2.bias",
@@ -449,12 +502,16 @@ class ZSLmodule(nn.Module):
         for name, param in generate_model.named_parameters():
             param.requires_grad = name in grad_list
         ranker = self._ranker()
-        self.centroid_matrix = self._centroids(ranker)
+        self.Extractor.train(extractor_training)
+        vecs_fn = None
+        if extractor_training:  # the reference's Extractor is still in training mode here: dropout vectors
+            vecs_fn = self._pretrain_step().vectors
+        self.centroid_matrix = self._centroids(ranker, vecs_fn)
         dev = self.device
         cls_table = generate_model.M3AEmodel.encode(self.des_tokens.to(dev), self.des_pad_masks.to(dev))
         self.gan_step = ZSLGANStep(generate_model.generator, self.Discriminator, cls_table, self.centroid_matrix,
                                    ranker, lr_G=self.lr_maximum, lr_D=self.lr_D, pretrain_margin=self.pretrain_margin,
-                                   gan_batch_rela=self.gan_batch_rela)
+                                   gan_batch_rela=self.gan_batch_rela, vecs_fn=vecs_fn)
         print("##LOADING TRAINING DATA")
         batches = train_generate_decription(self.train_tasks, self.rel2candidates, self.e1rel_e2, self.ent2id,
                                             self.rel2id, self.rela2label, self.G_batch_size, self.gan_batch_rela,

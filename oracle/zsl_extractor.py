@@ -145,3 +145,49 @@ def zsl_eval_ranks(extractor, symbol2id, ent2id, connections, e1_degrees, relati
             ranks.append(order.index(0) + 1)
             all_scores.append(scores)
     return np.asarray(ranks), all_scores
+
+
+# ------------------------------------------------------------------ pretraining (training mode) --
+def train_encode_ref(ref, pairs, meta, masks, p=0.2):
+    """Training-mode Extractor rows (zsl_module.py:47-99 with SupportEncoder submodule.py:254-258),
+    every nn.Dropout replaced by its given 0/1 mask: dropout(x) = x * mask / (1 - p). Literal op
+    order of the reference: per-slot gcn_w then the slot sum. masks = (nb_left (B, M, d),
+    nb_right (B, M, d), ent (B, 2, d), support_encoder (B, d))."""
+    nb_l, nb_r, ent_m, se_m = (torch.as_tensor(np.asarray(m)).to(ref.gcn_w.weight.dtype) for m in masks)
+    scale = 1.0 / (1.0 - p)
+    lc, ld, rc, rd = meta
+    w = ref.gcn_w.weight.dtype
+
+    def nb(conn, deg, m):                                       # :47-59
+        e = ref.symbol_emb(conn[:, :, 1]) * (m * scale)
+        return (ref.gcn_w(e).sum(dim=1) / deg.to(w).unsqueeze(1)).tanh()
+
+    e1 = ref.symbol_emb(pairs[:, 0]) * (ent_m[:, 0] * scale)  # :61-67
+    e2 = ref.symbol_emb(pairs[:, 1]) * (ent_m[:, 1] * scale)
+    ent = torch.cat((ref.fc1(e1), ref.fc2(e2)), dim=-1).tanh()
+    x = ref.reshape_layer(torch.cat((nb(lc, ld, nb_l), ent, nb(rc, rd, nb_r)), dim=-1))
+    se = ref.support_encoder
+    y = se.proj2(F.relu(se.proj1(x))) * (se_m * scale)
+    return se.layer_norm(y + x)
+
+
+def pretrain_step_ref(ref, pairs, meta, sizes, masks, margin, lr, p=0.2):
+    """One pretrain_Extractor step (zsl_module.py:296-344) on rows [support | query | support |
+    false] (sizes = (S, Q, F)): the two Extractor calls' query / false scores against their own
+    support means (:318-323), loss relu(margin - (q - f)).mean() (:325-326), backward and one
+    torch.optim.Adam step (lr, default betas; optim_E :183-186). Returns (loss, grads {name:
+    tensor}, updated parameters {name: tensor}); run it on a float64 copy for a float64 oracle."""
+    S, Q, F_ = sizes
+    params = {n: q for n, q in ref.named_parameters() if q.requires_grad and not n.startswith("symbol_emb")}
+    opt = torch.optim.Adam(list(params.values()), lr=lr)
+    opt.zero_grad()
+    g = train_encode_ref(ref, pairs, meta, masks, p)
+    s1 = g[:S].mean(dim=0, keepdim=True)
+    s2 = g[S + Q:2 * S + Q].mean(dim=0, keepdim=True)
+    qs = torch.matmul(g[S:S + Q], s1.t()).squeeze()
+    fs = torch.matmul(g[2 * S + Q:], s2.t()).squeeze()
+    loss = F.relu(margin - (qs - fs)).mean()
+    loss.backward()
+    grads = {n: (None if q.grad is None else q.grad.detach().clone()) for n, q in params.items()}
+    opt.step()
+    return loss.detach(), grads, {n: q.detach().clone() for n, q in params.items()}

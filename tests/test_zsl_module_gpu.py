@@ -50,6 +50,7 @@ def _args(tmp, **kw):
     a = read_options([])
     a.model_type, a.save_path = "tiny", os.path.join(tmp, "Embed_used")
     a.train_times, a.loss_every, a.G_batch_size = 3, 1, 64
+    a.pretrain_times, a.pretrain_loss_every, a.pretrain_batch_size, a.pretrain_subepoch = 12, 4, 16, 3
     for k, v in kw.items():
         setattr(a, k, v)
     return a
@@ -184,10 +185,17 @@ def test_zsl_module_train_runs_gan_and_saves(tmp_path):
     ent, rel = embeddings(g, 200, seed=7)
     zsl.update_embed(ent, rel)
     before = um.des_rel_map_layer1.weight_orig.detach().clone()
+    ex_before = zsl.Extractor.fc1.weight.detach().clone()
+    assert zsl.Extractor.training                       # as the reference's: train mode until eval()
     res = zsl.train(um)
     assert len(res) == 3 and all(0.0 <= float(x) <= 1.0 for x in res)
     assert not torch.equal(before, um.des_rel_map_layer1.weight_orig.detach())   # G was trained
-    assert {"Generator", "Discriminator"} <= set(os.listdir(args.save_path))
+    assert not torch.equal(ex_before, zsl.Extractor.fc1.weight.detach())         # the Extractor was pretrained
+    assert len(zsl.pretrain_losses) == args.pretrain_times + 1 and np.all(np.isfinite(zsl.pretrain_losses))
+    assert {"Generator", "Discriminator", "Extractor"} <= set(os.listdir(args.save_path))
+    # after eval() the Extractor stays in eval mode: a second train() pretrains without dropout
+    assert not zsl.Extractor.training
+    zsl.train(um)
     # the saved Generator is the reference-layout UnifiedModel state dict
     sd = torch.load(os.path.join(args.save_path, "Generator"), weights_only=True)
     assert "layer_norm.a_2" in sd and not any(k.startswith("gen.") for k in sd)
