@@ -74,12 +74,16 @@ float getTestLinkMR(bool type_constrain);
 float getTestLinkMRR(bool type_constrain);
 
 /* Not in Base.so, whose void API crashes on bad input (Reader.h:59-90 ignores fopen
- * failures; OpenKE/README.md:129): here a failure -- a file that cannot be opened, a test
- * index out of range, type_constrain without importTypeFiles, a HIP error -- is latched
- * instead of ending the process. While an error is latched every entry point above returns
- * at once. mmre_base_last_error returns the code (0: none; mmre.h MMRE_ERR_*, HIP errors
- * as MMRE_ERR_HIP_BASE + hipError_t) and copies the message into msg[cap];
- * mmre_base_clear_error resets the latch. */
+ * failures; OpenKE/README.md:129). Here a failure -- a file that cannot be opened, a test
+ * index out of range, type_constrain without importTypeFiles, a HIP error -- prints its
+ * message and, by default, abort()s: an unmodified OpenKE caller never checks for errors.
+ * mmre_base_set_error_mode(1) (or MMRE_BASE_LATCH_ERRORS=1 in the environment) latches it
+ * instead: the failing call returns, every entry point above returns at once while the latch
+ * is set, and their outputs are poisoned (sampling / getHeadBatch / getTailBatch ids -1,
+ * batch_y NaN, getTestLink* NaN). mmre_base_last_error returns the code (0: none; mmre.h
+ * MMRE_ERR_*, HIP errors as MMRE_ERR_HIP_BASE + hipError_t) and copies the message into
+ * msg[cap]; mmre_base_clear_error resets the latch. */
+void mmre_base_set_error_mode(int latch);
 int mmre_base_last_error(char* msg, int cap);
 void mmre_base_clear_error(void);
 

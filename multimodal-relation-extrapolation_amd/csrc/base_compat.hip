@@ -110,16 +110,31 @@ struct Device {
 };
 Device D;
 
-// Errors never end the host process (Base.so's void API has no status return): a failure
-// throws BaseError up to the exported function, which latches it (code + message, printed
-// once to stderr) and returns; while an error is latched every other entry point returns at
-// once. mmre_base_last_error reads the latch, mmre_base_clear_error resets it.
+// Error policy. Base.so's void API has no status return, and an unmodified OpenKE caller never
+// asks for one, so by default a failure ENDS THE PROCESS (message on stderr, abort()): a
+// silent no-op would leave its batch / score buffers stale and train or evaluate on garbage.
+// A caller that checks (mmre.base.load(), or MMRE_BASE_LATCH_ERRORS=1 in the environment)
+// opts into the latched mode with mmre_base_set_error_mode(1): a failure throws BaseError up
+// to the exported function, which latches it (code + message, printed once to stderr) and
+// returns; while an error is latched every other entry point returns at once, and the outputs
+// it would have written are poisoned (sampling's ids -1 and labels NaN, getHeadBatch /
+// getTailBatch ids -1, getTestLink* NaN). mmre_base_last_error reads the latch,
+// mmre_base_clear_error resets it.
 struct BaseError : std::runtime_error {
   int code;
   BaseError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 int g_err_code = 0;
 std::string g_err_msg;
+int g_latch = -1;  // -1: not chosen yet (environment), 0: abort (default), 1: latch
+
+bool latch_mode() {
+  if (g_latch < 0) {
+    const char* e = getenv("MMRE_BASE_LATCH_ERRORS");
+    g_latch = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_latch == 1;
+}
 
 [[noreturn]] void fail(int code, const std::string& msg) { throw BaseError(code, msg); }
 
@@ -128,20 +143,37 @@ void hip_check(hipError_t e, const char* what) {
 }
 #define HIP_OR_DIE(x) hip_check((x), #x)
 
+void on_error(int code, const char* what) {
+  fprintf(stderr, "libmmre_base: %s\n", what);
+  if (!latch_mode()) {
+    fprintf(stderr, "libmmre_base: aborting (Base.so-compatible default; set MMRE_BASE_LATCH_ERRORS=1 or call "
+                    "mmre_base_set_error_mode(1) to latch errors instead)\n");
+    fflush(stderr);
+    abort();
+  }
+  g_err_code = code;
+  g_err_msg = what;
+}
+
+// returns false (f not run) while an error is latched, or when f fails
 template <class F>
-void guarded(F&& f) {
-  if (g_err_code) return;
+bool guarded(F&& f) {
+  if (g_err_code) return false;
   try {
     f();
+    return true;
   } catch (const BaseError& e) {
-    g_err_code = e.code;
-    g_err_msg = e.what();
-    fprintf(stderr, "libmmre_base: %s\n", e.what());
+    on_error(e.code, e.what());
   } catch (const std::exception& e) {
-    g_err_code = MMRE_ERR_ARG;
-    g_err_msg = e.what();
-    fprintf(stderr, "libmmre_base: %s\n", e.what());
+    on_error(MMRE_ERR_ARG, e.what());
   }
+  return false;
+}
+
+template <class T>
+void poison(T* p, int64_t n, T v) {
+  if (p)
+    for (int64_t i = 0; i < n; ++i) p[i] = v;
 }
 
 template <class T>
@@ -638,11 +670,21 @@ static void test_link_prediction_impl(bool type_constrain) {
   }
 }
 
-extern "C" REAL getTestLinkHit10(bool type_constrain) { return type_constrain ? S.hit10_tc : S.hit10; }
-extern "C" REAL getTestLinkHit3(bool type_constrain) { return type_constrain ? S.hit3_tc : S.hit3; }
-extern "C" REAL getTestLinkHit1(bool type_constrain) { return type_constrain ? S.hit1_tc : S.hit1; }
-extern "C" REAL getTestLinkMR(bool type_constrain) { return type_constrain ? S.mr_tc : S.mr; }
-extern "C" REAL getTestLinkMRR(bool type_constrain) { return type_constrain ? S.mrr_tc : S.mrr; }
+extern "C" REAL getTestLinkHit10(bool type_constrain) {
+  return g_err_code ? NAN : (type_constrain ? S.hit10_tc : S.hit10);
+}
+extern "C" REAL getTestLinkHit3(bool type_constrain) {
+  return g_err_code ? NAN : (type_constrain ? S.hit3_tc : S.hit3);
+}
+extern "C" REAL getTestLinkHit1(bool type_constrain) {
+  return g_err_code ? NAN : (type_constrain ? S.hit1_tc : S.hit1);
+}
+extern "C" REAL getTestLinkMR(bool type_constrain) {
+  return g_err_code ? NAN : (type_constrain ? S.mr_tc : S.mr);
+}
+extern "C" REAL getTestLinkMRR(bool type_constrain) {
+  return g_err_code ? NAN : (type_constrain ? S.mrr_tc : S.mrr);
+}
 
 // --------------------------------------------------- exported entry points ----
 extern "C" void importTrainFiles() {
@@ -658,7 +700,13 @@ extern "C" void importTypeFiles() {
 }
 
 extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y, INT batch_size, INT neg_rate, INT neg_rel_rate, INT mode, bool filter_flag, bool p, bool val_loss) {
-  guarded([&] { sampling_impl(batch_h, batch_t, batch_r, batch_y, batch_size, neg_rate, neg_rel_rate, mode, filter_flag, p, val_loss); });
+  if (!guarded([&] { sampling_impl(batch_h, batch_t, batch_r, batch_y, batch_size, neg_rate, neg_rel_rate, mode, filter_flag, p, val_loss); })) {
+    const int64_t n = batch_size > 0 ? batch_size * (1 + (neg_rate > 0 ? neg_rate : 0) + (neg_rel_rate > 0 ? neg_rel_rate : 0)) : 0;
+    poison<INT>(batch_h, n, -1);
+    poison<INT>(batch_t, n, -1);
+    poison<INT>(batch_r, n, -1);
+    poison<REAL>(batch_y, n, NAN);
+  }
 }
 
 extern "C" void initTest() {
@@ -666,11 +714,19 @@ extern "C" void initTest() {
 }
 
 extern "C" void getHeadBatch(INT* ph, INT* pt, INT* pr) {
-  guarded([&] { getHeadBatch_impl(ph, pt, pr); });
+  if (!guarded([&] { getHeadBatch_impl(ph, pt, pr); })) {
+    poison<INT>(ph, S.ent_total, -1);
+    poison<INT>(pt, S.ent_total, -1);
+    poison<INT>(pr, S.ent_total, -1);
+  }
 }
 
 extern "C" void getTailBatch(INT* ph, INT* pt, INT* pr) {
-  guarded([&] { getTailBatch_impl(ph, pt, pr); });
+  if (!guarded([&] { getTailBatch_impl(ph, pt, pr); })) {
+    poison<INT>(ph, S.ent_total, -1);
+    poison<INT>(pt, S.ent_total, -1);
+    poison<INT>(pr, S.ent_total, -1);
+  }
 }
 
 extern "C" void test_link_prediction(bool type_constrain) {
@@ -690,3 +746,5 @@ extern "C" void mmre_base_clear_error() {
   g_err_code = 0;
   g_err_msg.clear();
 }
+
+extern "C" void mmre_base_set_error_mode(int latch) { g_latch = latch ? 1 : 0; }

@@ -2,7 +2,9 @@
 //
 // Replaces, for the reference's default optimizer (OpenKE Trainer.py:82-86, optim.SGD with
 // no momentum / weight decay), torch's multi-tensor SGD kernel after the fused gradient:
-// p <- p - lr g elementwise (one fma), float4 streams over every tensor, one workgroup per
+// p <- p - lr g elementwise as one fma with lr in float32 -- bit-identical to torch's default
+// (foreach) SGD step on this ROCm build, which is the same fma (scripts/probes/sgd_rounding.py),
+// float4 streams over every tensor, one workgroup per
 // 4,096 elements so the whole table is in flight at once (torch's multi_tensor_apply gives a
 // 2.9 M-float table ~45 workgroups).
 #include "mmre_common.h"

@@ -32,13 +32,16 @@ SIGNATURES = {
     "getTestLinkHit10": (_F, [_I]), "getTestLinkHit3": (_F, [_I]), "getTestLinkHit1": (_F, [_I]),
     "getTestLinkMR": (_F, [_I]), "getTestLinkMRR": (_F, [_I]),
     "mmre_base_last_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]), "mmre_base_clear_error": (None, []),
+    "mmre_base_set_error_mode": (None, [ctypes.c_int]),
 }
 
 _base = None
 
 
-def load():
-    """Load libmmre_base.so once (after libmmre_hip.so, which it links)."""
+def load(latch_errors: bool = True):
+    """Load libmmre_base.so once (after libmmre_hip.so, which it links). This binding checks
+    for errors (check()), so it switches the library to the latched error mode; a caller that
+    never checks -- the reference's own Tester over ctypes.CDLL -- keeps the default, abort."""
     global _base
     if _base is None:
         if not os.path.exists(BASE_PATH):
@@ -51,6 +54,7 @@ def load():
             fn.restype = res
             fn.argtypes = args
         _base = L
+    _base.mmre_base_set_error_mode(1 if latch_errors else 0)
     return _base
 
 

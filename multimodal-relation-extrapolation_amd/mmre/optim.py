@@ -1,7 +1,9 @@
 """SGD whose plain step (no momentum, dampening, weight decay, nesterov or maximize) runs as one
 HIP launch over every parameter tensor (mmre_sgd_step, csrc/optim.hip) -- the OpenKE Trainer's
 default optimizer (Trainer.py:82-86, optim.SGD(parameters, lr, weight_decay)) after the fused
-negative-sampling gradient. Any other configuration is torch.optim.SGD's own step."""
+negative-sampling gradient. Any other configuration is torch.optim.SGD's own step; such steps
+are counted in SGD.fallback_steps (reason in SGD.fallback_reason), so a run can show that the
+HIP step was the one that ran."""
 from __future__ import annotations
 
 import ctypes
@@ -19,23 +21,44 @@ class SGD(torch.optim.SGD):
                 and not group["maximize"])
 
     def _eligible(self, group, ps) -> bool:
-        return self._plain(group) and all(
-            p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and not p.grad.is_sparse
-            and p.grad.dtype == torch.float32 and p.grad.is_contiguous()
-            and p.data_ptr() % 16 == 0 and p.grad.data_ptr() % 16 == 0 for p in ps)  # float4 streams
+        return self._why_not(group, ps) is None
+
+    # steps that took torch's own SGD path instead of mmre_sgd_step, and why (last reason)
+    fallback_steps = 0
+    fallback_reason = None
+
+    def _why_not(self, group, ps):
+        if not self._plain(group):
+            return "momentum / weight_decay / nesterov / maximize"
+        for p in ps:
+            if not p.is_cuda or p.dtype != torch.float32 or p.grad.dtype != torch.float32:
+                return "not a float32 device tensor"
+            if p.grad.is_sparse:
+                return "sparse gradient"
+            if not p.is_contiguous() or not p.grad.is_contiguous():
+                return "non-contiguous parameter or gradient"
+            if p.data_ptr() % 16 or p.grad.data_ptr() % 16:
+                return "parameter or gradient not 16-B aligned (float4 streams)"
+        return None
 
     @torch.no_grad()
     def step(self, closure=None):
-        work = []
-        for group in self.param_groups:
-            ps = [p for p in group["params"] if p.grad is not None]
-            if ps and not self._eligible(group, ps):
-                return super().step(closure)  # torch's own SGD step for every group
-            work.append((group, ps))
+        # torch.optim.SGD's order: the closure first (it may create or refresh the gradients),
+        # then the parameters that have one
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        work = []
+        for group in self.param_groups:
+            ps = [p for p in group["params"] if p.grad is not None]
+            why = self._why_not(group, ps) if ps else None
+            if why is not None:  # torch's own SGD step for every group -- counted, not silent
+                type(self).fallback_steps += 1
+                type(self).fallback_reason = why
+                super().step()
+                return loss
+            work.append((group, ps))
         for group, ps in work:
             lr = float(group["lr"])
             for i in range(0, len(ps), _MAX_T):

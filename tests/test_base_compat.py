@@ -48,6 +48,12 @@ def test_errors_are_latched_not_fatal(tmp_path):
     assert code == 1 and "cannot open" in msg
     L.setInPath(SMALL.encode())
     L.importTestFiles()                       # refused while latched: totals unchanged
+    # outputs written while latched are poisoned, not left stale
+    bh, bt, br = (np.full(8, 7, np.int64) for _ in range(3))
+    by = np.zeros(8, np.float32)
+    L.sampling(bh.ctypes.data, bt.ctypes.data, br.ctypes.data, by.ctypes.data, 4, 1, 0, 0, True, False, False)
+    assert np.all(bh == -1) and np.all(bt == -1) and np.all(br == -1) and np.all(np.isnan(by))
+    assert np.isnan(L.getTestLinkHit10(0)) and np.isnan(L.getTestLinkMRR(0))
     with pytest.raises(MMREError):
         base.check()
     assert base.last_error()[0] == 0          # check() cleared the latch
@@ -60,6 +66,23 @@ def test_errors_are_latched_not_fatal(tmp_path):
     assert code == 1 and "out of range" in msg
     L.mmre_base_clear_error()
     assert base.last_error() == (0, "")
+
+
+def test_errors_abort_by_default(tmp_path):
+    """An unmodified OpenKE caller (ctypes.CDLL, no error checks) gets Base.so's loud failure:
+    the process ends (SIGABRT) instead of continuing on stale buffers."""
+    import subprocess
+    import sys
+    so = os.path.join(REPO, "multimodal-relation-extrapolation_amd", "mmre", "lib", "libmmre_base.so")
+    code = ("import ctypes, torch; L = ctypes.CDLL(%r); L.setInPath.argtypes = [ctypes.c_char_p]; "
+            "L.setInPath(%r); L.importTrainFiles(); print('survived')" % (so, (str(tmp_path) + "/nowhere/").encode()))
+    env = dict(os.environ)
+    env.pop("MMRE_BASE_LATCH_ERRORS", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == -6 and "survived" not in r.stdout and "aborting" in r.stderr
+    env["MMRE_BASE_LATCH_ERRORS"] = "1"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0 and "survived" in r.stdout
 
 
 def test_readers_and_batches(golden):

@@ -263,3 +263,29 @@ def test_sgd_routes_only_plain_cuda_steps_to_hip():
     assert opt._plain(opt.param_groups[0])
     assert not opt._plain(dict(opt.param_groups[0], momentum=0.9))
     assert not opt._plain(dict(opt.param_groups[0], weight_decay=1e-4))
+
+
+def test_sgd_closure_runs_first_and_fallbacks_are_counted():
+    """step(closure) runs the closure before choosing the parameters (a parameter
+    whose .grad the closure creates is updated, as torch.optim.SGD does), and every step that
+    takes torch's path is counted with its reason."""
+    import torch
+    from mmre.optim import SGD
+    p = torch.ones(4, requires_grad=True)
+    q = torch.ones(4, requires_grad=True)
+    opt = SGD([p], lr=0.5)
+    ref = torch.optim.SGD([q], lr=0.5)
+    before = SGD.fallback_steps
+
+    def closure(x):
+        def f():
+            x.grad = None
+            loss = (x * x).sum()
+            loss.backward()
+            return loss
+        return f
+
+    opt.step(closure(p))
+    ref.step(closure(q))
+    assert torch.equal(p, q) and not torch.equal(p, torch.ones(4))
+    assert SGD.fallback_steps == before + 1 and "device" in SGD.fallback_reason
