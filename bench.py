@@ -87,16 +87,25 @@ def pmc_traffic(config: str, model: str):
     """HBM-side bytes per sweep launch from the committed rocprofv3 PMC passes
     (profiles/pmc_<config>.json, made by scripts/pmc.sh + scripts/pmc_summary.py on this
     workload at N=1): (2 x FETCH_SIZE + WRITE_SIZE) KiB -- FETCH_SIZE reads half the bytes of
-    wide coalesced loads on gfx950 (MI355X_MICROARCH.md §HBM)."""
+    wide coalesced loads on gfx950 (MI355X_MICROARCH.md §HBM). Only counters captured on the
+    library this process loaded count: the file's __build__.lib_sha256 must equal
+    lib_identity()'s, else (None, reason) -- a stale summary is never quoted as traffic.
+    Returns (bytes or None, source or reason)."""
+    from mmre._lib import lib_identity
     path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
+    rel = os.path.relpath(path, REPO)
+    sha = (d.get("__build__") or {}).get("lib_sha256")
+    mine = lib_identity()["sha256"]
+    if sha != mine:
+        return None, f"{rel} was captured on libmmre_hip.so {sha or '(unrecorded)'}, not this build ({mine})"
     for name, c in d.items():
         if KERNEL_NAMES[model] in name and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, REPO)
-    return None, None
+            return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0, rel
+    return None, f"{rel} holds no FETCH_SIZE / WRITE_SIZE of {KERNEL_NAMES[model]}"
 
 
 REF_SAMPLE = {"c1": 1000, "c2": 1000, "c3": 1000, "c4": 10, "c5": 24}   # test triples in the CPU leg
@@ -394,7 +403,7 @@ def bench_ns(args, world, rank, dev, dist):
         if ev:
             ev[0].record()
         loss, _ = fused_ns_loss(spec, ent, rel, b["batch_h"], b["batch_t"], b["batch_r"], B, k, margin,
-                                events=ev[3:7] if ev else None)
+                                events=ev[3:7] if ev else None, optimizer=opt)
         if ev:
             ev[1].record()
         loss.backward()
@@ -420,7 +429,8 @@ def bench_ns(args, world, rank, dev, dist):
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             g_b = smp.sample(B, k, out=bufs[0])
-            g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k, margin)
+            g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k, margin,
+                                      optimizer=opt)
             g_loss.backward()
             opt.step()
         torch.cuda.synchronize()
@@ -454,7 +464,7 @@ def bench_ns(args, world, rank, dev, dist):
     # one-shot C-ABI call mmre_ns_forward_backward captured in a hipGraph, events around replays
     from mmre._lib import call, lib, ptr, stream_ptr
     g_in = smp.sample(B, k, out=bufs[0])
-    wk = torch.empty(int(lib().mmre_ns_fused_workspace(B, k, E, R, d)), dtype=torch.float32, device=dev)
+    wk = torch.empty(int(lib().mmre_ns_fused_workspace(0, 1, B, k, E, R, d)), dtype=torch.float32, device=dev)
     s1 = torch.empty(n_rows, dtype=torch.float32, device=dev)
     l1 = torch.empty(1, dtype=torch.float32, device=dev)
     ge, gr = torch.empty_like(ent), torch.empty_like(rel)
@@ -504,9 +514,9 @@ def bench_ns(args, world, rank, dev, dist):
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": None,
                             "kernel": "mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false> + "
-                                      "k_ns_transe_fused_generic (empty for OpenKE batches) + k_ns_scan + k_ns_place "
-                                      "(+ the loss) + k_ns_row_owner<4, false>: events around hipGraph replays of the "
-                                      "one-shot C-ABI call",
+                                      "k_ns_transe_finish<4, false> (deferred generic positives: none for OpenKE "
+                                      "batches; the loss) + k_ns_row_owner<4, false>: events around hipGraph replays of "
+                                      "the one-shot C-ABI call",
                             "kernel_ms": fused_ms, "eager_fused_forward_ms": fused_fwd_ms,
                             "eager_fused_grad_ms": fused_grad_ms,
                             "algorithmic_bytes": fwd_bytes + grad_bytes, "slot_bytes": slot_bytes,
@@ -515,9 +525,9 @@ def bench_ns(args, world, rank, dev, dist):
                             "step_forward_ms": fwd_ms, "step_backward_ms": bwd_ms,
                             "note": "no float atomics: the gradient contributions are bucketed by table row and "
                                     "one wave per table row summing them in batch order (bit-reproducible); the "
-                                    "rest of the step is the sampler and SGD. The fused call is a chain of six "
-                                    "short kernels over ~74 MB of gathers (9 us at the HBM peak): latency-bound, "
-                                    "its largest kernel k_ns_transe_fused ~39 us (profiles/r2/ns_kernel_stats.csv)"},
+                                    "step is five launches: the sampler (seed advance folded in), the pre-pass, the "
+                                    "fused kernel, the finish workgroup (loss), the row-owner pass with the SGD step "
+                                    "fused in (mmre_ns_fused_grad_sgd, bit-identical to backward() + step())"},
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
@@ -837,6 +847,51 @@ def bench_m3ae(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def rank_breakdown(ev, dist, dev, sweep_ms, n_local, entity_sharded, reps=20):
+    """Where an N > 1 evaluation's time goes, measured on EVERY rank after the timed region and
+    all-gathered: the rank's local evaluation (entity / query prep, truth + filter kernels,
+    sweep; a graph replay unless --eager), its sweep kernel alone, the fixed per-rank cost
+    (local - sweep), and the collective alone (the all-gather of the count lists with its
+    scatter into query order, or the entity-sharded all-reduce), each the median of `reps`
+    runs timed with events on the launch stream (barrier before every collective). Returns
+    {name: [per-rank values]} and {name_min / name_max}."""
+    from mmre.sharding import gather_counts, reduce_counts
+    med = lambda xs: float(np.median(xs)) if xs else 0.0
+    torch.cuda.synchronize()
+    ev_pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    local = None
+    for a, b in ev_pairs:
+        a.record()
+        local = ev._local()
+        b.record()
+    torch.cuda.synchronize()
+    local_ms = med([a.elapsed_time(b) for a, b in ev_pairs])
+    coll = []
+    for a, b in ev_pairs:
+        dist.barrier()
+        torch.cuda.synchronize()
+        a.record()
+        if entity_sharded:
+            reduce_counts(local.clone(), ev.group)
+        else:
+            gather_counts(local, ev.plan, ev.group)
+        b.record()
+        torch.cuda.synchronize()
+        coll.append(a.elapsed_time(b))
+    mine = torch.tensor([local_ms, sweep_ms, max(local_ms - sweep_ms, 0.0), med(coll), float(n_local)],
+                        dtype=torch.float64, device=_coll_dev(dist, dev))
+    allv = torch.empty((dist.get_world_size(), 5), dtype=torch.float64, device=mine.device)
+    dist.all_gather_into_tensor(allv, mine)
+    allv = allv.cpu().numpy()
+    names = ["local_ms", "sweep_ms", "fixed_ms", "collective_ms", "sweeps"]
+    per = {k: [round(float(x), 5) for x in allv[:, i]] for i, k in enumerate(names)}
+    summ = {}
+    for k in names:
+        summ[k + "_min"] = float(allv[:, names.index(k)].min())
+        summ[k + "_max"] = float(allv[:, names.index(k)].max())
+    return per, summ
+
+
 def _with_build(out):
     """Name the binary that produced the line (path, size, sha256 prefix of libmmre_hip.so)."""
     from mmre._lib import lib_identity
@@ -985,6 +1040,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     _, counts = ev.run()  # one more evaluation outside the timed region: the counts the parity check reads
+    breakdown = None
+    if world > 1:  # every rank's local / sweep / fixed / collective time, gathered (all ranks take part)
+        breakdown = rank_breakdown(ev, dist, dev, sweep_ms, n_local, args.shard == "entity")
 
     total_triples = 2 * n * E
     value = total_triples * args.steps / elapsed
@@ -1048,6 +1106,12 @@ def main():
             out["config"]["tables"] = w["trained"]
         elif "tables" in w:
             out["config"]["tables"] = w["tables"]
+        if breakdown is not None:
+            out["per_rank"], out["per_rank_summary"] = breakdown
+            out["per_rank_note"] = ("medians of 20 runs per rank after the timed region: local_ms = the rank's local "
+                                    "evaluation (prep, truth + filter, sweep), sweep_ms = its sweep kernel, fixed_ms = "
+                                    "local - sweep, collective_ms = the count exchange alone (barrier before each); "
+                                    "roofline.kernel_ms is rank 0's sweep")
         if world > 1:
             # the sharded evaluation's gathered counts vs one-GPU evaluation of every query on
             # rank 0 (itself checked against the reference Base.so at N = 1): bit-equal counts

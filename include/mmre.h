@@ -199,6 +199,20 @@ int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t train_total
                                 int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
                                 int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
                                 int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, void* stream);
+/* mmre_sampler_openke_blocked that also leaves d_seeds advanced for the next call (what
+ * mmre_sampler_advance_device does, without a launch of its own): the last workgroup to finish
+ * -- an integer ticket in d_ticket, zero before the first call and reset by each call --
+ * writes the advanced states once every workgroup has read the old ones. One launch per
+ * batch, as Base.cpp's sampling is one call (Base.cpp:161-197). */
+int mmre_sampler_openke_step(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                             const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                             const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                             const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                             const float* d_right_mean, int64_t n_ent, int64_t n_rel, uint64_t* d_seeds,
+                             int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                             int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
+                             int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
+                             void* stream);
 
 /* The repo's per-edge filtered sampler (module/NegativeSampling.py:114-140,
  * 321-375): per positive edge b (local ids d_eh/d_et, relation d_er), neg
@@ -246,20 +260,24 @@ int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model
                      const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
                      float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
 
-/* Training: forward, loss and d(loss)/d(tables). mmre_ns_fused_forward computes everything
- * mmre_ns_forward computes and keeps what the gradient needs in d_work; mmre_ns_fused_grad
- * then WRITES every row of the dense gradient tables (no caller fill): d(loss)/d(table) *
- * d_grad_loss[0] (NULL: 1). mmre_ns_forward_backward is the two in sequence with an upstream
- * gradient of 1. TransE (L1 / L2, dim <= 512, neg <= 32): a norm pre-pass, the fused kernel
- * (each row read once, the gradient contributions written to slots and counted per table
- * row), the fixed-order loss reduction, and the slots bucketed by table row; the gradient is
- * one wave per table row summing its bucket in batch order -- no float atomics,
- * bit-reproducible. Other
- * models run the forward above and, in mmre_ns_fused_grad, zero the tables and run the
- * backward above. Replaces strategy NegativeSampling.forward + loss.backward()
- * (NegativeSampling.py:23-32, Trainer.py:43-54) for one batch. d_work: >=
- * mmre_ns_fused_workspace(B, k, n_ent, n_rel, dim) floats, kept between the two calls. */
-int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel, int dim);
+/* Training: forward, loss and d(loss)/d(tables). mmre_ns_fused_forward computes the scores and
+ * the loss and keeps what the gradient needs in d_work; mmre_ns_fused_grad then WRITES every
+ * row of the dense gradient tables (no caller fill): d(loss)/d(table) * d_grad_loss[0] (NULL:
+ * 1). mmre_ns_forward_backward is the two in sequence with an upstream gradient of 1. No float
+ * atomics for any model -- every gradient contribution goes to a SLOT whose id is dropped into
+ * its table row's bucket (integer atomics), and one wave per table row sums its bucket in
+ * increasing slot id (batch order): bit-reproducible gradients.
+ *   TransE (L1 / L2, dim <= 512, neg <= 32): a norm pre-pass, the fused kernel (each row read
+ *   once, scores, loss partials and the contributions of a positive's group of rows), one
+ *   workgroup for batches that are not OpenKE-shaped and the fixed-order loss reduction; the
+ *   gradient is the row-owner pass.
+ *   DistMult / ComplEx / RotatE (dim <= 512): the scoring pass + the loss reduction; the
+ *   gradient is a slot pass (one wave per positive) + the row-owner pass.
+ * Replaces strategy NegativeSampling.forward + loss.backward() (NegativeSampling.py:23-32,
+ * Trainer.py:43-54) for one batch. d_work: >= mmre_ns_fused_workspace(model, norm_flag, B, k,
+ * n_ent, n_rel, dim) floats, kept between the two calls. */
+int64_t mmre_ns_fused_workspace(int model, int norm_flag, int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel,
+                                int dim);
 int mmre_ns_fused_forward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
                           const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent,
                           int64_t n_rel, int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,
@@ -271,6 +289,17 @@ int mmre_ns_fused_grad(int model, int norm_flag, float model_margin, int use_mod
                        int64_t batch, int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
                        const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
                        float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
+/* mmre_ns_fused_grad with the optimizer's plain SGD step fused in (OpenKE Trainer.py:82-86,
+ * optim.SGD without momentum / weight decay; mmre.optim.SGD's fused mode): the gradient tables
+ * are written as above AND every parameter row with a nonzero gradient becomes
+ * fma(-lr, g, p) -- torch's SGD arithmetic, bit for bit -- in the same pass (rows outside the
+ * batch keep p = p - lr 0). The tables are updated in place (d_ent ... are the parameters). */
+int mmre_ns_fused_grad_sgd(int model, int norm_flag, float model_margin, int use_model_margin, float* d_ent,
+                           float* d_ent_im, float* d_rel, float* d_rel_im, int64_t n_ent, int64_t n_rel, int dim,
+                           float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r,
+                           int64_t batch, int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
+                           const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
+                           float* d_grad_rel, float* d_grad_rel_im, float* d_work, float lr, void* stream);
 int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
                              const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent,
                              int64_t n_rel, int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,

@@ -197,8 +197,13 @@ __device__ void row_sq(const NSArgs& A, int64_t row, int lane, float* sq) {
 }
 
 // per-positive hinge terms; returns (sum_j w_j x_j) and fills gcoef (dL/dscore scale) on request
-__global__ __launch_bounds__(256) void k_ns_forward(NSArgs A, float* __restrict__ score, float* __restrict__ part) {
+__global__ __launch_bounds__(256) void k_ns_forward(NSArgs A, float* __restrict__ score, float* __restrict__ part,
+                                                     int32_t* __restrict__ zero, int64_t n_zero) {
   __shared__ float s_n[NS_WAVES][NS_MAXK];
+  // the fused path's bucket counts (+ overflow count) for the gradient call that follows
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; zero && i < n_zero;
+       i += (int64_t)gridDim.x * blockDim.x)
+    zero[i] = 0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * NS_WAVES + w;
   if (b >= A.B) return;  // whole wave exits together
@@ -720,32 +725,48 @@ __global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const floa
 // three rows is summed in registers across the negatives; per negative one row is left, the
 // corrupted one.
 // No float atomics anywhere: k_ns_transe_fused writes every contribution to a SLOT (its
-// values + the table row it belongs to) and counts the slots per table row; k_ns_scan turns
-// the counts into bucket offsets and k_ns_place drops each slot id into its row's bucket
-// (integer atomics: the bucket's CONTENT is fixed, its order is not); k_ns_row_owner -- one
-// wave per table row -- takes its bucket's slots in increasing slot id (batch order, the same
-// every run), sums them, maps the sum through the row's normalisation, adds the
-// regularization term, scales by the upstream gradient and writes the row, every row
-// (untouched ones as zeros): no fills, no scaling pass, bit-reproducible gradient tables.
+// values + the table row it belongs to) and drops the slot's id into its row's BUCKET: the
+// place is the return value of the row's integer count atomic (the bucket's CONTENT is fixed,
+// its order is not); a bucket holds NS_BUCKET ids, further ones go to an overflow list of
+// (row, slot) pairs. k_ns_row_owner -- one wave per table row -- takes its bucket's slots in
+// increasing slot id (batch order, the same every run), sums them, maps the sum through the
+// row's normalisation, adds the regularization term, scales by the upstream gradient and
+// writes the row, every row (untouched ones as zeros): no fills, no scaling pass, no scan,
+// bit-reproducible gradient tables.
 // Slots of positive b start at b (3 + 3K): slot q < 3 is the positive's h / r / t (row 3b + q
 // of `shared` holds its signed sum), slot 3 + 3j + q is negative j's h / r / t when that row
 // is not shared with the positive (record bK + j of `rec` holds the negative's gx; a t slot
-// takes -gx). Keys: entity id, n_ent + relation id, or the sentinel n_ent + n_rel.
+// takes -gx). Keys: entity id, n_ent + relation id, or the sentinel n_ent + n_rel (no slot).
 // For L1 TransE a negative's gx is g sign(x) elementwise, so its record is |g| and two bit
 // planes (x > 0, x < 0) -- 2 + 4 NC words instead of d floats (72 B instead of 800 at d 200);
 // the row-owner pass rebuilds the same floats (|g| times +-1 is exact). L2 stores gx.
 // ---------------------------------------------------------------------------------------
 constexpr int NSF_MAXJ = 8;
+constexpr int NS_BUCKET = 64;   // slot ids kept in a table row's own bucket (one wave's width)
+constexpr int NS_HUB = 1024;    // a row with more slots than a bucket orders them in LDS up to this many
 
 struct NSSlots {        // the row-owner gradient's workspace
-  float* shared;        // 3 B rows of dim floats: the positives' own rows
-  float* rec;           // K B records of a negative's gx (ns_rec_words)
+  float* shared;        // 3 B rows of dim floats: the positives' own rows (TransE)
+  float* rec;           // K B records of a negative's gx (ns_rec_words); other models: per slot, 2 d_pad floats
   float* mult;          // per slot: occurrences of its row in the batch (regularization)
-  uint32_t* keys;       // per slot: table row
-  int32_t* pos;         // per slot: its place in the row's bucket (arrival order of the count)
-  int32_t* counts;      // per table row: its slots (zeroed by the pre-pass)
+  int32_t* counts;      // per table row: its slots (zeroed every call)
+  int32_t* bucket;      // per table row: NS_BUCKET slot ids, in arrival order
+  int32_t* ovf;         // (row, slot) pairs past a full bucket
+  int32_t* ovf_n;       // overflow pairs (zeroed every call)
   uint32_t sentinel;    // n_ent + n_rel: no slot
 };
+
+// a slot id into its row's bucket (or the overflow list)
+__device__ __forceinline__ void put_slot(const NSSlots& S, uint32_t key, int64_t slot) {
+  const int p = atomicAdd(&S.counts[key], 1);
+  if (p < NS_BUCKET) {
+    S.bucket[(int64_t)key * NS_BUCKET + p] = (int32_t)slot;
+  } else {
+    const int o = atomicAdd(S.ovf_n, 1);
+    S.ovf[2 * (int64_t)o] = (int32_t)key;
+    S.ovf[2 * (int64_t)o + 1] = (int32_t)slot;
+  }
+}
 
 // words per negative record: gx itself (L2), or |g| + pad + NC (x > 0, x < 0) 64-bit masks (L1)
 __host__ __device__ constexpr int ns_rec_words(int nc, bool l2, int d) { return l2 ? d : 2 + 4 * nc; }
@@ -808,8 +829,9 @@ __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ en
                                                     const float* __restrict__ rel, int64_t n_rel, int d,
                                                     float* __restrict__ nrm_e, float* __restrict__ nrm_r,
                                                     float* __restrict__ ent_n, float* __restrict__ rel_n,
-                                                    int32_t* __restrict__ counts, int32_t* __restrict__ defer) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) defer[0] = 0;  // no deferred positives yet
+                                                    int32_t* __restrict__ counts, int32_t* __restrict__ defer,
+                                                    int32_t* __restrict__ ovf_n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) { defer[0] = 0; ovf_n[0] = 0; }  // no deferred positives / overflow yet
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;
@@ -1114,9 +1136,10 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     if (lane < 3) {
       const int64_t sl = sb + 3 + 3 * j + lane;
       const uint32_t key = lane == 0 ? kq0 : (lane == 1 ? kq1 : kq2);
-      S.keys[sl] = key;
-      S.mult[sl] = 1.0f;
-      if (key != S.sentinel) S.pos[sl] = atomicAdd(&S.counts[key], 1);
+      if (key != S.sentinel) {
+        S.mult[sl] = 1.0f;
+        put_slot(S, key, sl);
+      }
     }
   }
   if (w > 0) {
@@ -1145,9 +1168,8 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     vstore_row(S.shared, 3 * b + 2, Gt, d, lane);
     if (lane < 3) {
       const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
-      S.keys[sb + lane] = key;
       S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
-      S.pos[sb + lane] = atomicAdd(&S.counts[key], 1);
+      put_slot(S, key, sb + lane);
     }
   }
 }
@@ -1161,90 +1183,24 @@ __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* 
   ns_fused_body<NC, L2, false>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, defer, ent_n, rel_n);
 }
 
-// the deferred positives (defer[0] of them, ids from defer[1]); nothing to do for OpenKE batches
+// The forward's last launch, one workgroup: the deferred positives (defer[0] of them, ids from
+// defer[1]; none for OpenKE batches) through the generic-row instance, one after another, then
+// the loss: the fixed-order reduction of every positive's partials (ns_reduce_block). Folding
+// both into one launch keeps the OpenKE step at three forward launches; a batch of arbitrary
+// rows pays for it with a serial generic pass.
 template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_transe_fused_generic(NSArgs A, const float* __restrict__ nrm_e,
-                                                                 const float* __restrict__ nrm_r,
-                                                                 float* __restrict__ score, float* __restrict__ part,
-                                                                 NSSlots S, int64_t n_ent,
-                                                                 const int32_t* __restrict__ defer,
-                                                                 const float* __restrict__ ent_n,
-                                                                 const float* __restrict__ rel_n) {
+__global__ __launch_bounds__(256) void k_ns_transe_finish(NSArgs A, const float* __restrict__ nrm_e,
+                                                          const float* __restrict__ nrm_r, float* __restrict__ score,
+                                                          float* __restrict__ part, NSSlots S, int64_t n_ent,
+                                                          const int32_t* __restrict__ defer,
+                                                          const float* __restrict__ ent_n,
+                                                          const float* __restrict__ rel_n, float* __restrict__ loss) {
   const int n = defer[0];
-  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+  for (int i = 0; i < n; ++i) {
     ns_fused_body<NC, L2, true>(A, nrm_e, nrm_r, score, part, S, n_ent, defer[1 + i], nullptr, ent_n, rel_n);
-    __syncthreads();  // the body's LDS is reused by the next deferred positive
+    __syncthreads();  // the body's LDS is reused by the next deferred positive; its partials are read below
   }
-}
-
-// Exclusive scan of the per-row slot counts into bucket offsets (offs[n] = all slots), one
-// 1,024-thread workgroup over tiles of 16,384 counts (one tile up to 16 k table rows): each
-// thread loads its 16 consecutive counts with four 16-B loads before any arithmetic (one
-// memory round trip per tile), wave scans of the thread totals by shuffles, the 16 wave totals
-// in LDS.
-__global__ __launch_bounds__(1024) void k_ns_scan(const int32_t* __restrict__ counts, int64_t n,
-                                                  int32_t* __restrict__ offs) {
-  constexpr int PT = 16;
-  __shared__ int32_t s_w[16];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  int32_t carry = 0;
-  for (int64_t base = 0; base < n; base += 1024 * PT) {
-    const int64_t i = base + (int64_t)PT * t;
-    int32_t c[PT];
-#pragma unroll
-    for (int q = 0; q < PT; q += 4) {
-      if (i + q + 3 < n) {
-        const int4 v = *reinterpret_cast<const int4*>(counts + i + q);
-        c[q] = v.x; c[q + 1] = v.y; c[q + 2] = v.z; c[q + 3] = v.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) c[q + e] = i + q + e < n ? counts[i + q + e] : 0;
-      }
-    }
-    int32_t tot = 0;
-#pragma unroll
-    for (int q = 0; q < PT; ++q) tot += c[q];
-    int32_t inc = tot;  // inclusive scan of the thread totals within the wave
-#pragma unroll
-    for (int sh = 1; sh < 64; sh <<= 1) {
-      const int32_t v = __shfl_up(inc, sh);
-      if (lane >= sh) inc += v;
-    }
-    if (lane == 63) s_w[wv] = inc;
-    __syncthreads();
-    int32_t before = carry, all = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int32_t x = s_w[k];
-      before += k < wv ? x : 0;
-      all += x;
-    }
-    int32_t run = before + inc - tot;
-#pragma unroll
-    for (int q = 0; q < PT; ++q) {
-      if (i + q < n) offs[i + q] = run;
-      run += c[q];
-    }
-    carry += all;
-    __syncthreads();  // s_w is rewritten by the next tile
-  }
-  if (t == 0) offs[n] = carry;
-}
-
-// Each slot's id into its row's bucket, at the place its count's atomic returned in the
-// fused kernel (arrival order: the owner restores the batch order): a plain scatter.
-// Workgroup 0 also reduces the loss (ns_reduce_block, the fixed order and arithmetic of
-// k_ns_reduce).
-__global__ __launch_bounds__(256) void k_ns_place(NSArgs A, const float* __restrict__ part, float* __restrict__ loss,
-                                                  const uint32_t* __restrict__ keys, const int32_t* __restrict__ pos,
-                                                  int64_t n_slots, uint32_t sentinel,
-                                                  const int32_t* __restrict__ offs, int32_t* __restrict__ sslot) {
-  if (blockIdx.x == 0) ns_reduce_block(A, part, loss);  // uniform per workgroup
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_slots) return;
-  const uint32_t k = keys[i];
-  if (k == sentinel) return;
-  sslot[offs[k] + pos[i]] = (int32_t)i;
+  ns_reduce_block(A, part, loss);
 }
 
 __device__ __forceinline__ int wave_min_i32(int v) {
@@ -1253,33 +1209,118 @@ __device__ __forceinline__ int wave_min_i32(int v) {
   return v;
 }
 
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// One wave per table row (entities, then relations): the row's slots (a contiguous run of
-// the sorted keys) summed in batch order, d(loss)/d(raw row) = (dy - y (y . dy)) / |v| with
-// y = v / max(|v|, eps) when the model normalises (dy / eps below eps), + reg * (occurrences)
-// * v, times the upstream gradient; written to every row of the gradient table.
+// The slot ids of table row `row` (n = counts[row] of them) in increasing order, 64 at a time.
+//   n <= NS_BUCKET (nearly every row): the bucket is ranked in registers -- lane l's rank = how
+//     many of the bucket's ids are smaller -- and a ds_permute sends each id to the lane of
+//     its rank;
+//   NS_BUCKET < n <= NS_HUB (a hub row, e.g. a frequent relation): bucket + the row's overflow
+//     pairs collected into the wave's LDS list and bitonic-sorted there;
+//   n > NS_HUB: the next 64 ids by repeated wave minima over bucket + overflow (slow, rare).
+// chunk(c0) returns lane u's id = the (c0 + u)-th smallest (INT_MAX past n).
+struct SlotOrder {
+  const int32_t* bucket;
+  const int32_t* ovf;
+  int n_ovf, n, lane;
+  int64_t row;
+  int* hub;          // this wave's LDS list (NS_HUB ints)
+  int regs;          // n <= 64: lane u's ordered id
+  int prev;          // selection path: the last id taken
+
+  __device__ void init() {
+    prev = -1;
+    if (n <= NS_BUCKET) {
+      const int mine = lane < n ? bucket[row * NS_BUCKET + lane] : INT_MAX;
+      int rank = 0;
+      for (int m = 0; m < n; ++m) rank += __builtin_amdgcn_readlane(mine, m) < mine;
+      regs = __builtin_amdgcn_ds_permute((lane < n ? rank : lane) * 4, mine);
+      return;
+    }
+    if (n > NS_HUB) return;
+    hub[lane] = bucket[row * NS_BUCKET + lane];  // a full bucket
+    int m = NS_BUCKET;
+    for (int base = 0; base < n_ovf; base += kWave) {
+      const int e = base + lane;
+      const bool mine = e < n_ovf && ovf[2 * (int64_t)e] == (int32_t)row;
+      const uint64_t mask = __ballot(mine);
+      const int at = m + __popcll(mask & lanes_below(lane));
+      if (mine && at < NS_HUB) hub[at] = ovf[2 * (int64_t)e + 1];
+      m += __popcll(mask);
+    }
+    int M = NS_BUCKET;
+    while (M < n) M <<= 1;
+    for (int i = n + lane; i < M; i += kWave) hub[i] = INT_MAX;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int k = 2; k <= M; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = lane; i < M; i += kWave) {
+          const int x = i ^ j;
+          if (x > i) {
+            const int a = hub[i], b = hub[x];
+            const bool up = (i & k) == 0;
+            if ((a > b) == up) { hub[i] = b; hub[x] = a; }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+
+  __device__ int chunk(int c0) {
+    if (n <= NS_BUCKET) return regs;
+    if (n <= NS_HUB) return c0 + lane < n ? hub[c0 + lane] : INT_MAX;
+    int out = INT_MAX;
+    const int take = n - c0 < kWave ? n - c0 : kWave;
+    for (int u = 0; u < take; ++u) {
+      int v = bucket[row * NS_BUCKET + lane];
+      v = v > prev ? v : INT_MAX;
+      for (int e = lane; e < n_ovf; e += kWave) {
+        if (ovf[2 * (int64_t)e] == (int32_t)row) {
+          const int sv = ovf[2 * (int64_t)e + 1];
+          if (sv > prev && sv < v) v = sv;
+        }
+      }
+      v = wave_min_i32(v);
+      if (lane == u) out = v;
+      prev = v;
+    }
+    return out;
+  }
+};
+
+// One wave per table row (entities, then relations): the row's slots summed in batch order,
+// d(loss)/d(raw row) = (dy - y (y . dy)) / |v| with y = v / max(|v|, eps) when the model
+// normalises (dy / eps below eps), + reg * (occurrences) * v, times the upstream gradient;
+// written to every row of the gradient table. sgd_lr > 0 (the optimizer's plain SGD step fused
+// in, mmre_ns_fused_grad_sgd): the row's parameters also become fma(-lr, g, v), torch's SGD
+// arithmetic; rows without slots keep theirs (p - lr * 0 = p).
 template <int NC, bool L2>
 __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ ent, const float* __restrict__ rel,
                                                       int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
                                                       const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
                                                       const float* __restrict__ shared, const float* __restrict__ rec,
-                                                      const float* __restrict__ mult,
-                                                      const int32_t* __restrict__ offs,
-                                                      const int32_t* __restrict__ sslot, int64_t K,
+                                                      const float* __restrict__ mult, const int32_t* __restrict__ counts,
+                                                      const int32_t* __restrict__ bucket, const int32_t* __restrict__ ovf,
+                                                      const int32_t* __restrict__ ovf_n, int64_t K,
                                                       const float* __restrict__ grad_loss, float* __restrict__ gent,
-                                                      float* __restrict__ grel) {
+                                                      float* __restrict__ grel, float sgd_lr, float* __restrict__ pent,
+                                                      float* __restrict__ prel) {
+  __shared__ int s_hub[4][NS_HUB];
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
   float* o = (is_ent ? gent : grel) + id * d;
-  const int64_t i0 = offs[row], i1 = offs[row + 1];
+  const int n = counts[row];
   // the row itself and its norm, in flight while the bucket is ordered and summed
   Vec<NC> v;
   vload_row(v, is_ent ? ent : rel, id, d, lane);
   const float nv = (is_ent ? nrm_e : nrm_r)[id];
-  if (i0 == i1) {  // not in the batch: zero gradient
+  if (n == 0) {  // not in the batch: zero gradient (and an unchanged parameter row)
     Vec<NC> z;
 #pragma unroll
     for (int c = 0; c < NC; ++c) z.v[c] = 0.0f;
@@ -1291,35 +1332,14 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
 #pragma unroll
   for (int c = 0; c < NC; ++c) dy.v[c] = 0.0f;
   float cnt = 0.0f;
-  // the bucket's slots in increasing slot id (batch order), 64 at a time: lane u gets the
-  // u-th. A bucket of <= 64 (nearly all rows) is ranked in registers: lane l's rank = how many
-  // of the bucket's ids are smaller, and a ds_permute sends each id to the lane of its rank.
-  // A larger bucket (a hub row) selects its next 64 by repeated wave minima over the bucket.
-  const int64_t c = i1 - i0;
-  int prev = -1;
-  for (int64_t c0 = 0; c0 < c; c0 += kWave) {
-    const int n = (int)((c - c0) < kWave ? (c - c0) : kWave);
-    int ordered = 0;
-    if (c <= kWave) {
-      const int mine = lane < c ? sslot[i0 + lane] : INT_MAX;
-      int rank = 0;
-      for (int m = 0; m < n; ++m) rank += __builtin_amdgcn_readlane(mine, m) < mine;
-      ordered = __builtin_amdgcn_ds_permute((lane < n ? rank : lane) * 4, mine);
-    } else {
-      for (int u = 0; u < n; ++u) {
-        int v = INT_MAX;
-        for (int64_t e = i0 + lane; e < i1; e += kWave) {
-          const int sv = sslot[e];
-          if (sv > prev && sv < v) v = sv;
-        }
-        v = wave_min_i32(v);
-        if (lane == u) ordered = v;
-        prev = v;
-      }
-    }
+  SlotOrder ord{bucket, ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], 0, -1};
+  ord.init();
+  for (int c0 = 0; c0 < n; c0 += kWave) {
+    const int take = (n - c0) < kWave ? (n - c0) : kWave;
+    const int ordered = ord.chunk(c0);
     int64_t src = 0;  // shared row index, or -(record index + 1) for a negative's record
     float sg = 0.0f, m = 0.0f;
-    if (lane < n) {  // lane u decodes its slot: where its contribution lives, and its sign
+    if (lane < take) {  // lane u decodes its slot: where its contribution lives, and its sign
       const int64_t sl = ordered;
       const int64_t b = sl / spp, t = sl - b * spp;
       if (t < 3) { src = 3 * b + t; sg = 1.0f; }
@@ -1328,7 +1348,7 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
     }
     cnt += wave_sum(m);  // integer-valued: exact in any order
     int u = 0;
-    for (; u + 4 <= n; u += 4) {  // four slots in flight, added in slot order
+    for (; u + 4 <= take; u += 4) {  // four slots in flight, added in slot order
       Vec<NC> v0, v1, v2, v3;
       const int64_t s0 = readlane64u(src, u), s1 = readlane64u(src, u + 1);
       const int64_t s2 = readlane64u(src, u + 2), s3 = readlane64u(src, u + 3);
@@ -1348,7 +1368,7 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
         dy.v[c] += g3 * v3.v[c];
       }
     }
-    for (; u < n; ++u) {
+    for (; u < take; ++u) {
       Vec<NC> v0;
       const int64_t s0 = readlane64u(src, u);
       load_slot<NC, L2>(v0, shared, rec, s0 < 0 ? -s0 - 1 : s0, s0 < 0, d, lane);
@@ -1369,11 +1389,265 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
     const float proj = nv > 1e-12f ? dot : 0.0f;
 #pragma unroll
     for (int c = 0; c < NC; ++c) dy.v[c] = ((dy.v[c] - (v.v[c] / cv) * proj) * scale + rr * v.v[c]) * G;
-    vstore_row(o, 0, dy, d, lane);
   } else {
 #pragma unroll
     for (int c = 0; c < NC; ++c) dy.v[c] = (dy.v[c] + rr * v.v[c]) * G;
-    vstore_row(o, 0, dy, d, lane);
+  }
+  vstore_row(o, 0, dy, d, lane);
+  if (sgd_lr != 0.0f) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) v.v[c] = __builtin_fmaf(-sgd_lr, dy.v[c], v.v[c]);
+    vstore_row(is_ent ? pent : prel, id, v, d, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Row-owner gradient for DistMult / ComplEx / RotatE: the same slots and buckets, no float
+// atomics, bit-reproducible gradient tables. The forward is k_ns_forward + k_ns_reduce (which
+// also zeroes the bucket counts); the gradient is k_ns_gen_slots + k_ns_gen_owner.
+// A row is two halves of d floats (element lane + 64 c in slot c of each half): DistMult the
+// row alone; ComplEx (re, im) -- entity rows from ent / ent_im, relation rows from rel /
+// rel_im; RotatE entity rows (first d, last d) of the 2d row, relation rows the phase row.
+// ---------------------------------------------------------------------------------------
+template <int NC>
+struct Row2 {
+  Vec<NC> a, b;
+};
+
+template <int NC>
+__device__ __forceinline__ void vzero(Vec<NC>& o) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) o.v[c] = 0.0f;
+}
+
+template <int NC>
+__device__ __forceinline__ void gen_load(Row2<NC>& o, const NSArgs& A, bool is_ent, int64_t id, int lane) {
+  const int d = A.dim;
+  if (is_ent) {
+    if (A.model == MMRE_COMPLEX) { vload(o.a, A.ent + id * d, d, lane); vload(o.b, A.ent_im + id * d, d, lane); }
+    else if (A.model == MMRE_ROTATE) { vload(o.a, A.ent + id * 2 * d, d, lane); vload(o.b, A.ent + id * 2 * d + d, d, lane); }
+    else { vload(o.a, A.ent + id * d, d, lane); vzero(o.b); }
+  } else {
+    vload(o.a, A.rel + id * d, d, lane);
+    if (A.model == MMRE_COMPLEX) vload(o.b, A.rel_im + id * d, d, lane); else vzero(o.b);
+  }
+}
+
+// g * d(forward score)/d(h, r, t) of one row (the per-element formulas of row_backward)
+template <int NC>
+__device__ __forceinline__ void gen_row_grad(const NSArgs& A, const Row2<NC>& H, const Row2<NC>& R,
+                                             const Row2<NC>& T, float g, Row2<NC>& dH, Row2<NC>& dR, Row2<NC>& dT) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (A.model == MMRE_DISTMULT) {
+      dH.a.v[c] = g * R.a.v[c] * T.a.v[c];
+      dT.a.v[c] = g * H.a.v[c] * R.a.v[c];
+      dR.a.v[c] = g * H.a.v[c] * T.a.v[c];
+      dH.b.v[c] = dT.b.v[c] = dR.b.v[c] = 0.0f;
+    } else if (A.model == MMRE_COMPLEX) {
+      const float hr = H.a.v[c], hi = H.b.v[c], tr = T.a.v[c], ti = T.b.v[c], rr = R.a.v[c], ri = R.b.v[c];
+      dH.a.v[c] = g * (tr * rr + ti * ri);
+      dH.b.v[c] = g * (ti * rr - tr * ri);
+      dT.a.v[c] = g * (hr * rr - hi * ri);
+      dT.b.v[c] = g * (hi * rr + hr * ri);
+      dR.a.v[c] = g * (hr * tr + hi * ti);
+      dR.b.v[c] = g * (hr * ti - hi * tr);
+    } else {  // RotatE, forward = m - sum_k rho_k
+      float sn, cs;
+      canon_sincos(R.a.v[c] / A.phase_denom, &sn, &cs);
+      const float hre = H.a.v[c], him = H.b.v[c];
+      const float re = hre * cs - him * sn - T.a.v[c];
+      const float im = hre * sn + him * cs - T.b.v[c];
+      const float rho = sqrtf(re * re + im * im);
+      const float ga = rho > 0.0f ? -g * re / rho : 0.0f;
+      const float gb = rho > 0.0f ? -g * im / rho : 0.0f;
+      dH.a.v[c] = ga * cs + gb * sn;
+      dH.b.v[c] = -ga * sn + gb * cs;
+      dT.a.v[c] = -ga;
+      dT.b.v[c] = -gb;
+      dR.a.v[c] = (ga * (-hre * sn - him * cs) + gb * (hre * cs - him * sn)) / A.phase_denom;
+      dR.b.v[c] = 0.0f;
+    }
+  }
+}
+
+template <int NC>
+__device__ __forceinline__ void row2_add(Row2<NC>& a, const Row2<NC>& b) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) { a.a.v[c] += b.a.v[c]; a.b.v[c] += b.b.v[c]; }
+}
+
+// record of slot sl: 2 halves of dpad floats
+template <int NC>
+__device__ __forceinline__ void rec_store(float* rec, int64_t sl, int dpad, const Row2<NC>& r, int lane) {
+  float* o = rec + sl * 2 * dpad;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) { o[c * kWave + lane] = r.a.v[c]; o[dpad + c * kWave + lane] = r.b.v[c]; }
+}
+
+template <int NC>
+__device__ __forceinline__ void rec_load(Row2<NC>& r, const float* rec, int64_t sl, int dpad, int lane) {
+  const float* o = rec + sl * 2 * dpad;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) { r.a.v[c] = o[c * kWave + lane]; r.b.v[c] = o[dpad + c * kWave + lane]; }
+}
+
+// One wave per positive: the loss's d/d(score) coefficients of its rows (k_ns_backward's
+// formulas, unit upstream gradient), each row's gradient; what a negative adds to a row it
+// shares with its positive (same role, same id) is summed in registers, every other row gets
+// a slot of its own. Inactive rows (zero coefficient, no regularization) add nothing.
+template <int NC>
+__global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A, const float* __restrict__ score, NSSlots S,
+                                                      int64_t n_ent, int dpad, int with_reg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + (threadIdx.x >> 6);
+  if (b >= A.B) return;  // wave-uniform
+  const float p = score[b];
+  float mx = -INFINITY, den = 0.0f;
+  if (A.adv_t > 0.0f) {
+    for (int64_t j = lane; j < A.K; j += kWave) mx = fmaxf(mx, -score[b + (j + 1) * A.B] * A.adv_t);
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+    for (int64_t j = lane; j < A.K; j += kWave) den += expf(-score[b + (j + 1) * A.B] * A.adv_t - mx);
+    den = wave_sum(den);
+  }
+  auto coef = [&](int64_t j) {
+    const float n = score[b + (j + 1) * A.B];
+    const float x = p - n, m = -A.loss_margin;
+    const float ind = x > m ? 1.0f : (x == m ? 0.5f : 0.0f);  // maximum(): ties split the gradient
+    const float c = A.adv_t > 0.0f ? (expf(-n * A.adv_t - mx) / den) / (float)A.B : 1.0f / (float)(A.B * A.K);
+    return c * ind;
+  };
+  float gp = 0.0f;
+  for (int64_t j = lane; j < A.K; j += kWave) gp += coef(j);
+  gp = wave_sum(gp);
+  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
+  Row2<NC> H, R, T, Gh, Gr, Gt, dH, dR, dT;
+  gen_load(H, A, true, ph, lane);
+  gen_load(R, A, false, pr, lane);
+  gen_load(T, A, true, pt, lane);
+  gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt);
+  float kh = 1.0f, kr = 1.0f, kt = 1.0f;  // occurrences of the positive's rows (regularization)
+  const int64_t sb = b * (3 + 3 * A.K);
+  for (int64_t j = 0; j < A.K; ++j) {
+    const int64_t row = b + (j + 1) * A.B;
+    const int64_t nh = A.h[row], nr = A.r[row], nt = A.t[row];
+    const bool oh = nh == ph, orr = nr == pr, ot = nt == pt;
+    const float g = -coef(j);
+    if (g == 0.0f && !with_reg) {
+      kh += oh ? 1.0f : 0.0f; kr += orr ? 1.0f : 0.0f; kt += ot ? 1.0f : 0.0f;
+      continue;
+    }
+    Row2<NC> Hj, Rj, Tj;
+    if (oh) Hj = H; else gen_load(Hj, A, true, nh, lane);
+    if (orr) Rj = R; else gen_load(Rj, A, false, nr, lane);
+    if (ot) Tj = T; else gen_load(Tj, A, true, nt, lane);
+    gen_row_grad(A, Hj, Rj, Tj, g, dH, dR, dT);
+    const int64_t sl = sb + 3 + 3 * j;
+    if (oh) { row2_add(Gh, dH); kh += 1.0f; } else { rec_store(S.rec, sl, dpad, dH, lane); }
+    if (orr) { row2_add(Gr, dR); kr += 1.0f; } else { rec_store(S.rec, sl + 1, dpad, dR, lane); }
+    if (ot) { row2_add(Gt, dT); kt += 1.0f; } else { rec_store(S.rec, sl + 2, dpad, dT, lane); }
+    if (lane < 3) {
+      const bool own = lane == 0 ? oh : (lane == 1 ? orr : ot);
+      if (!own) {
+        const uint32_t key = lane == 0 ? (uint32_t)nh : (lane == 1 ? (uint32_t)(n_ent + nr) : (uint32_t)nt);
+        S.mult[sl + lane] = 1.0f;
+        put_slot(S, key, sl + lane);
+      }
+    }
+  }
+  rec_store(S.rec, sb, dpad, Gh, lane);
+  rec_store(S.rec, sb + 1, dpad, Gr, lane);
+  rec_store(S.rec, sb + 2, dpad, Gt, lane);
+  if (lane < 3) {
+    const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
+    S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
+    put_slot(S, key, sb + lane);
+  }
+}
+
+// One wave per table row: its slots' records summed in slot order, + reg (occurrences) v, times
+// the upstream gradient, written to every row of the gradient tables (and, with sgd_lr, the
+// parameter rows updated by fma(-lr, g, v)).
+template <int NC>
+__global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, int64_t n_rel, float reg_ent,
+                                                      float reg_rel, const float* __restrict__ rec,
+                                                      const float* __restrict__ mult, const int32_t* __restrict__ counts,
+                                                      const int32_t* __restrict__ bucket,
+                                                      const int32_t* __restrict__ ovf, const int32_t* __restrict__ ovf_n,
+                                                      int dpad, const float* __restrict__ grad_loss, float* gent,
+                                                      float* gent_im, float* grel, float* grel_im, float sgd_lr,
+                                                      float* pent, float* pent_im, float* prel, float* prel_im) {
+  __shared__ int s_hub[4][NS_HUB];
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_ent + n_rel) return;  // wave-uniform
+  const bool is_ent = row < n_ent;
+  const int64_t id = is_ent ? row : row - n_ent;
+  const int d = A.dim;
+  const bool two = A.model == MMRE_COMPLEX || (A.model == MMRE_ROTATE && is_ent);
+  // output rows of the two halves
+  float *oa, *ob = nullptr, *pa = nullptr, *pb = nullptr;
+  if (is_ent) {
+    if (A.model == MMRE_COMPLEX) { oa = gent + id * d; ob = gent_im + id * d; pa = pent ? pent + id * d : nullptr; pb = pent_im ? pent_im + id * d : nullptr; }
+    else if (A.model == MMRE_ROTATE) { oa = gent + id * 2 * d; ob = oa + d; pa = pent ? pent + id * 2 * d : nullptr; pb = pa ? pa + d : nullptr; }
+    else { oa = gent + id * d; pa = pent ? pent + id * d : nullptr; }
+  } else {
+    oa = grel + id * d;
+    pa = prel ? prel + id * d : nullptr;
+    if (A.model == MMRE_COMPLEX) { ob = grel_im + id * d; pb = prel_im ? prel_im + id * d : nullptr; }
+  }
+  const int n = counts[row];
+  Row2<NC> dy;
+  vzero(dy.a);
+  vzero(dy.b);
+  if (n == 0) {
+    vstore(oa, dy.a, d, lane);
+    if (two) vstore(ob, dy.b, d, lane);
+    return;
+  }
+  Row2<NC> v;
+  gen_load(v, A, is_ent, id, lane);
+  float cnt = 0.0f;
+  SlotOrder ord{bucket, ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], 0, -1};
+  ord.init();
+  for (int c0 = 0; c0 < n; c0 += kWave) {
+    const int take = (n - c0) < kWave ? (n - c0) : kWave;
+    const int ordered = ord.chunk(c0);
+    float mo = 0.0f;
+    if (lane < take) mo = mult[ordered];
+    cnt += wave_sum(mo);  // integer-valued: exact in any order
+    int u = 0;
+    for (; u + 2 <= take; u += 2) {  // two records in flight, added in slot order
+      Row2<NC> r0, r1;
+      rec_load(r0, rec, __builtin_amdgcn_readlane(ordered, u), dpad, lane);
+      rec_load(r1, rec, __builtin_amdgcn_readlane(ordered, u + 1), dpad, lane);
+      row2_add(dy, r0);
+      row2_add(dy, r1);
+    }
+    if (u < take) {
+      Row2<NC> r0;
+      rec_load(r0, rec, __builtin_amdgcn_readlane(ordered, u), dpad, lane);
+      row2_add(dy, r0);
+    }
+  }
+  const float G = grad_loss ? grad_loss[0] : 1.0f;
+  const float rr = (is_ent ? reg_ent : reg_rel) * cnt;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    dy.a.v[c] = (dy.a.v[c] + rr * v.a.v[c]) * G;
+    dy.b.v[c] = (dy.b.v[c] + rr * v.b.v[c]) * G;
+  }
+  vstore(oa, dy.a, d, lane);
+  if (two) vstore(ob, dy.b, d, lane);
+  if (sgd_lr != 0.0f) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      v.a.v[c] = __builtin_fmaf(-sgd_lr, dy.a.v[c], v.a.v[c]);
+      v.b.v[c] = __builtin_fmaf(-sgd_lr, dy.b.v[c], v.b.v[c]);
+    }
+    vstore(pa, v.a, d, lane);
+    if (two) vstore(pb, v.b, d, lane);
   }
 }
 
@@ -1439,7 +1713,7 @@ extern "C" int mmre_ns_forward(int model, int norm_flag, float model_margin, int
   else if (nc == 8) MMRE_NS_FWD(8);
   else {
     hipLaunchKernelGGL(k_ns_forward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
-                       d_score, d_work);
+                       d_score, d_work, nullptr, (int64_t)0);
   }
 #undef MMRE_NS_FWD
   MMRE_CHECK_LAUNCH();
@@ -1508,44 +1782,61 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
 }
 
 // Workspace of the fused path, in 4-byte words, 256-B aligned pieces: loss partials, row
-// norms, the slot contributions / occurrences / keys / bucket places, the per-row slot
-// counts, bucket offsets, the bucketed slot ids, the deferred positives.
+// norms (+ the normalised tables with norm_flag), the slot contributions / occurrences, the
+// per-row slot counts (then the overflow count), the buckets, the overflow pairs, the deferred
+// positives. TransE keeps the positives' sums (3 rows of d) and the negatives' records
+// (ns_rec_words each); the other models one record of 2 d_pad floats per slot.
 struct FusedWs {
-  int64_t part, nrm_e, nrm_r, ent_n, rel_n, shared, rec, mult, keys, pos, counts, offs, sslot, defer, total, slots;
+  int64_t part, nrm_e, nrm_r, ent_n, rel_n, shared, rec, mult, counts, bucket, ovf, defer, total, slots;
+  int dpad;
   uint32_t sentinel;
 };
 
 static int64_t al64(int64_t x) { return (x + 63) & ~(int64_t)63; }
 
-static void fused_ws(int64_t B, int64_t K, int64_t E, int64_t R, int d, FusedWs& w) {
+static bool is_transe(int model) { return model == MMRE_TRANSE_L1 || model == MMRE_TRANSE_L2; }
+
+static void fused_ws(int model, int norm_flag, int64_t B, int64_t K, int64_t E, int64_t R, int d, FusedWs& w) {
   w.slots = (3 + 3 * K) * B;
   w.sentinel = (uint32_t)(E + R);
+  w.dpad = (int)round_up(d, kWave);
+  const bool te = is_transe(model);
   int64_t o = 0;
   w.part = o;    o = al64(o + 7 * B);
-  w.nrm_e = o;   o = al64(o + E);
-  w.nrm_r = o;   o = al64(o + R);
-  w.ent_n = o;   o = al64(o + E * d);
-  w.rel_n = o;   o = al64(o + R * d);
-  w.shared = o;  o = al64(o + 3 * B * d);
-  w.rec = o;     o = al64(o + K * B * (d > ns_rec_words(8, false, d) ? d : ns_rec_words(8, false, d)));
+  w.nrm_e = o;   o = al64(o + (te ? E : 0));
+  w.nrm_r = o;   o = al64(o + (te ? R : 0));
+  w.ent_n = o;   o = al64(o + (te && norm_flag ? E * d : 0));
+  w.rel_n = o;   o = al64(o + (te && norm_flag ? R * d : 0));
+  w.shared = o;  o = al64(o + (te ? 3 * B * d : 0));
+  const int64_t rw = ns_rec_words(8, false, d);
+  w.rec = o;     o = al64(o + (te ? K * B * (d > rw ? d : rw) : w.slots * 2 * w.dpad));
   w.mult = o;    o = al64(o + w.slots);
-  w.keys = o;    o = al64(o + w.slots);
-  w.pos = o;     o = al64(o + w.slots);
-  w.counts = o;  o = al64(o + E + R);
-  w.offs = o;    o = al64(o + E + R + 1);
-  w.sslot = o;   o = al64(o + w.slots);
+  w.counts = o;  o = al64(o + E + R + 1);   // + the overflow count
+  w.bucket = o;  o = al64(o + (E + R) * NS_BUCKET);
+  w.ovf = o;     o = al64(o + 2 * w.slots);
   w.defer = o;   o = al64(o + B + 1);
   w.total = o;
 }
 
-extern "C" int64_t mmre_ns_fused_workspace(int64_t batch, int64_t neg, int64_t n_ent, int64_t n_rel, int dim) {
+static NSSlots ws_slots(float* d_work, const FusedWs& w, int64_t E, int64_t R) {
+  int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
+  return NSSlots{d_work + w.shared, d_work + w.rec, d_work + w.mult, counts,
+                 reinterpret_cast<int32_t*>(d_work + w.bucket), reinterpret_cast<int32_t*>(d_work + w.ovf),
+                 counts + E + R, w.sentinel};
+}
+
+extern "C" int64_t mmre_ns_fused_workspace(int model, int norm_flag, int64_t batch, int64_t neg, int64_t n_ent,
+                                           int64_t n_rel, int dim) {
   FusedWs w;
-  fused_ws(batch > 0 ? batch : 1, neg > 0 ? neg : 0, n_ent > 0 ? n_ent : 0, n_rel > 0 ? n_rel : 0, dim > 0 ? dim : 1,
-           w);
+  fused_ws(model, norm_flag, batch > 0 ? batch : 1, neg > 0 ? neg : 0, n_ent > 0 ? n_ent : 0, n_rel > 0 ? n_rel : 0,
+           dim > 0 ? dim : 1, w);
   return w.total > 7 * batch ? w.total : 7 * batch;
 }
 
 static bool fused_fast(const NSArgs& A) { return transe_fast_nc(A) != 0 && A.K <= NSW * NSF_MAXJ; }
+
+// elements per lane of the row-owner path of the other models (d <= 512)
+static int gen_nc(int dim) { return dim <= 64 ? 1 : dim <= 128 ? 2 : dim <= 256 ? 4 : dim <= 512 ? 8 : 0; }
 
 extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margin, int use_model_margin,
                                      const float* d_ent, const float* d_ent_im, const float* d_rel,
@@ -1559,59 +1850,107 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   if (rc) return rc;
   if (!d_score || !d_loss || !d_work || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
   if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
-  if (!fused_fast(A))  // other models: the plain forward; mmre_ns_fused_grad runs their backward
-    return mmre_ns_forward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
-                           phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
-                           d_loss, d_work, stream);
   hipStream_t st = (hipStream_t)stream;
   FusedWs w;
-  fused_ws(batch, neg, n_ent, n_rel, dim, w);
+  fused_ws(model, norm_flag, batch, neg, n_ent, n_rel, dim, w);
   float* part = d_work + w.part;
+  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
+  if (!fused_fast(A)) {  // other models: scores + partials (zeroing the bucket counts), then the loss
+    if (!is_transe(model) && gen_nc(dim) == 0) return MMRE_ERR_SHAPE;
+    hipLaunchKernelGGL(k_ns_forward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
+                       d_score, part, S.counts, n_ent + n_rel + 1);
+    MMRE_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_ns_reduce, dim3(1), dim3(256), 0, st, A, part, d_loss);
+    MMRE_CHECK_LAUNCH();
+    return MMRE_OK;
+  }
   float* nrm_e = d_work + w.nrm_e;
   float* nrm_r = d_work + w.nrm_r;
-  int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
-  int32_t* offs = reinterpret_cast<int32_t*>(d_work + w.offs);
   int32_t* defer = reinterpret_cast<int32_t*>(d_work + w.defer);
-  NSSlots S{d_work + w.shared, d_work + w.rec, d_work + w.mult, reinterpret_cast<uint32_t*>(d_work + w.keys),
-            reinterpret_cast<int32_t*>(d_work + w.pos), counts, w.sentinel};
   // norm_flag: the fused kernel reads the rows normalised by the pre-pass; else the tables
   float* ent_n = norm_flag ? d_work + w.ent_n : nullptr;
   float* rel_n = norm_flag ? d_work + w.rel_n : nullptr;
   hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
-                     n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, counts, defer);
+                     n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, S.counts, defer, S.ovf_n);
+  MMRE_CHECK_LAUNCH();
   const float* ent_u = norm_flag ? ent_n : d_ent;
   const float* rel_u = norm_flag ? rel_n : d_rel;
-  MMRE_CHECK_LAUNCH();
   const dim3 grid((unsigned)batch), blk(256);
   const bool l2 = model == MMRE_TRANSE_L2;
   const int nc = transe_fast_nc(A);
-  const dim3 ggrid((unsigned)(batch < 128 ? batch : 128));
-#define MMRE_NS_FUSED(NC_)                                                                                       \
-  do {                                                                                                           \
-    if (l2) {                                                                                                    \
-      hipLaunchKernelGGL((k_ns_transe_fused<NC_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,   \
-                         n_ent, defer, ent_u, rel_u);                                                                          \
-      hipLaunchKernelGGL((k_ns_transe_fused_generic<NC_, true>), ggrid, blk, 0, st, A, nrm_e, nrm_r, d_score,    \
-                         part, S, n_ent, defer, ent_u, rel_u);                                                   \
-    } else {                                                                                                     \
-      hipLaunchKernelGGL((k_ns_transe_fused<NC_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,  \
-                         n_ent, defer, ent_u, rel_u);                                                                          \
-      hipLaunchKernelGGL((k_ns_transe_fused_generic<NC_, false>), ggrid, blk, 0, st, A, nrm_e, nrm_r, d_score,   \
-                         part, S, n_ent, defer, ent_u, rel_u);                                                   \
-    }                                                                                                            \
+#define MMRE_NS_FUSED(NC_, L2_)                                                                                    \
+  do {                                                                                                            \
+    hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, n_ent, \
+                       defer, ent_u, rel_u);                                                                      \
+    hipLaunchKernelGGL((k_ns_transe_finish<NC_, L2_>), dim3(1), blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,    \
+                       n_ent, defer, ent_u, rel_u, d_loss);                                                       \
   } while (0)
-  if (nc == 1) MMRE_NS_FUSED(1);
-  else if (nc == 2) MMRE_NS_FUSED(2);
-  else if (nc == 4) MMRE_NS_FUSED(4);
-  else MMRE_NS_FUSED(8);
+  if (nc == 1) { if (l2) MMRE_NS_FUSED(1, true); else MMRE_NS_FUSED(1, false); }
+  else if (nc == 2) { if (l2) MMRE_NS_FUSED(2, true); else MMRE_NS_FUSED(2, false); }
+  else if (nc == 4) { if (l2) MMRE_NS_FUSED(4, true); else MMRE_NS_FUSED(4, false); }
+  else { if (l2) MMRE_NS_FUSED(8, true); else MMRE_NS_FUSED(8, false); }
 #undef MMRE_NS_FUSED
   MMRE_CHECK_LAUNCH();
-  // the slot buckets per table row: offsets, then every slot id into its bucket (+ the loss)
-  hipLaunchKernelGGL(k_ns_scan, dim3(1), dim3(1024), 0, st, counts, n_ent + n_rel, offs);
-  MMRE_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_ns_place, dim3((unsigned)((w.slots + 255) / 256)), dim3(256), 0, st, A, part, d_loss,
-                     reinterpret_cast<const uint32_t*>(S.keys), S.pos, w.slots, w.sentinel, offs,
-                     reinterpret_cast<int32_t*>(d_work + w.sslot));
+  return MMRE_OK;
+}
+
+static int fused_grad_impl(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
+                           const float* d_ent_im, const float* d_rel, const float* d_rel_im, int64_t n_ent,
+                           int64_t n_rel, int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,
+                           const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
+                           float regul_rate, const float* d_score, const float* d_grad_loss, float* d_grad_ent,
+                           float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work, float lr,
+                           float* pe, float* pei, float* pr, float* pri, void* stream) {
+  NSArgs A;
+  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
+                   phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
+  if (rc) return rc;
+  if (!d_score || !d_work || !d_grad_ent || !d_grad_rel || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
+  if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
+  if (lr != 0.0f && (!pe || !pr || (model == MMRE_COMPLEX && (!pei || !pri)))) return MMRE_ERR_ARG;
+  if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
+  hipStream_t st = (hipStream_t)stream;
+  FusedWs w;
+  fused_ws(model, norm_flag, batch, neg, n_ent, n_rel, dim, w);
+  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
+  const double N = (double)batch * (1.0 + (double)neg);
+  const dim3 ogrid((unsigned)((n_ent + n_rel + 3) / 4)), blk(256);
+  if (!fused_fast(A)) {
+    const int nc = gen_nc(dim);
+    if (is_transe(model) || nc == 0) return MMRE_ERR_SHAPE;
+    const double nterms = model == MMRE_COMPLEX ? 6.0 : 3.0;
+    const double ew = model == MMRE_ROTATE ? 2.0 * dim : (double)dim;
+    const float reg_ent = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * ew)) : 0.0f;
+    const float reg_rel = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * dim)) : 0.0f;
+    const dim3 sgrid((unsigned)((batch + NS_WAVES - 1) / NS_WAVES));
+#define MMRE_NS_GEN(NC_)                                                                                            \
+  do {                                                                                                              \
+    hipLaunchKernelGGL((k_ns_gen_slots<NC_>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,                      \
+                       (int)(regul_rate != 0.0f));                                                                  \
+    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), ogrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec, S.mult,  \
+                       S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, \
+                       d_grad_rel_im, lr, pe, pei, pr, pri);                                                        \
+  } while (0)
+    if (nc == 1) MMRE_NS_GEN(1);
+    else if (nc == 2) MMRE_NS_GEN(2);
+    else if (nc == 4) MMRE_NS_GEN(4);
+    else MMRE_NS_GEN(8);
+#undef MMRE_NS_GEN
+    MMRE_CHECK_LAUNCH();
+    return MMRE_OK;
+  }
+  const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
+#define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
+  hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
+                     d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.mult, S.counts, S.bucket, S.ovf, S.ovf_n, \
+                     neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr)
+  const int nc = transe_fast_nc(A);
+  const bool l2 = model == MMRE_TRANSE_L2;
+  if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }
+  else if (nc == 2) { if (l2) MMRE_NS_OWNER(2, true); else MMRE_NS_OWNER(2, false); }
+  else if (nc == 4) { if (l2) MMRE_NS_OWNER(4, true); else MMRE_NS_OWNER(4, false); }
+  else { if (l2) MMRE_NS_OWNER(8, true); else MMRE_NS_OWNER(8, false); }
+#undef MMRE_NS_OWNER
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
@@ -1623,45 +1962,25 @@ extern "C" int mmre_ns_fused_grad(int model, int norm_flag, float model_margin, 
                                   float loss_margin, float adv_temperature, float regul_rate, const float* d_score,
                                   const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im, float* d_grad_rel,
                                   float* d_grad_rel_im, float* d_work, void* stream) {
-  NSArgs A;
-  int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
-                   phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
-  if (rc) return rc;
-  if (!d_score || !d_work || !d_grad_ent || !d_grad_rel || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
-  if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
-  if (neg > NS_MAXK) return MMRE_ERR_SHAPE;
-  hipStream_t st = (hipStream_t)stream;
-  if (!fused_fast(A)) {  // other models: zeroed tables, then the atomic backward
-    const int64_t ew = model == MMRE_ROTATE ? 2 * (int64_t)dim : dim;
-    MMRE_CHECK(hipMemsetAsync(d_grad_ent, 0, (size_t)(n_ent * ew) * sizeof(float), st));
-    MMRE_CHECK(hipMemsetAsync(d_grad_rel, 0, (size_t)(n_rel * dim) * sizeof(float), st));
-    if (model == MMRE_COMPLEX) {
-      MMRE_CHECK(hipMemsetAsync(d_grad_ent_im, 0, (size_t)(n_ent * dim) * sizeof(float), st));
-      MMRE_CHECK(hipMemsetAsync(d_grad_rel_im, 0, (size_t)(n_rel * dim) * sizeof(float), st));
-    }
-    return mmre_ns_backward(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
-                            phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
-                            d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, stream);
-  }
-  FusedWs w;
-  fused_ws(batch, neg, n_ent, n_rel, dim, w);
-  const double N = (double)batch * (1.0 + (double)neg);
-  const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
-  const dim3 grid((unsigned)((n_ent + n_rel + 3) / 4)), blk(256);
-#define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
-  hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), grid, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
-                     d_work + w.nrm_e, d_work + w.nrm_r, d_work + w.shared, d_work + w.rec, d_work + w.mult,          \
-                     reinterpret_cast<const int32_t*>(d_work + w.offs),                                               \
-                     reinterpret_cast<const int32_t*>(d_work + w.sslot), neg, d_grad_loss, d_grad_ent, d_grad_rel)
-  const int nc = transe_fast_nc(A);
-  const bool l2 = model == MMRE_TRANSE_L2;
-  if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }
-  else if (nc == 2) { if (l2) MMRE_NS_OWNER(2, true); else MMRE_NS_OWNER(2, false); }
-  else if (nc == 4) { if (l2) MMRE_NS_OWNER(4, true); else MMRE_NS_OWNER(4, false); }
-  else { if (l2) MMRE_NS_OWNER(8, true); else MMRE_NS_OWNER(8, false); }
-#undef MMRE_NS_OWNER
-  MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  return fused_grad_impl(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, n_ent,
+                         n_rel, dim, phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate,
+                         d_score, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, 0.0f,
+                         nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+extern "C" int mmre_ns_fused_grad_sgd(int model, int norm_flag, float model_margin, int use_model_margin,
+                                      float* d_ent, float* d_ent_im, float* d_rel, float* d_rel_im, int64_t n_ent,
+                                      int64_t n_rel, int dim, float phase_denom, const int64_t* d_h,
+                                      const int64_t* d_t, const int64_t* d_r, int64_t batch, int64_t neg,
+                                      float loss_margin, float adv_temperature, float regul_rate,
+                                      const float* d_score, const float* d_grad_loss, float* d_grad_ent,
+                                      float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work,
+                                      float lr, void* stream) {
+  if (!(lr != 0.0f)) return MMRE_ERR_ARG;
+  return fused_grad_impl(model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, n_ent,
+                         n_rel, dim, phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate,
+                         d_score, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, lr, d_ent,
+                         d_ent_im, d_rel, d_rel_im, stream);
 }
 
 extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int use_model_margin,

@@ -129,7 +129,7 @@ __device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64_t* __r
 // pthread's seed advanced by an affine jump, so the rows of one positive -- a chain of up to
 // 1 + 2 neg dependent draws and binary searches in the reference -- are produced in parallel
 // (B (1 + neg + neg_rel) threads instead of B).
-__global__ __launch_bounds__(256) void k_sampler_openke(
+__device__ __forceinline__ void sampler_openke_row(int64_t row, 
     const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
     const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
     const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
@@ -138,8 +138,6 @@ __global__ __launch_bounds__(256) void k_sampler_openke(
     int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk,
     int64_t n_blk, int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br,
     float* __restrict__ by) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= B * (1 + neg + neg_rel)) return;
   const int64_t b = row % B, j = row / B;  // j = 0: the positive; 1..neg: entity negatives; then relation ones
   // slice of the reference's pthread `id` that owns position b (Base.cpp:93-100)
   const int64_t per = B % work_threads == 0 ? B / work_threads : B / work_threads + 1;
@@ -184,6 +182,54 @@ __global__ __launch_bounds__(256) void k_sampler_openke(
     bh[row] = h; bt[row] = t; br[row] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r);
   }
   by[row] = -1.0f;
+}
+
+
+// The per-pthread LCG states after one sampling call (mmre_sampler_advance's arithmetic):
+// thread id's state jumps by (its positives) x (draws per positive), its positives being
+// Base.cpp:161-197's [lef, rig) split of the batch.
+__device__ __forceinline__ uint64_t advanced_seed(uint64_t seed, int64_t id, int64_t work_threads,
+                                                  int64_t batch_size, int64_t per) {
+  int64_t lef, rig;
+  if (batch_size % work_threads == 0) {
+    lef = id * (batch_size / work_threads);
+    rig = (id + 1) * (batch_size / work_threads);
+  } else {
+    lef = id * (batch_size / work_threads + 1);
+    rig = (id + 1) * (batch_size / work_threads + 1);
+    if (rig > batch_size) rig = batch_size;
+  }
+  const int64_t cnt = rig > lef ? rig - lef : 0;
+  return lcg_jump(seed, (uint64_t)(cnt * per));
+}
+
+// One thread per output row. With `ticket` (mmre_sampler_openke_step) the call also advances
+// the seeds for the next call: every workgroup takes a ticket once all its threads have read
+// the seeds; the last one writes the advanced states and resets the ticket -- no separate
+// advance launch behind every batch.
+__global__ __launch_bounds__(256) void k_sampler_openke(
+    const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
+    const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
+    const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
+    const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
+    const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, uint64_t* seeds, int64_t work_threads,
+    int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk, int64_t n_blk,
+    int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br, float* __restrict__ by,
+    int32_t* ticket, int64_t adv_per) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row < B * (1 + neg + neg_rel))
+    sampler_openke_row(row, train_list, train_total, head_hrt, tail_hrt, rel_hrt, lef_head, rig_head, lef_tail,
+                       rig_tail, lef_rel, rig_rel, left_mean, right_mean, n_ent, n_rel, seeds, work_threads, B, neg,
+                       neg_rel, mode, blk, n_blk, bh, bt, br, by);
+  if (ticket == nullptr) return;  // uniform
+  __syncthreads();  // every thread of the workgroup has read (and used) its seed
+  __shared__ int s_last;
+  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  for (int64_t id = threadIdx.x; id < work_threads; id += blockDim.x)
+    seeds[id] = advanced_seed(seeds[id], id, work_threads, B, adv_per);
+  if (threadIdx.x == 0) *ticket = 0;
 }
 
 // ---------------------------------------------------------------- repo sampler --
@@ -251,23 +297,11 @@ __global__ void k_sampler_repo(const int64_t* __restrict__ eh, const int64_t* __
   }
 }
 
-// The per-pthread LCG states after one sampling call, on the device (mmre_sampler_advance's
-// arithmetic): thread id's state jumps by (its positives) x (draws per positive), its
-// positives being Base.cpp:161-197's [lef, rig) split of the batch.
+// The per-pthread LCG states after one sampling call, on the device (a launch of its own).
 __global__ void k_sampler_advance(uint64_t* seeds, int64_t work_threads, int64_t batch_size, int64_t per) {
   const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (id >= work_threads) return;
-  int64_t lef, rig;
-  if (batch_size % work_threads == 0) {
-    lef = id * (batch_size / work_threads);
-    rig = (id + 1) * (batch_size / work_threads);
-  } else {
-    lef = id * (batch_size / work_threads + 1);
-    rig = (id + 1) * (batch_size / work_threads + 1);
-    if (rig > batch_size) rig = batch_size;
-  }
-  const int64_t cnt = rig > lef ? rig - lef : 0;
-  seeds[id] = lcg_jump(seeds[id], (uint64_t)(cnt * per));
+  seeds[id] = advanced_seed(seeds[id], id, work_threads, batch_size, per);
 }
 
 }  // namespace mmre
@@ -284,14 +318,14 @@ extern "C" int mmre_sampler_advance_device(uint64_t* d_seeds, int64_t work_threa
   return MMRE_OK;
 }
 
-extern "C" int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
-                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
-                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
-                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
-                                   const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
-                                   int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
-                                   int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
-                                   int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, void* stream) {
+static int sampler_impl(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                        const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                        const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                        const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                        const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
+                        int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate, int64_t mode,
+                        const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
+                        int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, void* stream) {
   if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
       !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y)
     return MMRE_ERR_ARG;
@@ -306,11 +340,42 @@ extern "C" int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t 
   const int64_t rows = batch_size * (1 + neg_rate + neg_rel_rate);
   hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((rows + threads - 1) / threads)), dim3(threads), 0, st,
                      d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
-                     d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
-                     work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
-                     d_batch_t, d_batch_r, d_batch_y);
+                     d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel,
+                     const_cast<uint64_t*>(d_seeds), work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks,
+                     n_blocks, d_batch_h, d_batch_t, d_batch_r, d_batch_y, d_ticket,
+                     mmre_sampler_draws_per_positive(neg_rate, neg_rel_rate, mode));
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
+}
+
+extern "C" int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                   const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
+                                   int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                                   int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
+                                   int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, void* stream) {
+  return sampler_impl(d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
+                      d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
+                      work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
+                      d_batch_t, d_batch_r, d_batch_y, nullptr, stream);
+}
+
+extern "C" int mmre_sampler_openke_step(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                        const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                        const int64_t* d_rig_head, const int64_t* d_lef_tail,
+                                        const int64_t* d_rig_tail, const int64_t* d_lef_rel, const int64_t* d_rig_rel,
+                                        const float* d_left_mean, const float* d_right_mean, int64_t n_ent,
+                                        int64_t n_rel, uint64_t* d_seeds, int64_t work_threads, int64_t batch_size,
+                                        int64_t neg_rate, int64_t neg_rel_rate, int64_t mode, const int32_t* d_blocks,
+                                        int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r,
+                                        float* d_batch_y, int32_t* d_ticket, void* stream) {
+  if (!d_ticket) return MMRE_ERR_ARG;
+  return sampler_impl(d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
+                      d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
+                      work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
+                      d_batch_t, d_batch_r, d_batch_y, d_ticket, stream);
 }
 
 extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,

@@ -40,6 +40,8 @@ SIGNATURES = {
     "mmre_sampler_blocks": (I32, [P, I64, P, P, P, P, P, P, P, P]),
     "mmre_sampler_openke_blocked": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64,
                                           I64, P, I64, P, P, P, P, P]),
+    "mmre_sampler_openke_step": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64,
+                                       I64, P, I64, P, P, P, P, P, P]),
     "mmre_sampler_repo": (I32, [P, P, P, I64, I64, I64, P, I64, P, P, P, I64, P, P, P, I64, ctypes.c_uint64, I32,
                                 P, P, P, P]),
     "mmre_sgd_step": (I32, [P, P, P, I32, F32, P]),
@@ -48,11 +50,13 @@ SIGNATURES = {
                               P]),
     "mmre_ns_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
                                P, P, P, P, P]),
-    "mmre_ns_fused_workspace": (I64, [I64, I64, I64, I64, I32]),
+    "mmre_ns_fused_workspace": (I64, [I32, I32, I64, I64, I64, I64, I32]),
     "mmre_ns_fused_forward": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
                                     F32, P, P, P, P]),
     "mmre_ns_fused_grad": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32, F32,
                                  P, P, P, P, P, P, P, P]),
+    "mmre_ns_fused_grad_sgd": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
+                                     F32, P, P, P, P, P, P, P, F32, P]),
     "mmre_ns_forward_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
                                        F32, P, P, P, P, P, P, P, P]),
     "mmre_score_rows_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, P, P, P, P, P, P]),

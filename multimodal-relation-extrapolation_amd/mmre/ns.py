@@ -4,9 +4,13 @@ forward  = model(data) in 'normal' mode for B*(1+k) rows -> MarginLoss (optional
            self-adversarial) + regul_rate * regularization, one launch + one fixed-order
            reduction (OpenKE strategy/NegativeSampling.py:23-32, MarginLoss.py:24-28,
            TransE.py:92-102; repo module/NegativeSampling.py:204-229).
-backward = d(loss)/d(embedding tables) into dense gradient tables: for TransE one wave per table
-           row sums the row's contributions in batch order (no float atomics, bit-reproducible);
-           other models scatter with float atomics.
+backward = d(loss)/d(embedding tables) into dense gradient tables: for every model one wave per
+           table row sums the row's contributions in batch order (no float atomics,
+           bit-reproducible). With `optimizer` (an mmre.optim.SGD doing plain SGD on the tables)
+           the same pass also applies its step, p <- fma(-lr, g, p) -- torch's SGD arithmetic,
+           so the parameters are bit-identical to backward() + step() -- and step() then skips
+           those tables (mmre_ns_fused_grad_sgd: the optimizer's re-read of the tables and the
+           gradients is gone).
 """
 from __future__ import annotations
 
@@ -43,7 +47,8 @@ class _FusedNS(torch.autograd.Function):
     with mmre_ns_backward as the backward."""
 
     @staticmethod
-    def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate, events):
+    def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate, events,
+                sgd):
         dev = ent.device
         N = batch * (1 + neg)
         score = torch.empty(N, dtype=torch.float32, device=dev)
@@ -53,10 +58,11 @@ class _FusedNS(torch.autograd.Function):
         ctx.fused = any(ctx.needs_input_grad[:4])
         ctx.has_im = ent_im is not None
         ctx.cfg = (spec, batch, neg, loss_margin, adv_t, regul_rate)
+        ctx.sgd = sgd if ctx.fused else None
         if ctx.fused:
             E, R = int(ent.shape[0]), int(rel.shape[0])
-            work = torch.empty(int(lib().mmre_ns_fused_workspace(batch, neg, E, R, spec.dim)), dtype=torch.float32,
-                               device=dev)
+            work = torch.empty(int(lib().mmre_ns_fused_workspace(spec.model_id, int(spec.norm_flag), batch, neg, E, R,
+                                                                 spec.dim)), dtype=torch.float32, device=dev)
             if events is not None:
                 events[0].record()
             call("mmre_ns_fused_forward", spec.model_id, int(spec.norm_flag), spec.model_margin,
@@ -80,7 +86,7 @@ class _FusedNS(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_score):
         if g_loss is None:
-            return (None,) * 14
+            return (None,) * 15
         ent, rel, ent_im, rel_im, h, t, r, score = ctx.saved_tensors
         spec, batch, neg, loss_margin, adv_t, regul_rate = ctx.cfg
         if not ctx.has_im:
@@ -94,15 +100,20 @@ class _FusedNS(torch.autograd.Function):
             ev = ctx.events
             if ev is not None and len(ev) > 2:
                 ev[2].record()
-            call("mmre_ns_fused_grad", spec.model_id, int(spec.norm_flag), spec.model_margin,
-                 int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), int(ent.shape[0]),
-                 int(rel.shape[0]), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg,
-                 float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei),
-                 ptr(gr), ptr(gri), ptr(ctx.work), stream_ptr(dev))
+            args = (spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin), ptr(ent),
+                    ptr(ent_im), ptr(rel), ptr(rel_im), int(ent.shape[0]), int(rel.shape[0]), spec.dim,
+                    spec.phase_denom, ptr(h), ptr(t), ptr(r), batch, neg, float(loss_margin), float(adv_t),
+                    float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei), ptr(gr), ptr(gri), ptr(ctx.work))
+            if ctx.sgd is not None:  # the optimizer's plain SGD step in the same pass (step() skips these tables)
+                opt, lr, tables = ctx.sgd
+                call("mmre_ns_fused_grad_sgd", *args, float(lr), stream_ptr(dev))
+                opt._fused_applied(tables)
+            else:
+                call("mmre_ns_fused_grad", *args, stream_ptr(dev))
             if ev is not None and len(ev) > 2:
                 ev[3].record()
-            ctx.work = ctx.events = None
-            return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None
+            ctx.work = ctx.events = ctx.sgd = None
+            return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None, None
         ge = torch.zeros_like(ent)
         gr = torch.zeros_like(rel)
         gei = torch.zeros_like(ent_im) if ent_im is not None else None
@@ -111,23 +122,34 @@ class _FusedNS(torch.autograd.Function):
              ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
              batch, neg, float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei),
              ptr(gr), ptr(gri), None, stream_ptr(dev))
-        return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None
+        return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None, None
 
 
 def fused_ns_loss(spec: NSSpec, ent, rel, h, t, r, batch: int, neg: int, loss_margin: float,
                   adv_temperature: float | None = None, regul_rate: float = 0.0, ent_im=None, rel_im=None,
-                  events=None):
+                  events=None, optimizer=None):
     """Returns (loss scalar tensor, scores (B*(1+k),)). Differentiable w.r.t. the tables.
     events: optional torch.cuda.Events recorded around the C-ABI calls alone (training mode), for
     kernel timing: (start, end) of mmre_ns_fused_forward, and with four, (start, end) of the
-    backward's mmre_ns_fused_grad."""
+    backward's mmre_ns_fused_grad.
+    optimizer: an mmre.optim.SGD over the tables; when its step is plain SGD and the tables have
+    no gradient yet (zero_grad(set_to_none=True): autograd will assign, not accumulate), the
+    backward applies the step as well (mmre_ns_fused_grad_sgd) and optimizer.step() skips the
+    tables. The parameters afterwards are bit-identical to backward() + step(); p.grad is still
+    written. Otherwise the optimizer is ignored here."""
     require_cuda(ent, rel, h, t, r, ent_im, rel_im)
     h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
     if ent.dtype != torch.float32 or rel.dtype != torch.float32:
         raise TypeError("fused_ns_loss: float32 tables")
+    tables = [x for x in (ent, rel, ent_im, rel_im) if x is not None]
+    sgd = None
+    if optimizer is not None and hasattr(optimizer, "fusable_lr"):
+        lr = optimizer.fusable_lr(tables)
+        if lr is not None:
+            sgd = (optimizer, lr, tables)
     return _FusedNS.apply(ent.contiguous(), rel.contiguous(), None if ent_im is None else ent_im.contiguous(),
                           None if rel_im is None else rel_im.contiguous(), h, t, r, spec, int(batch), int(neg),
-                          float(loss_margin), float(adv_temperature or 0.0), float(regul_rate), events)
+                          float(loss_margin), float(adv_temperature or 0.0), float(regul_rate), events, sgd)
 
 
 class _ScoreRows(torch.autograd.Function):

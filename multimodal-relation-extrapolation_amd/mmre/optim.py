@@ -27,6 +27,31 @@ class SGD(torch.optim.SGD):
     fallback_steps = 0
     fallback_reason = None
 
+    # ---- fused mode: the fused negative-sampling backward applies this optimizer's step to the
+    # embedding tables in its row-owner pass (mmre.ns.fused_ns_loss(..., optimizer=opt)); step()
+    # then skips them. Bit-identical parameters (same fma), one pass over the tables fewer.
+    def fusable_lr(self, tables):
+        """lr when `tables` can take the fused step: all in one plain group, eligible for the HIP
+        step, and without a gradient yet (autograd will assign theirs, not accumulate); else None."""
+        ids = {id(t) for t in tables}
+        for group in self.param_groups:
+            mine = [p for p in group["params"] if id(p) in ids]
+            if not mine:
+                continue
+            if len(mine) != len(ids) or any(p.grad is not None or not p.requires_grad or not p.is_leaf for p in mine):
+                return None
+            if not self._plain(group) or float(group["lr"]) == 0.0:
+                return None
+            if any(not p.is_cuda or p.dtype != torch.float32 or not p.is_contiguous() for p in mine):
+                return None
+            return float(group["lr"])
+        return None
+
+    def _fused_applied(self, tables):
+        if not hasattr(self, "_fused_done"):
+            self._fused_done = set()
+        self._fused_done.update(id(t) for t in tables)
+
     def _why_not(self, group, ps):
         if not self._plain(group):
             return "momentum / weight_decay / nesterov / maximize"
@@ -49,9 +74,11 @@ class SGD(torch.optim.SGD):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        done = getattr(self, "_fused_done", set())
+        self._fused_done = set()
         work = []
         for group in self.param_groups:
-            ps = [p for p in group["params"] if p.grad is not None]
+            ps = [p for p in group["params"] if p.grad is not None and id(p) not in done]
             why = self._why_not(group, ps) if ps else None
             if why is not None:  # torch's own SGD step for every group -- counted, not silent
                 type(self).fallback_steps += 1

@@ -30,6 +30,7 @@ class OpenKESampler:
         self.work_threads = int(work_threads)
         self.bern = bool(bern)
         self._seeds_dev = torch.empty(self.work_threads, dtype=torch.int64, device=self.device)
+        self._ticket = torch.zeros(1, dtype=torch.int32, device=self.device)  # mmre_sampler_openke_step
         self.seeds = (np.asarray(seeds, np.uint64).copy() if seeds is not None
                       else glibc_seeds(self.work_threads, seed_skip))
         self.train_total = int(train_total if train_total is not None else index.train_total)
@@ -67,17 +68,16 @@ class OpenKESampler:
                        batch_r=torch.empty(n, dtype=torch.int64, device=dev),
                        batch_y=torch.empty(n, dtype=torch.float32, device=dev))
         d = self._d
-        call("mmre_sampler_openke_blocked", ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]),
+        # one launch: the batch, and the per-thread LCG states advanced (by a fixed number of draws
+        # per positive) for the next call by the kernel's last workgroup -- no host copy per batch
+        call("mmre_sampler_openke_step", ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]),
              ptr(d["tail_hrt"]), ptr(d["rel_hrt"]), ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]),
              ptr(d["rig_tail"]), ptr(d["lef_rel"]), ptr(d["rig_rel"]), ptr(d["left_mean"]) if self.bern else None,
              ptr(d["right_mean"]) if self.bern else None, self.index.n_ent, self.index.n_rel,
              ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel), int(mode),
              ptr(self._blocks), self._n_blocks, ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]),
-             ptr(out["batch_y"]), stream_ptr(dev))
-        # the per-thread LCG states advance by a fixed number of draws per positive: on the device,
-        # behind the sampling kernel on the same stream (no host copy per batch), and on the mirror
-        call("mmre_sampler_advance_device", ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel),
-             int(mode), stream_ptr(dev))
+             ptr(out["batch_y"]), ptr(self._ticket), stream_ptr(dev))
+        # ... and the host mirror
         call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, B,
              int(neg_ent), int(neg_rel), int(mode))
         return out

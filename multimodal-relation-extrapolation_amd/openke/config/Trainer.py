@@ -61,6 +61,9 @@ class Trainer(object):
             self.model.cuda()
         if self.optimizer is None:
             self.optimizer = self.make_optimizer()
+        if hasattr(self.model, "fuse_optimizer") and hasattr(self.optimizer, "fusable_lr"):
+            # the fused negative-sampling backward applies the plain SGD step itself (bit-identical)
+            self.model.fuse_optimizer(self.optimizer)
         for epoch in range(self.train_times):
             res = 0.0
             for data in self.data_loader:

@@ -57,6 +57,52 @@ def transe_ns_loss(ent, rel, h, t, r, batch_size, margin, norm_flag=True, p_norm
     return loss[0] if loss.dim() else loss, score
 
 
+def model_ns_loss(model, tables, h, t, r, batch_size, margin, adv_temperature=None, regul_rate=0.0,
+                  model_margin=6.0, epsilon=2.0):
+    """strategy NegativeSampling.forward (strategy/NegativeSampling.py:13-32) over DistMult /
+    ComplEx / RotatE in 'normal' mode + MarginLoss (+ regularization), the reference's op
+    sequences (DistMult.py:34-66, ComplEx.py:20-55, RotatE.py:45-103) over explicit tables
+    {ent, rel[, ent_im, rel_im]}; differentiable w.r.t. them (any dtype)."""
+    import math
+
+    import torch
+    import torch.nn.functional as F
+    if model == "distmult":
+        hv, tv, rv = tables["ent"][h], tables["ent"][t], tables["rel"][r]
+        score = torch.sum((hv * rv) * tv, -1).flatten()
+        regs = [hv, tv, rv]
+    elif model == "complex":
+        er, ei, rr_, ri = tables["ent"], tables["ent_im"], tables["rel"], tables["rel_im"]
+        h_re, h_im, t_re, t_im, r_re, r_im = er[h], ei[h], er[t], ei[t], rr_[r], ri[r]
+        score = torch.sum(h_re * t_re * r_re + h_im * t_im * r_re + h_re * t_im * r_im - h_im * t_re * r_im, -1)
+        regs = [h_re, h_im, t_re, t_im, r_re, r_im]
+    elif model == "rotate":
+        hv, tv, rv = tables["ent"][h], tables["ent"][t], tables["rel"][r]
+        dim = rv.shape[-1]
+        rng = torch.tensor([(model_margin + epsilon) / dim], dtype=torch.float32).to(rv.dtype)
+        re_h, im_h = torch.chunk(hv, 2, dim=-1)
+        re_t, im_t = torch.chunk(tv, 2, dim=-1)
+        phase = rv / (rng.item() / math.pi)
+        re_r, im_r = torch.cos(phase), torch.sin(phase)
+        re_s = re_h * re_r - im_h * im_r - re_t
+        im_s = re_h * im_r + im_h * re_r - im_t
+        score = model_margin - torch.stack([re_s, im_s], dim=0).norm(dim=0).sum(dim=-1).flatten()
+        regs = [hv, tv, rv]
+    else:
+        raise ValueError(model)
+    p = score[:batch_size].view(-1, batch_size).permute(1, 0)
+    n = score[batch_size:].view(-1, batch_size).permute(1, 0)
+    m = torch.tensor([margin], dtype=score.dtype)
+    if adv_temperature is not None:
+        w = F.softmax(-n * adv_temperature, dim=-1).detach()
+        loss = (w * torch.max(p - n, -m)).sum(dim=-1).mean() + m
+    else:
+        loss = torch.max(p - n, -m).mean() + m
+    if regul_rate != 0:
+        loss = loss + regul_rate * sum(torch.mean(x ** 2) for x in regs) / len(regs)
+    return loss[0] if loss.dim() else loss, score
+
+
 def run_trainer(workdir: str, base_so: str = REF_BASE_SO):
     import torch
     with open(os.path.join(workdir, "meta.json")) as f:

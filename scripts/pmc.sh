@@ -6,6 +6,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/pmc_$tag
 mkdir -p $out
+# the binary these counters belong to (bench.py reports traffic only for this build)
+python -c "import hashlib; print(hashlib.sha256(open('multimodal-relation-extrapolation_amd/mmre/lib/libmmre_hip.so','rb').read()).hexdigest()[:16])" > $out/lib_sha256.txt
 i=0
 for grp in "GRBM_GUI_ACTIVE SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS" \

@@ -18,6 +18,11 @@ for k, d in acc.items():
     print(k[:90])
     for c, v in sorted(summary[k].items()):
         print(f"   {c:28s} {v:.4g}")
+try:  # the build the passes ran (scripts/pmc.sh wrote it): bench.py ignores counters of another build
+    summary["__build__"] = {"lib_sha256": open(f"gpurun_out/pmc_{tag}/lib_sha256.txt").read().strip(),
+                            "tag": tag}
+except OSError:
+    pass
 if "--json" in sys.argv:
     out = sys.argv[sys.argv.index("--json") + 1]
     json.dump(summary, open(out, "w"), indent=1, sort_keys=True)

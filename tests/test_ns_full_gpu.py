@@ -120,7 +120,7 @@ def test_one_shot_abi_equals_autograd_pair(c2_training):
                                 b["batch_r"], B, k, 3.0, None, 0.5)
     loss.backward()
     e0, r0 = ent.detach(), rel.detach()
-    work = torch.empty(int(lib().mmre_ns_fused_workspace(B, k, E, R, d)), dtype=torch.float32, device=DEV)
+    work = torch.empty(int(lib().mmre_ns_fused_workspace(0, 1, B, k, E, R, d)), dtype=torch.float32, device=DEV)
     s1 = torch.empty(B * (1 + k), dtype=torch.float32, device=DEV)
     l1 = torch.empty(1, dtype=torch.float32, device=DEV)
     ge = torch.full_like(e0, float("nan"))  # poisoned: every row must be written
@@ -184,3 +184,132 @@ def test_fused_ns_deferred_generic_rows(c2_training, frac, p_norm, adv):
     for got, want in ((grads[0][0], e64.grad), (grads[0][1], r64.grad)):
         gw, gg = want.numpy(), got.cpu().double().numpy()
         assert np.linalg.norm(gg - gw) <= 1e-3 * np.linalg.norm(gw)
+
+
+def _tables(model, w, seed=0):
+    """Float32 tables of the C2 id space for another model (OpenKE-like init, seed fixed)."""
+    g = torch.Generator().manual_seed(seed)
+    E, R, d = int(w["n_ent"]), int(w["n_rel"]), 200
+    u = lambda n, c, s: (torch.rand((n, c), generator=g) * 2 - 1) * s
+    if model == "distmult":
+        return {"ent": u(E, d, 0.5), "rel": u(R, d, 0.5)}
+    if model == "complex":
+        return {"ent": u(E, d, 0.3), "ent_im": u(E, d, 0.3), "rel": u(R, d, 0.3), "rel_im": u(R, d, 0.3)}
+    return {"ent": u(E, 2 * d, 8.0 / (2 * d)), "rel": u(R, d, 8.0 / d)}   # RotatE: (margin + eps) / (2) d
+
+
+@pytest.mark.parametrize("model,neg,margin,adv,regul", [
+    ("distmult", 25, 5.0, None, 0.0), ("distmult", 10, 3.0, 1.0, 0.5),
+    ("complex", 25, 5.0, None, 0.5), ("complex", 10, 3.0, 1.0, 0.0),
+    ("rotate", 25, 5.0, None, 0.0), ("rotate", 10, 6.0, 1.0, 0.5)])
+def test_other_models_row_owner_gradients_at_c2_shape(c2_training, model, neg, margin, adv, regul):
+    """DistMult / ComplEx / RotatE at the C2 training shape (B 2,721, d 200): the row-owner
+    gradient (no float atomics): loss, scores and gradients vs the float64 reference op sequence
+    (oracle/ref_trainer.model_ns_loss) -- gradients within 1e-4 of the table's largest entry --
+    and bit-identical gradient tables run to run."""
+    import ref_trainer
+    from mmre.link import rotate_phase_denom
+    from mmre.ns import NSSpec, fused_ns_loss
+    w, _ = c2_training
+    B, d = 2721, 200
+    b = _c2_batch(c2_training, neg)
+    tabs = _tables(model, w)
+    spec = NSSpec(model, d, model_margin=6.0 if model == "rotate" else None,
+                  phase_denom=rotate_phase_denom(6.0, 2.0, d) if model == "rotate" else 0.0)
+    runs = []
+    for _ in range(2):
+        T = {k: v.to(DEV).requires_grad_(True) for k, v in tabs.items()}
+        loss, score = fused_ns_loss(spec, T["ent"], T["rel"], b["batch_h"], b["batch_t"], b["batch_r"], B, neg, margin,
+                                    adv, regul, ent_im=T.get("ent_im"), rel_im=T.get("rel_im"))
+        loss.backward()
+        runs.append((loss.detach().clone(), score.clone(), {k: v.grad.clone() for k, v in T.items()}))
+    torch.cuda.synchronize()
+    for k in tabs:
+        assert torch.equal(runs[0][2][k], runs[1][2][k]), k
+    T64 = {k: v.double().requires_grad_(True) for k, v in tabs.items()}
+    h, t, r = (b[x].cpu() for x in ("batch_h", "batch_t", "batch_r"))
+    ref_loss, ref_score = ref_trainer.model_ns_loss(model, T64, h, t, r, B, margin, adv, regul, model_margin=6.0)
+    ref_loss.backward()
+    rs = ref_score.detach().numpy()
+    assert np.abs(runs[0][1].cpu().numpy() - rs).max() <= 1e-4 * max(1.0, np.abs(rs).max())
+    assert abs(float(runs[0][0]) - float(ref_loss)) <= 1e-5 * max(1.0, abs(float(ref_loss)))
+    for k in tabs:
+        gw, gg = T64[k].grad.numpy(), runs[0][2][k].cpu().double().numpy()
+        assert np.abs(gg - gw).max() <= 1e-4 * np.abs(gw).max(), (k, np.abs(gg - gw).max(), np.abs(gw).max())
+
+
+@pytest.mark.parametrize("model", ["transe", "distmult", "complex", "rotate"])
+def test_fused_sgd_step_equals_backward_then_step(c2_training, model):
+    """fused_ns_loss(..., optimizer=mmre.optim.SGD): the backward applies the SGD step in its
+    row-owner pass and step() skips the tables -- parameters and gradients bit-identical to the
+    unfused backward() + step(), over three training steps."""
+    from mmre.link import rotate_phase_denom
+    from mmre.ns import NSSpec, fused_ns_loss
+    from mmre.optim import SGD
+    w, _ = c2_training
+    B, k, d = 2721, 10, 200
+    tabs = _tables(model, w) if model != "transe" else {"ent": w["ent"], "rel": w["rel"]}
+    spec = NSSpec(model, d, norm_flag=model == "transe", model_margin=6.0 if model == "rotate" else None,
+                  phase_denom=rotate_phase_denom(6.0, 2.0, d) if model == "rotate" else 0.0)
+    batches = [_c2_batch(c2_training, k, skip=s) for s in (1, 2, 3)]
+    out = []
+    for fuse in (False, True):
+        T = {n: v.to(DEV).clone().requires_grad_(True) for n, v in tabs.items()}
+        opt = SGD(list(T.values()), lr=0.7)
+        for b in batches:
+            opt.zero_grad(set_to_none=True)
+            loss, _ = fused_ns_loss(spec, T["ent"], T["rel"], b["batch_h"], b["batch_t"], b["batch_r"], B, k, 4.0,
+                                    None, 0.25, ent_im=T.get("ent_im"), rel_im=T.get("rel_im"),
+                                    optimizer=opt if fuse else None)
+            loss.backward()
+            if fuse:
+                assert len(opt._fused_done) == len(T)
+            opt.step()
+        torch.cuda.synchronize()
+        out.append({n: (v.detach().clone(), v.grad.clone()) for n, v in T.items()})
+    for n in tabs:
+        assert torch.equal(out[0][n][0], out[1][n][0]), n
+        assert torch.equal(out[0][n][1], out[1][n][1]), n
+        assert not torch.equal(out[0][n][0], tabs[n].to(DEV))
+
+
+@pytest.mark.parametrize("model,n_pos", [("transe", 700), ("transe", 3000), ("distmult", 700), ("rotate", 3000)])
+def test_hub_rows_ordered_deterministically(c2_training, model, n_pos):
+    """Hub rows: every positive of a batch shares one relation, so that relation's bucket holds
+    n_pos slots -- past the 64-slot bucket into the overflow list, ordered in LDS (700) or by
+    the repeated-minimum fallback (3,000). Gradients vs the float64 reference, bit-reproducible."""
+    import ref_trainer
+    from mmre.link import rotate_phase_denom
+    from mmre.ns import NSSpec, fused_ns_loss
+    w, _ = c2_training
+    k, d = 5, 200
+    b = _c2_batch(c2_training, k)
+    B0 = 2721
+    sel = torch.arange(n_pos) % B0
+    rows = torch.cat([sel + j * B0 for j in range(1 + k)]).to(DEV)
+    h, t, r = (b[x][rows].clone() for x in ("batch_h", "batch_t", "batch_r"))
+    r[:] = 17                                           # one hub relation
+    tabs = _tables(model, w) if model != "transe" else {"ent": w["ent"], "rel": w["rel"]}
+    spec = NSSpec(model, d, norm_flag=model == "transe", model_margin=6.0 if model == "rotate" else None,
+                  phase_denom=rotate_phase_denom(6.0, 2.0, d) if model == "rotate" else 0.0)
+    grads = []
+    for _ in range(2):
+        T = {n: v.to(DEV).clone().requires_grad_(True) for n, v in tabs.items()}
+        loss, _ = fused_ns_loss(spec, T["ent"], T["rel"], h, t, r, n_pos, k, 5.0, None, 0.5, ent_im=T.get("ent_im"),
+                                rel_im=T.get("rel_im"))
+        loss.backward()
+        grads.append({n: v.grad.clone() for n, v in T.items()})
+    torch.cuda.synchronize()
+    for n in tabs:
+        assert torch.equal(grads[0][n], grads[1][n]), n
+    T64 = {n: v.double().requires_grad_(True) for n, v in tabs.items()}
+    hc, tc, rc = h.cpu(), t.cpu(), r.cpu()
+    if model == "transe":
+        ref_loss, _ = ref_trainer.transe_ns_loss(T64["ent"], T64["rel"], hc, tc, rc, n_pos, 5.0, norm_flag=True,
+                                                 regul_rate=0.5)
+    else:
+        ref_loss, _ = ref_trainer.model_ns_loss(model, T64, hc, tc, rc, n_pos, 5.0, None, 0.5, model_margin=6.0)
+    ref_loss.backward()
+    for n in tabs:
+        gw, gg = T64[n].grad.numpy(), grads[0][n].cpu().double().numpy()
+        assert np.linalg.norm(gg - gw) <= 1e-4 * np.linalg.norm(gw), (n, np.linalg.norm(gg - gw), np.linalg.norm(gw))

@@ -65,7 +65,7 @@ def _worker(rank, world, port, res_path, keep_rel=None):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,keep_rel", [(2, None), (3, None), (3, 2)])
+@pytest.mark.parametrize("world,keep_rel", [(2, None), (3, None), (3, 2), (8, 2)])
 def test_sharded_counts_equal_single_rank(tmp_path, world, keep_rel):
     """keep_rel=2 at world 3: one rank owns no relation and joins the all-gather empty."""
     import oracle
@@ -92,26 +92,39 @@ def test_sharded_counts_equal_single_rank(tmp_path, world, keep_rel):
 
 
 # ------------------------------------------------------------------ GPU --
-def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph):
+def _workload(dataset, model, dim, keep_triples=None):
+    from mmre.workloads import synthetic_large, zs_workload
+    w = synthetic_large(dim=dim) if dataset == "synthetic-1M" else zs_workload(dataset, model, dim)
+    if keep_triples is not None:  # fewer queries than ranks: some ranks own an empty shard
+        for k in ("test_h", "test_r", "test_t"):
+            w[k] = np.asarray(w[k])[:keep_triples]
+    return w
+
+
+def _spec(w, model, dim, dev):
+    from mmre.link import ScoreSpec, rotate_phase_denom
+    pk = {"transe": 0, "distmult": 2, "complex": 2, "rotate": 3}[model]
+    return ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
+                     ent_im=w["ent_im"].to(dev) if "ent_im" in w else None,
+                     rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=model == "transe",
+                     pred_kind=pk, margin=float(w.get("margin", 0.0)),
+                     phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
+
+
+def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_triples=None):
     """Each rank: the HIP sweep on cuda:0 through ShardedLinkEvaluation.launch/finish (counts
     exchanged over gloo through host memory); rank 0 also runs the single-process evaluation
     and the out-of-order ticket sequence."""
     sys.path[:0] = [PKG, os.path.join(REPO, "oracle"), REPO]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mmre.link import FilterIndex, ScoreSpec, evaluate_link_prediction, rotate_phase_denom
+    from mmre.link import FilterIndex, evaluate_link_prediction
     from mmre.sharding import ShardedLinkEvaluation
-    from mmre.workloads import zs_workload
     dev = torch.device("cuda:0")
-    w = zs_workload(dataset, model, dim)
+    w = _workload(dataset, model, dim, keep_triples)
     E = w["n_ent"]
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
-    pk = {"transe": 0, "distmult": 2, "complex": 2, "rotate": 3}[model]
-    spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
-                     ent_im=w["ent_im"].to(dev) if "ent_im" in w else None,
-                     rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=model == "transe",
-                     pred_kind=pk, margin=float(w.get("margin", 0.0)),
-                     phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
+    spec = _spec(w, model, dim, dev)
     ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev, graph=graph)
     a = ev.launch()
     b = ev.launch()
@@ -129,17 +142,21 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dataset,model,dim,world,graph", [("FB15K-237-ZS", "transe", 200, 2, False),
-                                                            ("FB15K-237-ZS", "transe", 200, 2, True),
-                                                            ("DB15K-ZS", "complex", 200, 3, True)])
-def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph):
+@pytest.mark.parametrize("dataset,model,dim,world,graph,keep", [("FB15K-237-ZS", "transe", 200, 2, False, None),
+                                                                 ("FB15K-237-ZS", "transe", 200, 2, True, None),
+                                                                 ("DB15K-ZS", "complex", 200, 3, True, None),
+                                                                 ("FB15K-237-ZS", "rotate", 512, 8, True, None),
+                                                                 ("FB15K-237-ZS", "transe", 200, 8, True, 3)])
+def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph, keep):
     """The multi-rank path with the real HIP sweep at full size (C2; C3 with its largest
-    relation split across ranks), eager and with each rank's local evaluation replayed from a
-    hipGraph: every rank's gathered counts -- for three overlapping evaluations finished out of
-    order -- and rank 0's metrics are bit-equal to one process."""
+    relation split across ranks; C4 RotatE d 512 at world 8, the driver's node size, every
+    rank on the one GPU of the box), eager and with each rank's local evaluation replayed from
+    a hipGraph: every rank's gathered counts -- for three overlapping evaluations finished out
+    of order -- and rank 0's metrics are bit-equal to one process. keep=3: three test triples
+    (6 sweeps) over 8 ranks, so two ranks own an empty shard and still join the all-gather."""
     port = _free_port()
     res = str(tmp_path / "hip")
-    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph), nprocs=world, join=True)
+    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph, keep), nprocs=world, join=True)
     outs = [dict(np.load(f"{res}_{k}.npz")) for k in range(world)]
     single = outs[0]["single"]
     assert bool(outs[0]["metrics_equal"])
@@ -156,18 +173,13 @@ def _entity_worker(rank, world, port, res_path, dataset, model, dim):
     sys.path[:0] = [PKG, os.path.join(REPO, "oracle"), REPO]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from mmre.link import FilterIndex, ScoreSpec, evaluate_link_prediction
+    from mmre.link import FilterIndex, evaluate_link_prediction
     from mmre.sharding import EntityShardedLinkEvaluation
-    from mmre.workloads import zs_workload
     dev = torch.device("cuda:0")
-    w = zs_workload(dataset, model, dim)
+    w = _workload(dataset, model, dim)
     E = w["n_ent"]
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
-    pk = {"transe": 0, "distmult": 2, "complex": 2}[model]
-    spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
-                     ent_im=w["ent_im"].to(dev) if "ent_im" in w else None,
-                     rel_im=w["rel_im"].to(dev) if "rel_im" in w else None, norm_flag=model == "transe",
-                     pred_kind=pk, margin=0.0)
+    spec = _spec(w, model, dim, dev)
     ev = EntityShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
     a = ev.launch()
     b = ev.launch()
@@ -184,11 +196,13 @@ def _entity_worker(rank, world, port, res_path, dataset, model, dim):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dataset,model,dim,world", [("FB15K-237-ZS", "transe", 200, 2),
-                                                      ("DB15K-ZS", "complex", 200, 3)])
+                                                      ("DB15K-ZS", "complex", 200, 3),
+                                                      ("synthetic-1M", "distmult", 256, 8)])
 def test_entity_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world):
     """SURVEY 8(e)'s alternative for huge E: each rank sweeps every query against a contiguous
-    slice of the entity tiles (VALU TransE and MFMA ComplEx kernels), counts summed by one
-    all-reduce: every rank's counts and rank 0's metrics are bit-equal to one process."""
+    slice of the entity tiles (VALU TransE and MFMA ComplEx / DistMult kernels), counts summed
+    by one all-reduce: every rank's counts and rank 0's metrics are bit-equal to one process --
+    C5 (1 M entities, DistMult d 256) at world 8, every rank on the one GPU of the box."""
     port = _free_port()
     res = str(tmp_path / "ent")
     mp.spawn(_entity_worker, args=(world, port, res, dataset, model, dim), nprocs=world, join=True)
