@@ -424,15 +424,36 @@ def bench_ns(args, world, rank, dev, dist):
     torch.cuda.current_stream(dev).wait_stream(side)
     torch.cuda.synchronize()
     graph = None
+    one = torch.ones((), dtype=torch.float32, device=dev)  # the upstream gradient loss.backward() would fill
     if not args.ns_eager:
-        opt.zero_grad(set_to_none=True)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            g_b = smp.sample(B, k, out=bufs[0])
-            g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k, margin,
-                                      optimizer=opt)
-            g_loss.backward()
-            opt.step()
+        # two hipGraphs, one per batch buffer: graph p trains on bufs[p] while a forked stream
+        # samples the next batch into bufs[1 - p] (the data loader's prefetch: the sampler's
+        # batches and LCG states are the serial sequence, batch i + 1 drawn after batch i), then
+        # joins. --ns-serial: one graph, the batch sampled in line before the step.
+        graphs = []
+        fork = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev)
+        for par in ((0,) if (not args.ns_prefetch) else (0, 1)):
+            opt.zero_grad(set_to_none=True)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                if (not args.ns_prefetch):
+                    g_b = smp.sample(B, k, out=bufs[0])
+                else:
+                    g_b = bufs[par]
+                    fork.wait_stream(torch.cuda.current_stream(dev))
+                    with torch.cuda.stream(fork):
+                        smp.sample(B, k, out=bufs[1 - par])
+                g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k,
+                                          margin, optimizer=opt)
+                torch.autograd.backward(g_loss, grad_tensors=one)
+                opt.step()
+                if not (not args.ns_prefetch):
+                    torch.cuda.current_stream(dev).wait_stream(fork)
+            graphs.append(g)
+        graph = graphs[0]
+        if not (not args.ns_prefetch):
+            smp.sample(B, k, out=bufs[0])  # the first batch; every replay then prefetches the next
         torch.cuda.synchronize()
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(7)) for _ in range(args.steps)]
     if dist:
@@ -441,7 +462,7 @@ def bench_ns(args, world, rank, dev, dist):
     t0 = time.perf_counter()
     for i in range(args.steps):
         if graph is not None:
-            graph.replay()
+            graphs[i % len(graphs)].replay()
         else:
             loss = step(i, evs[i])
     torch.cuda.synchronize()
@@ -450,7 +471,7 @@ def bench_ns(args, world, rank, dev, dist):
     elapsed = time.perf_counter() - t0
     if graph is not None:  # the fused call and the step's parts timed on eager steps after the timed region
         loss = g_loss.detach().clone()
-        del g_loss, g_b, graph  # drop the captured autograd graph before eager backward passes
+        del g_loss, g_b, graph, graphs  # drop the captured autograd graphs before eager backward passes
         graph = True
         evs = evs[:20]
         for i in range(len(evs)):
@@ -510,13 +531,13 @@ def bench_ns(args, world, rank, dev, dist):
                        "+ the FB15K-237-ZS test triples",
                "config": {"workload": CONFIGS["ns"]["workload"], "batch": B, "neg_ent": k, "rows_per_step": n_rows,
                           "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}",
-                          "launch": "hipGraph replay of the whole step" if graph else "eager"},
+                          "launch": ("eager" if not graph else "hipGraph replay of the whole step" +
+                                     ("" if (not args.ns_prefetch) else ", next batch sampled on a forked stream (prefetch)"))},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": None,
                             "kernel": "mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false> + "
-                                      "k_ns_transe_finish<4, false> (deferred generic positives: none for OpenKE "
-                                      "batches; the loss) + k_ns_row_owner<4, false>: events around hipGraph replays of "
-                                      "the one-shot C-ABI call",
+                                      "k_ns_reduce (the loss) + k_ns_row_owner<4, false>: events around hipGraph "
+                                      "replays of the one-shot C-ABI call",
                             "kernel_ms": fused_ms, "eager_fused_forward_ms": fused_fwd_ms,
                             "eager_fused_grad_ms": fused_grad_ms,
                             "algorithmic_bytes": fwd_bytes + grad_bytes, "slot_bytes": slot_bytes,
@@ -526,8 +547,8 @@ def bench_ns(args, world, rank, dev, dist):
                             "note": "no float atomics: the gradient contributions are bucketed by table row and "
                                     "one wave per table row summing them in batch order (bit-reproducible); the "
                                     "step is five launches: the sampler (seed advance folded in), the pre-pass, the "
-                                    "fused kernel, the finish workgroup (loss), the row-owner pass with the SGD step "
-                                    "fused in (mmre_ns_fused_grad_sgd, bit-identical to backward() + step())"},
+                                    "fused kernel, the loss reduction, the row-owner pass with the SGD step fused in "
+                                    "(mmre_ns_fused_grad_sgd, bit-identical to backward() + step())"},
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
@@ -916,6 +937,9 @@ def main():
                     help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
     ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
     ap.add_argument("--ns-eager", action="store_true", help="--config ns: launch each step eagerly (no hipGraph)")
+    ap.add_argument("--ns-prefetch", action="store_true",
+                    help="--config ns: sample the next batch on a forked stream while the current one trains "
+                         "(default: in line before each step; the fork/join graph measured slower)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--init-tables", action="store_true",
                     help="C3/C4/C5: OpenKE-initialised tables (truths rank ~E/2) instead of structured ones")

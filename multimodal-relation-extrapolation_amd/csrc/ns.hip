@@ -243,24 +243,41 @@ __global__ __launch_bounds__(256) void k_ns_forward(NSArgs A, float* __restrict_
 }
 
 // Fixed-order reduction of the per-positive partials (bit-reproducible loss) by threads
-// 0..255 of the workgroup (every thread of it must call: it synchronises).
+// 0..255 of the workgroup (every thread of it must call: it synchronises): strided double sums
+// per thread, xor-butterfly wave sums (a + b and b + a agree, so every lane holds the same
+// total), the four wave totals in a fixed order; one barrier.
 __device__ void ns_reduce_block(const NSArgs& A, const float* part, float* loss) {
-  __shared__ double red[7][256];
+  __shared__ double red[7][4];
   double acc[7] = {0, 0, 0, 0, 0, 0, 0};
   const bool mine = threadIdx.x < 256;
-  for (int64_t b = threadIdx.x; mine && b < A.B; b += 256)
-    for (int i = 0; i < 7; ++i) acc[i] += part[b * 7 + i];
-  if (mine)
-    for (int i = 0; i < 7; ++i) red[i][threadIdx.x] = acc[i];
-  __syncthreads();
-  for (int s = 128; s >= 1; s >>= 1) {
-    if ((int)threadIdx.x < s)
-      for (int i = 0; i < 7; ++i) red[i][threadIdx.x] += red[i][threadIdx.x + s];
-    __syncthreads();
+  if (A.regul_rate != 0.0f) {
+    for (int64_t b = threadIdx.x; mine && b < A.B; b += 256) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) acc[i] += part[b * 7 + i];
+    }
+  } else {  // only the hinge partials: eight positives' loads in flight per round trip
+    for (int64_t b0 = threadIdx.x; mine && b0 < A.B; b0 += 256 * 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = b0 + 256 * u < A.B ? part[(b0 + 256 * u) * 7] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[0] += x[u];
+    }
   }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) acc[i] += __shfl_xor(acc[i], s);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0 && w < 4)
+    for (int i = 0; i < 7; ++i) red[i][w] = acc[i];
+  __syncthreads();
   if (threadIdx.x == 0) {
+    double t[7];
+    for (int i = 0; i < 7; ++i) t[i] = (red[i][0] + red[i][1]) + (red[i][2] + red[i][3]);
     const double Bd = (double)A.B, Kd = (double)A.K;
-    double l = A.adv_t > 0.0f ? red[0][0] / Bd : red[0][0] / (Bd * Kd);
+    double l = A.adv_t > 0.0f ? t[0] / Bd : t[0] / (Bd * Kd);
     l += A.loss_margin;
     if (A.regul_rate != 0.0f) {
       const double N = Bd * (1.0 + Kd);
@@ -268,10 +285,9 @@ __device__ void ns_reduce_block(const NSArgs& A, const float* part, float* loss)
       const double ew = A.model == MMRE_ROTATE ? 2.0 * d : d;
       double reg;
       if (A.model == MMRE_COMPLEX)
-        reg = (red[1][0] / (N * d) + red[4][0] / (N * d) + red[2][0] / (N * d) + red[5][0] / (N * d) +
-               red[3][0] / (N * d) + red[6][0] / (N * d)) / 6.0;
+        reg = (t[1] / (N * d) + t[4] / (N * d) + t[2] / (N * d) + t[5] / (N * d) + t[3] / (N * d) + t[6] / (N * d)) / 6.0;
       else
-        reg = (red[1][0] / (N * ew) + red[2][0] / (N * ew) + red[3][0] / (N * d)) / 3.0;
+        reg = (t[1] / (N * ew) + t[2] / (N * ew) + t[3] / (N * d)) / 3.0;
       l += (double)A.regul_rate * reg;
     }
     loss[0] = (float)l;
@@ -743,28 +759,36 @@ __global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const floa
 // ---------------------------------------------------------------------------------------
 constexpr int NSF_MAXJ = 8;
 constexpr int NS_BUCKET = 64;   // slot ids kept in a table row's own bucket (one wave's width)
-constexpr int NS_HUB = 1024;    // a row with more slots than a bucket orders them in LDS up to this many
+constexpr int NS_HUB = 512;     // a row with more slots than a bucket orders them in LDS up to this many
 
 struct NSSlots {        // the row-owner gradient's workspace
   float* shared;        // 3 B rows of dim floats: the positives' own rows (TransE)
   float* rec;           // K B records of a negative's gx (ns_rec_words); other models: per slot, 2 d_pad floats
-  float* mult;          // per slot: occurrences of its row in the batch (regularization)
   int32_t* counts;      // per table row: its slots (zeroed every call)
-  int32_t* bucket;      // per table row: NS_BUCKET slot ids, in arrival order
-  int32_t* ovf;         // (row, slot) pairs past a full bucket
+  int64_t* bucket;      // per table row: NS_BUCKET entries (slot id << 32 | occurrences as float bits), arrival order
+  int64_t* ovf;         // (row, entry) pairs past a full bucket
   int32_t* ovf_n;       // overflow pairs (zeroed every call)
   uint32_t sentinel;    // n_ent + n_rel: no slot
 };
 
-// a slot id into its row's bucket (or the overflow list)
-__device__ __forceinline__ void put_slot(const NSSlots& S, uint32_t key, int64_t slot) {
+// slot id and its row's occurrences in the batch (the regularization weight) as one bucket entry:
+// ordering entries orders the slot ids
+__device__ __forceinline__ int64_t slot_entry(int64_t slot, float mult) {
+  return (int64_t)(((uint64_t)slot << 32) | (uint64_t)__float_as_uint(mult));
+}
+__device__ __forceinline__ int64_t entry_slot(int64_t e) { return (int64_t)((uint64_t)e >> 32); }
+__device__ __forceinline__ float entry_mult(int64_t e) { return __uint_as_float((uint32_t)(uint64_t)e); }
+
+// a slot into its row's bucket (or the overflow list)
+__device__ __forceinline__ void put_slot(const NSSlots& S, uint32_t key, int64_t slot, float mult) {
   const int p = atomicAdd(&S.counts[key], 1);
+  const int64_t e = slot_entry(slot, mult);
   if (p < NS_BUCKET) {
-    S.bucket[(int64_t)key * NS_BUCKET + p] = (int32_t)slot;
+    S.bucket[(int64_t)key * NS_BUCKET + p] = e;
   } else {
     const int o = atomicAdd(S.ovf_n, 1);
-    S.ovf[2 * (int64_t)o] = (int32_t)key;
-    S.ovf[2 * (int64_t)o + 1] = (int32_t)slot;
+    S.ovf[2 * (int64_t)o] = (int64_t)key;
+    S.ovf[2 * (int64_t)o + 1] = e;
   }
 }
 
@@ -822,16 +846,15 @@ __device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ 
 // Pre-pass of the fused launch, one wave per row over the entity rows then the relation
 // rows: the row's L2 norm (one scalar per row instead of a wave reduction per use), with
 // norm_flag the normalised row itself, x / max(|x|, eps) (the fused kernel's operands, so it
-// divides nothing), and the row's slot count zeroed (and the deferred-positive count).
+// divides nothing), and the row's slot count zeroed (and the overflow count).
 // (A last-workgroup loss reduction inside the fused kernel was tried instead of k_ns_reduce:
 // its per-workgroup device-scope fence writes back the XCD's L2 each time, 0.12 -> 0.19 ms.)
 __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
                                                     const float* __restrict__ rel, int64_t n_rel, int d,
                                                     float* __restrict__ nrm_e, float* __restrict__ nrm_r,
                                                     float* __restrict__ ent_n, float* __restrict__ rel_n,
-                                                    int32_t* __restrict__ counts, int32_t* __restrict__ defer,
-                                                    int32_t* __restrict__ ovf_n) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) { defer[0] = 0; ovf_n[0] = 0; }  // no deferred positives / overflow yet
+                                                    int32_t* __restrict__ counts, int32_t* __restrict__ ovf_n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) ovf_n[0] = 0;  // no overflow pairs yet
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;
@@ -886,7 +909,9 @@ __device__ __forceinline__ void vnorm(Vec<NC>& o, const Vec<NC>& v, float c) {
 }
 
 // x of a row given the normalised positive rows and the normalised corrupted row (code 0: h,
-// 1: t, 2: r, 3: none), |x|_1 or |x|_2^2 partial of this lane; x kept for the gradient
+// 1: t, 2: r, 3: none; 4: a row sharing fewer than two rows with its positive, whose x =
+// (h + r) - t was built in cn when its rows arrived), |x|_1 or |x|_2^2 partial of this lane; x
+// kept for the gradient
 template <int NC, bool L2>
 __device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Vec<NC>& rn, const Vec<NC>& tn,
                                          const Vec<NC>& cn, int code) {
@@ -896,7 +921,7 @@ __device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Ve
     const float h = code == 0 ? cn.v[q] : hn.v[q];
     const float r = code == 2 ? cn.v[q] : rn.v[q];
     const float t = code == 1 ? cn.v[q] : tn.v[q];
-    const float e = (h + r) - t;
+    const float e = code == 4 ? cn.v[q] : (h + r) - t;
     x.v[q] = e;
     acc += L2 ? e * e : fabsf(e);
   }
@@ -924,18 +949,18 @@ __device__ __forceinline__ float wave_sum_u(float v) {
   return (r0 + r1) + (r2 + r3);
 }
 
-// One positive's workgroup. GEN = false (k_ns_transe_fused, every positive): the OpenKE batch
-// shape, each negative sharing two of the positive's rows; a positive with any other negative
-// is appended to the `defer` list after the forward (only its scores written, all rewritten). GEN = true
-// (k_ns_transe_fused_generic, the deferred positives only): also the generic-row path. The
-// split keeps the generic path's registers out of the fast instance (122 -> ~90 VGPRs).
-template <int NC, bool L2, bool GEN>
+// One positive's workgroup (k_ns_transe_fused). A negative of the OpenKE batch shape shares two
+// of its positive's rows (Base.cpp:111-124): one corrupted row is read. Any other negative
+// (a relation corruption sharing h and t is code 2; a copy of the positive code 3; a row
+// sharing fewer than two rows, code 4) is handled in the same pass: code 4 builds its x =
+// (h + r) - t in the corrupted-row registers as its rows arrive, and each of its rows that is
+// not the positive's gets a slot of its own. Every operand is a normalised row of the pre-pass
+// (norm_flag) or the table row itself.
+template <int NC, bool L2>
 __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __restrict__ nrm_e,
                                               const float* __restrict__ nrm_r, float* __restrict__ score,
                                               float* __restrict__ part, const NSSlots& S, int64_t n_ent, int64_t b,
-                                              int32_t* __restrict__ defer, const float* __restrict__ ent_n,
-                                              const float* __restrict__ rel_n) {
-  __shared__ int s_gen[NSW];
+                                              const float* __restrict__ ent_n, const float* __restrict__ rel_n) {
   __shared__ float s_n[NSW * NSF_MAXJ];
   __shared__ float s_c[NSW * NSF_MAXJ];
   __shared__ float s_gp;
@@ -972,27 +997,24 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], ent_n, h, d, lane); cnr[u] = nrm_e[h]; }
       else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], ent_n, t, d, lane); cnr[u] = nrm_e[t]; }
       else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], rel_n, r, d, lane); cnr[u] = nrm_r[r]; }
-      else if (!(oh && ot && orr)) code[u] = 4;  // shares less than two rows: generic path
-    }
-  }
-  if constexpr (!GEN) {  // a generic row in this wave: the positive is deferred after the forward barrier
-    bool gen = false;
+      else if (!(oh && ot && orr)) {  // shares fewer than two rows: x = (h + r) - t, built here
+        code[u] = 4;
+        if (oh) C[u] = hn; else vload_row(C[u], ent_n, h, d, lane);
+        Vec<NC> o;
+        if (orr) o = rn; else vload_row(o, rel_n, r, d, lane);
 #pragma unroll
-    for (int u = 0; u < NSF_MAXJ; ++u) gen |= code[u] == 4;
-    if (lane == 0) s_gen[w] = gen;
+        for (int q = 0; q < NC; ++q) C[u].v[q] = C[u].v[q] + o.v[q];
+        if (ot) o = tn; else vload_row(o, ent_n, t, d, lane);
+#pragma unroll
+        for (int q = 0; q < NC; ++q) C[u].v[q] = C[u].v[q] - o.v[q];
+      }
+    }
   }
   Vec<NC> x;
   float p_raw = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
   if (L2) p_raw = sqrtf(p_raw);
   const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
   const float psh = nph * nph, psr = npr * npr, pst = npt * npt;
-  // the positive's raw rows for the generic-row helpers (a negative sharing fewer than two
-  // rows: not an OpenKE batch), re-read there so that they hold no registers on the fast path
-  auto pos_ctx = [&](RowCtx<NC>& P) {
-    vload(P.h, A.ent + ph * d, d, lane); vload(P.r, A.rel + pr * d, d, lane); vload(P.t, A.ent + pt * d, d, lane);
-    P.sh = psh; P.sr = psr; P.st = pst;
-    P.own_h = P.own_r = P.own_t = true;
-  };
   float qh = 0.f, qt = 0.f, qr = 0.f;
   if (w == 0) {
     if (lane == 0) score[b] = p;
@@ -1004,19 +1026,15 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     sraw[u] = 0.0f;
     if (u >= nj) continue;
     const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
-    float n;
-    if (GEN && code[u] == 4) {
-      RowCtx<NC> P, R;
-      pos_ctx(P);
-      row_ctx_load(R, A, row, ph, pr, pt, P, lane);
-      row_ctx_norms(R, P);
-      n = row_fwd<NC, L2>(A, R, lane);
-      qh += R.sh; qt += R.st; qr += R.sr;
+    float sv = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
+    if (L2) sv = sqrtf(sv);
+    sraw[u] = sv;
+    const float n = A.use_model_margin ? A.model_margin - sv : sv;
+    if (code[u] == 4) {  // rare: its raw norms read here (the regularization's squared norms)
+      const int64_t h = readlane64u(my_h, u), r = readlane64u(my_r, u), t = readlane64u(my_t, u);
+      const float a = h == ph ? nph : nrm_e[h], c = r == pr ? npr : nrm_r[r], e = t == pt ? npt : nrm_e[t];
+      qh += a * a; qr += c * c; qt += e * e;
     } else {
-      float sv = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
-      if (L2) sv = sqrtf(sv);
-      sraw[u] = sv;
-      n = A.use_model_margin ? A.model_margin - sv : sv;
       const float sq = cnr[u] * cnr[u];
       qh += code[u] == 0 ? sq : psh;
       qt += code[u] == 1 ? sq : pst;
@@ -1026,18 +1044,6 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   }
   if (lane == 0) { s_sq[w][0] = qh; s_sq[w][1] = qt; s_sq[w][2] = qr; }
   __syncthreads();
-  if constexpr (!GEN) {
-    // any generic row in this positive: hand it whole to the generic instance. Nothing but its
-    // scores was written (those of its generic rows are meaningless here), and the generic
-    // instance, which runs after this kernel, rewrites every score of the positive.
-    bool any = false;
-#pragma unroll
-    for (int i = 0; i < NSW; ++i) any |= s_gen[i] != 0;
-    if (any) {
-      if (threadIdx.x == 0) defer[1 + atomicAdd(defer, 1)] = (int32_t)b;
-      return;
-    }
-  }
   if (w == 0) {  // loss partial and d(loss)/d(forward score) of every row, per unit upstream gradient
     const float m = A.loss_margin;
     const bool have = lane < A.K;
@@ -1100,46 +1106,35 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
 #pragma unroll
   for (int u = 0; u < NSF_MAXJ; ++u) {
     if (u >= nj) continue;
-    const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
+    const int64_t j = w + NSW * u;
     const float g = -sgn * s_c[j];
+    // which of this negative's rows are the positive's own (summed in registers) -- the others
+    // get slots
+    bool own_h = code[u] != 0, own_r = code[u] != 2, own_t = code[u] != 1;
+    if (code[u] == 4) {
+      own_h = readlane64u(my_h, u) == ph;
+      own_r = readlane64u(my_r, u) == pr;
+      own_t = readlane64u(my_t, u) == pt;
+    }
     uint32_t kq0 = S.sentinel, kq1 = S.sentinel, kq2 = S.sentinel;  // this negative's h / r / t slots
-    if (GEN && code[u] == 4) {  // shares fewer than two rows: every row it does not share gets a slot
-      RowCtx<NC> P, R;
-      pos_ctx(P);
-      row_ctx_load(R, A, row, ph, pr, pt, P, lane);
-      row_ctx_norms(R, P);
-      if (g == 0.0f && reg == 0.0f) {
-        oh += R.own_h ? 1.0f : 0.0f;
-        orr += R.own_r ? 1.0f : 0.0f;
-        ot += R.own_t ? 1.0f : 0.0f;
-      } else {
-        row_gx<NC, L2>(gx, A, R, g, lane);
-        if (R.own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)A.h[row];
-        if (R.own_r) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + A.r[row]);
-        if (R.own_t) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)A.t[row];
-        store_rec<NC, L2>(S.rec, b * A.K + j, gx, g, d, lane);
-      }
-    } else if (g == 0.0f && reg == 0.0f) {  // inactive hinge, no regularization: adds nothing
-      oh += code[u] != 0 ? 1.0f : 0.0f;
-      orr += code[u] != 2 ? 1.0f : 0.0f;
-      ot += code[u] != 1 ? 1.0f : 0.0f;
+    if (g == 0.0f && reg == 0.0f) {  // inactive hinge, no regularization: adds nothing
+      oh += own_h ? 1.0f : 0.0f;
+      orr += own_r ? 1.0f : 0.0f;
+      ot += own_t ? 1.0f : 0.0f;
     } else {
       fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]);  // C[u] normalised by the forward
       const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
 #pragma unroll
       for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
-      if (code[u] != 0) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)readlane64u(my_h, u);
-      if (code[u] != 2) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + readlane64u(my_r, u));
-      if (code[u] != 1) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)readlane64u(my_t, u);
-      if (code[u] != 3) store_rec<NC, L2>(S.rec, b * A.K + j, gx, L2 ? 0.0f : gs, d, lane);
+      if (own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)readlane64u(my_h, u);
+      if (own_r) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + readlane64u(my_r, u));
+      if (own_t) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)readlane64u(my_t, u);
+      if (!(own_h && own_r && own_t)) store_rec<NC, L2>(S.rec, b * A.K + j, gx, L2 ? 0.0f : gs, d, lane);
     }
     if (lane < 3) {
       const int64_t sl = sb + 3 + 3 * j + lane;
       const uint32_t key = lane == 0 ? kq0 : (lane == 1 ? kq1 : kq2);
-      if (key != S.sentinel) {
-        S.mult[sl] = 1.0f;
-        put_slot(S, key, sl);
-      }
+      if (key != S.sentinel) put_slot(S, key, sl, 1.0f);
     }
   }
   if (w > 0) {
@@ -1168,8 +1163,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     vstore_row(S.shared, 3 * b + 2, Gt, d, lane);
     if (lane < 3) {
       const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
-      S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
-      put_slot(S, key, sb + lane);
+      put_slot(S, key, sb + lane, lane == 0 ? kh : (lane == 1 ? kr : kt));
     }
   }
 }
@@ -1178,71 +1172,57 @@ template <int NC, bool L2>
 __global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
                                                          const float* __restrict__ nrm_r, float* __restrict__ score,
                                                          float* __restrict__ part, NSSlots S, int64_t n_ent,
-                                                         int32_t* __restrict__ defer, const float* __restrict__ ent_n,
+                                                         const float* __restrict__ ent_n,
                                                          const float* __restrict__ rel_n) {
-  ns_fused_body<NC, L2, false>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, defer, ent_n, rel_n);
-}
-
-// The forward's last launch, one workgroup: the deferred positives (defer[0] of them, ids from
-// defer[1]; none for OpenKE batches) through the generic-row instance, one after another, then
-// the loss: the fixed-order reduction of every positive's partials (ns_reduce_block). Folding
-// both into one launch keeps the OpenKE step at three forward launches; a batch of arbitrary
-// rows pays for it with a serial generic pass.
-template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_transe_finish(NSArgs A, const float* __restrict__ nrm_e,
-                                                          const float* __restrict__ nrm_r, float* __restrict__ score,
-                                                          float* __restrict__ part, NSSlots S, int64_t n_ent,
-                                                          const int32_t* __restrict__ defer,
-                                                          const float* __restrict__ ent_n,
-                                                          const float* __restrict__ rel_n, float* __restrict__ loss) {
-  const int n = defer[0];
-  for (int i = 0; i < n; ++i) {
-    ns_fused_body<NC, L2, true>(A, nrm_e, nrm_r, score, part, S, n_ent, defer[1 + i], nullptr, ent_n, rel_n);
-    __syncthreads();  // the body's LDS is reused by the next deferred positive; its partials are read below
-  }
-  ns_reduce_block(A, part, loss);
-}
-
-__device__ __forceinline__ int wave_min_i32(int v) {
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) v = min(v, __shfl_xor(v, s));
-  return v;
+  ns_fused_body<NC, L2>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, ent_n, rel_n);
 }
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// The slot ids of table row `row` (n = counts[row] of them) in increasing order, 64 at a time.
-//   n <= NS_BUCKET (nearly every row): the bucket is ranked in registers -- lane l's rank = how
-//     many of the bucket's ids are smaller -- and a ds_permute sends each id to the lane of
-//     its rank;
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const int64_t o = __shfl_xor(v, s);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// The bucket entries of table row `row` (n = counts[row] of them) in increasing slot id, 64 at
+// a time. `pre` is the lane's entry of the row's bucket, loaded together with the count.
+//   n <= NS_BUCKET (nearly every row): ranked in registers -- lane l's rank = how many of the
+//     bucket's entries are smaller -- and a ds_permute sends each entry to the lane of its rank;
 //   NS_BUCKET < n <= NS_HUB (a hub row, e.g. a frequent relation): bucket + the row's overflow
 //     pairs collected into the wave's LDS list and bitonic-sorted there;
-//   n > NS_HUB: the next 64 ids by repeated wave minima over bucket + overflow (slow, rare).
-// chunk(c0) returns lane u's id = the (c0 + u)-th smallest (INT_MAX past n).
+//   n > NS_HUB: the next 64 by repeated wave minima over bucket + overflow (slow, rare).
+// chunk(c0) returns lane u's entry = the (c0 + u)-th smallest (INT64_MAX past n).
 struct SlotOrder {
-  const int32_t* bucket;
-  const int32_t* ovf;
+  const int64_t* ovf;
   int n_ovf, n, lane;
   int64_t row;
-  int* hub;          // this wave's LDS list (NS_HUB ints)
-  int regs;          // n <= 64: lane u's ordered id
-  int prev;          // selection path: the last id taken
+  int64_t* hub;      // this wave's LDS list (NS_HUB entries)
+  int64_t pre;       // lane's bucket entry
+  int64_t regs;      // n <= 64: lane u's ordered entry
+  int64_t prev;      // selection path: the last entry taken
 
   __device__ void init() {
     prev = -1;
     if (n <= NS_BUCKET) {
-      const int mine = lane < n ? bucket[row * NS_BUCKET + lane] : INT_MAX;
+      const int64_t mine = lane < n ? pre : INT64_MAX;
       int rank = 0;
-      for (int m = 0; m < n; ++m) rank += __builtin_amdgcn_readlane(mine, m) < mine;
-      regs = __builtin_amdgcn_ds_permute((lane < n ? rank : lane) * 4, mine);
+      for (int m = 0; m < n; ++m) rank += readlane64u(mine, m) < mine;
+      const int to = (lane < n ? rank : lane) * 4;
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)(uint32_t)(uint64_t)mine);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute(to, (int)((uint64_t)mine >> 32));
+      regs = (int64_t)(((uint64_t)hi << 32) | lo);
       return;
     }
     if (n > NS_HUB) return;
-    hub[lane] = bucket[row * NS_BUCKET + lane];  // a full bucket
+    hub[lane] = pre;  // a full bucket
     int m = NS_BUCKET;
     for (int base = 0; base < n_ovf; base += kWave) {
       const int e = base + lane;
-      const bool mine = e < n_ovf && ovf[2 * (int64_t)e] == (int32_t)row;
+      const bool mine = e < n_ovf && ovf[2 * (int64_t)e] == row;
       const uint64_t mask = __ballot(mine);
       const int at = m + __popcll(mask & lanes_below(lane));
       if (mine && at < NS_HUB) hub[at] = ovf[2 * (int64_t)e + 1];
@@ -1250,7 +1230,7 @@ struct SlotOrder {
     }
     int M = NS_BUCKET;
     while (M < n) M <<= 1;
-    for (int i = n + lane; i < M; i += kWave) hub[i] = INT_MAX;
+    for (int i = n + lane; i < M; i += kWave) hub[i] = INT64_MAX;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     for (int k = 2; k <= M; k <<= 1) {
@@ -1258,7 +1238,7 @@ struct SlotOrder {
         for (int i = lane; i < M; i += kWave) {
           const int x = i ^ j;
           if (x > i) {
-            const int a = hub[i], b = hub[x];
+            const int64_t a = hub[i], b = hub[x];
             const bool up = (i & k) == 0;
             if ((a > b) == up) { hub[i] = b; hub[x] = a; }
           }
@@ -1269,21 +1249,20 @@ struct SlotOrder {
     }
   }
 
-  __device__ int chunk(int c0) {
+  __device__ int64_t chunk(int c0) {
     if (n <= NS_BUCKET) return regs;
-    if (n <= NS_HUB) return c0 + lane < n ? hub[c0 + lane] : INT_MAX;
-    int out = INT_MAX;
+    if (n <= NS_HUB) return c0 + lane < n ? hub[c0 + lane] : INT64_MAX;
+    int64_t out = INT64_MAX;
     const int take = n - c0 < kWave ? n - c0 : kWave;
     for (int u = 0; u < take; ++u) {
-      int v = bucket[row * NS_BUCKET + lane];
-      v = v > prev ? v : INT_MAX;
+      int64_t v = pre > prev ? pre : INT64_MAX;
       for (int e = lane; e < n_ovf; e += kWave) {
-        if (ovf[2 * (int64_t)e] == (int32_t)row) {
-          const int sv = ovf[2 * (int64_t)e + 1];
+        if (ovf[2 * (int64_t)e] == row) {
+          const int64_t sv = ovf[2 * (int64_t)e + 1];
           if (sv > prev && sv < v) v = sv;
         }
       }
-      v = wave_min_i32(v);
+      v = wave_min_i64(v);
       if (lane == u) out = v;
       prev = v;
     }
@@ -1302,21 +1281,23 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
                                                       int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
                                                       const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
                                                       const float* __restrict__ shared, const float* __restrict__ rec,
-                                                      const float* __restrict__ mult, const int32_t* __restrict__ counts,
-                                                      const int32_t* __restrict__ bucket, const int32_t* __restrict__ ovf,
+                                                      const int32_t* __restrict__ counts,
+                                                      const int64_t* __restrict__ bucket, const int64_t* __restrict__ ovf,
                                                       const int32_t* __restrict__ ovf_n, int64_t K,
                                                       const float* __restrict__ grad_loss, float* __restrict__ gent,
                                                       float* __restrict__ grel, float sgd_lr, float* __restrict__ pent,
                                                       float* __restrict__ prel) {
-  __shared__ int s_hub[4][NS_HUB];
+  __shared__ int64_t s_hub[4][NS_HUB];
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
   float* o = (is_ent ? gent : grel) + id * d;
+  // the count, the lane's bucket entry (meaningful below the count), the row itself and its
+  // norm: one round trip, all in flight together
   const int n = counts[row];
-  // the row itself and its norm, in flight while the bucket is ordered and summed
+  const int64_t pre = bucket[row * NS_BUCKET + lane];
   Vec<NC> v;
   vload_row(v, is_ent ? ent : rel, id, d, lane);
   const float nv = (is_ent ? nrm_e : nrm_r)[id];
@@ -1332,19 +1313,19 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
 #pragma unroll
   for (int c = 0; c < NC; ++c) dy.v[c] = 0.0f;
   float cnt = 0.0f;
-  SlotOrder ord{bucket, ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], 0, -1};
+  SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, -1};
   ord.init();
   for (int c0 = 0; c0 < n; c0 += kWave) {
     const int take = (n - c0) < kWave ? (n - c0) : kWave;
-    const int ordered = ord.chunk(c0);
+    const int64_t ordered = ord.chunk(c0);
     int64_t src = 0;  // shared row index, or -(record index + 1) for a negative's record
     float sg = 0.0f, m = 0.0f;
     if (lane < take) {  // lane u decodes its slot: where its contribution lives, and its sign
-      const int64_t sl = ordered;
+      const int64_t sl = entry_slot(ordered);
       const int64_t b = sl / spp, t = sl - b * spp;
       if (t < 3) { src = 3 * b + t; sg = 1.0f; }
       else { const int64_t jq = t - 3; src = -(b * K + jq / 3) - 1; sg = jq % 3 == 2 ? -1.0f : 1.0f; }
-      m = mult[sl];
+      m = entry_mult(ordered);
     }
     cnt += wave_sum(m);  // integer-valued: exact in any order
     int u = 0;
@@ -1551,8 +1532,7 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A, const float* __r
       const bool own = lane == 0 ? oh : (lane == 1 ? orr : ot);
       if (!own) {
         const uint32_t key = lane == 0 ? (uint32_t)nh : (lane == 1 ? (uint32_t)(n_ent + nr) : (uint32_t)nt);
-        S.mult[sl + lane] = 1.0f;
-        put_slot(S, key, sl + lane);
+        put_slot(S, key, sl + lane, 1.0f);
       }
     }
   }
@@ -1561,8 +1541,7 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A, const float* __r
   rec_store(S.rec, sb + 2, dpad, Gt, lane);
   if (lane < 3) {
     const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
-    S.mult[sb + lane] = lane == 0 ? kh : (lane == 1 ? kr : kt);
-    put_slot(S, key, sb + lane);
+    put_slot(S, key, sb + lane, lane == 0 ? kh : (lane == 1 ? kr : kt));
   }
 }
 
@@ -1572,19 +1551,20 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A, const float* __r
 template <int NC>
 __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, int64_t n_rel, float reg_ent,
                                                       float reg_rel, const float* __restrict__ rec,
-                                                      const float* __restrict__ mult, const int32_t* __restrict__ counts,
-                                                      const int32_t* __restrict__ bucket,
-                                                      const int32_t* __restrict__ ovf, const int32_t* __restrict__ ovf_n,
+                                                      const int32_t* __restrict__ counts,
+                                                      const int64_t* __restrict__ bucket,
+                                                      const int64_t* __restrict__ ovf, const int32_t* __restrict__ ovf_n,
                                                       int dpad, const float* __restrict__ grad_loss, float* gent,
                                                       float* gent_im, float* grel, float* grel_im, float sgd_lr,
                                                       float* pent, float* pent_im, float* prel, float* prel_im) {
-  __shared__ int s_hub[4][NS_HUB];
+  __shared__ int64_t s_hub[4][NS_HUB];
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
   const int d = A.dim;
+  const int64_t pre = bucket[row * NS_BUCKET + lane];
   const bool two = A.model == MMRE_COMPLEX || (A.model == MMRE_ROTATE && is_ent);
   // output rows of the two halves
   float *oa, *ob = nullptr, *pa = nullptr, *pb = nullptr;
@@ -1609,25 +1589,24 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
   Row2<NC> v;
   gen_load(v, A, is_ent, id, lane);
   float cnt = 0.0f;
-  SlotOrder ord{bucket, ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], 0, -1};
+  SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, -1};
   ord.init();
   for (int c0 = 0; c0 < n; c0 += kWave) {
     const int take = (n - c0) < kWave ? (n - c0) : kWave;
-    const int ordered = ord.chunk(c0);
-    float mo = 0.0f;
-    if (lane < take) mo = mult[ordered];
-    cnt += wave_sum(mo);  // integer-valued: exact in any order
+    const int64_t ordered = ord.chunk(c0);
+    const int sl = lane < take ? (int)entry_slot(ordered) : 0;
+    cnt += wave_sum(lane < take ? entry_mult(ordered) : 0.0f);  // integer-valued: exact in any order
     int u = 0;
     for (; u + 2 <= take; u += 2) {  // two records in flight, added in slot order
       Row2<NC> r0, r1;
-      rec_load(r0, rec, __builtin_amdgcn_readlane(ordered, u), dpad, lane);
-      rec_load(r1, rec, __builtin_amdgcn_readlane(ordered, u + 1), dpad, lane);
+      rec_load(r0, rec, __builtin_amdgcn_readlane(sl, u), dpad, lane);
+      rec_load(r1, rec, __builtin_amdgcn_readlane(sl, u + 1), dpad, lane);
       row2_add(dy, r0);
       row2_add(dy, r1);
     }
     if (u < take) {
       Row2<NC> r0;
-      rec_load(r0, rec, __builtin_amdgcn_readlane(ordered, u), dpad, lane);
+      rec_load(r0, rec, __builtin_amdgcn_readlane(sl, u), dpad, lane);
       row2_add(dy, r0);
     }
   }
@@ -1783,11 +1762,10 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
 
 // Workspace of the fused path, in 4-byte words, 256-B aligned pieces: loss partials, row
 // norms (+ the normalised tables with norm_flag), the slot contributions / occurrences, the
-// per-row slot counts (then the overflow count), the buckets, the overflow pairs, the deferred
-// positives. TransE keeps the positives' sums (3 rows of d) and the negatives' records
+// per-row slot counts (then the overflow count), the buckets, the overflow pairs. TransE keeps the positives' sums (3 rows of d) and the negatives' records
 // (ns_rec_words each); the other models one record of 2 d_pad floats per slot.
 struct FusedWs {
-  int64_t part, nrm_e, nrm_r, ent_n, rel_n, shared, rec, mult, counts, bucket, ovf, defer, total, slots;
+  int64_t part, nrm_e, nrm_r, ent_n, rel_n, shared, rec, counts, bucket, ovf, total, slots;
   int dpad;
   uint32_t sentinel;
 };
@@ -1810,19 +1788,16 @@ static void fused_ws(int model, int norm_flag, int64_t B, int64_t K, int64_t E, 
   w.shared = o;  o = al64(o + (te ? 3 * B * d : 0));
   const int64_t rw = ns_rec_words(8, false, d);
   w.rec = o;     o = al64(o + (te ? K * B * (d > rw ? d : rw) : w.slots * 2 * w.dpad));
-  w.mult = o;    o = al64(o + w.slots);
   w.counts = o;  o = al64(o + E + R + 1);   // + the overflow count
-  w.bucket = o;  o = al64(o + (E + R) * NS_BUCKET);
-  w.ovf = o;     o = al64(o + 2 * w.slots);
-  w.defer = o;   o = al64(o + B + 1);
+  w.bucket = o;  o = al64(o + 2 * (E + R) * NS_BUCKET);   // int64 entries
+  w.ovf = o;     o = al64(o + 4 * w.slots);                // int64 (row, entry) pairs
   w.total = o;
 }
 
 static NSSlots ws_slots(float* d_work, const FusedWs& w, int64_t E, int64_t R) {
   int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
-  return NSSlots{d_work + w.shared, d_work + w.rec, d_work + w.mult, counts,
-                 reinterpret_cast<int32_t*>(d_work + w.bucket), reinterpret_cast<int32_t*>(d_work + w.ovf),
-                 counts + E + R, w.sentinel};
+  return NSSlots{d_work + w.shared, d_work + w.rec, counts, reinterpret_cast<int64_t*>(d_work + w.bucket),
+                 reinterpret_cast<int64_t*>(d_work + w.ovf), counts + E + R, w.sentinel};
 }
 
 extern "C" int64_t mmre_ns_fused_workspace(int model, int norm_flag, int64_t batch, int64_t neg, int64_t n_ent,
@@ -1866,12 +1841,11 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   }
   float* nrm_e = d_work + w.nrm_e;
   float* nrm_r = d_work + w.nrm_r;
-  int32_t* defer = reinterpret_cast<int32_t*>(d_work + w.defer);
   // norm_flag: the fused kernel reads the rows normalised by the pre-pass; else the tables
   float* ent_n = norm_flag ? d_work + w.ent_n : nullptr;
   float* rel_n = norm_flag ? d_work + w.rel_n : nullptr;
   hipLaunchKernelGGL(k_ns_prepass, dim3((unsigned)((n_ent + n_rel + 3) / 4)), dim3(256), 0, st, d_ent, n_ent, d_rel,
-                     n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, S.counts, defer, S.ovf_n);
+                     n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, S.counts, S.ovf_n);
   MMRE_CHECK_LAUNCH();
   const float* ent_u = norm_flag ? ent_n : d_ent;
   const float* rel_u = norm_flag ? rel_n : d_rel;
@@ -1879,17 +1853,15 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   const bool l2 = model == MMRE_TRANSE_L2;
   const int nc = transe_fast_nc(A);
 #define MMRE_NS_FUSED(NC_, L2_)                                                                                    \
-  do {                                                                                                            \
-    hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, n_ent, \
-                       defer, ent_u, rel_u);                                                                      \
-    hipLaunchKernelGGL((k_ns_transe_finish<NC_, L2_>), dim3(1), blk, 0, st, A, nrm_e, nrm_r, d_score, part, S,    \
-                       n_ent, defer, ent_u, rel_u, d_loss);                                                       \
-  } while (0)
+  hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, n_ent,   \
+                     ent_u, rel_u)
   if (nc == 1) { if (l2) MMRE_NS_FUSED(1, true); else MMRE_NS_FUSED(1, false); }
   else if (nc == 2) { if (l2) MMRE_NS_FUSED(2, true); else MMRE_NS_FUSED(2, false); }
   else if (nc == 4) { if (l2) MMRE_NS_FUSED(4, true); else MMRE_NS_FUSED(4, false); }
   else { if (l2) MMRE_NS_FUSED(8, true); else MMRE_NS_FUSED(8, false); }
 #undef MMRE_NS_FUSED
+  MMRE_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_ns_reduce, dim3(1), dim3(256), 0, st, A, part, d_loss);  // the loss, fixed order
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
@@ -1927,7 +1899,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
   do {                                                                                                              \
     hipLaunchKernelGGL((k_ns_gen_slots<NC_>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,                      \
                        (int)(regul_rate != 0.0f));                                                                  \
-    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), ogrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec, S.mult,  \
+    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), ogrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec,         \
                        S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, \
                        d_grad_rel_im, lr, pe, pei, pr, pri);                                                        \
   } while (0)
@@ -1942,7 +1914,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
   const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
 #define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
   hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
-                     d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.mult, S.counts, S.bucket, S.ovf, S.ovf_n, \
+                     d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n,         \
                      neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr)
   const int nc = transe_fast_nc(A);
   const bool l2 = model == MMRE_TRANSE_L2;

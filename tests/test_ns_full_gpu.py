@@ -137,10 +137,10 @@ def test_one_shot_abi_equals_autograd_pair(c2_training):
 def test_fused_ns_deferred_generic_rows(c2_training, frac, p_norm, adv):
     """Batches that are not OpenKE-shaped: negatives replaced by random (h, r, t) rows (sharing
     fewer than two rows with their positive), by a relation corruption, or by the positive
-    itself. The fast fused instance defers every positive holding such a row to the generic
-    instance (k_ns_transe_fused_generic); frac = 1.0 defers all 2,721 of them, more than the
-    generic grid. Loss, scores and gradients vs the float64 reference op sequence; the
-    gradient tables stay bit-reproducible."""
+    itself. The fused kernel handles such rows in line (a row sharing fewer than two rows with
+    its positive builds its x as its rows arrive; each of its rows that is not the positive's
+    gets a slot); frac = 1.0 puts one in every positive. Loss, scores and gradients vs the
+    float64 reference op sequence; the gradient tables stay bit-reproducible."""
     import ref_trainer
     from mmre.ns import NSSpec, fused_ns_loss
     w, _ = c2_training
