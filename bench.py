@@ -917,7 +917,29 @@ def _with_build(out):
     """Name the binary that produced the line (path, size, sha256 prefix of libmmre_hip.so)."""
     from mmre._lib import lib_identity
     out["build"] = lib_identity()
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict):
+        cb.setdefault("cpu_model", _cpu_model())
     return out
+
+
+def _cpu_model():
+    """The host CPU's model string (/proc/cpuinfo 'model name', what lscpu prints) and the
+    number of CPUs this process may run on, so a cpu_baseline names the cores it ran on."""
+    name = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count()
+    return f"{name or 'unknown'} ({avail} CPUs available to the process)"
 
 
 def _coll_dev(dist, dev):
