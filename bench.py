@@ -901,9 +901,9 @@ def rank_breakdown(ev, dist, dev, sweep_ms, n_local, entity_sharded, reps=20):
         coll.append(a.elapsed_time(b))
     mine = torch.tensor([local_ms, sweep_ms, max(local_ms - sweep_ms, 0.0), med(coll), float(n_local)],
                         dtype=torch.float64, device=_coll_dev(dist, dev))
-    allv = torch.empty((dist.get_world_size(), 5), dtype=torch.float64, device=mine.device)
+    allv = torch.empty(dist.get_world_size() * 5, dtype=torch.float64, device=mine.device)  # flat: gloo's rule
     dist.all_gather_into_tensor(allv, mine)
-    allv = allv.cpu().numpy()
+    allv = allv.view(-1, 5).cpu().numpy()
     names = ["local_ms", "sweep_ms", "fixed_ms", "collective_ms", "sweeps"]
     per = {k: [round(float(x), 5) for x in allv[:, i]] for i, k in enumerate(names)}
     summ = {}
