@@ -71,15 +71,21 @@ def bytes_per_triple(model, dim):
 
 
 def valu_ops_per_triple(model, dim):
-    """VALU issue slots per scored triple in the sweep's inner loop: TransE L1
-    sub + add; RotatE 15.5: the round-1 count of 16.75 (12 f32 ops, 3/4 of a min for the
-    tiny-input check, v_rsq_f32 at quarter rate = 4 slots, measured by
-    scripts/probes/trans_rate.hip) less the add that v = fma(di, di, dr*dr) folds away and
-    a quarter min (the check is one v_min3 per two elements)."""
-    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 15.5 * dim}.get(model)
+    """VALU issue slots per scored triple in the sweep's inner loop, counted from
+    the instruction stream and checked against SQ_INSTS_VALU (profiles/pmc_*.json): TransE L1
+    sub + add per element; RotatE 9 per complex element: 5 full-rate f32 ops (dr, di, dr*dr,
+    fma(di, di, .), the accumulate) + the raw v_sqrt_f32 of the fast filter at quarter rate =
+    4 slots (scripts/probes/trans_rate.hip, rot_rate.hip). The rare exact rescoring of
+    undecided pairs is not counted (it is work the filter adds, not the triple's)."""
+    if model == "transe" and os.environ.get("MMRE_L1_FILTER", "1") != "0":
+        # the integer filter (mmre_link_sweep_l1q): one v_sad_u16 per two elements at half rate
+        # (scripts/probes/sad_rate.hip: 4.64 vs 2.36 cycles per wave-instruction) = 1 slot each
+        return 1 * dim
+    return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 9 * dim}.get(model)
 
 
-KERNEL_NAMES = {"transe": "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
+KERNEL_NAMES = {"transe": "k_sweep_valu<5, false, false, 0>" if os.environ.get("MMRE_L1_FILTER", "1") != "0"
+                else "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
                 "distmult": "k_sweep_mfma<false, false, 2", "complex": "k_sweep_mfma<false, false, 2"}
 
 
@@ -1114,7 +1120,9 @@ def main():
             "triples_per_launch": triples_launch, "bytes_per_triple": bpt,
             "hbm_algorithmic_x": tps * bpt / (HBM_PEAK_GBS * 1e9),
             "hbm_measured_GBs": (traffic / (sweep_ms * 1e-3) / 1e9) if traffic and sweep_ms else None,
-            "note": "binding roof: VALU for TransE/RotatE (|q-e| per element: sub + add-with-abs), f32 MFMA for "
+            "note": "binding roof: VALU for TransE/RotatE (TransE: the integer filter's v_sad_u16, two elements per "
+                    "half-rate instruction = 1 slot per element, MMRE_L1_FILTER=0: sub + add-with-abs; RotatE: sub, sub, mul, "
+                    "fma, add + v_sqrt_f32 at 4 slots, the fast filter's loop), f32 MFMA for "
                     "DistMult/ComplEx. hbm_algorithmic_x = SURVEY 8(d) algorithmic bytes (one entity row per "
                     "scored triple) / 8 TB/s: > 1 because each entity row is reused across a 128-query LDS tile; "
                     "the measured HBM traffic is in traffic / hbm_measured_GBs"})

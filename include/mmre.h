@@ -143,6 +143,22 @@ int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d
                           int64_t q_pad, int dim, const uint32_t* d_type_head, const uint32_t* d_type_tail,
                           int32_t* d_counts, const float* d_truth, void* stream);
 
+/* TransE L1 (model MMRE_TRANSE_L1) count-only sweep through an integer filter: same counts as
+ * mmre_link_sweep / mmre_link_sweep_range (bit for bit; replaces the same Test.h:65-192 scan),
+ * faster. The k-major planes are quantized to 16-bit codes over the largest |x| of both (three
+ * short launches on the stream), the sweep sums |code differences| with v_sad_u16 (one issue
+ * slot per element against two), and every pair the quantization error bound leaves on both
+ * sides of its query's threshold is rescored with the canonical f32 chain from the row-major
+ * copies d_ent_rows (whole table, mmre_link_prepare_entities) and d_q_rows
+ * (mmre_link_prepare_queries). e_begin / e_end as for mmre_link_sweep_range (0, n_ent: whole
+ * table). d_work: mmre_link_l1q_workspace(dim, e_pad, q_pad) bytes of device scratch. */
+int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
+int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
+                        int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,
+                        const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query,
+                        int64_t q_pad, int dim, const uint32_t* d_type_head, const uint32_t* d_type_tail,
+                        int32_t* d_counts, const float* d_truth, void* d_work, int64_t work_bytes, void* stream);
+
 /* Test.h:232-327 test_link_prediction + getTestLink* (Test.h:356-390), host side,
  * with the reference's float accumulation order (P14). Counts: int32, column c of
  * query i at counts[c*stride + i] (c = raw, filt, raw_tc, filt_tc).

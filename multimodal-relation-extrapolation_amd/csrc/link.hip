@@ -252,7 +252,8 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
 }
 
 // ------------------------------------------------------------ score ops ----
-// OP: 0 TransE L1, 1 TransE L2, 2 RotatE, 3 DistMult, 4 ComplEx. One k step.
+// OP: 0 TransE L1, 1 TransE L2, 2 RotatE, 3 DistMult, 4 ComplEx, 5 TransE L1 on 16-bit codes
+// (the integer filter; acc carries a uint32 in float bits). One k step.
 template <int OP>
 __device__ __forceinline__ float op_step(float acc, float qa, float qb, float x, float y) {
   if constexpr (OP == 0) {
@@ -263,6 +264,8 @@ __device__ __forceinline__ float op_step(float acc, float qa, float qb, float x,
   } else if constexpr (OP == 2) {
     float dr = qa - x, di = qb - y;
     return acc + sqrtf(__builtin_fmaf(di, di, dr * dr));
+  } else if constexpr (OP == 5) {  // TransE L1 integer filter: two 16-bit codes per dword
+    return __uint_as_float(__builtin_amdgcn_sad_u16(__float_as_uint(qa), __float_as_uint(x), __float_as_uint(acc)));
   } else {
     return __builtin_fmaf(x, qa, acc);
   }
@@ -284,6 +287,68 @@ __device__ __forceinline__ float rot_mag(float v, float y) {  // y = v_rsq_f32(v
   return __builtin_fmaf(e, h, s);
 }
 constexpr float kRotMin = 0x1p-96f;
+
+// RotatE's fast filter (the plain and type-constrained sweeps; the score-storing sweep keeps
+// the exact chain): the inner loop takes the raw v_sqrt_f32, which is within 1 ulp of the
+// correctly rounded sqrtf on every normal input and within 2^-63 on denormal ones
+// (scripts/probes/sqrt_ulp.hip, exhaustive on MI355X). Both chains add non-negative terms in
+// the same order, so with S' the fast sum and S the canonical one
+//   |S' - S| <= sum_k |m'_k - m_k| + the two chains' rounding errors
+//            <= (kp + 1) 2^-23 S' (1 + small) + kp 2^-63,
+// and rot_bound() returns a bound above that. A pair whose prediction is on the same side of
+// the threshold at both ends of [S' - B, S' + B] (every apply_pred kind is monotone in S) is
+// decided; the few others (~2e-4 of the pairs on the C4 tables) and any non-finite S' are
+// rescored exactly by rot_exact (IEEE sqrtf, the canonical chain), so the counts are the
+// canonical ones bit for bit.
+__device__ __forceinline__ float rot_bound(float s, int kp) {
+  const float f = (float)(kp + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+  return __builtin_fmaf(s, f, (float)kp * 0x1p-62f);
+}
+__device__ __forceinline__ float rot_exact(const float* __restrict__ q_km, int64_t q_pad, int64_t q,
+                                        const float* __restrict__ ent_km, int64_t e_pad, int64_t e, int kp) {
+  float acc = 0.0f;
+#pragma unroll 8
+  for (int k = 0; k < kp; ++k)
+    acc = op_step<2>(acc, q_km[(int64_t)k * q_pad + q], q_km[(int64_t)(kp + k) * q_pad + q],
+                     ent_km[(int64_t)k * e_pad + e], ent_km[(int64_t)(kp + k) * e_pad + e]);
+  return acc;
+}
+
+// TransE L1's integer filter (count-only sweeps, mmre_link_sweep_l1q). The k-major planes are
+// quantized once per evaluation to 16-bit codes Q(x) = rint((x + M) * 65535 / 2M), M the
+// largest |x| over both planes, two consecutive k per dword, and the sweep's inner loop is
+// one v_sad_u16 per two elements (|a.lo - b.lo| + |a.hi - b.hi| + acc: half rate, i.e. one
+// issue slot per element against two for sub + add-with-abs; scripts/probes/sad_rate.hip).
+// delta * sum|Qq - Qe| is within K delta (1 + small) of the real sum |q - e| (each code is off
+// by at most 1/2 + the float rounding of the map), and the canonical f32 chain is within
+// (K + 1) 2^-24 S of it, so B = 1.03 K delta + (K + 4) 2^-23 S' bounds |S' - S|; decided /
+// undecided pairs as for RotatE (rot_bound), the undecided rescored exactly from the
+// row-major copies (l1_exact_rows: the canonical chain, acc + |q_k - e_k| in k order).
+// M non-finite (an inf / NaN anywhere in the planes): delta = inf, every pair is undecided.
+struct L1Q {
+  const float* q_rows;     // (queries, kt) row-major query vectors
+  const float* ent_rows;   // (whole table, kt) row-major entity rows
+  const uint32_t* absmax;  // bits of M
+  int kt;                  // floats per row (the canonical chain's length, padding rows are 0)
+};
+__device__ __forceinline__ float l1q_delta(const uint32_t* absmax) {
+  const float m = __uint_as_float(*absmax);
+  return m == 0.0f ? 0.0f : (m < INFINITY ? (2.0f * m) / 65535.0f : INFINITY);
+}
+__device__ __forceinline__ float l1_exact_rows(const float* __restrict__ q, const float* __restrict__ e, int kt) {
+  const float4* q4 = reinterpret_cast<const float4*>(q);
+  const float4* e4 = reinterpret_cast<const float4*>(e);
+  float acc = 0.0f;
+#pragma unroll 10
+  for (int k = 0; k < kt / 4; ++k) {
+    const float4 a = q4[k], b = e4[k];
+    acc = acc + fabsf(a.x - b.x);
+    acc = acc + fabsf(a.y - b.y);
+    acc = acc + fabsf(a.z - b.z);
+    acc = acc + fabsf(a.w - b.w);
+  }
+  return acc;
+}
 
 __host__ __device__ inline int op_of_model(int model) {
   return model == MMRE_TRANSE_L1 ? 0 : model == MMRE_TRANSE_L2 ? 1 : model == MMRE_ROTATE ? 2
@@ -665,8 +730,10 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const float* __restrict__ thr, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,
     const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
     const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
-    float* __restrict__ scores) {
+    float* __restrict__ scores, L1Q l1) {
   constexpr int NPL = (OP == 2) ? 2 : 1;
+  // filters: RotatE's raw-sqrt sum (rot_bound / rot_exact), TransE L1's 16-bit codes (L1Q)
+  constexpr bool FAST = (OP == 2 || OP == 5) && !STORE;
   __shared__ float4 sq[2][NPL][KC][TQ / 4];
   __shared__ float4 se[2][NPL][KC][TE / 4];
   __shared__ float s_thr[2][TQ];
@@ -746,6 +813,13 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
   um.at(u0, cur_qt, cur_et);
   int slot = 0;
   uint32_t lo = 0xFFFFFFFFu;  // RotatE: min of the sqrt inputs' bits over this unit (see rot_mag)
+  // L1 filter constants (uniform): code step, bound slope and offset
+  float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
+  if constexpr (OP == 5) {
+    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.absmax))));
+    l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+    l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
+  }
   load_meta(cur_qt, 0);
   gload();
   swrite(0);
@@ -762,7 +836,19 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
         float4 x0 = se[buf][0][kk][te], x1 = se[buf][0][kk][16 + te];
         const float qa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-        if constexpr (OP == 2) {
+        if constexpr (OP == 2 && FAST) {
+          float4 b0 = sq[buf][NPL - 1][kk][tq], b1 = sq[buf][NPL - 1][kk][16 + tq];
+          float4 y0 = se[buf][NPL - 1][kk][te], y1 = se[buf][NPL - 1][kk][16 + te];
+          const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+          const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float dr = qa[i] - xv[j], di = qb[i] - yv[j];
+              acc[i][j] = acc[i][j] + __builtin_amdgcn_sqrtf(__builtin_fmaf(di, di, dr * dr));
+            }
+        } else if constexpr (OP == 2) {
           float4 b0 = sq[buf][NPL - 1][kk][tq], b1 = sq[buf][NPL - 1][kk][16 + tq];
           float4 y0 = se[buf][NPL - 1][kk][te], y1 = se[buf][NPL - 1][kk][16 + te];
           const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
@@ -810,6 +896,99 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
       if (kc == nkc - 1) {  // unit finished: rank epilogue
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE;
+        if constexpr (FAST) {
+          uint32_t unc[2] = {0u, 0u};  // undecided pairs, bit i * 8 + j (rows 0-3 / 4-7)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
+            const float th = s_thr[slot][ql];
+            const int32_t tr = s_true[slot][ql];
+            int c = 0, cc = 0;
+            if constexpr (OP == 5 && PK == 0) {
+              // prediction = the score: decide in the integer domain. With a = delta * S_int,
+              // |S - a| <= l1f a + l1c, so S_int < x = (th - l1c) / (delta (1 + l1f)) gives S < th
+              // and S_int >= y = (th + l1c) / (delta (1 - l1f)) gives S >= th; x, y are shrunk /
+              // grown by 2^-18 against the float rounding of their own computation.
+              uint32_t t_sure = 0u, t_out = 0xFFFFFFFFu;
+              if (l1d < INFINITY) {
+                const float x = (th - l1c) / (l1d * (1.0f + l1f)) * (1.0f - 0x1p-18f);
+                const float y = (th + l1c) / (l1d * (1.0f - l1f)) * (1.0f + 0x1p-18f);
+                t_sure = x > 0.0f ? (uint32_t)floorf(fminf(x, 0x1p31f)) : 0u;
+                t_out = y > 0.0f ? (uint32_t)ceilf(fminf(y, 0x1p31f)) : 0u;
+              }
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
+                const bool valid = (e + e_base != tr) & (e < n_ent);
+                const uint32_t si = __float_as_uint(acc[i][j]);
+                const bool sure = si < t_sure;
+                const bool better = sure & valid;
+                c += better;
+                if constexpr (TC) {
+                  const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                  cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
+                }
+                unc[i >> 2] |= (uint32_t)(!sure & (si < t_out) & valid) << ((i & 3) * 8 + j);
+                acc[i][j] = 0.0f;
+              }
+              s_cnt[0][i][tid] += c;
+              if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
+              continue;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
+              const bool valid = (e + e_base != tr) & (e < n_ent);
+              float a, bnd;
+              if constexpr (OP == 5) {
+                a = (float)__float_as_uint(acc[i][j]) * l1d;
+                bnd = __builtin_fmaf(a, l1f, l1c);
+              } else {
+                a = acc[i][j];
+                bnd = rot_bound(a, kp);
+              }
+              const float p1 = pred(a - bnd), p2 = pred(a + bnd);
+              const bool fin = a < INFINITY;  // false for inf and NaN: rescored
+              const bool sure = fin & (fmaxf(p1, p2) < th);
+              const bool out = (fin & (fminf(p1, p2) >= th)) | (th != th);
+              const bool better = sure & valid;
+              c += better;
+              if constexpr (TC) {
+                const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
+              }
+              unc[i >> 2] |= (uint32_t)(!sure & !out & valid) << ((i & 3) * 8 + j);
+              acc[i][j] = 0.0f;
+            }
+            s_cnt[0][i][tid] += c;
+            if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            uint32_t m = unc[h];
+            while (m) {  // rare: exact rescoring, one pair at a time
+              const int b = __builtin_ctz(m);
+              m &= m - 1u;
+              const int i = h * 4 + (b >> 3), j = b & 7;
+              const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
+              const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
+              float sx;
+              if constexpr (OP == 5)
+                sx = l1_exact_rows(l1.q_rows + (q0 + ql) * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt,
+                                   l1.kt);
+              else
+                sx = rot_exact(q_km, q_pad, q0 + ql, ent_km, e_pad, e, kp);
+              const float v = pred(sx);
+              if (v < s_thr[slot][ql]) {
+                s_cnt[0][i][tid] += 1;
+                if constexpr (TC) {
+                  const uint32_t* tm = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
+                  s_cnt[TC ? 1 : 0][i][tid] += type_bit(tm, type_words, s_rel[slot][ql], e + e_base) ? 1 : 0;
+                }
+              }
+            }
+          }
+        } else {
         if constexpr (OP == 2) {
           bool bad = lo < __float_as_uint(kRotMin);  // v = 0 or v < 2^-96
 #pragma unroll
@@ -865,6 +1044,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
           s_cnt[0][i][tid] += c;
           if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
         }
+        }  // !FAST
         const bool last = unit + 1 >= u1;
         int next_qt = cur_qt, next_et = cur_et;
         if (!last) um.at(unit + 1, next_qt, next_et);
@@ -1207,6 +1387,74 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
   }
 }
 
+// ------------------------------------------------------ L1 integer filter ---
+// M = max |x| over the query plane and the entity slice (non-finite values make M = inf),
+// as float bits in work[0] (zeroed by the caller's stream just before).
+__global__ __launch_bounds__(256) void k_l1q_absmax(const float* __restrict__ q_km, int64_t q_pad,
+                                                    const float* __restrict__ e_km, int64_t e_pad, int64_t e_cols,
+                                                    int kp, uint32_t* __restrict__ work) {
+  // work items (plane row r, column chunk y of 8) of both planes, strided over the blocks (no
+  // index division per element); one atomic per block at most (same-address atomics serialize)
+  float m = 0.0f;
+  for (int it = blockIdx.x; it < kp * 8; it += gridDim.x) {
+    const int r = it >> 3;
+    const int64_t st = 8 * (int64_t)blockDim.x, c0 = (int64_t)(it & 7) * blockDim.x + threadIdx.x;
+    const float4* q4 = reinterpret_cast<const float4*>(q_km + (int64_t)r * q_pad);
+#pragma unroll 4
+    for (int64_t c = c0; c < q_pad / 4; c += st) {
+      const float4 v = q4[c];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      if (!(v.x - v.x == 0.0f && v.y - v.y == 0.0f && v.z - v.z == 0.0f && v.w - v.w == 0.0f)) m = INFINITY;
+    }
+    const float4* e4 = reinterpret_cast<const float4*>(e_km + (int64_t)r * e_pad);
+#pragma unroll 4
+    for (int64_t c = c0; c < e_cols / 4; c += st) {
+      const float4 v = e4[c];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      if (!(v.x - v.x == 0.0f && v.y - v.y == 0.0f && v.z - v.z == 0.0f && v.w - v.w == 0.0f)) m = INFINITY;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float s_m[4];
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    // non-negative floats order as their bits; inf = no filter. Skip the atomic when the word
+    // already holds at least m (a stale read only costs a redundant atomic).
+    if (__float_as_uint(m) > __hip_atomic_load(work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(work, __float_as_uint(m));
+  }
+}
+
+// Codes of columns [c0, c0 + n) of a k-major float plane (kp rows, stride pad) into dword rows
+// out[r][pad] = Q(x[2r]) | Q(x[2r + 1]) << 16, rows r < k2 (k >= kp: code 0 in both planes).
+__global__ __launch_bounds__(256) void k_l1q_quant(const float* __restrict__ km, int64_t pad, int64_t c0, int64_t n,
+                                                   int kp, int k2, uint32_t* __restrict__ out,
+                                                   const uint32_t* __restrict__ work) {
+  const float mx = __uint_as_float(*work);
+  const float inv = (mx > 0.0f && mx < INFINITY) ? 65535.0f / (2.0f * mx) : 0.0f;
+  const float off = (mx < INFINITY) ? mx : 0.0f;
+  const int64_t total = (int64_t)k2 * n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int r = (int)(i / n);
+    const int64_t c = c0 + i % n;
+    uint32_t code[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 2 * r + h;
+      float t = k < kp ? (km[(int64_t)k * pad + c] + off) * inv : 0.0f;
+      t = t == t ? fminf(fmaxf(t, 0.0f), 65535.0f) : 0.0f;
+      code[h] = (uint32_t)rintf(t);
+    }
+    out[(int64_t)r * pad + c] = code[0] | (code[1] << 16);
+  }
+}
+
+static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
+
 // ---------------------------------------------------------------- launch ---
 // Resident workgroups of a persistent sweep: the occupancy API's blocks per CU (capped at 4,
 // the VGPR-limited residency of a 256-thread group at <= 128 VGPRs) x the device's CUs.
@@ -1225,7 +1473,8 @@ template <int OP, bool TCV, bool STV, int PK>
 static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, int64_t n_ent, int n_et, int e_base,
                             const float* q_km, int64_t q_pad, int64_t n_query, int kp, int pk, float m,
                             const float* thr, const int32_t* qtrue, const int64_t* qr, const int8_t* qmode,
-                            const uint32_t* th, const uint32_t* tt, int64_t tw, int32_t* counts, float* scores) {
+                            const uint32_t* th, const uint32_t* tt, int64_t tw, int32_t* counts, float* scores,
+                            L1Q l1) {
   // 16 workgroups per resident slot: short per-workgroup ranges let the dispatcher balance
   // CUs that run at different speeds (C2 on MI355X: 1,024 groups 4.0 ms, 8,192 3.43 ms,
   // 16,384 3.30 ms, 30,528 (one unit each) 3.36 ms).
@@ -1245,23 +1494,30 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   else if (gmode && gmode[0] >= '1' && gmode[0] <= '9') g = atoi(gmode);
   const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;
   hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad, n_ent, q_km,
-                     q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores);
+                     q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1);
 }
 
 template <int OP>
 static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km, int64_t e_pad, int64_t n_ent,
                        int n_et, int e_base, const float* q_km, int64_t q_pad, int64_t n_query, int kp, int pk, float m, const float* thr,
                        const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, const uint32_t* th,
-                       const uint32_t* tt, int64_t tw, int32_t* counts, float* scores) {
+                       const uint32_t* tt, int64_t tw, int32_t* counts, float* scores, L1Q l1 = {}) {
 #define MMRE_LV1(TCV, STV, PKV) \
-  launch_valu_one<OP, TCV, STV, PKV>(st, ent_km, e_pad, n_ent, n_et, e_base, q_km, q_pad, n_query, kp, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores)
+  launch_valu_one<OP, TCV, STV, PKV>(st, ent_km, e_pad, n_ent, n_et, e_base, q_km, q_pad, n_query, kp, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1)
   // the model's usual prediction kind is compiled into the epilogue of the plain sweep
   constexpr int fast = (OP == 2) ? 3 : 0;  // RotatE -(m - s), TransE s
-  if (tc && store) MMRE_LV1(true, true, -1);
-  else if (tc) MMRE_LV1(true, false, -1);
-  else if (store) MMRE_LV1(false, true, -1);
-  else if (pk == fast) MMRE_LV1(false, false, fast);  // C2 3.27 -> 3.23 ms
-  else MMRE_LV1(false, false, -1);
+  if constexpr (OP == 5) {  // the integer filter: count-only sweeps
+    if (store) return MMRE_ERR_ARG;
+    if (tc) MMRE_LV1(true, false, -1);
+    else if (pk == fast) MMRE_LV1(false, false, fast);
+    else MMRE_LV1(false, false, -1);
+  } else {
+    if (tc && store) MMRE_LV1(true, true, -1);
+    else if (tc) MMRE_LV1(true, false, -1);
+    else if (store) MMRE_LV1(false, true, -1);
+    else if (pk == fast) MMRE_LV1(false, false, fast);  // C2 3.27 -> 3.23 ms
+    else MMRE_LV1(false, false, -1);
+  }
 #undef MMRE_LV1
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
@@ -1520,6 +1776,43 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
   if (n_ent <= 0) return MMRE_ERR_ARG;
   return sweep_impl(model, pred_kind, margin, d_ent_km, n_ent, e_pad, 0, n_ent, d_q_km, d_q_true, d_qr, d_qmode,
                     n_query, q_pad, dim, d_type_head, d_type_tail, d_counts, d_truth, d_scores, (hipStream_t)stream);
+}
+
+extern "C" int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
+  if (dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
+  return 256 + 4 * (int64_t)l1q_rows(dim) * (e_pad + q_pad);
+}
+
+extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows,
+                                   int64_t n_ent, int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km,
+                                   const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr,
+                                   const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
+                                   const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
+                                   const float* d_truth, void* d_work, int64_t work_bytes, void* stream) {
+  int rc = check_link_args(MMRE_TRANSE_L1, pred_kind, d_ent_km, n_ent, e_pad, d_q_km, d_q_true, d_qr, d_qmode, n_query,
+                           q_pad, d_type_head, d_type_tail, d_counts, d_truth);
+  if (rc) return rc;
+  if (!d_ent_rows || !d_q_rows || !d_work || work_bytes < mmre_link_l1q_workspace(dim, e_pad, q_pad)) return MMRE_ERR_WORKSPACE;
+  if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int kp = plane_rows(MMRE_TRANSE_L1, dim), k2 = l1q_rows(dim);
+  uint32_t* hdr = (uint32_t*)d_work;
+  uint32_t* uq = (uint32_t*)((char*)d_work + 256);
+  uint32_t* ue = uq + (int64_t)k2 * q_pad;
+  const int64_t e_cols = round_up(e_end, TE) - e_begin;  // the slice's whole tiles
+  MMRE_CHECK(hipMemsetAsync(hdr, 0, 4, st));
+  hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)std::min(kp * 8, 512)), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
+                     kp, hdr);
+  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr);
+  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr);
+  MMRE_CHECK_LAUNCH();
+  const int64_t tw = (n_ent + 31) / 32;
+  const int64_t n_slice = e_end - e_begin;
+  const int n_et = (int)((n_slice + TE - 1) / TE);
+  const L1Q l1{d_q_rows, d_ent_rows, hdr, n_planes(MMRE_TRANSE_L1) * kp};
+  return launch_valu<5>(d_type_head != nullptr, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et,
+                        (int)e_begin, (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr,
+                        d_qmode, d_type_head, d_type_tail, tw, d_counts, nullptr, l1);
 }
 
 extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,

@@ -9,6 +9,8 @@ integer rank counts come back.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -170,6 +172,9 @@ class LinkSweep:
         self.ent_rows = torch.empty((self.n_ent, self.K), dtype=torch.float32, device=dev)
         self.rel_work = torch.empty((self.n_rel, spec.dim), dtype=torch.float32, device=dev)
         self.prepared = False
+        # TransE L1 count-only sweeps through the integer filter (mmre_link_sweep_l1q);
+        # MMRE_L1_FILTER=0 keeps the f32 sweep (A/B measurements)
+        self.l1_filter = os.environ.get("MMRE_L1_FILTER", "1") != "0"
 
     def prepare_entities(self):
         s = self.spec
@@ -236,9 +241,21 @@ class LinkSweep:
             call("mmre_link_truth", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
                  self.e_pad, ptr(self.ent_rows), ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n,
                  b["q_pad"], s.dim, ptr(off), ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
+        l1q = (self.model_id == MODEL_IDS["transe"] and not return_scores and q_rows and self.l1_filter)
+        if l1q:
+            need = int(_lib.lib().mmre_link_l1q_workspace(s.dim, self.e_pad, b["q_pad"]))
+            wk = b.get("l1q_work")
+            if wk is None or wk.numel() < need:
+                wk = b["l1q_work"] = torch.empty(need, dtype=torch.uint8, device=self.device)
         if sweep_events is not None:
             sweep_events[0].record()
-        if entity_range is not None:
+        if l1q:  # TransE L1 count-only: the integer filter (same counts, bit for bit)
+            e0, e1 = (0, self.n_ent) if entity_range is None else (int(entity_range[0]), int(entity_range[1]))
+            call("mmre_link_sweep_l1q", int(s.pred_kind), float(s.margin), ptr(self.ent_km), ptr(self.ent_rows),
+                 self.n_ent, self.e_pad, e0, e1, ptr(b["q_km"]), ptr(b["q_rows"]), ptr(b["q_true"]), ptr(qr),
+                 ptr(qmode), n, b["q_pad"], s.dim, ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(wk),
+                 int(wk.numel()), st)
+        elif entity_range is not None:
             if return_scores:
                 raise ValueError("entity_range sweeps keep no score rows")
             call("mmre_link_sweep_range", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km),

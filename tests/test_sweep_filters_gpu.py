@@ -1,0 +1,112 @@
+"""GPU parity of the sweep's filters (csrc/link.hip): the count-only RotatE sweeps sum the raw
+v_sqrt_f32 -- within 1 ulp of sqrtf (scripts/probes/sqrt_ulp.hip, exhaustive) -- and the
+count-only TransE L1 sweeps sum |code differences| of 16-bit quantized planes with v_sad_u16
+(mmre_link_sweep_l1q); both rescore with the canonical chain every pair whose prediction the
+error bound cannot place on one side of the threshold.
+
+Bar: raw / filtered / type-constrained counts bit-equal to the score-storing (exact) sweep's
+and to the oracle's Test.h restatement, on tables built to put many pairs inside the bound:
+exact copies of the truth row (exact ties: strict < must not count them), copies one ulp away
+in a few coordinates (scores a few ulps from the threshold), zero rows, rows of subnormal and
+of overflowing magnitude, NaN rows, and an identity rotation (v = 0 on every k).
+"""
+import numpy as np
+import pytest
+
+from test_link_gpu import _run, _spec_from
+
+pytestmark = pytest.mark.gpu
+
+
+def _adversarial(E=1500, R=6, d=48, Q=257, seed=0, margin=6.0, model="rotate", huge=True):
+    rng = np.random.default_rng(seed)
+    er = (margin + 2.0) / (2 * d)
+    ent = rng.uniform(-er, er, (E, 2 * d if model == "rotate" else d)).astype(np.float32)
+    rel = rng.uniform(-(margin + 2.0) / d, (margin + 2.0) / d, (R, d)).astype(np.float32)
+    rel[0] = 0.0                                       # RotatE phase 0 / TransE r = 0: v = 0 at the anchor
+    qh, qr, qt = rng.integers(0, E, Q), rng.integers(0, R, Q), rng.integers(0, E, Q)
+    qm = rng.integers(0, 2, Q).astype(np.int8)
+    free = iter(rng.permutation(np.arange(E)))
+    used = set(qh.tolist()) | set(qt.tolist())
+    nxt = lambda: next(e for e in free if e not in used)
+    for i in range(0, Q, 3):
+        truth = qh[i] if qm[i] == 0 else qt[i]
+        for _ in range(3):                             # exact ties with the truth
+            ent[nxt()] = ent[truth]
+        for k in range(4):                             # a few ulps away from the truth's score
+            e = nxt()
+            ent[e] = ent[truth]
+            cols = rng.choice(ent.shape[1], 1 + k, replace=False)
+            bump = np.where(rng.random(len(cols)) < 0.5, -np.inf, np.inf).astype(np.float32)
+            ent[e, cols] = np.nextafter(ent[e, cols], bump)
+    for _ in range(5):
+        ent[nxt()] = 0.0
+    e = nxt(); ent[e] = ent[qt[0]]; ent[e, ::5] += np.float32(1e-22)     # v subnormal
+    e = nxt(); ent[e] = ent[qt[1]]; ent[e, 1::4] += np.float32(3e-16)    # v < 2^-96
+    if huge:
+        e = nxt(); ent[e] = 3e19                                          # v = inf
+        e = nxt(); ent[e, 7] = np.nan
+    return ent, rel, qh, qr, qt, qm
+
+
+@pytest.mark.parametrize("model,seed,huge", [("rotate", 0, True), ("rotate", 1, True), ("transe", 0, False),
+                                             ("transe", 1, False), ("transe", 2, True)])
+def test_fast_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, model, seed, huge):
+    """huge: a row of 3e19 and a NaN -- for TransE these make the quantization scale
+    non-finite, so every pair is rescored (slow, exact)."""
+    from mmre.link import FilterIndex
+    margin = 6.0 if model == "rotate" else None
+    ent, rel, qh, qr, qt, qm = _adversarial(seed=seed, margin=margin or 6.0, model=model, huge=huge)
+    E, R, d = ent.shape[0], rel.shape[0], rel.shape[1]
+    rng = np.random.default_rng(seed + 10)
+    fh, fr, ft = rng.integers(0, E, 3 * E), rng.integers(0, R, 3 * E), rng.integers(0, E, 3 * E)
+    fh, fr, ft = np.concatenate([fh, qh]), np.concatenate([fr, qr]), np.concatenate([ft, qt])
+    heads = [np.unique(np.concatenate([rng.choice(E, E // 3, replace=False), qh[qr == r]])) for r in range(R)]
+    tails = [np.unique(np.concatenate([rng.choice(E, E // 3, replace=False), qt[qr == r]])) for r in range(R)]
+    index = FilterIndex(fh, fr, ft, E, R, heads, tails)
+    spec = _spec_from(model, ent, rel, margin=margin, dim=d, norm=model == "transe")
+    exact = _run(spec, qh, qr, qt, qm, index=index, tc=True, scores=True)
+    fast = _run(spec, qh, qr, qt, qm, index=index, tc=True, scores=False)
+    plain = _run(spec, qh, qr, qt, qm, index=index, tc=False, scores=False)
+    assert np.array_equal(fast["counts"], exact["counts"])
+    assert np.array_equal(plain["counts"][:2], exact["counts"][:2])
+    assert np.array_equal(fast["truth"].view(np.uint32), exact["truth"].view(np.uint32))
+    hrt = oracle_mod.sorted_hrt(fh, fr, ft)
+    for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+        sel = qm == mode_id
+        o_pred = oracle_mod.link_predict(model, mode, ent, rel, qh[sel], qr[sel], qt[sel], margin=margin,
+                                         phase_denom=spec.phase_denom, norm_flag=model == "transe")
+        lists = heads if mode_id == 0 else tails
+        toff = np.cumsum([0] + [len(x) for x in lists])
+        tids = np.concatenate([np.asarray(x, np.int64) for x in lists])
+        o_c = oracle_mod.test_rank(mode, o_pred, qh[sel], qr[sel], qt[sel], hrt, toff, tids)
+        assert np.array_equal(fast["counts"][:, sel].T, o_c)
+    # the construction really exercises the rescoring: many truths have exact ties
+    assert (exact["counts"][0] < E - 1).all()
+
+
+def test_l1_filter_on_and_off_and_entity_slices(oracle_mod, monkeypatch):
+    """TransE L1: the integer-filter sweep equals the f32 sweep (MMRE_L1_FILTER=0) on the whole
+    table and on entity slices (mmre_link_sweep_l1q with e_begin / e_end), whose counts sum to
+    the whole-table ones; the margin prediction kind takes the generic epilogue."""
+    import torch
+    from mmre.link import FilterIndex, LinkSweep
+    for margin in (None, 4.0):
+        ent, rel, qh, qr, qt, qm = _adversarial(E=2100, d=40, Q=200, seed=5, model="transe", huge=False)
+        E, R = ent.shape[0], rel.shape[0]
+        index = FilterIndex(qh, qr, qt, E, R)
+        spec = _spec_from("transe", ent, rel, margin=margin, dim=40, norm=True)
+        on = _run(spec, qh, qr, qt, qm, index=index, scores=False)
+        monkeypatch.setenv("MMRE_L1_FILTER", "0")
+        off = _run(spec, qh, qr, qt, qm, index=index, scores=False)
+        monkeypatch.delenv("MMRE_L1_FILTER")
+        assert np.array_equal(on["counts"], off["counts"])
+        dev = spec.ent.device
+        tq = lambda a, dt=np.int64: torch.from_numpy(np.asarray(a, dt)).to(dev)
+        total = np.zeros_like(on["counts"])
+        for e0, e1 in ((0, 512), (512, 1536), (1536, E)):
+            filt = tuple(torch.from_numpy(a).to(dev) for a in index.groups(qh, qr, qt, qm, entity_range=(e0, e1)))
+            sw = LinkSweep(spec)
+            res = sw.run(tq(qh), tq(qr), tq(qt), tq(qm, np.int8), filt=filt, entity_range=(e0, e1))
+            total += res["counts"].cpu().numpy()
+        assert np.array_equal(total, on["counts"])
