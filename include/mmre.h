@@ -230,6 +230,23 @@ int mmre_sampler_openke_step(const int64_t* d_train_list, int64_t train_total, c
                              int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
                              void* stream);
 
+/* importProb (Reader.h:26-49): kl_prob.txt at `path` (n_rel x (n_rel - 1) floats, fscanf
+ * "%f") -> h_prob[n_rel][n_rel - 1] = exp(-kl / temperature) / row sum, in float. Host only. */
+int mmre_import_prob(const char* path, int64_t n_rel, float temperature, float* h_prob);
+/* mmre_sampler_openke_step with sampling(..., p = true): relation negatives drawn by
+ * corrupt_rel's KL-weighted path (Corrupt.h:111-147) from d_rel_prob = mmre_import_prob's
+ * table on the device; d_ticket may be NULL (seeds then left as they were, like
+ * mmre_sampler_openke_blocked). Replaces Base.cpp:142's corrupt_rel(..., p). */
+int mmre_sampler_openke_p(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                          const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                          const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                          const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                          const float* d_right_mean, int64_t n_ent, int64_t n_rel, uint64_t* d_seeds,
+                          int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                          int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
+                          int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
+                          const float* d_rel_prob, void* stream);
+
 /* The repo's per-edge filtered sampler (module/NegativeSampling.py:114-140,
  * 321-375): per positive edge b (local ids d_eh/d_et, relation d_er), neg
  * negatives split head/tail by Bernoulli(0.5); candidates uniform over the local

@@ -8,8 +8,7 @@
  * rank the caller's score vector on the GPU; everything else is host bookkeeping.
  * Errors the reference would crash on (missing files, out-of-range index) print a message
  * to stderr and abort. Not exported (outside the link-prediction path): triple
- * classification (getNegTest/getTestBatch), relation prediction (getRelBatch/testRel),
- * importProb and the kl_prob relation corruption (sampling with p=true aborts).
+ * classification (getNegTest/getTestBatch), relation prediction (getRelBatch/testRel).
  */
 #ifndef MMRE_BASE_H
 #define MMRE_BASE_H
@@ -51,10 +50,15 @@ void importTrainFiles(void);
 void importTestFiles(void);
 /* Reader.h:267-317 -- type_constrain.txt: allowed heads / tails per relation. */
 void importTypeFiles(void);
+/* Reader.h:26-49 -- inPath + "kl_prob.txt" (relationTotal x (relationTotal - 1) KL distances)
+ * weighted as exp(-kl / temp), normalised per relation: the table sampling(p = true) draws
+ * relation negatives from (Corrupt.h:111-147). Call after importTrainFiles. */
+void importProb(float temp);
 
 /* Base.cpp:161-197 -- a training batch into caller arrays of length
  * batch_size * (1 + neg_rate + neg_rel_rate); negative k at [k*B, (k+1)*B). Bit-identical
- * to Base.so for the same seeds; filter_flag is ignored as in the reference. */
+ * to Base.so for the same seeds; filter_flag is ignored as in the reference; p = true (with
+ * neg_rel_rate > 0) draws relation negatives from importProb's table. */
 void sampling(int64_t* batch_h, int64_t* batch_t, int64_t* batch_r, float* batch_y, int64_t batch_size,
               int64_t neg_rate, int64_t neg_rel_rate, int64_t mode, bool filter_flag, bool p, bool val_loss);
 

@@ -93,6 +93,7 @@ struct Device {
   int64_t *d_train = nullptr, *d_head = nullptr, *d_tail = nullptr, *d_rel = nullptr;
   int64_t *d_lh = nullptr, *d_rh = nullptr, *d_lt = nullptr, *d_rt = nullptr, *d_lr = nullptr, *d_rr = nullptr;
   float *d_lm = nullptr, *d_rm = nullptr;
+  float* d_prob = nullptr;  // importProb's table (sampling with p = true)
   uint64_t* d_seeds = nullptr;
   int64_t *d_bh = nullptr, *d_bt = nullptr, *d_br = nullptr;
   float* d_by = nullptr;
@@ -550,7 +551,8 @@ static void sampling_impl(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_
     }
     return;
   }
-  if (p && neg_rel_rate > 0) fail(MMRE_ERR_ARG, "sampling(p=true) relation corruption by kl_prob.txt is not supported");
+  const bool use_p = p && neg_rel_rate > 0;
+  if (use_p && !D.d_prob) fail(MMRE_ERR_ARG, "sampling(p=true) needs importProb() first (Reader.h:26)");
   if (S.seeds.size() != (size_t)S.work_threads) fail(MMRE_ERR_ARG, "call randReset() after setWorkThreads() before sampling");
   train_device();
   const int64_t n = batch_size * (1 + neg_rate + neg_rel_rate);
@@ -564,10 +566,15 @@ static void sampling_impl(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_
   }
   HIP_OR_DIE(hipMemcpyAsync(D.d_seeds, S.seeds.data(), sizeof(uint64_t) * S.work_threads, hipMemcpyHostToDevice,
                             D.st));
-  const int rc = mmre_sampler_openke(D.d_train, S.train_total, D.d_head, D.d_tail, D.d_rel, D.d_lh, D.d_rh, D.d_lt,
-                                     D.d_rt, D.d_lr, D.d_rr, S.bern ? D.d_lm : nullptr, S.bern ? D.d_rm : nullptr,
-                                     S.ent_total, S.rel_total, D.d_seeds, S.work_threads, batch_size, neg_rate,
-                                     neg_rel_rate, mode, D.d_bh, D.d_bt, D.d_br, D.d_by, D.st);
+  const int rc = use_p
+      ? mmre_sampler_openke_p(D.d_train, S.train_total, D.d_head, D.d_tail, D.d_rel, D.d_lh, D.d_rh, D.d_lt, D.d_rt,
+                              D.d_lr, D.d_rr, S.bern ? D.d_lm : nullptr, S.bern ? D.d_rm : nullptr, S.ent_total,
+                              S.rel_total, D.d_seeds, S.work_threads, batch_size, neg_rate, neg_rel_rate, mode,
+                              nullptr, 0, D.d_bh, D.d_bt, D.d_br, D.d_by, nullptr, D.d_prob, D.st)
+      : mmre_sampler_openke(D.d_train, S.train_total, D.d_head, D.d_tail, D.d_rel, D.d_lh, D.d_rh, D.d_lt, D.d_rt,
+                            D.d_lr, D.d_rr, S.bern ? D.d_lm : nullptr, S.bern ? D.d_rm : nullptr, S.ent_total,
+                            S.rel_total, D.d_seeds, S.work_threads, batch_size, neg_rate, neg_rel_rate, mode, D.d_bh,
+                            D.d_bt, D.d_br, D.d_by, D.st);
   if (rc != MMRE_OK) fail(rc, "mmre_sampler_openke failed (" + std::to_string(rc) + ")");
   HIP_OR_DIE(hipMemcpyAsync(batch_h, D.d_bh, sizeof(int64_t) * n, hipMemcpyDeviceToHost, D.st));
   HIP_OR_DIE(hipMemcpyAsync(batch_t, D.d_bt, sizeof(int64_t) * n, hipMemcpyDeviceToHost, D.st));
@@ -708,6 +715,23 @@ extern "C" void sampling(INT* batch_h, INT* batch_t, INT* batch_r, REAL* batch_y
     poison<REAL>(batch_y, n, NAN);
   }
 }
+
+// Reader.h:26-49: kl_prob.txt from the input path, weighted by the temperature (the table
+// sampling(p = true) draws relation negatives from); rereading replaces the table.
+static void importProb_impl(REAL temp) {
+  if (S.rel_total < 2) fail(MMRE_ERR_ARG, "importProb: call importTrainFiles() first (relationTotal < 2)");
+  printf("Current temperature:%f\n", temp);
+  std::vector<float> prob((size_t)(S.rel_total * (S.rel_total - 1)));
+  const std::string path = S.in_path + "kl_prob.txt";
+  const int rc = mmre_import_prob(path.c_str(), S.rel_total, temp, prob.data());
+  if (rc != MMRE_OK) fail(rc, "importProb: cannot read " + path);
+  device_init();
+  release(D.d_prob);
+  D.d_prob = upload(prob);
+  HIP_OR_DIE(hipStreamSynchronize(D.st));
+}
+
+extern "C" void importProb(REAL temp) { guarded([&] { importProb_impl(temp); }); }
 
 extern "C" void initTest() {
   guarded([&] { initTest_impl(); });

@@ -1,7 +1,9 @@
 // host.cpp -- host-side parts of the C ABI: version, the Test.h metric reduction
 // with the reference's float accumulation order, glibc rand() seeds and the
 // sampler's per-thread LCG bookkeeping.
+#include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <emmintrin.h>
@@ -135,6 +137,32 @@ extern "C" int mmre_sampler_advance(uint64_t* h_seeds, int64_t work_threads, int
     }
     const int64_t cnt = rig > lef ? rig - lef : 0;
     h_seeds[id] = lcg_pow_apply(h_seeds[id], (uint64_t)(cnt * per));
+  }
+  return MMRE_OK;
+}
+
+// importProb (Reader.h:26-49): kl_prob.txt holds n_rel x (n_rel - 1) floats (relation i's KL
+// distance to every other relation, i's own column left out), read with fscanf("%f") like the
+// reference (a short file leaves the remaining entries 0, as its calloc does); each row becomes
+// exp(-kl / temperature) normalised by the row's sum, in float, summed in column order.
+extern "C" int mmre_import_prob(const char* path, int64_t n_rel, float temperature, float* h_prob) {
+  if (!path || !h_prob || n_rel < 2) return MMRE_ERR_ARG;
+  FILE* fin = fopen(path, "r");
+  if (!fin) return MMRE_ERR_ARG;
+  const int64_t n = n_rel * (n_rel - 1);
+  for (int64_t i = 0; i < n; ++i) h_prob[i] = 0.0f;
+  for (int64_t i = 0; i < n; ++i)
+    if (fscanf(fin, "%f", &h_prob[i]) != 1) break;
+  fclose(fin);
+  for (int64_t i = 0; i < n_rel; ++i) {
+    float* row = h_prob + i * (n_rel - 1);
+    float sum = 0.0f;
+    for (int64_t j = 0; j < n_rel - 1; ++j) {
+      const float e = expf(-row[j] / temperature);
+      sum += e;
+      row[j] = e;
+    }
+    for (int64_t j = 0; j < n_rel - 1; ++j) row[j] /= sum;
   }
   return MMRE_OK;
 }

@@ -110,14 +110,64 @@ __global__ __launch_bounds__(256) void k_sampler_blocks(const int64_t* __restric
   o[1] = make_int4((int)tl, (int)tr, (int)tail_hrt[3 * tl + 0], (int)tail_hrt[3 * tr + 0]);
 }
 
-// corrupt_rel with p == false (Corrupt.h:85-162); T rows (h, r, t) sorted by (h, t, r).
+// corrupt_rel with p == true (Corrupt.h:111-147): the draw among the relations not in the (h, t)
+// block, weighted by r's row of importProb's table P (Reader.h:26-49; n_rel - 1 columns, r's own
+// left out: column c is relation c below r, c + 1 from r on). The reference builds, per draw, the
+// cumulative list of P[c] / sum over the unmarked columns (sum = 1 - the marked columns' mass,
+// subtracted in block order) and binary-searches it for m = rand_max(10000) / 10000. Here the
+// list is never stored: each probe of the same binary search recomputes its prefix in the same
+// order (the block's columns are ascending, so one merge walk marks them), which yields the
+// same float values, hence the same index (the compacted index; corrupt_rel maps it to an id).
+__device__ float rel_prob_prefix(const int64_t* __restrict__ T, const float* __restrict__ P, int64_t n_rel,
+                                 int64_t r, int64_t ll, int64_t rr, float sum, int64_t upto) {
+  float rec = 0.0f;
+  int64_t q = ll, c = 0;
+  for (int64_t i = 0; i < n_rel - 1; ++i) {
+    int64_t col = -1;  // the next marked column at or after i
+    while (q <= rr) {
+      const int64_t rel = T[3 * q + 1];
+      col = rel > r ? rel - 1 : (rel < r ? rel : -1);
+      if (col >= i) break;
+      ++q;
+      col = -1;
+    }
+    if (col == i) continue;  // in the (h, t) block
+    rec += P[i] / sum;
+    if (c == upto) return rec;
+    ++c;
+  }
+  return rec;
+}
+
+__device__ int64_t rel_prob_draw(const int64_t* __restrict__ T, const float* __restrict__ prob, int64_t n_rel,
+                                 uint64_t* st, int64_t r, int64_t ll, int64_t rr) {
+  const float* P = prob + r * (n_rel - 1);
+  float sum = 1.0f;
+  int64_t marked = 0;
+  for (int64_t i = ll; i <= rr; ++i) {
+    const int64_t rel = T[3 * i + 1];
+    if (rel > r) { sum -= P[rel - 1]; ++marked; }
+    else if (rel < r) { sum -= P[rel]; ++marked; }
+  }
+  const int64_t cnt = (n_rel - 1) - marked;
+  const float m = (float)((double)rand_max(st, 10000) / 10000.0);
+  int64_t lef = 0, rig = cnt - 1;
+  while (lef < rig) {
+    const int64_t mid = (lef + rig) >> 1;
+    if (rel_prob_prefix(T, P, n_rel, r, ll, rr, sum, mid) < m) lef = mid + 1;
+    else rig = mid;
+  }
+  return rig;
+}
+
+// corrupt_rel (Corrupt.h:85-162); T rows (h, r, t) sorted by (h, t, r). prob NULL: p == false,
+// a uniform draw; else importProb's table (p == true).
 __device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_rel,
                                const int64_t* __restrict__ rig_rel, int64_t n_rel, uint64_t* st, int64_t h, int64_t t,
-                               int64_t r) {
-  (void)r;
+                               int64_t r, const float* __restrict__ prob) {
   int64_t lef, rig, mid, ll, rr;
   key_block(T, 2, lef_rel[h], rig_rel[h], t, ll, rr);
-  const int64_t tmp = rand_max(st, n_rel - (rr - ll + 1));
+  const int64_t tmp = prob ? rel_prob_draw(T, prob, n_rel, st, r, ll, rr) : rand_max(st, n_rel - (rr - ll + 1));
   if (tmp < T[3 * ll + 1]) return tmp;
   if (tmp > T[3 * rr + 1] - rr + ll - 1) return tmp + rr - ll + 1;
   lef = ll; rig = rr + 1;
@@ -137,7 +187,7 @@ __device__ __forceinline__ void sampler_openke_row(int64_t row,
     const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* __restrict__ seeds,
     int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk,
     int64_t n_blk, int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br,
-    float* __restrict__ by) {
+    float* __restrict__ by, const float* __restrict__ rel_prob) {
   const int64_t b = row % B, j = row / B;  // j = 0: the positive; 1..neg: entity negatives; then relation ones
   // slice of the reference's pthread `id` that owns position b (Base.cpp:93-100)
   const int64_t per = B % work_threads == 0 ? B / work_threads : B / work_threads + 1;
@@ -179,7 +229,7 @@ __device__ __forceinline__ void sampler_openke_row(int64_t row,
   } else {
     const int64_t k = j - 1 - neg;
     st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * neg + k));
-    bh[row] = h; bt[row] = t; br[row] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r);
+    bh[row] = h; bt[row] = t; br[row] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r, rel_prob);
   }
   by[row] = -1.0f;
 }
@@ -215,12 +265,12 @@ __global__ __launch_bounds__(256) void k_sampler_openke(
     const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, uint64_t* seeds, int64_t work_threads,
     int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk, int64_t n_blk,
     int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br, float* __restrict__ by,
-    int32_t* ticket, int64_t adv_per) {
+    int32_t* ticket, int64_t adv_per, const float* __restrict__ rel_prob) {
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row < B * (1 + neg + neg_rel))
     sampler_openke_row(row, train_list, train_total, head_hrt, tail_hrt, rel_hrt, lef_head, rig_head, lef_tail,
                        rig_tail, lef_rel, rig_rel, left_mean, right_mean, n_ent, n_rel, seeds, work_threads, B, neg,
-                       neg_rel, mode, blk, n_blk, bh, bt, br, by);
+                       neg_rel, mode, blk, n_blk, bh, bt, br, by, rel_prob);
   if (ticket == nullptr) return;  // uniform
   __syncthreads();  // every thread of the workgroup has read (and used) its seed
   __shared__ int s_last;
@@ -325,7 +375,8 @@ static int sampler_impl(const int64_t* d_train_list, int64_t train_total, const 
                         const float* d_right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* d_seeds,
                         int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate, int64_t mode,
                         const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
-                        int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, void* stream) {
+                        int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, const float* d_rel_prob,
+                        void* stream) {
   if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
       !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y)
     return MMRE_ERR_ARG;
@@ -335,6 +386,7 @@ static int sampler_impl(const int64_t* d_train_list, int64_t train_total, const 
     return MMRE_ERR_ARG;
   if (mode < -1 || mode > 1) return MMRE_ERR_ARG;
   if (n_blocks < 0 || (n_blocks > 0 && !d_blocks)) return MMRE_ERR_ARG;
+  if (d_rel_prob && n_rel < 2) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
   const int threads = 256;
   const int64_t rows = batch_size * (1 + neg_rate + neg_rel_rate);
@@ -343,7 +395,7 @@ static int sampler_impl(const int64_t* d_train_list, int64_t train_total, const 
                      d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel,
                      const_cast<uint64_t*>(d_seeds), work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks,
                      n_blocks, d_batch_h, d_batch_t, d_batch_r, d_batch_y, d_ticket,
-                     mmre_sampler_draws_per_positive(neg_rate, neg_rel_rate, mode));
+                     mmre_sampler_draws_per_positive(neg_rate, neg_rel_rate, mode), d_rel_prob);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }
@@ -359,7 +411,7 @@ extern "C" int mmre_sampler_openke_blocked(const int64_t* d_train_list, int64_t 
   return sampler_impl(d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
                       d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
                       work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
-                      d_batch_t, d_batch_r, d_batch_y, nullptr, stream);
+                      d_batch_t, d_batch_r, d_batch_y, nullptr, nullptr, stream);
 }
 
 extern "C" int mmre_sampler_openke_step(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
@@ -375,7 +427,23 @@ extern "C" int mmre_sampler_openke_step(const int64_t* d_train_list, int64_t tra
   return sampler_impl(d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
                       d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
                       work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
-                      d_batch_t, d_batch_r, d_batch_y, d_ticket, stream);
+                      d_batch_t, d_batch_r, d_batch_y, d_ticket, nullptr, stream);
+}
+
+extern "C" int mmre_sampler_openke_p(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                     const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                     const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                     const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                     const float* d_right_mean, int64_t n_ent, int64_t n_rel, uint64_t* d_seeds,
+                                     int64_t work_threads, int64_t batch_size, int64_t neg_rate, int64_t neg_rel_rate,
+                                     int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
+                                     int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
+                                     const float* d_rel_prob, void* stream) {
+  if (!d_rel_prob) return MMRE_ERR_ARG;
+  return sampler_impl(d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
+                      d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel, d_seeds,
+                      work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks, n_blocks, d_batch_h,
+                      d_batch_t, d_batch_r, d_batch_y, d_ticket, d_rel_prob, stream);
 }
 
 extern "C" int mmre_sampler_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,

@@ -45,6 +45,9 @@ SIGNATURES = {
                                           I64, P, I64, P, P, P, P, P]),
     "mmre_sampler_openke_step": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64,
                                        I64, P, I64, P, P, P, P, P, P]),
+    "mmre_sampler_openke_p": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, I64, I64, I64,
+                                    I64, P, I64, P, P, P, P, P, P, P]),
+    "mmre_import_prob": (I32, [ctypes.c_char_p, I64, F32, P]),
     "mmre_sampler_repo": (I32, [P, P, P, I64, I64, I64, P, I64, P, P, P, I64, P, P, P, I64, ctypes.c_uint64, I32,
                                 P, P, P, P]),
     "mmre_sgd_step": (I32, [P, P, P, I32, F32, P]),

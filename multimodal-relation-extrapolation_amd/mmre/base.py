@@ -24,7 +24,7 @@ SIGNATURES = {
     "getEntityTotal": (_I, []), "getRelationTotal": (_I, []), "getTripleTotal": (_I, []),
     "getTrainTotal": (_I, []), "getTestTotal": (_I, []), "getValidTotal": (_I, []),
     "randReset": (None, []), "importTrainFiles": (None, []), "importTestFiles": (None, []),
-    "importTypeFiles": (None, []),
+    "importTypeFiles": (None, []), "importProb": (None, [_F]),
     "sampling": (None, [_P, _P, _P, _P, _I, _I, _I, _I, _B, _B, _B]),
     "initTest": (None, []), "getHeadBatch": (None, [_P, _P, _P]), "getTailBatch": (None, [_P, _P, _P]),
     "testHead": (None, [_P, _I, _I]), "testTail": (None, [_P, _I, _I]),

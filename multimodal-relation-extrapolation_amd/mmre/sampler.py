@@ -47,6 +47,19 @@ class OpenKESampler:
         call("mmre_sampler_blocks", ptr(d["train_list"]), self._n_blocks, ptr(d["head_hrt"]), ptr(d["tail_hrt"]),
              ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]), ptr(d["rig_tail"]), ptr(self._blocks),
              stream_ptr(self.device))
+        self.prob = None  # importProb's table (sample(..., p=True))
+        self._prob_dev = None
+
+    def import_prob(self, path: str, temperature: float):
+        """importProb (Reader.h:26-49): the KL-weighted relation table sample(..., p=True) draws
+        relation negatives from (Corrupt.h:111-147). path: the dataset's kl_prob.txt (n_rel x
+        (n_rel - 1) floats), read and weighted by mmre_import_prob exactly as the reference."""
+        R = self.index.n_rel
+        prob = np.zeros((R, R - 1), np.float32)
+        call("mmre_import_prob", str(path).encode(), R, float(temperature), prob.ctypes.data_as(ctypes.c_void_p))
+        self.prob = prob
+        self._prob_dev = torch.from_numpy(prob).to(self.device)
+        return prob
 
     @property
     def seeds(self) -> np.ndarray:
@@ -58,7 +71,9 @@ class OpenKESampler:
         self._seeds = np.asarray(value, np.uint64).copy()
         self._seeds_dev.copy_(torch.from_numpy(self._seeds.view(np.int64)))
 
-    def sample(self, batch_size: int, neg_ent: int = 1, neg_rel: int = 0, mode: int = 0, out=None):
+    def sample(self, batch_size: int, neg_ent: int = 1, neg_rel: int = 0, mode: int = 0, out=None, p: bool = False):
+        """Base.cpp:161-197 sampling(batch, neg_ent, neg_rel, mode, filter_flag, p); p=True draws the
+        relation negatives from import_prob's table (Corrupt.h:111-147)."""
         B = int(batch_size)
         n = B * (1 + neg_ent + neg_rel)
         dev = self.device
@@ -70,13 +85,20 @@ class OpenKESampler:
         d = self._d
         # one launch: the batch, and the per-thread LCG states advanced (by a fixed number of draws
         # per positive) for the next call by the kernel's last workgroup -- no host copy per batch
-        call("mmre_sampler_openke_step", ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]),
-             ptr(d["tail_hrt"]), ptr(d["rel_hrt"]), ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]),
-             ptr(d["rig_tail"]), ptr(d["lef_rel"]), ptr(d["rig_rel"]), ptr(d["left_mean"]) if self.bern else None,
-             ptr(d["right_mean"]) if self.bern else None, self.index.n_ent, self.index.n_rel,
-             ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel), int(mode),
-             ptr(self._blocks), self._n_blocks, ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]),
-             ptr(out["batch_y"]), ptr(self._ticket), stream_ptr(dev))
+        use_p = bool(p) and int(neg_rel) > 0
+        if use_p and self._prob_dev is None:
+            raise ValueError("sample(p=True) needs import_prob() first (Reader.h:26)")
+        args = (ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]),
+                ptr(d["tail_hrt"]), ptr(d["rel_hrt"]), ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]),
+                ptr(d["rig_tail"]), ptr(d["lef_rel"]), ptr(d["rig_rel"]), ptr(d["left_mean"]) if self.bern else None,
+                ptr(d["right_mean"]) if self.bern else None, self.index.n_ent, self.index.n_rel,
+                ptr(self._seeds_dev), self.work_threads, B, int(neg_ent), int(neg_rel), int(mode),
+                ptr(self._blocks), self._n_blocks, ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]),
+                ptr(out["batch_y"]), ptr(self._ticket))
+        if use_p:
+            call("mmre_sampler_openke_p", *args, ptr(self._prob_dev), stream_ptr(dev))
+        else:
+            call("mmre_sampler_openke_step", *args, stream_ptr(dev))
         # ... and the host mirror
         call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, B,
              int(neg_ent), int(neg_rel), int(mode))

@@ -32,6 +32,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -363,8 +364,12 @@ static int64_t corrupt_tail(const orc_train_index *ix, uint64_t *st, int64_t t, 
     return tmp + lef - ll + 1;
 }
 
-/* corrupt_rel with p == false (Corrupt.h:85-162): rel_hrt rows (h, r, t) sorted by (h, t, r). */
-static int64_t corrupt_rel(const orc_train_index *ix, uint64_t *st, int64_t h, int64_t t, int64_t r) {
+/* corrupt_rel (Corrupt.h:85-162): rel_hrt rows (h, r, t) sorted by (h, t, r). prob NULL: p == false
+ * (uniform draw); else importProb's table, p == true (Corrupt.h:111-147): the cumulative list of
+ * prob / sum over the relations outside the (h, t) block (r's own column excluded), binary-searched
+ * for m = rand_max(10000) / 10000, with the reference's record / prob_tmp arrays. */
+static int64_t corrupt_rel(const orc_train_index *ix, uint64_t *st, int64_t h, int64_t t, int64_t r,
+                           const float *prob) {
     const int64_t *T = ix->rel_hrt;
     int64_t lef = ix->lef_rel[h] - 1, rig = ix->rig_rel[h], mid, ll, rr;
     while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] >= t) rig = mid; else lef = mid; }
@@ -372,12 +377,61 @@ static int64_t corrupt_rel(const orc_train_index *ix, uint64_t *st, int64_t h, i
     lef = ix->lef_rel[h]; rig = ix->rig_rel[h] + 1;
     while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 2] <= t) lef = mid; else rig = mid; }
     rr = lef;
-    int64_t tmp = rand_max(st, ix->n_rel - (rr - ll + 1));
+    int64_t tmp;
+    if (!prob) {
+        tmp = rand_max(st, ix->n_rel - (rr - ll + 1));
+    } else {
+        const int64_t R = ix->n_rel, start = r * (R - 1);
+        float sum = 1;
+        unsigned char *record = (unsigned char *)calloc((size_t)(R - 1), 1);
+        for (int64_t i = ll; i <= rr; ++i) {
+            const int64_t rel = T[3 * i + 1];
+            if (rel > r) { sum -= prob[start + rel - 1]; record[rel - 1] = 1; }
+            else if (rel < r) { sum -= prob[start + rel]; record[rel] = 1; }
+        }
+        float *prob_tmp = (float *)calloc((size_t)(R - (rr - ll + 1)) + 1, sizeof(float));
+        int64_t cnt = 0;
+        float rec = 0;
+        for (int64_t i = start; i < start + R - 1; ++i) {
+            if (record[i - start]) continue;
+            rec += prob[i] / sum;
+            prob_tmp[cnt++] = rec;
+        }
+        const float m = (float)((double)rand_max(st, 10000) / 10000.0);
+        lef = 0; rig = cnt - 1;
+        while (lef < rig) { mid = (lef + rig) >> 1; if (prob_tmp[mid] < m) lef = mid + 1; else rig = mid; }
+        tmp = rig;
+        free(prob_tmp);
+        free(record);
+    }
     if (tmp < T[3 * ll + 1]) return tmp;
     if (tmp > T[3 * rr + 1] - rr + ll - 1) return tmp + rr - ll + 1;
     lef = ll; rig = rr + 1;
     while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
     return tmp + lef - ll + 1;
+}
+
+/* importProb (Reader.h:26-49): kl_prob.txt (n_rel x (n_rel - 1) floats) -> exp(-kl / temp)
+ * normalised per relation row, in float. Returns -1 when the file cannot be opened. */
+int orc_import_prob(const char *path, int64_t n_rel, float temp, float *prob) {
+    FILE *fin = fopen(path, "r");
+    if (!fin) return -1;
+    const int64_t n = n_rel * (n_rel - 1);
+    for (int64_t i = 0; i < n; ++i) prob[i] = 0.0f;
+    for (int64_t i = 0; i < n; ++i)
+        if (fscanf(fin, "%f", &prob[i]) != 1) break;
+    fclose(fin);
+    float sum = 0.0f;
+    for (int64_t i = 0; i < n_rel; ++i) {
+        for (int64_t j = 0; j < n_rel - 1; ++j) {
+            float e = expf(-prob[i * (n_rel - 1) + j] / temp);
+            sum += e;
+            prob[i * (n_rel - 1) + j] = e;
+        }
+        for (int64_t j = 0; j < n_rel - 1; ++j) prob[i * (n_rel - 1) + j] /= sum;
+        sum = 0;
+    }
+    return 0;
 }
 
 /* sampling / getBatch (Base.cpp:78-197), run thread-by-thread sequentially.
@@ -390,7 +444,7 @@ int orc_sampling(const int64_t *train_list, int64_t train_total, const int64_t *
                  const int64_t *lef_rel, const int64_t *rig_rel, const float *left_mean,
                  const float *right_mean, int64_t n_ent, int64_t n_rel, uint64_t *seeds, int64_t work_threads,
                  int64_t *batch_h, int64_t *batch_t, int64_t *batch_r, float *batch_y, int64_t batch_size,
-                 int64_t neg_rate, int64_t neg_rel_rate, int64_t mode) {
+                 int64_t neg_rate, int64_t neg_rel_rate, int64_t mode, const float *rel_prob) {
     orc_train_index ix = {head_hrt, tail_hrt, rel_hrt, lef_head, rig_head, lef_tail, rig_tail,
                           lef_rel, rig_rel, n_ent, n_rel};
     for (int64_t id = 0; id < work_threads; ++id) {
@@ -427,7 +481,7 @@ int orc_sampling(const int64_t *train_list, int64_t train_total, const int64_t *
                 last += batch_size;
             }
             for (int64_t k = 0; k < neg_rel_rate; ++k) {
-                batch_h[b + last] = h; batch_t[b + last] = t; batch_r[b + last] = corrupt_rel(&ix, st, h, t, r);
+                batch_h[b + last] = h; batch_t[b + last] = t; batch_r[b + last] = corrupt_rel(&ix, st, h, t, r, rel_prob);
                 batch_y[b + last] = -1;
                 last += batch_size;
             }

@@ -56,7 +56,8 @@ def lib():
         L.orc_link_metrics.argtypes = [_P, _P, _I, _P]
         L.orc_glibc_rand.argtypes = [_I, _P]
         L.orc_sampling.argtypes = [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _I,
-                                   _P, _P, _P, _P, _I, _I, _I, _I]
+                                   _P, _P, _P, _P, _I, _I, _I, _I, _P]
+        L.orc_import_prob.argtypes = [ctypes.c_char_p, _I, ctypes.c_float, _P]
         L.orc_candidate_rank_transe.argtypes = [_P, _P, ctypes.c_int, _P, _P, _P, _P, _I, _P, _P]
         L.orc_sincos_vec.argtypes = [_P, _I, _P, _P]
         L.orc_normalize_rows.argtypes = [_P, _I, ctypes.c_int, _P]
@@ -203,8 +204,17 @@ def train_index(h, t, r, n_ent, n_rel):
                 left_mean=left_mean, right_mean=right_mean, n_ent=n_ent, n_rel=n_rel)
 
 
-def sampling(ix, seeds, batch_size, neg_rate=1, neg_rel_rate=0, mode=0, bern=False, train_total=None):
-    """Base.cpp:161-197. seeds: uint64 per work thread (advanced in place)."""
+def import_prob(path, n_rel, temperature):
+    """importProb (Reader.h:26-49): float32 [n_rel, n_rel - 1]."""
+    out = np.zeros((n_rel, n_rel - 1), np.float32)
+    if lib().orc_import_prob(str(path).encode(), int(n_rel), ctypes.c_float(temperature), _ptr(out)) != 0:
+        raise FileNotFoundError(path)
+    return out
+
+
+def sampling(ix, seeds, batch_size, neg_rate=1, neg_rel_rate=0, mode=0, bern=False, train_total=None, prob=None):
+    """Base.cpp:161-197. seeds: uint64 per work thread (advanced in place). prob: import_prob's
+    table for sampling(..., p=True) (Corrupt.h:111-147), None for p=False."""
     B = batch_size
     n = B * (1 + neg_rate + neg_rel_rate)
     bh = np.zeros(n, np.int64)
@@ -218,7 +228,8 @@ def sampling(ix, seeds, batch_size, neg_rate=1, neg_rel_rate=0, mode=0, bern=Fal
                        _ptr(ix["lef_rel"]), _ptr(ix["rig_rel"]),
                        _ptr(ix["left_mean"]) if bern else None, _ptr(ix["right_mean"]) if bern else None,
                        ix["n_ent"], ix["n_rel"], seeds.ctypes.data_as(ctypes.c_void_p), seeds.shape[0],
-                       _ptr(bh), _ptr(bt), _ptr(br), _ptr(by), B, neg_rate, neg_rel_rate, mode)
+                       _ptr(bh), _ptr(bt), _ptr(br), _ptr(by), B, neg_rate, neg_rel_rate, mode,
+                       None if prob is None else _ptr(np.ascontiguousarray(prob, np.float32)))
     return bh, bt, br, by
 
 

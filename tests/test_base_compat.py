@@ -176,3 +176,30 @@ def test_sampling_bit_exact(golden, ds):
                        False, False)
             assert np.array_equal(np.stack([bh, bt, br]), g[f"{case}_step{step}"]), (case, step)
             assert np.array_equal(by, g[f"{case}_y{step}"]), (case, step)
+
+
+@pytest.mark.gpu
+def test_sampling_p_bit_exact(golden):
+    """importProb + sampling(..., p=True) through the Base.so-compatible ABI, against the reference
+    Base.so's batches (tests/golden/make_sampler_p.py)."""
+    L = _base()
+    g = golden("sampler_p")
+    path = (os.path.join(GOLDEN, "data", "prel") + "/").encode()
+    for case in sorted({k.rsplit("_cfg", 1)[0] for k in g.keys() if k.endswith("_cfg")}):
+        threads, B, neg, negrel, mode, bern = (int(x) for x in g[f"{case}_cfg"])
+        L.setInPath(path)
+        L.setWorkThreads(threads)
+        L.setBern(bern)
+        _position_rand_stream(g[f"{case}_seeds0"].astype(np.uint64))
+        L.randReset()
+        L.importTrainFiles()
+        L.importProb(float(g[f"{case}_temp"]))
+        n = B * (1 + neg + negrel)
+        for step in range(3):
+            bh, bt, br = (np.zeros(n, np.int64) for _ in range(3))
+            by = np.zeros(n, np.float32)
+            L.sampling(bh.ctypes.data, bt.ctypes.data, br.ctypes.data, by.ctypes.data, B, neg, negrel, mode, True,
+                       True, False)
+            assert np.array_equal(np.stack([bh, bt, br]), g[f"{case}_step{step}"]), (case, step)
+            assert np.array_equal(by, g[f"{case}_y{step}"]), (case, step)
+    assert L.mmre_base_last_error(None, 0) == 0

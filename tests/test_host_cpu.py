@@ -289,3 +289,18 @@ def test_sgd_closure_runs_first_and_fallbacks_are_counted():
     ref.step(closure(q))
     assert torch.equal(p, q) and not torch.equal(p, torch.ones(4))
     assert SGD.fallback_steps == before + 1 and "device" in SGD.fallback_reason
+
+
+def test_import_prob_is_the_reference(golden):
+    """mmre_import_prob (host, Reader.h:26-49) reproduces the reference Base.so's `prob` table bit
+    for bit at every fixture temperature (tests/golden/make_sampler_p.py)."""
+    from mmre._lib import call
+    g = golden("sampler_p")
+    path = os.path.join(GOLDEN, "data", "prel", "kl_prob.txt")
+    n_rel = int(open(os.path.join(GOLDEN, "data", "prel", "relation2id.txt")).readline())
+    for name in sorted(k[:-len("_temp")] for k in g if k.endswith("_temp")):
+        out = np.zeros((n_rel, n_rel - 1), np.float32)
+        call("mmre_import_prob", path.encode(), n_rel, float(g[f"{name}_temp"]), out.ctypes.data_as(ctypes.c_void_p))
+        assert np.array_equal(out.ravel(), g[f"{name}_prob"]), name
+    with pytest.raises(Exception):
+        call("mmre_import_prob", b"/nonexistent/kl_prob.txt", n_rel, 1.0, out.ctypes.data_as(ctypes.c_void_p))

@@ -156,6 +156,32 @@ def test_sampler_bit_exact(golden, oracle_mod, ds):
         assert np.array_equal(seeds, g[f"{name}_seeds_end"])
 
 
+def test_sampler_p_bit_exact(golden, oracle_mod):
+    """sampling(..., p=True): the oracle's importProb table and KL-weighted corrupt_rel
+    (Corrupt.h:111-147) against the reference Base.so's batches (tests/golden/make_sampler_p.py),
+    including relation lists emptied by the (h, t) block (the reference returns -1)."""
+    g = golden("sampler_p")
+    ds = f"{oracle_mod.HERE}/../tests/golden/data/prel"
+    tr = np.loadtxt(f"{ds}/train2id.txt", skiprows=1, dtype=np.int64, ndmin=2)
+    n_ent, n_rel = int(open(f"{ds}/entity2id.txt").readline()), int(open(f"{ds}/relation2id.txt").readline())
+    ix = oracle_mod.train_index(tr[:, 0], tr[:, 1], tr[:, 2], n_ent, n_rel)
+    names = sorted({k[:-len("_cfg")] for k in g if k.endswith("_cfg")})
+    empty = 0
+    for name in names:
+        threads, B, neg, negrel, mode, bern = g[f"{name}_cfg"].tolist()
+        prob = oracle_mod.import_prob(f"{ds}/kl_prob.txt", n_rel, float(g[f"{name}_temp"]))
+        assert np.array_equal(prob.ravel(), g[f"{name}_prob"]), name
+        seeds = g[f"{name}_seeds0"].copy()
+        for step in range(3):
+            bh, bt, br, by = oracle_mod.sampling(ix, seeds, B, neg, negrel, mode, bool(bern),
+                                                 train_total=int(g[f"{name}_train_total"]), prob=prob)
+            assert np.array_equal(np.stack([bh, bt, br]), g[f"{name}_step{step}"]), (name, step)
+            assert np.array_equal(by, g[f"{name}_y{step}"])
+            empty += int((br == -1).sum())
+        assert np.array_equal(seeds, g[f"{name}_seeds_end"])
+    assert empty > 0  # the empty-list edge is exercised
+
+
 def test_candidate_rank_rule(golden, oracle_mod):
     g = golden("repo")
     s, r = oracle_mod.candidate_rank_transe(g["ev_ent"], g["ev_rel"], g["ev_qh"], g["ev_qr"], g["ev_off"],

@@ -34,6 +34,30 @@ def test_openke_sampler_bit_exact(golden, ds):
         assert np.array_equal(s._seeds_dev.cpu().numpy().view(np.uint64), g[f"{name}_seeds_end"])
 
 
+def test_openke_sampler_p_bit_exact(golden):
+    """sampling(..., p=True) on the GPU (mmre_sampler_openke_p): KL-weighted relation negatives
+    bit-identical to the reference Base.so's (tests/golden/make_sampler_p.py), device seeds too."""
+    from mmre.data import OpenKEDataset, TrainIndex
+    from mmre.sampler import OpenKESampler
+    g = golden("sampler_p")
+    path = os.path.join(GOLDEN, "data", "prel")
+    d = OpenKEDataset(path)
+    ix = TrainIndex(d.train[:, 0], d.train[:, 1], d.train[:, 2], d.n_ent, d.n_rel)
+    names = sorted({k[:-len("_cfg")] for k in g if k.endswith("_cfg")})
+    for name in names:
+        threads, B, neg, negrel, mode, bern = g[f"{name}_cfg"].tolist()
+        s = OpenKESampler(ix, "cuda:0", work_threads=threads, bern=bool(bern), seeds=g[f"{name}_seeds0"],
+                          train_total=int(g[f"{name}_train_total"]))
+        prob = s.import_prob(os.path.join(path, "kl_prob.txt"), float(g[f"{name}_temp"]))
+        assert np.array_equal(prob.ravel(), g[f"{name}_prob"])
+        for step in range(3):
+            out = s.sample(B, neg, negrel, mode, p=True)
+            got = torch.stack([out["batch_h"], out["batch_t"], out["batch_r"]]).cpu().numpy()
+            assert np.array_equal(got, g[f"{name}_step{step}"]), (name, step)
+            assert np.array_equal(out["batch_y"].cpu().numpy(), g[f"{name}_y{step}"])
+        assert np.array_equal(s._seeds_dev.cpu().numpy().view(np.uint64), g[f"{name}_seeds_end"])
+
+
 def test_openke_sampler_full_size_properties():
     """FB15K237-sized synthetic train set (272,115 triples), B = 2,721, k = 25, 8 threads:
     every entity negative avoids the filter set of its positive (Corrupt.h:7-81)."""
