@@ -928,6 +928,38 @@ __device__ __forceinline__ float fused_x(Vec<NC>& x, const Vec<NC>& hn, const Ve
   return acc;
 }
 
+// fused_x specialised on the (wave-uniform) code: the OpenKE shapes replace one row, so x is one
+// or two operations per element instead of three selects and three operations. hr = h + r of
+// the positive (the same rounding as (h + r) - t computes first). Same values as fused_x.
+template <int NC, bool L2>
+__device__ __forceinline__ float code_x(Vec<NC>& x, const Vec<NC>& hr, const Vec<NC>& hn, const Vec<NC>& rn,
+                                        const Vec<NC>& tn, const Vec<NC>& cn, int code) {
+  float acc = 0.0f;
+  if (code == 1) {  // tail replaced
+#pragma unroll
+    for (int q = 0; q < NC; ++q) { x.v[q] = hr.v[q] - cn.v[q]; acc += L2 ? x.v[q] * x.v[q] : fabsf(x.v[q]); }
+  } else if (code == 0) {  // head replaced
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      x.v[q] = (cn.v[q] + rn.v[q]) - tn.v[q];
+      acc += L2 ? x.v[q] * x.v[q] : fabsf(x.v[q]);
+    }
+  } else if (code == 2) {  // relation replaced
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
+      x.v[q] = (hn.v[q] + cn.v[q]) - tn.v[q];
+      acc += L2 ? x.v[q] * x.v[q] : fabsf(x.v[q]);
+    }
+  } else if (code == 4) {  // x built when the rows arrived
+#pragma unroll
+    for (int q = 0; q < NC; ++q) { x.v[q] = cn.v[q]; acc += L2 ? x.v[q] * x.v[q] : fabsf(x.v[q]); }
+  } else {  // the positive's own rows
+#pragma unroll
+    for (int q = 0; q < NC; ++q) { x.v[q] = hr.v[q] - tn.v[q]; acc += L2 ? x.v[q] * x.v[q] : fabsf(x.v[q]); }
+  }
+  return acc;
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -967,7 +999,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   __shared__ float s_sq[NSW][3];
   __shared__ float s_acc[NSW - 1][3][NC * kWave];
   __shared__ float s_occ[NSW][3];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   const int d = A.dim;
   const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
   // this wave's negatives j = w + NSW u, u < nj; lane u holds negative u's row ids
@@ -1010,8 +1042,12 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       }
     }
   }
-  Vec<NC> x;
-  float p_raw = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, hn, 3));
+#pragma unroll
+  for (int u = 0; u < NSF_MAXJ; ++u) code[u] = __builtin_amdgcn_readfirstlane(code[u]);  // wave-uniform: scalar branches
+  Vec<NC> x, hr;
+#pragma unroll
+  for (int q = 0; q < NC; ++q) hr.v[q] = hn.v[q] + rn.v[q];
+  float p_raw = wave_sum_u(code_x<NC, L2>(x, hr, hn, rn, tn, hn, 3));
   if (L2) p_raw = sqrtf(p_raw);
   const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
   const float psh = nph * nph, psr = npr * npr, pst = npt * npt;
@@ -1021,12 +1057,24 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     qh = psh; qt = pst; qr = psr;
   }
   float sraw[NSF_MAXJ];
+  // occurrences of the positive's own rows among this wave's rows (the positive itself in wave
+  // 0): the regularization weights of its three slots, known before any gradient
+  float oh = w == 0 ? 1.0f : 0.0f, orr = oh, ot = oh;
 #pragma unroll
   for (int u = 0; u < NSF_MAXJ; ++u) {
     sraw[u] = 0.0f;
     if (u >= nj) continue;
     const int64_t j = w + NSW * u, row = b + (j + 1) * A.B;
-    float sv = wave_sum_u(fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]));
+    if (code[u] == 4) {
+      oh += readlane64u(my_h, u) == ph ? 1.0f : 0.0f;
+      orr += readlane64u(my_r, u) == pr ? 1.0f : 0.0f;
+      ot += readlane64u(my_t, u) == pt ? 1.0f : 0.0f;
+    } else {
+      oh += code[u] != 0 ? 1.0f : 0.0f;
+      orr += code[u] != 2 ? 1.0f : 0.0f;
+      ot += code[u] != 1 ? 1.0f : 0.0f;
+    }
+    float sv = wave_sum_u(code_x<NC, L2>(x, hr, hn, rn, tn, C[u], code[u]));
     if (L2) sv = sqrtf(sv);
     sraw[u] = sv;
     const float n = A.use_model_margin ? A.model_margin - sv : sv;
@@ -1042,7 +1090,10 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     }
     if (lane == 0) { score[row] = n; s_n[j] = n; }
   }
-  if (lane == 0) { s_sq[w][0] = qh; s_sq[w][1] = qt; s_sq[w][2] = qr; }
+  if (lane == 0) {
+    s_sq[w][0] = qh; s_sq[w][1] = qt; s_sq[w][2] = qr;
+    s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot;
+  }
   __syncthreads();
   if (w == 0) {  // loss partial and d(loss)/d(forward score) of every row, per unit upstream gradient
     const float m = A.loss_margin;
@@ -1091,50 +1142,86 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   Vec<NC> Gh, Gr, Gt, gx;
 #pragma unroll
   for (int q = 0; q < NC; ++q) Gh.v[q] = Gr.v[q] = Gt.v[q] = 0.0f;
-  float oh = 0.f, orr = 0.f, ot = 0.f;
+  // the slots this wave files, one per lane: lane 3u + k negative u's row k (h, r, t) when that
+  // row is not the positive's own; in wave 0 lanes 3 NSF_MAXJ + k the positive's own rows. The
+  // bucket places come back from ONE batched atomic round trip per wave, issued before the
+  // records are computed and stored.
+  uint32_t my_key = S.sentinel;
+  int64_t my_slot = 0;
+  float my_mult = 1.0f;
+  if (w == 0) {
+    const int k = lane - 3 * NSF_MAXJ;
+    if (k >= 0 && k < 3) {
+      float kh = 0.f, kr = 0.f, kt = 0.f;
+      for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
+      my_key = k == 0 ? (uint32_t)ph : (k == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
+      my_slot = sb + k;
+      my_mult = k == 0 ? kh : (k == 1 ? kr : kt);
+    }
+  }
+  bool active[NSF_MAXJ];
+#pragma unroll
+  for (int u = 0; u < NSF_MAXJ; ++u) {  // keys first (the hinge decides whether a negative adds anything)
+    active[u] = false;
+    if (u >= nj) continue;
+    const int64_t j = w + NSW * u;
+    if (s_c[j] == 0.0f && reg == 0.0f) continue;  // inactive hinge, no regularization: adds nothing
+    active[u] = true;
+    uint32_t kq0 = S.sentinel, kq1 = S.sentinel, kq2 = S.sentinel;
+    if (code[u] == 0) kq0 = (uint32_t)readlane64u(my_h, u);
+    else if (code[u] == 1) kq2 = (uint32_t)readlane64u(my_t, u);
+    else if (code[u] == 2) kq1 = (uint32_t)(n_ent + readlane64u(my_r, u));
+    else if (code[u] == 4) {
+      const int64_t h = readlane64u(my_h, u), r = readlane64u(my_r, u), t = readlane64u(my_t, u);
+      if (h != ph) kq0 = (uint32_t)h;
+      if (r != pr) kq1 = (uint32_t)(n_ent + r);
+      if (t != pt) kq2 = (uint32_t)t;
+    }
+    const int64_t sl = sb + 3 + 3 * j;
+    if (lane == 3 * u) { my_key = kq0; my_slot = sl; }
+    if (lane == 3 * u + 1) { my_key = kq1; my_slot = sl + 1; }
+    if (lane == 3 * u + 2) { my_key = kq2; my_slot = sl + 2; }
+  }
+  const bool filing = my_key != S.sentinel;
+  const int place = filing ? atomicAdd(&S.counts[my_key], 1) : 0;
   if (w == 0) {
     const float g = sgn * s_gp;
-    p_raw = fused_x<NC, L2>(x, hn, rn, tn, hn, 3);  // x of the positive again (registers)
+    p_raw = code_x<NC, L2>(x, hr, hn, rn, tn, hn, 3);  // x of the positive again (registers)
     const float gs = L2 ? (p_raw > 0.0f ? g / sqrtf(wave_sum_u(p_raw)) : 0.0f) : g;
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      const float gv = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
+      const float gv = L2 ? gs * x.v[q] : (x.v[q] > 0.0f ? g : (x.v[q] < 0.0f ? -g : 0.0f));
       Gh.v[q] += gv; Gr.v[q] += gv; Gt.v[q] -= gv;
     }
-    oh = orr = ot = 1.0f;
   }
 #pragma unroll
   for (int u = 0; u < NSF_MAXJ; ++u) {
-    if (u >= nj) continue;
+    if (!active[u]) continue;
     const int64_t j = w + NSW * u;
     const float g = -sgn * s_c[j];
-    // which of this negative's rows are the positive's own (summed in registers) -- the others
-    // get slots
     bool own_h = code[u] != 0, own_r = code[u] != 2, own_t = code[u] != 1;
     if (code[u] == 4) {
       own_h = readlane64u(my_h, u) == ph;
       own_r = readlane64u(my_r, u) == pr;
       own_t = readlane64u(my_t, u) == pt;
     }
-    uint32_t kq0 = S.sentinel, kq1 = S.sentinel, kq2 = S.sentinel;  // this negative's h / r / t slots
-    if (g == 0.0f && reg == 0.0f) {  // inactive hinge, no regularization: adds nothing
-      oh += own_h ? 1.0f : 0.0f;
-      orr += own_r ? 1.0f : 0.0f;
-      ot += own_t ? 1.0f : 0.0f;
-    } else {
-      fused_x<NC, L2>(x, hn, rn, tn, C[u], code[u]);  // C[u] normalised by the forward
-      const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
+    code_x<NC, L2>(x, hr, hn, rn, tn, C[u], code[u]);  // C[u] normalised by the forward
+    const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
 #pragma unroll
-      for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : g * (float)((x.v[q] > 0.0f) - (x.v[q] < 0.0f));
-      if (own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; } else kq0 = (uint32_t)readlane64u(my_h, u);
-      if (own_r) { vadd(Gr, gx, 1.0f); orr += 1.0f; } else kq1 = (uint32_t)(n_ent + readlane64u(my_r, u));
-      if (own_t) { vadd(Gt, gx, -1.0f); ot += 1.0f; } else kq2 = (uint32_t)readlane64u(my_t, u);
-      if (!(own_h && own_r && own_t)) store_rec<NC, L2>(S.rec, b * A.K + j, gx, L2 ? 0.0f : gs, d, lane);
-    }
-    if (lane < 3) {
-      const int64_t sl = sb + 3 + 3 * j + lane;
-      const uint32_t key = lane == 0 ? kq0 : (lane == 1 ? kq1 : kq2);
-      if (key != S.sentinel) put_slot(S, key, sl, 1.0f);
+    for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : (x.v[q] > 0.0f ? g : (x.v[q] < 0.0f ? -g : 0.0f));
+    if (own_h) vadd(Gh, gx, 1.0f);
+    if (own_r) vadd(Gr, gx, 1.0f);
+    if (own_t) vadd(Gt, gx, -1.0f);
+    if (!(own_h && own_r && own_t)) store_rec<NC, L2>(S.rec, b * A.K + j, gx, L2 ? 0.0f : gs, d, lane);
+  }
+  if (filing) {  // the entries, at the places the atomic returned
+    const int64_t e = slot_entry(my_slot, my_mult);
+    if (place < NS_BUCKET) {
+      S.bucket[(int64_t)my_key * NS_BUCKET + place] = e;
+    } else {
+      const int o = atomicAdd(S.ovf_n, 1);
+      S.ovf[2 * (int64_t)o] = (int64_t)my_key;
+      S.ovf[2 * (int64_t)o + 1] = e;
     }
   }
   if (w > 0) {
@@ -1145,7 +1232,6 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       s_acc[w - 1][2][q * kWave + lane] = Gt.v[q];
     }
   }
-  if (lane == 0) { s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot; }
   __syncthreads();
   if (w == 0) {  // the positive's own rows: one signed sum each, in the fixed wave order
     for (int i = 0; i < NSW - 1; ++i) {
@@ -1156,15 +1242,9 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
         Gt.v[q] += s_acc[i][2][q * kWave + lane];
       }
     }
-    float kh = 0.f, kr = 0.f, kt = 0.f;
-    for (int i = 0; i < NSW; ++i) { kh += s_occ[i][0]; kr += s_occ[i][1]; kt += s_occ[i][2]; }
     vstore_row(S.shared, 3 * b + 0, Gh, d, lane);
     vstore_row(S.shared, 3 * b + 1, Gr, d, lane);
     vstore_row(S.shared, 3 * b + 2, Gt, d, lane);
-    if (lane < 3) {
-      const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
-      put_slot(S, key, sb + lane, lane == 0 ? kh : (lane == 1 ? kr : kt));
-    }
   }
 }
 
