@@ -387,16 +387,26 @@ def bench_ns(args, world, rank, dev, dist):
     from mmre.ns import NSSpec, fused_ns_loss
     from mmre.sampler import OpenKESampler
     from mmre.workloads import zs_workload
-    w = zs_workload("FB15K-237-ZS", "transe", 200)
+    model = args.ns_model
+    w = zs_workload("FB15K-237-ZS", model, 200)
     E, R, d = w["n_ent"], w["n_rel"], w["dim"]
     B, k, margin = 2721, args.ns_neg, 5.0
     idx = TrainIndex(w["filter_h"], w["filter_t"], w["filter_r"], E, R)
     smp = OpenKESampler(idx, dev, bern=True, seed_skip=8 * rank)
     ent = w["ent"].to(dev).requires_grad_(True)
     rel = w["rel"].to(dev).requires_grad_(True)
-    spec = NSSpec("transe", d, norm_flag=True)
+    ent_im = w["ent_im"].to(dev).requires_grad_(True) if "ent_im" in w else None
+    rel_im = w["rel_im"].to(dev).requires_grad_(True) if "rel_im" in w else None
+    if model == "transe":
+        spec = NSSpec("transe", d, norm_flag=True)
+    elif model == "rotate":  # OpenKE RotatE (margin 6, epsilon 2): the model's own margin transform
+        from mmre.link import rotate_phase_denom
+        spec = NSSpec("rotate", d, model_margin=6.0, phase_denom=rotate_phase_denom(6.0, 2.0, d))
+    else:
+        spec = NSSpec(model, d)
+    tables = [x for x in (ent, rel, ent_im, rel_im) if x is not None]
     from mmre.optim import SGD
-    opt = SGD([ent, rel], lr=1.0)  # OpenKE Trainer's optimizer: one HIP launch per step
+    opt = SGD(tables, lr=1.0)  # OpenKE Trainer's optimizer: one HIP launch per step
     n_rows = B * (1 + k)
     bufs = [dict(batch_h=torch.empty(n_rows, dtype=torch.int64, device=dev),
                  batch_t=torch.empty(n_rows, dtype=torch.int64, device=dev),
@@ -409,7 +419,7 @@ def bench_ns(args, world, rank, dev, dist):
         if ev:
             ev[0].record()
         loss, _ = fused_ns_loss(spec, ent, rel, b["batch_h"], b["batch_t"], b["batch_r"], B, k, margin,
-                                events=ev[3:7] if ev else None, optimizer=opt)
+                                events=ev[3:7] if ev else None, optimizer=opt, ent_im=ent_im, rel_im=rel_im)
         if ev:
             ev[1].record()
         loss.backward()
@@ -451,7 +461,7 @@ def bench_ns(args, world, rank, dev, dist):
                     with torch.cuda.stream(fork):
                         smp.sample(B, k, out=bufs[1 - par])
                 g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k,
-                                          margin, optimizer=opt)
+                                          margin, optimizer=opt, ent_im=ent_im, rel_im=rel_im)
                 torch.autograd.backward(g_loss, grad_tensors=one)
                 opt.step()
                 if not (not args.ns_prefetch):
@@ -491,16 +501,22 @@ def bench_ns(args, world, rank, dev, dist):
     # one-shot C-ABI call mmre_ns_forward_backward captured in a hipGraph, events around replays
     from mmre._lib import call, lib, ptr, stream_ptr
     g_in = smp.sample(B, k, out=bufs[0])
-    wk = torch.empty(int(lib().mmre_ns_fused_workspace(0, 1, B, k, E, R, d)), dtype=torch.float32, device=dev)
+    wk = torch.empty(int(lib().mmre_ns_fused_workspace(spec.model_id, int(spec.norm_flag), B, k, E, R, d)),
+                     dtype=torch.float32, device=dev)
     s1 = torch.empty(n_rows, dtype=torch.float32, device=dev)
     l1 = torch.empty(1, dtype=torch.float32, device=dev)
     ge, gr = torch.empty_like(ent), torch.empty_like(rel)
+    gei = torch.empty_like(ent_im) if ent_im is not None else None
+    gri = torch.empty_like(rel_im) if rel_im is not None else None
     e0, r0 = ent.detach(), rel.detach()
+    ei0 = ent_im.detach() if ent_im is not None else None
+    ri0 = rel_im.detach() if rel_im is not None else None
 
     def one_shot():
-        call("mmre_ns_forward_backward", spec.model_id, int(spec.norm_flag), 0.0, 0, ptr(e0), None, ptr(r0), None, E, R,
-             d, 0.0, ptr(g_in["batch_h"]), ptr(g_in["batch_t"]), ptr(g_in["batch_r"]), B, k, margin, 0.0, 0.0,
-             ptr(s1), ptr(l1), ptr(ge), None, ptr(gr), None, ptr(wk), stream_ptr(dev))
+        call("mmre_ns_forward_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
+             int(spec.use_model_margin), ptr(e0), ptr(ei0), ptr(r0), ptr(ri0), E, R, d, spec.phase_denom,
+             ptr(g_in["batch_h"]), ptr(g_in["batch_t"]), ptr(g_in["batch_r"]), B, k, margin, 0.0, 0.0,
+             ptr(s1), ptr(l1), ptr(ge), ptr(gei), ptr(gr), ptr(gri), ptr(wk), stream_ptr(dev))
     one_shot()
     torch.cuda.synchronize()
     g_fused = torch.cuda.CUDAGraph()
@@ -525,25 +541,35 @@ def bench_ns(args, world, rank, dev, dist):
         # written by the fused kernel and read back by the row-owner pass: three d-float sum rows
         # per positive, a 72-B sign record per negative (L1, d 200: |g| + two 4 x 64-bit planes),
         # and per slot a key, an occurrence count and a bucketed id: slot_bytes.
-        fwd_bytes = B * 3 * 4 * d + B * k * 4 * d + n_rows * 3 * 8
-        grad_bytes = (E + R) * 4 * d
-        slot_bytes = 2 * (B * 3 * 4 * d + B * k * 4 * (2 + 4 * 4)) + 2 * 3 * 4 * B * (3 + 3 * k)
+        if model == "transe":
+            fwd_bytes = B * 3 * 4 * d + B * k * 4 * d + n_rows * 3 * 8
+            grad_bytes = (E + R) * 4 * d
+            slot_bytes = 2 * (B * 3 * 4 * d + B * k * 4 * (2 + 4 * 4)) + 2 * 3 * 4 * B * (3 + 3 * k)
+        else:  # k_ns_forward reads the three rows of every batch row; records of 2 d_pad floats per slot
+            eb = 4 * d * (2 if model in ("complex", "rotate") else 1)
+            rb = 4 * d * (2 if model == "complex" else 1)
+            fwd_bytes = n_rows * (2 * eb + rb) + n_rows * 3 * 8
+            grad_bytes = E * eb + R * rb
+            slot_bytes = 2 * (B * (3 + 3 * k)) * 2 * 4 * (256 if d > 128 else 128)
         ach = (fwd_bytes + grad_bytes) / (fused_ms * 1e-3) / 1e9
         out = {"metric": f"training triples/sec, {CONFIGS['ns']['workload']}",
                "value": n_rows * args.steps * world / elapsed, "unit": "training triples/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-               "data": "synthetic TransE tables (OpenKE xavier init, seed 0); training triples = 272,115 synthetic "
+               "data": f"synthetic {model} tables (OpenKE init, seed 0); training triples = 272,115 synthetic "
                        "+ the FB15K-237-ZS test triples",
-               "config": {"workload": CONFIGS["ns"]["workload"], "batch": B, "neg_ent": k, "rows_per_step": n_rows,
+               "config": {"workload": CONFIGS["ns"]["workload"] if model == "transe" else
+                          f"{model} d=200 training step at the C2 training shape (margin loss)", "model": model,
+                          "batch": B, "neg_ent": k, "rows_per_step": n_rows,
                           "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}",
                           "launch": ("eager" if not graph else "hipGraph replay of the whole step" +
                                      ("" if (not args.ns_prefetch) else ", next batch sampled on a forked stream (prefetch)"))},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                            "kernel": "mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false> + "
-                                      "k_ns_reduce (the loss) + k_ns_row_owner<4, false>: events around hipGraph "
-                                      "replays of the one-shot C-ABI call",
+                            "kernel": ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false> + "
+                                       "k_ns_reduce (the loss) + k_ns_row_owner<4, false>" if model == "transe" else
+                                       "mmre_ns_forward_backward = k_ns_forward + k_ns_reduce + k_ns_gen_slots + "
+                                       "k_ns_gen_owner") + ": events around hipGraph replays of the one-shot C-ABI call",
                             "kernel_ms": fused_ms, "eager_fused_forward_ms": fused_fwd_ms,
                             "eager_fused_grad_ms": fused_grad_ms,
                             "algorithmic_bytes": fwd_bytes + grad_bytes, "slot_bytes": slot_bytes,
@@ -556,7 +582,7 @@ def bench_ns(args, world, rank, dev, dist):
                                     "fused kernel, the loss reduction, the row-owner pass with the SGD step fused in "
                                     "(mmre_ns_fused_grad_sgd, bit-identical to backward() + step())"},
                "last_loss": float(loss.detach())}
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and model == "transe":
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
         print(json.dumps(_with_build(out)), flush=True)
     if dist:
@@ -965,6 +991,8 @@ def main():
                     help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
     ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
     ap.add_argument("--ns-eager", action="store_true", help="--config ns: launch each step eagerly (no hipGraph)")
+    ap.add_argument("--ns-model", default="transe", choices=["transe", "distmult", "complex", "rotate"],
+                    help="--config ns: the scored model (default transe, the C2 training step)")
     ap.add_argument("--ns-prefetch", action="store_true",
                     help="--config ns: sample the next batch on a forked stream while the current one trains "
                          "(default: in line before each step; the fork/join graph measured slower)")

@@ -1538,30 +1538,186 @@ __device__ __forceinline__ void row2_add(Row2<NC>& a, const Row2<NC>& b) {
   for (int c = 0; c < NC; ++c) { a.a.v[c] += b.a.v[c]; a.b.v[c] += b.b.v[c]; }
 }
 
-// record of slot sl: 2 halves of dpad floats
+// record of slot sl: the halves of a row gradient, d floats each, back to back (stride 2 d for
+// the two-half models -- ComplEx, RotatE -- d for DistMult; RotatE relation rows keep their
+// single half). Rows move through row-sized buffer resources (no padding lanes stored).
 template <int NC>
-__device__ __forceinline__ void rec_store(float* rec, int64_t sl, int dpad, const Row2<NC>& r, int lane) {
-  float* o = rec + sl * 2 * dpad;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) { o[c * kWave + lane] = r.a.v[c]; o[dpad + c * kWave + lane] = r.b.v[c]; }
+__device__ __forceinline__ void rec_store(float* rec, int64_t sl, int d, bool stride2, bool two, const Row2<NC>& r,
+                                          int lane) {
+  float* o = rec + sl * (stride2 ? 2 * (int64_t)d : (int64_t)d);
+  vstore_row(o, 0, r.a, d, lane);
+  if (two) vstore_row(o + d, 0, r.b, d, lane);
 }
 
 template <int NC>
-__device__ __forceinline__ void rec_load(Row2<NC>& r, const float* rec, int64_t sl, int dpad, int lane) {
-  const float* o = rec + sl * 2 * dpad;
+__device__ __forceinline__ void rec_load(Row2<NC>& r, const float* rec, int64_t sl, int d, bool stride2, bool two,
+                                         int lane) {
+  const float* o = rec + sl * (stride2 ? 2 * (int64_t)d : (int64_t)d);
+  vload_row(r.a, o, 0, d, lane);
+  if (two) vload_row(r.b, o + d, 0, d, lane);
+  else vzero(r.b);
+}
+
+// The corrupted row of a negative of the OpenKE shapes (Base.cpp:111-145): code 0 head, 1 tail,
+// 2 relation replaced (one row differs from its positive's), 3 the positive itself, 4 anything
+// else (handled by the per-row generic code).
+__device__ __forceinline__ int neg_code(int64_t h, int64_t r, int64_t t, int64_t ph, int64_t pr, int64_t pt) {
+  const bool oh = h == ph, orr = r == pr, ot = t == pt;
+  if (orr && ot && !oh) return 0;
+  if (orr && oh && !ot) return 1;
+  if (oh && ot && !orr) return 2;
+  if (oh && ot && orr) return 3;
+  return 4;
+}
+
+// row_score of DistMult / ComplEx / RotatE on rows already in registers (same per-element
+// expressions, elements in the same lane + 64 c order, padding elements adding +0: the same
+// floats bit for bit). RotatE: sn / cs of the relation row (canon_sincos(r / phase_denom)).
+template <int NC>
+__device__ __forceinline__ float gen_score(const NSArgs& A, const Row2<NC>& H, const Row2<NC>& R, const Row2<NC>& T,
+                                           const Vec<NC>& sn, const Vec<NC>& cs) {
+  float acc = 0.0f;
 #pragma unroll
-  for (int c = 0; c < NC; ++c) { r.a.v[c] = o[c * kWave + lane]; r.b.v[c] = o[dpad + c * kWave + lane]; }
+  for (int c = 0; c < NC; ++c) {
+    if (A.model == MMRE_DISTMULT) {
+      acc += (H.a.v[c] * R.a.v[c]) * T.a.v[c];
+    } else if (A.model == MMRE_COMPLEX) {
+      const float hr = H.a.v[c], hi = H.b.v[c], tr = T.a.v[c], ti = T.b.v[c], rr = R.a.v[c], ri = R.b.v[c];
+      acc += hr * tr * rr + hi * ti * rr + hr * ti * ri - hi * tr * ri;
+    } else {
+      const float re = H.a.v[c] * cs.v[c] - H.b.v[c] * sn.v[c] - T.a.v[c];
+      const float im = H.a.v[c] * sn.v[c] + H.b.v[c] * cs.v[c] - T.b.v[c];
+      acc += sqrtf(re * re + im * im);
+    }
+  }
+  acc = wave_sum(acc);
+  return A.model == MMRE_ROTATE ? A.model_margin - acc : acc;
+}
+
+template <int NC>
+__device__ __forceinline__ void rot_sincos(const NSArgs& A, const Row2<NC>& R, Vec<NC>& sn, Vec<NC>& cs) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (A.model == MMRE_ROTATE) canon_sincos(R.a.v[c] / A.phase_denom, &sn.v[c], &cs.v[c]);
+    else sn.v[c] = cs.v[c] = 0.0f;
+  }
+}
+
+constexpr int NSG = 4;  // negatives whose rows are in flight together (generic models)
+
+// Forward of the fused path for DistMult / ComplEx / RotatE (k_ns_forward's outputs: scores,
+// per-positive partials, zeroed bucket counts), one wave per positive: the positive's rows stay
+// in registers (RotatE: with its relation's sin / cos), the negatives' ids are read lane-parallel
+// and NSG corrupted rows are loaded together -- an OpenKE negative differs from its positive in
+// one row -- instead of one negative's three rows per dependent round trip.
+template <int NC, int MODEL>
+__global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __restrict__ score, float* __restrict__ part,
+                                                        int32_t* __restrict__ zero, int64_t n_zero) {
+  NSArgs A = A_;
+  A.model = MODEL;  // compile-time model: the other models' registers and branches fold away
+  __shared__ float s_n[NS_WAVES][NS_MAXK];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; zero && i < n_zero;
+       i += (int64_t)gridDim.x * blockDim.x)
+    zero[i] = 0;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + w;
+  if (b >= A.B) return;  // whole wave exits together
+  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
+  Row2<NC> H, R, T;
+  gen_load(H, A, true, ph, lane);
+  gen_load(R, A, false, pr, lane);
+  gen_load(T, A, true, pt, lane);
+  Vec<NC> psn, pcs;
+  rot_sincos(A, R, psn, pcs);
+  const float p = gen_score(A, H, R, T, psn, pcs);
+  if (lane == 0) score[b] = p;
+  float sq[6] = {0, 0, 0, 0, 0, 0};
+  if (A.regul_rate != 0.0f) row_sq(A, b, lane, sq);
+  float mx = -INFINITY;
+  for (int64_t j0 = 0; j0 < A.K; j0 += kWave) {
+    const int nch = (int)(A.K - j0 < kWave ? A.K - j0 : kWave);
+    int64_t mh = 0, mt = 0, mr = 0;
+    if (lane < nch) {
+      const int64_t row = b + (j0 + lane + 1) * A.B;
+      mh = A.h[row]; mt = A.t[row]; mr = A.r[row];
+    }
+    for (int u0 = 0; u0 < nch; u0 += NSG) {
+      Row2<NC> X[NSG];
+      int code[NSG];
+#pragma unroll
+      for (int i = 0; i < NSG; ++i) {
+        const int u = u0 + i;
+        code[i] = 3;
+        if (u >= nch) continue;
+        const int64_t h = readlane64u(mh, u), t = readlane64u(mt, u), r = readlane64u(mr, u);
+        code[i] = __builtin_amdgcn_readfirstlane(neg_code(h, r, t, ph, pr, pt));
+        if (code[i] == 0) gen_load(X[i], A, true, h, lane);
+        else if (code[i] == 1) gen_load(X[i], A, true, t, lane);
+        else if (code[i] == 2) gen_load(X[i], A, false, r, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < NSG; ++i) {
+        const int u = u0 + i;
+        if (u >= nch) continue;
+        const int64_t j = j0 + u, row = b + (j + 1) * A.B;
+        float n;
+        if (code[i] == 0) n = gen_score(A, X[i], R, T, psn, pcs);
+        else if (code[i] == 1) n = gen_score(A, H, R, X[i], psn, pcs);
+        else if (code[i] == 2) {
+          Vec<NC> sn, cs;
+          rot_sincos(A, X[i], sn, cs);
+          n = gen_score(A, H, X[i], T, sn, cs);
+        } else if (code[i] == 3) n = p;
+        else n = row_score(A, row, lane);
+        if (lane == 0) { score[row] = n; s_n[w][j] = n; }
+        if (A.regul_rate != 0.0f) row_sq(A, row, lane, sq);
+        if (A.adv_t > 0.0f) mx = fmaxf(mx, -n * A.adv_t);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  float loss = 0.0f;
+  if (lane == 0) {
+    if (A.adv_t > 0.0f) {
+      float den = 0.0f;
+      for (int64_t j = 0; j < A.K; ++j) den += expf(-s_n[w][j] * A.adv_t - mx);
+      for (int64_t j = 0; j < A.K; ++j) {
+        const float n = s_n[w][j];
+        loss += expf(-n * A.adv_t - mx) / den * fmaxf(p - n, -A.loss_margin);
+      }
+    } else {
+      for (int64_t j = 0; j < A.K; ++j) loss += fmaxf(p - s_n[w][j], -A.loss_margin);
+    }
+    part[b * 7] = loss;
+  }
+  for (int i = 0; i < 6; ++i) {
+    const float v = A.regul_rate != 0.0f ? wave_sum(sq[i]) : 0.0f;
+    if (lane == 0) part[b * 7 + 1 + i] = v;
+  }
 }
 
 // One wave per positive: the loss's d/d(score) coefficients of its rows (k_ns_backward's
 // formulas, unit upstream gradient), each row's gradient; what a negative adds to a row it
 // shares with its positive (same role, same id) is summed in registers, every other row gets
 // a slot of its own. Inactive rows (zero coefficient, no regularization) add nothing.
-template <int NC>
-__global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A, const float* __restrict__ score, NSSlots S,
+// Negatives go in chunks of 21 (63 slot lanes): their ids and coefficients are read
+// lane-parallel, the chunk's bucket places come back from ONE batched atomic round trip, and
+// NSG corrupted rows are loaded together; sums and records are those of the per-negative loop
+// (same formulas, same order).
+template <int NC, int MODEL>
+__global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __restrict__ score, NSSlots S,
                                                       int64_t n_ent, int dpad, int with_reg) {
+  constexpr int CH = 21;
+  constexpr int NG = MODEL == MMRE_DISTMULT ? NSG : 2;  // two-half rows: fewer in flight (registers)
+  // record layout (rec_store): stride 2 d for the two-half models; entity / relation records' halves
+  constexpr bool S2 = MODEL != MMRE_DISTMULT, E2 = MODEL != MMRE_DISTMULT, R2 = MODEL == MMRE_COMPLEX;
+  (void)dpad;
+  NSArgs A = A_;
+  A.model = MODEL;  // compile-time model
+  const int d = A.dim;
   const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + (threadIdx.x >> 6);
+  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (b >= A.B) return;  // wave-uniform
   const float p = score[b];
   float mx = -INFINITY, den = 0.0f;
@@ -1590,35 +1746,87 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A, const float* __r
   gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt);
   float kh = 1.0f, kr = 1.0f, kt = 1.0f;  // occurrences of the positive's rows (regularization)
   const int64_t sb = b * (3 + 3 * A.K);
-  for (int64_t j = 0; j < A.K; ++j) {
-    const int64_t row = b + (j + 1) * A.B;
-    const int64_t nh = A.h[row], nr = A.r[row], nt = A.t[row];
-    const bool oh = nh == ph, orr = nr == pr, ot = nt == pt;
-    const float g = -coef(j);
-    if (g == 0.0f && !with_reg) {
-      kh += oh ? 1.0f : 0.0f; kr += orr ? 1.0f : 0.0f; kt += ot ? 1.0f : 0.0f;
-      continue;
+  for (int64_t j0 = 0; j0 < A.K; j0 += CH) {
+    const int nch = (int)(A.K - j0 < CH ? A.K - j0 : CH);
+    int64_t mh = 0, mt = 0, mr = 0;
+    float mg = 0.0f;
+    if (lane < nch) {
+      const int64_t row = b + (j0 + lane + 1) * A.B;
+      mh = A.h[row]; mt = A.t[row]; mr = A.r[row];
+      mg = -coef(j0 + lane);
     }
-    Row2<NC> Hj, Rj, Tj;
-    if (oh) Hj = H; else gen_load(Hj, A, true, nh, lane);
-    if (orr) Rj = R; else gen_load(Rj, A, false, nr, lane);
-    if (ot) Tj = T; else gen_load(Tj, A, true, nt, lane);
-    gen_row_grad(A, Hj, Rj, Tj, g, dH, dR, dT);
-    const int64_t sl = sb + 3 + 3 * j;
-    if (oh) { row2_add(Gh, dH); kh += 1.0f; } else { rec_store(S.rec, sl, dpad, dH, lane); }
-    if (orr) { row2_add(Gr, dR); kr += 1.0f; } else { rec_store(S.rec, sl + 1, dpad, dR, lane); }
-    if (ot) { row2_add(Gt, dT); kt += 1.0f; } else { rec_store(S.rec, sl + 2, dpad, dT, lane); }
-    if (lane < 3) {
-      const bool own = lane == 0 ? oh : (lane == 1 ? orr : ot);
-      if (!own) {
-        const uint32_t key = lane == 0 ? (uint32_t)nh : (lane == 1 ? (uint32_t)(n_ent + nr) : (uint32_t)nt);
-        put_slot(S, key, sl + lane, 1.0f);
+    // keys of the chunk's slots (lane 3u + k: negative u's row k when it is not the positive's)
+    uint32_t my_key = S.sentinel;
+    int64_t my_slot = 0;
+    for (int u = 0; u < nch; ++u) {
+      const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mg), u));
+      if (g == 0.0f && !with_reg) continue;
+      const int64_t h = readlane64u(mh, u), t = readlane64u(mt, u), r = readlane64u(mr, u);
+      const int64_t sl = sb + 3 + 3 * (j0 + u);
+      if (lane == 3 * u && h != ph) { my_key = (uint32_t)h; my_slot = sl; }
+      if (lane == 3 * u + 1 && r != pr) { my_key = (uint32_t)(n_ent + r); my_slot = sl + 1; }
+      if (lane == 3 * u + 2 && t != pt) { my_key = (uint32_t)t; my_slot = sl + 2; }
+    }
+    const bool filing = my_key != S.sentinel;
+    const int place = filing ? atomicAdd(&S.counts[my_key], 1) : 0;
+    for (int u0 = 0; u0 < nch; u0 += NG) {
+      Row2<NC> X[NG];
+      int code[NG];
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const int u = u0 + i;
+        code[i] = 3;
+        if (u >= nch) continue;
+        const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mg), u));
+        if (g == 0.0f && !with_reg) { code[i] = -1; continue; }  // inactive
+        const int64_t h = readlane64u(mh, u), t = readlane64u(mt, u), r = readlane64u(mr, u);
+        code[i] = __builtin_amdgcn_readfirstlane(neg_code(h, r, t, ph, pr, pt));
+        if (code[i] == 0) gen_load(X[i], A, true, h, lane);
+        else if (code[i] == 1) gen_load(X[i], A, true, t, lane);
+        else if (code[i] == 2) gen_load(X[i], A, false, r, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < NG; ++i) {
+        const int u = u0 + i;
+        if (u >= nch) continue;
+        const int64_t h = readlane64u(mh, u), t = readlane64u(mt, u), r = readlane64u(mr, u);
+        const bool oh = h == ph, orr = r == pr, ot = t == pt;
+        if (code[i] < 0) {
+          kh += oh ? 1.0f : 0.0f; kr += orr ? 1.0f : 0.0f; kt += ot ? 1.0f : 0.0f;
+          continue;
+        }
+        const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mg), u));
+        if (code[i] == 0) gen_row_grad(A, X[i], R, T, g, dH, dR, dT);
+        else if (code[i] == 1) gen_row_grad(A, H, R, X[i], g, dH, dR, dT);
+        else if (code[i] == 2) gen_row_grad(A, H, X[i], T, g, dH, dR, dT);
+        else if (code[i] == 3) gen_row_grad(A, H, R, T, g, dH, dR, dT);
+        else {
+          Row2<NC> Hj, Rj, Tj;
+          if (oh) Hj = H; else gen_load(Hj, A, true, h, lane);
+          if (orr) Rj = R; else gen_load(Rj, A, false, r, lane);
+          if (ot) Tj = T; else gen_load(Tj, A, true, t, lane);
+          gen_row_grad(A, Hj, Rj, Tj, g, dH, dR, dT);
+        }
+        const int64_t sl = sb + 3 + 3 * (j0 + u);
+        if (oh) { row2_add(Gh, dH); kh += 1.0f; } else { rec_store(S.rec, sl, d, S2, E2, dH, lane); }
+        if (orr) { row2_add(Gr, dR); kr += 1.0f; } else { rec_store(S.rec, sl + 1, d, S2, R2, dR, lane); }
+        if (ot) { row2_add(Gt, dT); kt += 1.0f; } else { rec_store(S.rec, sl + 2, d, S2, E2, dT, lane); }
+      }
+    }
+    if (filing) {  // the chunk's entries, at the places the atomic returned
+      const int64_t e = slot_entry(my_slot, 1.0f);
+      if (place < NS_BUCKET) {
+        S.bucket[(int64_t)my_key * NS_BUCKET + place] = e;
+      } else {
+        const int o = atomicAdd(S.ovf_n, 1);
+        S.ovf[2 * (int64_t)o] = (int64_t)my_key;
+        S.ovf[2 * (int64_t)o + 1] = e;
       }
     }
   }
-  rec_store(S.rec, sb, dpad, Gh, lane);
-  rec_store(S.rec, sb + 1, dpad, Gr, lane);
-  rec_store(S.rec, sb + 2, dpad, Gt, lane);
+  rec_store(S.rec, sb, d, S2, E2, Gh, lane);
+  rec_store(S.rec, sb + 1, d, S2, R2, Gr, lane);
+  rec_store(S.rec, sb + 2, d, S2, E2, Gt, lane);
   if (lane < 3) {
     const uint32_t key = lane == 0 ? (uint32_t)ph : (lane == 1 ? (uint32_t)(n_ent + pr) : (uint32_t)pt);
     put_slot(S, key, sb + lane, lane == 0 ? kh : (lane == 1 ? kr : kt));
@@ -1646,6 +1854,7 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
   const int d = A.dim;
   const int64_t pre = bucket[row * NS_BUCKET + lane];
   const bool two = A.model == MMRE_COMPLEX || (A.model == MMRE_ROTATE && is_ent);
+  const bool s2 = A.model != MMRE_DISTMULT;  // record stride (rec_store)
   // output rows of the two halves
   float *oa, *ob = nullptr, *pa = nullptr, *pb = nullptr;
   if (is_ent) {
@@ -1679,14 +1888,14 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
     int u = 0;
     for (; u + 2 <= take; u += 2) {  // two records in flight, added in slot order
       Row2<NC> r0, r1;
-      rec_load(r0, rec, __builtin_amdgcn_readlane(sl, u), dpad, lane);
-      rec_load(r1, rec, __builtin_amdgcn_readlane(sl, u + 1), dpad, lane);
+      rec_load(r0, rec, __builtin_amdgcn_readlane(sl, u), d, s2, two, lane);
+      rec_load(r1, rec, __builtin_amdgcn_readlane(sl, u + 1), d, s2, two, lane);
       row2_add(dy, r0);
       row2_add(dy, r1);
     }
     if (u < take) {
       Row2<NC> r0;
-      rec_load(r0, rec, __builtin_amdgcn_readlane(sl, u), dpad, lane);
+      rec_load(r0, rec, __builtin_amdgcn_readlane(sl, u), d, s2, two, lane);
       row2_add(dy, r0);
     }
   }
@@ -1867,7 +2076,7 @@ static void fused_ws(int model, int norm_flag, int64_t B, int64_t K, int64_t E, 
   w.rel_n = o;   o = al64(o + (te && norm_flag ? R * d : 0));
   w.shared = o;  o = al64(o + (te ? 3 * B * d : 0));
   const int64_t rw = ns_rec_words(8, false, d);
-  w.rec = o;     o = al64(o + (te ? K * B * (d > rw ? d : rw) : w.slots * 2 * w.dpad));
+  w.rec = o;     o = al64(o + (te ? K * B * (d > rw ? d : rw) : w.slots * (model == MMRE_DISTMULT ? 1 : 2) * d));
   w.counts = o;  o = al64(o + E + R + 1);   // + the overflow count
   w.bucket = o;  o = al64(o + 2 * (E + R) * NS_BUCKET);   // int64 entries
   w.ovf = o;     o = al64(o + 4 * w.slots);                // int64 (row, entry) pairs
@@ -1911,9 +2120,28 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   float* part = d_work + w.part;
   NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
   if (!fused_fast(A)) {  // other models: scores + partials (zeroing the bucket counts), then the loss
-    if (!is_transe(model) && gen_nc(dim) == 0) return MMRE_ERR_SHAPE;
-    hipLaunchKernelGGL(k_ns_forward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
-                       d_score, part, S.counts, n_ent + n_rel + 1);
+    const int gnc = gen_nc(dim);
+    if (!is_transe(model) && gnc == 0) return MMRE_ERR_SHAPE;
+    const dim3 fgrid((unsigned)((batch + NS_WAVES - 1) / NS_WAVES));
+    if (is_transe(model)) {
+      hipLaunchKernelGGL(k_ns_forward, fgrid, dim3(256), 0, st, A, d_score, part, S.counts, n_ent + n_rel + 1);
+    } else {
+#define MMRE_NS_GF(NC_, M_)                                                                                        \
+  hipLaunchKernelGGL((k_ns_gen_forward<NC_, M_>), fgrid, dim3(256), 0, st, A, d_score, part, S.counts,             \
+                     n_ent + n_rel + 1)
+#define MMRE_NS_GF_M(NC_)                                                                                          \
+  do {                                                                                                             \
+    if (model == MMRE_DISTMULT) MMRE_NS_GF(NC_, MMRE_DISTMULT);                                                    \
+    else if (model == MMRE_COMPLEX) MMRE_NS_GF(NC_, MMRE_COMPLEX);                                                 \
+    else MMRE_NS_GF(NC_, MMRE_ROTATE);                                                                             \
+  } while (0)
+      if (gnc == 1) MMRE_NS_GF_M(1);
+      else if (gnc == 2) MMRE_NS_GF_M(2);
+      else if (gnc == 4) MMRE_NS_GF_M(4);
+      else MMRE_NS_GF_M(8);
+#undef MMRE_NS_GF_M
+#undef MMRE_NS_GF
+    }
     MMRE_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_ns_reduce, dim3(1), dim3(256), 0, st, A, part, d_loss);
     MMRE_CHECK_LAUNCH();
@@ -1977,8 +2205,15 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     const dim3 sgrid((unsigned)((batch + NS_WAVES - 1) / NS_WAVES));
 #define MMRE_NS_GEN(NC_)                                                                                            \
   do {                                                                                                              \
-    hipLaunchKernelGGL((k_ns_gen_slots<NC_>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,                      \
-                       (int)(regul_rate != 0.0f));                                                                  \
+    if (model == MMRE_DISTMULT)                                                                                     \
+      hipLaunchKernelGGL((k_ns_gen_slots<NC_, MMRE_DISTMULT>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,     \
+                         (int)(regul_rate != 0.0f));                                                                \
+    else if (model == MMRE_COMPLEX)                                                                                 \
+      hipLaunchKernelGGL((k_ns_gen_slots<NC_, MMRE_COMPLEX>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,      \
+                         (int)(regul_rate != 0.0f));                                                                \
+    else                                                                                                            \
+      hipLaunchKernelGGL((k_ns_gen_slots<NC_, MMRE_ROTATE>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,       \
+                         (int)(regul_rate != 0.0f));                                                                \
     hipLaunchKernelGGL((k_ns_gen_owner<NC_>), ogrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec,         \
                        S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, \
                        d_grad_rel_im, lr, pe, pei, pr, pri);                                                        \
