@@ -1484,20 +1484,23 @@ __device__ __forceinline__ void vzero(Vec<NC>& o) {
 template <int NC>
 __device__ __forceinline__ void gen_load(Row2<NC>& o, const NSArgs& A, bool is_ent, int64_t id, int lane) {
   const int d = A.dim;
-  if (is_ent) {
-    if (A.model == MMRE_COMPLEX) { vload(o.a, A.ent + id * d, d, lane); vload(o.b, A.ent_im + id * d, d, lane); }
-    else if (A.model == MMRE_ROTATE) { vload(o.a, A.ent + id * 2 * d, d, lane); vload(o.b, A.ent + id * 2 * d + d, d, lane); }
-    else { vload(o.a, A.ent + id * d, d, lane); vzero(o.b); }
+  if (is_ent) {  // row id (wave-uniform) through row-sized buffer resources: no per-element bounds
+    if (A.model == MMRE_COMPLEX) { vload_row(o.a, A.ent, id, d, lane); vload_row(o.b, A.ent_im, id, d, lane); }
+    else if (A.model == MMRE_ROTATE) { vload_row(o.a, A.ent, 2 * id, d, lane); vload_row(o.b, A.ent, 2 * id + 1, d, lane); }
+    else { vload_row(o.a, A.ent, id, d, lane); vzero(o.b); }
   } else {
-    vload(o.a, A.rel + id * d, d, lane);
-    if (A.model == MMRE_COMPLEX) vload(o.b, A.rel_im + id * d, d, lane); else vzero(o.b);
+    vload_row(o.a, A.rel, id, d, lane);
+    if (A.model == MMRE_COMPLEX) vload_row(o.b, A.rel_im, id, d, lane); else vzero(o.b);
   }
 }
 
-// g * d(forward score)/d(h, r, t) of one row (the per-element formulas of row_backward)
+// g * d(forward score)/d(h, r, t) of one row (the per-element formulas of row_backward).
+// RotatE: psn / pcs, when given, are canon_sincos(R / phase_denom) already computed (the
+// positive's relation, shared by its entity-corrupted negatives): the same values.
 template <int NC>
 __device__ __forceinline__ void gen_row_grad(const NSArgs& A, const Row2<NC>& H, const Row2<NC>& R,
-                                             const Row2<NC>& T, float g, Row2<NC>& dH, Row2<NC>& dR, Row2<NC>& dT) {
+                                             const Row2<NC>& T, float g, Row2<NC>& dH, Row2<NC>& dR, Row2<NC>& dT,
+                                             const Vec<NC>* psn = nullptr, const Vec<NC>* pcs = nullptr) {
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     if (A.model == MMRE_DISTMULT) {
@@ -1515,7 +1518,8 @@ __device__ __forceinline__ void gen_row_grad(const NSArgs& A, const Row2<NC>& H,
       dR.b.v[c] = g * (hr * ti - hi * tr);
     } else {  // RotatE, forward = m - sum_k rho_k
       float sn, cs;
-      canon_sincos(R.a.v[c] / A.phase_denom, &sn, &cs);
+      if (psn) { sn = psn->v[c]; cs = pcs->v[c]; }
+      else canon_sincos(R.a.v[c] / A.phase_denom, &sn, &cs);
       const float hre = H.a.v[c], him = H.b.v[c];
       const float re = hre * cs - him * sn - T.a.v[c];
       const float im = hre * sn + him * cs - T.b.v[c];
@@ -1743,7 +1747,9 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
   gen_load(H, A, true, ph, lane);
   gen_load(R, A, false, pr, lane);
   gen_load(T, A, true, pt, lane);
-  gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt);
+  Vec<NC> psn, pcs;
+  rot_sincos(A, R, psn, pcs);
+  gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt, &psn, &pcs);
   float kh = 1.0f, kr = 1.0f, kt = 1.0f;  // occurrences of the positive's rows (regularization)
   const int64_t sb = b * (3 + 3 * A.K);
   for (int64_t j0 = 0; j0 < A.K; j0 += CH) {
@@ -1796,10 +1802,10 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
           continue;
         }
         const float g = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mg), u));
-        if (code[i] == 0) gen_row_grad(A, X[i], R, T, g, dH, dR, dT);
-        else if (code[i] == 1) gen_row_grad(A, H, R, X[i], g, dH, dR, dT);
+        if (code[i] == 0) gen_row_grad(A, X[i], R, T, g, dH, dR, dT, &psn, &pcs);
+        else if (code[i] == 1) gen_row_grad(A, H, R, X[i], g, dH, dR, dT, &psn, &pcs);
         else if (code[i] == 2) gen_row_grad(A, H, X[i], T, g, dH, dR, dT);
-        else if (code[i] == 3) gen_row_grad(A, H, R, T, g, dH, dR, dT);
+        else if (code[i] == 3) gen_row_grad(A, H, R, T, g, dH, dR, dT, &psn, &pcs);
         else {
           Row2<NC> Hj, Rj, Tj;
           if (oh) Hj = H; else gen_load(Hj, A, true, h, lane);
