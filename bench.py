@@ -114,6 +114,30 @@ def pmc_traffic(config: str, model: str):
     return None, f"{rel} holds no FETCH_SIZE / WRITE_SIZE of {KERNEL_NAMES[model]}"
 
 
+def pmc_step_traffic(config: str, kernels):
+    """HBM-side bytes of one training step: (2 x FETCH_SIZE + WRITE_SIZE) KiB summed over the
+    step's kernels (a substring each) from profiles/pmc_<config>.json, under the same build tie
+    as pmc_traffic. Returns (bytes or None, source or reason, per-kernel bytes)."""
+    from mmre._lib import lib_identity
+    path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None, None, None
+    with open(path) as f:
+        d = json.load(f)
+    rel = os.path.relpath(path, REPO)
+    sha = (d.get("__build__") or {}).get("lib_sha256")
+    mine = lib_identity()["sha256"]
+    if sha != mine:
+        return None, f"{rel} was captured on libmmre_hip.so {sha or '(unrecorded)'}, not this build ({mine})", None
+    per = {}
+    for k in kernels:
+        hits = [c for name, c in d.items() if k in name and "FETCH_SIZE" in c and "WRITE_SIZE" in c]
+        if not hits:
+            return None, f"{rel} holds no FETCH_SIZE / WRITE_SIZE of {k}", None
+        per[k] = (2.0 * hits[0]["FETCH_SIZE"] + hits[0]["WRITE_SIZE"]) * 1024.0
+    return sum(per.values()), rel, per
+
+
 REF_SAMPLE = {"c1": 1000, "c2": 1000, "c3": 1000, "c4": 10, "c5": 24}   # test triples in the CPU leg
 
 
@@ -552,6 +576,11 @@ def bench_ns(args, world, rank, dev, dist):
             grad_bytes = E * eb + R * rb
             slot_bytes = 2 * (B * (3 + 3 * k)) * 2 * 4 * (256 if d > 128 else 128)
         ach = (fwd_bytes + grad_bytes) / (fused_ms * 1e-3) / 1e9
+        step_kernels = (["k_ns_prepass(", "k_ns_transe_fused<4, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
+                        if model == "transe" else
+                        ["k_ns_gen_forward<4, ", "k_ns_reduce(", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"])
+        traffic, tsrc, tper = (pmc_step_traffic("ns", step_kernels) if (model == "transe" and world == 1 and d == 200 and k == 25)
+                               else (None, None, None))
         out = {"metric": f"training triples/sec, {CONFIGS['ns']['workload']}",
                "value": n_rows * args.steps * world / elapsed, "unit": "training triples/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
@@ -565,7 +594,11 @@ def bench_ns(args, world, rank, dev, dist):
                           "launch": ("eager" if not graph else "hipGraph replay of the whole step" +
                                      ("" if (not args.ns_prefetch) else ", next batch sampled on a forked stream (prefetch)"))},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                            "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
+                            "traffic_unit": "HBM bytes per step's loss + gradient kernels (rocprofv3 PMC, "
+                                            "2 x FETCH_SIZE + WRITE_SIZE)",
+                            "traffic_source": tsrc, "traffic_per_kernel": tper,
+                            "traffic_x_algorithmic": (traffic / (fwd_bytes + grad_bytes)) if traffic else None,
                             "kernel": ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false> + "
                                        "k_ns_reduce (the loss) + k_ns_row_owner<4, false>" if model == "transe" else
                                        "mmre_ns_forward_backward = k_ns_forward + k_ns_reduce + k_ns_gen_slots + "

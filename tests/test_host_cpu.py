@@ -304,3 +304,31 @@ def test_import_prob_is_the_reference(golden):
         assert np.array_equal(out.ravel(), g[f"{name}_prob"]), name
     with pytest.raises(Exception):
         call("mmre_import_prob", b"/nonexistent/kl_prob.txt", n_rel, 1.0, out.ctypes.data_as(ctypes.c_void_p))
+
+
+def test_bench_quotes_pmc_traffic_only_for_this_build(tmp_path, monkeypatch):
+    """bench.py reads roofline.traffic from profiles/pmc_<config>.json only when the summary's
+    __build__.lib_sha256 is the loaded library's; any other build's counters give None and a reason."""
+    import json as _json
+    import bench
+    from mmre._lib import lib_identity
+    mine = lib_identity()["sha256"]
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    k = bench.KERNEL_NAMES["transe"]
+    for sha, want in ((mine, (2 * 100.0 + 50.0) * 1024.0), ("0123456789abcdef", None)):
+        (prof / "pmc_c2.json").write_text(_json.dumps({
+            "__build__": {"lib_sha256": sha},
+            f"void mmre::{k}(float const*)": {"FETCH_SIZE": 100.0, "WRITE_SIZE": 50.0}}))
+        got, src = bench.pmc_traffic("c2", "transe")
+        assert got == want, (sha, got, src)
+        if want is None:
+            assert "not this build" in src
+    (prof / "pmc_ns.json").write_text(_json.dumps({
+        "__build__": {"lib_sha256": mine},
+        "mmre::k_ns_prepass(x)": {"FETCH_SIZE": 1.0, "WRITE_SIZE": 1.0},
+        "void mmre::k_ns_transe_fused<4, false>(x)": {"FETCH_SIZE": 2.0, "WRITE_SIZE": 1.0}}))
+    tot, src, per = bench.pmc_step_traffic("ns", ["k_ns_prepass(", "k_ns_transe_fused<4, false>"])
+    assert tot == (3.0 + 5.0) * 1024.0 and len(per) == 2
+    assert bench.pmc_step_traffic("ns", ["k_ns_row_owner"])[0] is None
