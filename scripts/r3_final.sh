@@ -3,7 +3,7 @@
 #   A: full -m gpu suite + smoke + C2 bench line + C2 kernel trace
 #   B: C1 / C3 / C4 / C5 bench lines (cpu_baseline + reference parity legs) + kernel traces
 #   C: NS bench lines (TransE k 25 / k 10 with the reference CPU leg; DistMult / ComplEx / RotatE) + traces
-#   D1 / D2: PMC passes (scripts/pmc.sh) of c2 c4 ns / c3 c5
+#   D1 / D2: PMC passes (scripts/pmc.sh) of c2 c4 ns / c3 c5; E: C1 PMC + C2 bench again; F: C1 bench again
 # usage: scripts/r3_final.sh <A|B|C|D1|D2>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,5 +42,12 @@ case $1 in
     ;;
   D2)
     for c in c3 c5; do bash scripts/pmc.sh final_$c --config $c || exit $?; done
+    ;;
+  E)  # C1's PMC passes, then the C2 bench line again (its PMC summary installed in profiles/ by now)
+    bash scripts/pmc.sh final_c1 --config c1 || exit $?
+    timeout -k 10 300 python bench.py > $o/bench_c2.json 2> $o/bench_c2.err || exit $?
+    ;;
+  F)  # the C1 bench line with its PMC summary installed
+    timeout -k 10 300 python bench.py --config c1 > $o/bench_c1.json 2> $o/bench_c1.err || exit $?
     ;;
 esac
