@@ -437,7 +437,24 @@ def bench_ns(args, world, rank, dev, dist):
                  batch_r=torch.empty(n_rows, dtype=torch.int64, device=dev),
                  batch_y=torch.empty(n_rows, dtype=torch.float32, device=dev)) for _ in range(2)]
 
+    tstep = None
+    if model == "transe" and not args.ns_autograd:
+        # the whole step as ONE C-ABI call (mmre_ns_step_openke: sampler + pre-pass in one launch,
+        # the fused loss kernel, the row owner with SGD and the loss reduction), bit-identical to the
+        # drop-in path below (tests/test_ns_full_gpu.py::test_train_step_equals_the_autograd_path)
+        from mmre.ns import OpenKETrainStep
+        tstep = OpenKETrainStep(smp, spec, ent, rel, B, k, margin, 1.0)
+
     def step(i, ev=None):
+        if tstep is not None:
+            if ev:
+                for e in ev[:4]:
+                    e.record()
+            loss = tstep()
+            if ev:
+                for e in ev[4:]:
+                    e.record()
+            return loss
         b = smp.sample(B, k, out=bufs[i & 1])
         opt.zero_grad(set_to_none=True)
         if ev:
@@ -477,20 +494,25 @@ def bench_ns(args, world, rank, dev, dist):
             opt.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                if (not args.ns_prefetch):
-                    g_b = smp.sample(B, k, out=bufs[0])
+                if tstep is not None:  # the one-call step (no prefetch variant)
+                    g_loss, g_b = tstep(), None
                 else:
-                    g_b = bufs[par]
-                    fork.wait_stream(torch.cuda.current_stream(dev))
-                    with torch.cuda.stream(fork):
-                        smp.sample(B, k, out=bufs[1 - par])
-                g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k,
-                                          margin, optimizer=opt, ent_im=ent_im, rel_im=rel_im)
-                torch.autograd.backward(g_loss, grad_tensors=one)
-                opt.step()
-                if not (not args.ns_prefetch):
-                    torch.cuda.current_stream(dev).wait_stream(fork)
+                    if (not args.ns_prefetch):
+                        g_b = smp.sample(B, k, out=bufs[0])
+                    else:
+                        g_b = bufs[par]
+                        fork.wait_stream(torch.cuda.current_stream(dev))
+                        with torch.cuda.stream(fork):
+                            smp.sample(B, k, out=bufs[1 - par])
+                    g_loss, _ = fused_ns_loss(spec, ent, rel, g_b["batch_h"], g_b["batch_t"], g_b["batch_r"], B, k,
+                                              margin, optimizer=opt, ent_im=ent_im, rel_im=rel_im)
+                    torch.autograd.backward(g_loss, grad_tensors=one)
+                    opt.step()
+                    if not (not args.ns_prefetch):
+                        torch.cuda.current_stream(dev).wait_stream(fork)
             graphs.append(g)
+            if tstep is not None:
+                break
         graph = graphs[0]
         if not (not args.ns_prefetch):
             smp.sample(B, k, out=bufs[0])  # the first batch; every replay then prefetches the next
@@ -591,6 +613,9 @@ def bench_ns(args, world, rank, dev, dist):
                           f"{model} d=200 training step at the C2 training shape (margin loss)", "model": model,
                           "batch": B, "neg_ent": k, "rows_per_step": n_rows,
                           "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}",
+                          "step": ("mmre_ns_step_openke (sampler + pre-pass, fused loss, row owner + SGD + loss "
+                                   "reduction: 3 launches)" if tstep is not None else
+                                   "sampler.sample + fused_ns_loss + backward + SGD.step (drop-in path)"),
                           "launch": ("eager" if not graph else "hipGraph replay of the whole step" +
                                      ("" if (not args.ns_prefetch) else ", next batch sampled on a forked stream (prefetch)"))},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -611,9 +636,9 @@ def bench_ns(args, world, rank, dev, dist):
                             "step_forward_ms": fwd_ms, "step_backward_ms": bwd_ms,
                             "note": "no float atomics: the gradient contributions are bucketed by table row and "
                                     "one wave per table row summing them in batch order (bit-reproducible); the "
-                                    "step is five launches: the sampler (seed advance folded in), the pre-pass, the "
-                                    "fused kernel, the loss reduction, the row-owner pass with the SGD step fused in "
-                                    "(mmre_ns_fused_grad_sgd, bit-identical to backward() + step())"},
+                                    "TransE step is three launches (mmre_ns_step_openke): the sampler's workgroups beside the "
+                                    "pre-pass, the fused loss kernel, the row-owner pass with the SGD step and the loss "
+                                    "reduction folded in -- bit-identical to the drop-in path's five (--ns-autograd)"},
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline and model == "transe":
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)
@@ -1024,6 +1049,9 @@ def main():
                     help="HIP training steps that give the TransE configs non-degenerate tables (0: init tables)")
     ap.add_argument("--ns-neg", type=int, default=25, help="--config ns: negatives per positive (25 or 10)")
     ap.add_argument("--ns-eager", action="store_true", help="--config ns: launch each step eagerly (no hipGraph)")
+    ap.add_argument("--ns-autograd", action="store_true",
+                    help="--config ns (TransE): the drop-in path (sampler.sample + fused_ns_loss + backward + "
+                         "SGD.step) instead of the one-call training step mmre_ns_step_openke")
     ap.add_argument("--ns-model", default="transe", choices=["transe", "distmult", "complex", "rotate"],
                     help="--config ns: the scored model (default transe, the C2 training step)")
     ap.add_argument("--ns-prefetch", action="store_true",

@@ -340,6 +340,25 @@ int mmre_ns_forward_backward(int model, int norm_flag, float model_margin, int u
                              float regul_rate, float* d_score, float* d_loss, float* d_grad_ent, float* d_grad_ent_im,
                              float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
 
+/* One OpenKE training step for TransE (Trainer.train_one_step, Trainer.py:43-54: Base.cpp:161-197's
+ * sampling + strategy/NegativeSampling + MarginLoss forward/backward + optim.SGD): the sampler
+ * arguments of mmre_sampler_openke_step (neg_rel_rate 0; d_ticket required; the batch lands in
+ * d_batch_*), then the loss arguments of mmre_ns_fused_forward / mmre_ns_fused_grad_sgd (upstream
+ * gradient 1; d_ent / d_rel updated in place by fma(-lr, g, p)). Values bit-identical to those
+ * three calls in sequence; three launches instead of five (the sampler and the pre-pass share one
+ * grid, the loss reduction rides in the gradient's). d_work: mmre_ns_fused_workspace. Only the
+ * fused TransE shapes (dim <= 512, neg <= 32): MMRE_ERR_SHAPE otherwise. */
+int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                        const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                        const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                        const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                        const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode,
+                        const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
+                        int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, int model, int norm_flag,
+                        float* d_ent, float* d_rel, int64_t n_ent, int64_t n_rel, int dim, int64_t batch, int64_t neg,
+                        float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
+                        float* d_grad_ent, float* d_grad_rel, float* d_work, float lr, void* stream);
+
 /* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
  * batch = n_rows, neg = 0, d_loss = NULL. Its backward: accumulate
  * d_grad_score[i] * d(score_i)/d(tables) into the dense gradient tables. */

@@ -15,6 +15,7 @@
 // recomputes each row's intermediates and scatters d(loss)/d(row) into the dense
 // gradient tables with float atomics.
 #include "mmre_common.h"
+#include "sampler_openke.h"
 
 namespace mmre {
 
@@ -849,14 +850,15 @@ __device__ __forceinline__ void load_slot(Vec<NC>& v, const float* __restrict__ 
 // divides nothing), and the row's slot count zeroed (and the overflow count).
 // (A last-workgroup loss reduction inside the fused kernel was tried instead of k_ns_reduce:
 // its per-workgroup device-scope fence writes back the XCD's L2 each time, 0.12 -> 0.19 ms.)
-__global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
-                                                    const float* __restrict__ rel, int64_t n_rel, int d,
-                                                    float* __restrict__ nrm_e, float* __restrict__ nrm_r,
-                                                    float* __restrict__ ent_n, float* __restrict__ rel_n,
-                                                    int32_t* __restrict__ counts, int32_t* __restrict__ ovf_n) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) ovf_n[0] = 0;  // no overflow pairs yet
+__device__ __forceinline__ void ns_prepass_block(const float* __restrict__ ent, int64_t n_ent,
+                                                 const float* __restrict__ rel, int64_t n_rel, int d,
+                                                 float* __restrict__ nrm_e, float* __restrict__ nrm_r,
+                                                 float* __restrict__ ent_n, float* __restrict__ rel_n,
+                                                 int32_t* __restrict__ counts, int32_t* __restrict__ ovf_n,
+                                                 int64_t block) {
+  if (block == 0 && threadIdx.x == 0) ovf_n[0] = 0;  // no overflow pairs yet
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = block * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;
   if (lane == 0) counts[row] = 0;  // the row's slot bucket, for this call
   const bool is_ent = row < n_ent;
@@ -893,6 +895,32 @@ __global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ en
     const float cn = fmaxf(nr, 1e-12f);
     for (int i = lane; i < d; i += kWave) o[i] = p[i] / cn;
   }
+}
+
+__global__ __launch_bounds__(256) void k_ns_prepass(const float* __restrict__ ent, int64_t n_ent,
+                                                    const float* __restrict__ rel, int64_t n_rel, int d,
+                                                    float* __restrict__ nrm_e, float* __restrict__ nrm_r,
+                                                    float* __restrict__ ent_n, float* __restrict__ rel_n,
+                                                    int32_t* __restrict__ counts, int32_t* __restrict__ ovf_n) {
+  ns_prepass_block(ent, n_ent, rel, n_rel, d, nrm_e, nrm_r, ent_n, rel_n, counts, ovf_n, blockIdx.x);
+}
+
+// First launch of the training step (mmre_ns_step_openke): the sampler's workgroups
+// [0, n_sampler) and the pre-pass's after them, in ONE grid -- the two are independent (the
+// pre-pass reads only the tables), so the pre-pass runs on the CUs the latency-bound sampler
+// leaves idle instead of after it. The sampler's seed ticket counts its own workgroups only.
+__global__ __launch_bounds__(256) void k_ns_step_prep(OpenKESamplerArgs sa, int64_t n_sampler,
+                                                      const float* __restrict__ ent, int64_t n_ent,
+                                                      const float* __restrict__ rel, int64_t n_rel, int d,
+                                                      float* __restrict__ nrm_e, float* __restrict__ nrm_r,
+                                                      float* __restrict__ ent_n, float* __restrict__ rel_n,
+                                                      int32_t* __restrict__ counts, int32_t* __restrict__ ovf_n) {
+  if ((int64_t)blockIdx.x < n_sampler) {
+    sampler_openke_block(sa, blockIdx.x, n_sampler);
+    return;
+  }
+  ns_prepass_block(ent, n_ent, rel, n_rel, d, nrm_e, nrm_r, ent_n, rel_n, counts, ovf_n,
+                   (int64_t)blockIdx.x - n_sampler);
 }
 
 // lane src's 64-bit value as a wave-uniform (scalar) value; src must be wave-uniform
@@ -1366,8 +1394,13 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
                                                       const int32_t* __restrict__ ovf_n, int64_t K,
                                                       const float* __restrict__ grad_loss, float* __restrict__ gent,
                                                       float* __restrict__ grel, float sgd_lr, float* __restrict__ pent,
-                                                      float* __restrict__ prel) {
+                                                      float* __restrict__ prel, NSArgs RA, const float* __restrict__ part,
+                                                      float* __restrict__ loss, int64_t reduce_block) {
   __shared__ int64_t s_hub[4][NS_HUB];
+  if ((int64_t)blockIdx.x == reduce_block) {  // the training step's loss (mmre_ns_step_openke): one extra workgroup
+    ns_reduce_block(RA, part, loss);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
@@ -2186,7 +2219,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
                            const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
                            float regul_rate, const float* d_score, const float* d_grad_loss, float* d_grad_ent,
                            float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work, float lr,
-                           float* pe, float* pei, float* pr, float* pri, void* stream) {
+                           float* pe, float* pei, float* pr, float* pri, void* stream, float* d_loss_out = nullptr) {
   NSArgs A;
   int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                    phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
@@ -2233,10 +2266,14 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     return MMRE_OK;
   }
   const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
+  // the training step (d_loss_out): one more workgroup reduces the forward's loss partials
+  const int64_t reduce_block = d_loss_out ? (int64_t)ogrid.x : -1;
+  const dim3 ogrid2((unsigned)(ogrid.x + (d_loss_out ? 1 : 0)));
 #define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
-  hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
+  hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid2, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
                      d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n,         \
-                     neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr)
+                     neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr, A, d_work + w.part, d_loss_out,           \
+                     reduce_block)
   const int nc = transe_fast_nc(A);
   const bool l2 = model == MMRE_TRANSE_L2;
   if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }
@@ -2292,4 +2329,77 @@ extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_ma
                             n_rel, dim, phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature,
                             regul_rate, d_score, nullptr, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work,
                             stream);
+}
+
+// One OpenKE training step (Trainer.train_one_step, Trainer.py:43-54, over Base.cpp's sampling)
+// for TransE with the fused path's shapes: sample the batch, margin loss + gradients, plain SGD.
+// Three launches: the sampler's workgroups beside the pre-pass (k_ns_step_prep), the fused loss
+// kernel, the row owner (gradient + SGD) with the loss reduction as one extra workgroup. Same
+// values as mmre_sampler_openke_step + mmre_ns_fused_forward + mmre_ns_fused_grad_sgd (upstream
+// gradient 1), bit for bit: the same device functions in the same order, only regrouped into
+// fewer launches (tests/test_ns_full_gpu.py holds them equal over several steps).
+extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                   const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode,
+                                   const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
+                                   int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, int model, int norm_flag,
+                                   float* d_ent, float* d_rel, int64_t n_ent, int64_t n_rel, int dim, int64_t batch,
+                                   int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
+                                   float* d_score, float* d_loss, float* d_grad_ent, float* d_grad_rel,
+                                   float* d_work, float lr, void* stream) {
+  if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
+      !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y || !d_ticket)
+    return MMRE_ERR_ARG;
+  if ((d_left_mean == nullptr) != (d_right_mean == nullptr)) return MMRE_ERR_ARG;
+  if (train_total <= 0 || n_ent <= 1 || work_threads <= 0 || batch <= 0 || neg <= 0 || mode < -1 || mode > 1)
+    return MMRE_ERR_ARG;
+  if (n_blocks < 0 || (n_blocks > 0 && !d_blocks)) return MMRE_ERR_ARG;
+  if (!d_score || !d_loss || !d_grad_ent || !d_grad_rel || !d_work || n_rel <= 0 || !(lr != 0.0f))
+    return MMRE_ERR_ARG;
+  NSArgs A;
+  int rc = ns_args(A, model, norm_flag, 0.0f, 0, d_ent, nullptr, d_rel, nullptr, dim, 0.0f, d_batch_h, d_batch_t,
+                   d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate);
+  if (rc) return rc;
+  if (!is_transe(model) || !fused_fast(A)) return MMRE_ERR_SHAPE;  // the fused TransE path's shapes only
+  hipStream_t st = (hipStream_t)stream;
+  FusedWs w;
+  fused_ws(model, norm_flag, batch, neg, n_ent, n_rel, dim, w);
+  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
+  float* nrm_e = d_work + w.nrm_e;
+  float* nrm_r = d_work + w.nrm_r;
+  float* ent_n = norm_flag ? d_work + w.ent_n : nullptr;
+  float* rel_n = norm_flag ? d_work + w.rel_n : nullptr;
+  // 1. sampler workgroups + pre-pass workgroups
+  const int64_t rows = batch * (1 + neg);
+  const int64_t n_sampler = (rows + 255) / 256;
+  const OpenKESamplerArgs sa{d_train_list, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head, d_lef_tail,
+                             d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, train_total, n_ent, n_rel,
+                             d_seeds, work_threads, batch, neg, 0, mode, d_blocks, n_blocks, d_batch_h, d_batch_t,
+                             d_batch_r, d_batch_y, d_ticket, mmre_sampler_draws_per_positive(neg, 0, mode), nullptr};
+  hipLaunchKernelGGL(k_ns_step_prep, dim3((unsigned)(n_sampler + (n_ent + n_rel + 3) / 4)), dim3(256), 0, st, sa,
+                     n_sampler, d_ent, n_ent, d_rel, n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, S.counts, S.ovf_n);
+  MMRE_CHECK_LAUNCH();
+  // 2. the fused loss kernel (scores, loss partials, slots)
+  const float* ent_u = norm_flag ? ent_n : d_ent;
+  const float* rel_u = norm_flag ? rel_n : d_rel;
+  const bool l2 = model == MMRE_TRANSE_L2;
+  const int nc = transe_fast_nc(A);
+  float* part = d_work + w.part;
+  const dim3 grid((unsigned)batch), blk(256);
+#define MMRE_NS_FUSED(NC_, L2_)                                                                                    \
+  hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, n_ent,   \
+                     ent_u, rel_u)
+  if (nc == 1) { if (l2) MMRE_NS_FUSED(1, true); else MMRE_NS_FUSED(1, false); }
+  else if (nc == 2) { if (l2) MMRE_NS_FUSED(2, true); else MMRE_NS_FUSED(2, false); }
+  else if (nc == 4) { if (l2) MMRE_NS_FUSED(4, true); else MMRE_NS_FUSED(4, false); }
+  else { if (l2) MMRE_NS_FUSED(8, true); else MMRE_NS_FUSED(8, false); }
+#undef MMRE_NS_FUSED
+  MMRE_CHECK_LAUNCH();
+  // 3. gradient + SGD, and the loss
+  return fused_grad_impl(model, norm_flag, 0.0f, 0, d_ent, nullptr, d_rel, nullptr, n_ent, n_rel, dim, 0.0f,
+                         d_batch_h, d_batch_t, d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
+                         nullptr, d_grad_ent, nullptr, d_grad_rel, nullptr, d_work, lr, d_ent, nullptr, d_rel, nullptr,
+                         stream, d_loss);
 }

@@ -16,77 +16,9 @@
 //    so parity is distributional; this kernel uses a counter-based generator (SplitMix64) so
 //    a given seed is reproducible.
 #include "mmre_common.h"
+#include "sampler_openke.h"
 
 namespace mmre {
-
-__device__ __forceinline__ uint64_t lcg_next(uint64_t* st) {
-  *st = *st * 25214903917ULL + 11ULL;
-  return *st;
-}
-__device__ __forceinline__ int64_t rand_max(uint64_t* st, int64_t x) {
-  return (int64_t)(lcg_next(st) % (uint64_t)x);
-}
-__device__ uint64_t lcg_jump(uint64_t x, uint64_t n) {
-  uint64_t A = 1, C = 0, a = 25214903917ULL, c = 11ULL;
-  while (n) {
-    if (n & 1) { A = A * a; C = C * a + c; }
-    c = c * a + c;
-    a = a * a;
-    n >>= 1;
-  }
-  return A * x + C;
-}
-
-// The block [ll, rr] of rows whose column `kc` equals `key` inside the sorted range
-// [lef0, rig0] (Corrupt.h's two binary searches, same midpoints and results) -- the lower and
-// upper searches advance together, so their dependent loads are issued in pairs and the chain
-// is as long as one search.
-__device__ __forceinline__ void key_block(const int64_t* __restrict__ T, int kc, int64_t lef0, int64_t rig0,
-                                          int64_t key, int64_t& ll, int64_t& rr) {
-  int64_t al = lef0 - 1, ar = rig0, bl = lef0, br = rig0 + 1;
-  while (al + 1 < ar || bl + 1 < br) {
-    const bool ga = al + 1 < ar, gb = bl + 1 < br;
-    const int64_t ma = (al + ar) >> 1, mb = (bl + br) >> 1;
-    const int64_t va = ga ? T[3 * ma + kc] : 0, vb = gb ? T[3 * mb + kc] : 0;
-    if (ga) { if (va >= key) ar = ma; else al = ma; }
-    if (gb) { if (vb <= key) bl = mb; else br = mb; }
-  }
-  ll = ar;
-  rr = bl;
-}
-
-// The draw and the final skip of Corrupt.h's corruption, given the block [ll, rr] of rows of T
-// sharing the kept (entity, relation) and its first / last value `tll` / `trr` in column col:
-// a uniform id among the n - (rr - ll + 1) ids not in the block.
-__device__ int64_t corrupt_in_block(const int64_t* __restrict__ T, int col, int64_t n, uint64_t* st, int64_t ll,
-                                    int64_t rr, int64_t tll, int64_t trr) {
-  const int64_t tmp = rand_max(st, n - (rr - ll + 1));
-  if (tmp < tll) return tmp;
-  if (tmp > trr - rr + ll - 1) return tmp + rr - ll + 1;
-  int64_t lef = ll, rig = rr + 1, mid;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + col] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
-  return tmp + lef - ll + 1;
-}
-
-// corrupt_head (Corrupt.h:7-43): uniform entity not among the known TAILS of (h, r),
-// found by skipping the sorted tails of the (h, r) block of trainHead.
-__device__ int64_t corrupt_head(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_head,
-                                const int64_t* __restrict__ rig_head, int64_t n_ent, uint64_t* st, int64_t h,
-                                int64_t r) {
-  int64_t ll, rr;
-  key_block(T, 1, lef_head[h], rig_head[h], r, ll, rr);
-  return corrupt_in_block(T, 2, n_ent, st, ll, rr, T[3 * ll + 2], T[3 * rr + 2]);
-}
-
-// corrupt_tail (Corrupt.h:45-81): uniform entity not among the known HEADS of (t, r);
-// T rows are (h, r, t) sorted by (t, r, h).
-__device__ int64_t corrupt_tail(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_tail,
-                                const int64_t* __restrict__ rig_tail, int64_t n_ent, uint64_t* st, int64_t t,
-                                int64_t r) {
-  int64_t ll, rr;
-  key_block(T, 1, lef_tail[t], rig_tail[t], r, ll, rr);
-  return corrupt_in_block(T, 0, n_ent, st, ll, rr, T[3 * ll + 0], T[3 * rr + 0]);
-}
 
 // Per train row i (h, r, t): the (h, r) block of head_hrt with its first / last tail and the
 // (t, r) block of tail_hrt with its first / last head -- what corrupt_head / corrupt_tail find
@@ -110,176 +42,9 @@ __global__ __launch_bounds__(256) void k_sampler_blocks(const int64_t* __restric
   o[1] = make_int4((int)tl, (int)tr, (int)tail_hrt[3 * tl + 0], (int)tail_hrt[3 * tr + 0]);
 }
 
-// corrupt_rel with p == true (Corrupt.h:111-147): the draw among the relations not in the (h, t)
-// block, weighted by r's row of importProb's table P (Reader.h:26-49; n_rel - 1 columns, r's own
-// left out: column c is relation c below r, c + 1 from r on). The reference builds, per draw, the
-// cumulative list of P[c] / sum over the unmarked columns (sum = 1 - the marked columns' mass,
-// subtracted in block order) and binary-searches it for m = rand_max(10000) / 10000. Here the
-// list is never stored: each probe of the same binary search recomputes its prefix in the same
-// order (the block's columns are ascending, so one merge walk marks them), which yields the
-// same float values, hence the same index (the compacted index; corrupt_rel maps it to an id).
-__device__ float rel_prob_prefix(const int64_t* __restrict__ T, const float* __restrict__ P, int64_t n_rel,
-                                 int64_t r, int64_t ll, int64_t rr, float sum, int64_t upto) {
-  float rec = 0.0f;
-  int64_t q = ll, c = 0;
-  for (int64_t i = 0; i < n_rel - 1; ++i) {
-    int64_t col = -1;  // the next marked column at or after i
-    while (q <= rr) {
-      const int64_t rel = T[3 * q + 1];
-      col = rel > r ? rel - 1 : (rel < r ? rel : -1);
-      if (col >= i) break;
-      ++q;
-      col = -1;
-    }
-    if (col == i) continue;  // in the (h, t) block
-    rec += P[i] / sum;
-    if (c == upto) return rec;
-    ++c;
-  }
-  return rec;
-}
-
-__device__ int64_t rel_prob_draw(const int64_t* __restrict__ T, const float* __restrict__ prob, int64_t n_rel,
-                                 uint64_t* st, int64_t r, int64_t ll, int64_t rr) {
-  const float* P = prob + r * (n_rel - 1);
-  float sum = 1.0f;
-  int64_t marked = 0;
-  for (int64_t i = ll; i <= rr; ++i) {
-    const int64_t rel = T[3 * i + 1];
-    if (rel > r) { sum -= P[rel - 1]; ++marked; }
-    else if (rel < r) { sum -= P[rel]; ++marked; }
-  }
-  const int64_t cnt = (n_rel - 1) - marked;
-  const float m = (float)((double)rand_max(st, 10000) / 10000.0);
-  int64_t lef = 0, rig = cnt - 1;
-  while (lef < rig) {
-    const int64_t mid = (lef + rig) >> 1;
-    if (rel_prob_prefix(T, P, n_rel, r, ll, rr, sum, mid) < m) lef = mid + 1;
-    else rig = mid;
-  }
-  return rig;
-}
-
-// corrupt_rel (Corrupt.h:85-162); T rows (h, r, t) sorted by (h, t, r). prob NULL: p == false,
-// a uniform draw; else importProb's table (p == true).
-__device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64_t* __restrict__ lef_rel,
-                               const int64_t* __restrict__ rig_rel, int64_t n_rel, uint64_t* st, int64_t h, int64_t t,
-                               int64_t r, const float* __restrict__ prob) {
-  int64_t lef, rig, mid, ll, rr;
-  key_block(T, 2, lef_rel[h], rig_rel[h], t, ll, rr);
-  const int64_t tmp = prob ? rel_prob_draw(T, prob, n_rel, st, r, ll, rr) : rand_max(st, n_rel - (rr - ll + 1));
-  if (tmp < T[3 * ll + 1]) return tmp;
-  if (tmp > T[3 * rr + 1] - rr + ll - 1) return tmp + rr - ll + 1;
-  lef = ll; rig = rr + 1;
-  while (lef + 1 < rig) { mid = (lef + rig) >> 1; if (T[3 * mid + 1] - mid + ll - 1 < tmp) lef = mid; else rig = mid; }
-  return tmp + lef - ll + 1;
-}
-
-// One GPU thread per output ROW (positive or negative): the state before any draw is the
-// pthread's seed advanced by an affine jump, so the rows of one positive -- a chain of up to
-// 1 + 2 neg dependent draws and binary searches in the reference -- are produced in parallel
-// (B (1 + neg + neg_rel) threads instead of B).
-__device__ __forceinline__ void sampler_openke_row(int64_t row, 
-    const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
-    const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
-    const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
-    const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
-    const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* __restrict__ seeds,
-    int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk,
-    int64_t n_blk, int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br,
-    float* __restrict__ by, const float* __restrict__ rel_prob) {
-  const int64_t b = row % B, j = row / B;  // j = 0: the positive; 1..neg: entity negatives; then relation ones
-  // slice of the reference's pthread `id` that owns position b (Base.cpp:93-100)
-  const int64_t per = B % work_threads == 0 ? B / work_threads : B / work_threads + 1;
-  const int64_t id = b / per, lef = id * per;
-  const int64_t per_neg = mode == 0 ? 2 : 1;  // draws per entity negative: [prob draw,] corrupt draw
-  const int64_t draws = 1 + per_neg * neg + neg_rel;
-  const uint64_t base = (uint64_t)((b - lef) * draws);
-  uint64_t st = lcg_jump(seeds[id], base);
-  const int64_t i = rand_max(&st, train_total);  // Base.cpp:104
-  const int64_t h = train_list[3 * i], r = train_list[3 * i + 1], t = train_list[3 * i + 2];
-  if (j == 0) {
-    bh[row] = h; bt[row] = t; br[row] = r; by[row] = 1.0f;
-    return;
-  }
-  if (j <= neg) {
-    const int64_t k = j - 1;
-    st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * k));
-    bool replace_tail;
-    if (mode == 0) {
-      float prob = 500.0f;
-      if (left_mean) prob = 1000.0f * right_mean[r] / (right_mean[r] + left_mean[r]);
-      replace_tail = (float)(lcg_next(&st) % 1000ULL) < prob;
-    } else {
-      replace_tail = mode != -1;
-    }
-    // the kept (entity, relation)'s block: from the per-train-row table when there is one
-    const bool pre = i < n_blk;
-    int4 kb = make_int4(0, 0, 0, 0);
-    if (pre) kb = reinterpret_cast<const int4*>(blk + 8 * i)[replace_tail ? 0 : 1];
-    if (replace_tail) {  // corrupt_head returns a replacement TAIL (Base.cpp:116)
-      bh[row] = h; br[row] = r;
-      bt[row] = pre ? corrupt_in_block(head_hrt, 2, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
-                    : corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r);
-    } else {
-      bt[row] = t; br[row] = r;
-      bh[row] = pre ? corrupt_in_block(tail_hrt, 0, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
-                    : corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r);
-    }
-  } else {
-    const int64_t k = j - 1 - neg;
-    st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * neg + k));
-    bh[row] = h; bt[row] = t; br[row] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r, rel_prob);
-  }
-  by[row] = -1.0f;
-}
-
-
-// The per-pthread LCG states after one sampling call (mmre_sampler_advance's arithmetic):
-// thread id's state jumps by (its positives) x (draws per positive), its positives being
-// Base.cpp:161-197's [lef, rig) split of the batch.
-__device__ __forceinline__ uint64_t advanced_seed(uint64_t seed, int64_t id, int64_t work_threads,
-                                                  int64_t batch_size, int64_t per) {
-  int64_t lef, rig;
-  if (batch_size % work_threads == 0) {
-    lef = id * (batch_size / work_threads);
-    rig = (id + 1) * (batch_size / work_threads);
-  } else {
-    lef = id * (batch_size / work_threads + 1);
-    rig = (id + 1) * (batch_size / work_threads + 1);
-    if (rig > batch_size) rig = batch_size;
-  }
-  const int64_t cnt = rig > lef ? rig - lef : 0;
-  return lcg_jump(seed, (uint64_t)(cnt * per));
-}
-
-// One thread per output row. With `ticket` (mmre_sampler_openke_step) the call also advances
-// the seeds for the next call: every workgroup takes a ticket once all its threads have read
-// the seeds; the last one writes the advanced states and resets the ticket -- no separate
-// advance launch behind every batch.
-__global__ __launch_bounds__(256) void k_sampler_openke(
-    const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
-    const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
-    const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
-    const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
-    const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, uint64_t* seeds, int64_t work_threads,
-    int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk, int64_t n_blk,
-    int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br, float* __restrict__ by,
-    int32_t* ticket, int64_t adv_per, const float* __restrict__ rel_prob) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row < B * (1 + neg + neg_rel))
-    sampler_openke_row(row, train_list, train_total, head_hrt, tail_hrt, rel_hrt, lef_head, rig_head, lef_tail,
-                       rig_tail, lef_rel, rig_rel, left_mean, right_mean, n_ent, n_rel, seeds, work_threads, B, neg,
-                       neg_rel, mode, blk, n_blk, bh, bt, br, by, rel_prob);
-  if (ticket == nullptr) return;  // uniform
-  __syncthreads();  // every thread of the workgroup has read (and used) its seed
-  __shared__ int s_last;
-  if (threadIdx.x == 0) s_last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  for (int64_t id = threadIdx.x; id < work_threads; id += blockDim.x)
-    seeds[id] = advanced_seed(seeds[id], id, work_threads, B, adv_per);
-  if (threadIdx.x == 0) *ticket = 0;
+// One sampling() call: sampler_openke_block over the grid.
+__global__ __launch_bounds__(256) void k_sampler_openke(OpenKESamplerArgs a) {
+  sampler_openke_block(a, blockIdx.x, gridDim.x);
 }
 
 // ---------------------------------------------------------------- repo sampler --
@@ -390,12 +155,12 @@ static int sampler_impl(const int64_t* d_train_list, int64_t train_total, const 
   hipStream_t st = (hipStream_t)stream;
   const int threads = 256;
   const int64_t rows = batch_size * (1 + neg_rate + neg_rel_rate);
-  hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((rows + threads - 1) / threads)), dim3(threads), 0, st,
-                     d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head,
-                     d_lef_tail, d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, n_ent, n_rel,
-                     const_cast<uint64_t*>(d_seeds), work_threads, batch_size, neg_rate, neg_rel_rate, mode, d_blocks,
-                     n_blocks, d_batch_h, d_batch_t, d_batch_r, d_batch_y, d_ticket,
-                     mmre_sampler_draws_per_positive(neg_rate, neg_rel_rate, mode), d_rel_prob);
+  const OpenKESamplerArgs a{d_train_list, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head, d_lef_tail,
+                            d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, train_total, n_ent, n_rel,
+                            const_cast<uint64_t*>(d_seeds), work_threads, batch_size, neg_rate, neg_rel_rate, mode,
+                            d_blocks, n_blocks, d_batch_h, d_batch_t, d_batch_r, d_batch_y, d_ticket,
+                            mmre_sampler_draws_per_positive(neg_rate, neg_rel_rate, mode), d_rel_prob};
+  hipLaunchKernelGGL(k_sampler_openke, dim3((unsigned)((rows + threads - 1) / threads)), dim3(threads), 0, st, a);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
 }

@@ -191,3 +191,44 @@ def score_rows(spec: NSSpec, ent, rel, h, t, r, ent_im=None, rel_im=None):
     h, t, r = (x.to(torch.int64).contiguous() for x in (h, t, r))
     c = lambda x: None if x is None else x.contiguous()
     return _ScoreRows.apply(c(ent), c(rel), c(ent_im), c(rel_im), h, t, r, spec)
+
+
+class OpenKETrainStep:
+    """One OpenKE training step for TransE -- Trainer.train_one_step (Trainer.py:43-54) over the
+    loader's Base.cpp sampling, strategy/NegativeSampling + MarginLoss, optim.SGD -- as ONE C-ABI
+    call (mmre_ns_step_openke, three launches): the values of sampler.sample(B, neg, 0, mode) +
+    fused_ns_loss(...).backward() + SGD.step(), bit for bit (tests/test_ns_full_gpu.py). The
+    parameters are updated in place; ent.grad / rel.grad hold the step's gradient tables, `batch`
+    the sampled batch, `score` the row scores. Calling it returns the loss tensor (device)."""
+
+    def __init__(self, sampler, spec: NSSpec, ent, rel, batch: int, neg: int, loss_margin: float, lr: float,
+                 adv_temperature: float | None = None, regul_rate: float = 0.0, mode: int = 0):
+        if spec.model not in ("transe", "transe_l2") or spec.use_model_margin:
+            raise ValueError("OpenKETrainStep: TransE without a model margin (the fused path)")
+        require_cuda(ent, rel)
+        dev = ent.device
+        self.sampler, self.spec, self.ent, self.rel = sampler, spec, ent, rel
+        self.B, self.K, self.mode = int(batch), int(neg), int(mode)
+        self.margin, self.lr = float(loss_margin), float(lr)
+        self.adv, self.regul = float(adv_temperature or 0.0), float(regul_rate)
+        E, R = int(ent.shape[0]), int(rel.shape[0])
+        n = self.B * (1 + self.K)
+        self.work = torch.empty(int(lib().mmre_ns_fused_workspace(spec.model_id, int(spec.norm_flag), self.B, self.K, E,
+                                                                  R, spec.dim)), dtype=torch.float32, device=dev)
+        self.score = torch.empty(n, dtype=torch.float32, device=dev)
+        self.loss = torch.empty(1, dtype=torch.float32, device=dev)
+        self.batch = dict(batch_h=torch.empty(n, dtype=torch.int64, device=dev),
+                          batch_t=torch.empty(n, dtype=torch.int64, device=dev),
+                          batch_r=torch.empty(n, dtype=torch.int64, device=dev),
+                          batch_y=torch.empty(n, dtype=torch.float32, device=dev))
+        self.ge, self.gr = torch.empty_like(ent), torch.empty_like(rel)  # the step's gradient tables
+
+    def __call__(self):
+        s = self.spec
+        E, R = int(self.ent.shape[0]), int(self.rel.shape[0])
+        call("mmre_ns_step_openke", *self.sampler.step_args(self.B, self.K, self.mode, self.batch), s.model_id,
+             int(s.norm_flag), ptr(self.ent), ptr(self.rel), E, R, s.dim, self.B, self.K, self.margin, self.adv,
+             self.regul, ptr(self.score), ptr(self.loss), ptr(self.ge), ptr(self.gr), ptr(self.work),
+             self.lr, stream_ptr(self.ent.device))
+        self.ent.grad, self.rel.grad = self.ge, self.gr  # as backward() leaves them
+        return self.loss[0]

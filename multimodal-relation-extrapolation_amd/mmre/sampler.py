@@ -105,6 +105,21 @@ class OpenKESampler:
         return out
 
 
+    def step_args(self, batch_size: int, neg_ent: int, mode: int, out):
+        """The sampler half of mmre_ns_step_openke's arguments (the step's launch samples the batch
+        into `out` and advances the device seeds); the host mirror advances here, as sample() does."""
+        d = self._d
+        args = (ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]), ptr(d["tail_hrt"]), ptr(d["rel_hrt"]),
+                ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]), ptr(d["rig_tail"]), ptr(d["lef_rel"]),
+                ptr(d["rig_rel"]), ptr(d["left_mean"]) if self.bern else None,
+                ptr(d["right_mean"]) if self.bern else None, ptr(self._seeds_dev), self.work_threads, int(mode),
+                ptr(self._blocks), self._n_blocks, ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]),
+                ptr(out["batch_y"]), ptr(self._ticket))
+        call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, int(batch_size),
+             int(neg_ent), 0, int(mode))
+        return args
+
+
 class RepoSampler:
     """module/NegativeSampling.py's filtered per-edge sampler on the GPU.
 

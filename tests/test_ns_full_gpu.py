@@ -313,3 +313,42 @@ def test_hub_rows_ordered_deterministically(c2_training, model, n_pos):
     for n in tabs:
         gw, gg = T64[n].grad.numpy(), grads[0][n].cpu().double().numpy()
         assert np.linalg.norm(gg - gw) <= 1e-4 * np.linalg.norm(gw), (n, np.linalg.norm(gg - gw), np.linalg.norm(gw))
+
+
+@pytest.mark.parametrize("regul,adv", [(0.0, None), (0.5, None), (0.0, 1.0)])
+def test_train_step_equals_the_autograd_path(c2_training, regul, adv):
+    """mmre_ns_step_openke (mmre.ns.OpenKETrainStep: sampler + pre-pass in one launch, the fused
+    loss kernel, the row owner with SGD and the loss reduction) against the drop-in path
+    (OpenKESampler.sample + fused_ns_loss + backward + mmre.optim.SGD.step) over four steps at the
+    C2 training shape: batches, losses, scores, gradients, parameters and LCG states bit-identical."""
+    from mmre.ns import NSSpec, OpenKETrainStep, fused_ns_loss
+    from mmre.optim import SGD
+    from mmre.sampler import OpenKESampler
+    w, idx = c2_training
+    B, k, margin, lr = 2721, 25, 5.0, 1.0
+    spec = NSSpec("transe", 200, norm_flag=True)
+    ea = w["ent"].to(DEV).clone().requires_grad_(True)
+    ra = w["rel"].to(DEV).clone().requires_grad_(True)
+    eb = w["ent"].to(DEV).clone().requires_grad_(True)
+    rb = w["rel"].to(DEV).clone().requires_grad_(True)
+    sa = OpenKESampler(idx, DEV, bern=True)
+    sb = OpenKESampler(idx, DEV, bern=True)
+    opt = SGD([ea, ra], lr=lr)
+    step = OpenKETrainStep(sb, spec, eb, rb, B, k, margin, lr, adv_temperature=adv, regul_rate=regul)
+    for i in range(4):
+        ba = sa.sample(B, k)
+        opt.zero_grad(set_to_none=True)
+        la, sc_a = fused_ns_loss(spec, ea, ra, ba["batch_h"], ba["batch_t"], ba["batch_r"], B, k, margin, adv, regul,
+                                 optimizer=opt)
+        la.backward()
+        opt.step()
+        lb = step()
+        torch.cuda.synchronize()
+        for key in ("batch_h", "batch_t", "batch_r", "batch_y"):
+            assert torch.equal(ba[key], step.batch[key]), (i, key)
+        assert torch.equal(la.detach().reshape(1), lb.reshape(1)), (i, float(la), float(lb))
+        assert torch.equal(sc_a, step.score), i
+        assert torch.equal(ea.grad, eb.grad) and torch.equal(ra.grad, rb.grad), i
+        assert torch.equal(ea.detach(), eb.detach()) and torch.equal(ra.detach(), rb.detach()), i
+    assert np.array_equal(sa.seeds, sb.seeds)
+    assert torch.equal(sa._seeds_dev, sb._seeds_dev)
