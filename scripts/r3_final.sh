@@ -38,7 +38,7 @@ case $1 in
     done
     ;;
   D1)
-    for c in c2 c4 ns; do bash scripts/pmc.sh final_$c --config $c || exit $?; done
+    for c in c1 c2 c4 ns; do bash scripts/pmc.sh final_$c --config $c || exit $?; done
     ;;
   D2)
     for c in c3 c5; do bash scripts/pmc.sh final_$c --config $c || exit $?; done
