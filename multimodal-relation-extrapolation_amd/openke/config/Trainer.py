@@ -1,6 +1,8 @@
 """Trainer (OpenKE/openke/config/Trainer.py:16-134): same constructor, setters and run() loop.
 Batches arrive from the GPU sampler already on the device; the strategy's forward/backward is
-the fused HIP loss; the optimizer step is torch's."""
+the fused HIP loss; plain SGD runs inside the fused backward (mmre.optim.SGD). For TransE +
+MarginLoss + SGD with 'normal' sampling, run() takes the whole step as one C-ABI call
+(mmre.ns.OpenKETrainStep: same batches, losses and parameters, bit for bit)."""
 import os
 
 import numpy as np
@@ -24,6 +26,10 @@ class Trainer(object):
         self.save_steps = save_steps
         self.checkpoint_dir = checkpoint_dir
         self.log = []
+        # run() takes the one-call TransE step (mmre_ns_step_openke) when the configuration allows
+        # it -- same values as train_one_step, bit for bit (tests/test_api_gpu.py); False forces the
+        # per-batch path
+        self.one_call_step = True
 
     def to_var(self, x, use_gpu):
         if isinstance(x, torch.Tensor):
@@ -64,13 +70,53 @@ class Trainer(object):
         if hasattr(self.model, "fuse_optimizer") and hasattr(self.optimizer, "fusable_lr"):
             # the fused negative-sampling backward applies the plain SGD step itself (bit-identical)
             self.model.fuse_optimizer(self.optimizer)
+        fast = self._one_call_step() if self.one_call_step else None
+        self.used_one_call_step = fast is not None
         for epoch in range(self.train_times):
             res = 0.0
-            for data in self.data_loader:
-                res += self.train_one_step(data)
+            if fast is not None:
+                step, group = fast
+                for _ in range(len(self.data_loader)):
+                    step.lr = float(group["lr"])
+                    res += float(step().item())
+            else:
+                for data in self.data_loader:
+                    res += self.train_one_step(data)
             self.log.append(res)
             if self.save_steps and self.checkpoint_dir and (epoch + 1) % self.save_steps == 0:
                 self.model.save_checkpoint(os.path.join(self.checkpoint_dir + "-" + str(epoch) + ".ckpt"))
+
+    def _one_call_step(self):
+        """(mmre.ns.OpenKETrainStep, its optimizer group) when the whole step -- the loader's
+        Base.cpp sampling, NegativeSampling + MarginLoss on TransE, plain SGD -- can run as one
+        C-ABI call; else None (train_one_step)."""
+        try:
+            from ..data.TrainDataLoader import TrainDataLoader
+            from ..module.loss.MarginLoss import MarginLoss
+            from ..module.strategy.NegativeSampling import NegativeSampling
+            from mmre.ns import OpenKETrainStep
+        except ImportError:
+            return None
+        m, dl = self.model, self.data_loader
+        if not (isinstance(m, NegativeSampling) and isinstance(m.loss, MarginLoss) and isinstance(dl, TrainDataLoader)):
+            return None
+        if m.l3_regul_rate != 0 or dl.sampling_mode != "normal" or dl.negative_rel != 0 or m.batch_size != dl.batch_size:
+            return None
+        if not (hasattr(m.model, "ns_spec") and hasattr(m.model, "_tables")):
+            return None
+        spec = m.model.ns_spec()
+        ent, rel, ent_im, rel_im = m.model._tables()
+        if spec.model not in ("transe", "transe_l2") or spec.use_model_margin or ent_im is not None:
+            return None
+        if not hasattr(self.optimizer, "fusable_lr") or self.optimizer.fusable_lr([ent, rel]) is None:
+            return None
+        if spec.dim > 512 or dl.negative_ent > 32 or dl.negative_ent < 1:  # the fused kernel's shapes
+            return None
+        group = next(g for g in self.optimizer.param_groups if any(p is ent for p in g["params"]))
+        margin, adv = m.loss.fused_args()
+        step = OpenKETrainStep(dl.sampler, spec, ent, rel, dl.batch_size, dl.negative_ent, margin, float(group["lr"]),
+                               adv_temperature=adv, regul_rate=m.regul_rate)
+        return step, group
 
     def set_model(self, model):
         self.model = model

@@ -85,6 +85,37 @@ def test_openke_training_example_runs():
     assert 0.0 <= hit1 <= hit3 <= hit10 <= 1.0 and mr >= 1.0
 
 
+@pytest.mark.parametrize("regul", [0.0, 0.25])
+def test_trainer_one_call_step_equals_per_batch_path(regul):
+    """Trainer.run() on TransE + MarginLoss + SGD takes the one-call step (mmre_ns_step_openke):
+    over 3 epochs of 10 batches its epoch losses, embedding tables and sampler states equal the
+    per-batch path's (train_one_step: loader sampling, fused loss, backward, SGD) bit for bit."""
+    import torch
+    from openke.config import Trainer
+    from openke.data import TrainDataLoader
+    from openke.module.loss import MarginLoss
+    from openke.module.model import TransE
+    from openke.module.strategy import NegativeSampling
+    runs = []
+    for one_call in (True, False):
+        torch.manual_seed(0)
+        tdl = TrainDataLoader(in_path=SMALL, nbatches=10, threads=8, sampling_mode="normal", bern_flag=1,
+                              filter_flag=1, neg_ent=25, neg_rel=0)
+        transe = TransE(ent_tot=tdl.get_ent_tot(), rel_tot=tdl.get_rel_tot(), dim=32, p_norm=1, norm_flag=True)
+        model = NegativeSampling(model=transe, loss=MarginLoss(margin=5.0), batch_size=tdl.get_batch_size(),
+                                 regul_rate=regul)
+        trainer = Trainer(model=model, data_loader=tdl, train_times=3, alpha=1.0, use_gpu=True)
+        trainer.one_call_step = one_call
+        trainer.run()
+        assert trainer.used_one_call_step == one_call
+        runs.append((list(trainer.log), transe.ent_embeddings.weight.detach().clone(),
+                     transe.rel_embeddings.weight.detach().clone(), tdl.sampler.seeds.copy()))
+    (la, ea, ra, sa), (lb, eb, rb, sb) = runs
+    assert la == lb
+    assert torch.equal(ea, eb) and torch.equal(ra, rb)
+    assert np.array_equal(sa, sb)
+
+
 def test_cross_sampling_mode_trains():
     from openke.config import Trainer
     from openke.data import TrainDataLoader
