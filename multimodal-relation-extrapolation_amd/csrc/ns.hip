@@ -1016,7 +1016,7 @@ __device__ __forceinline__ float wave_sum_u(float v) {
 // (h + r) - t in the corrupted-row registers as its rows arrive, and each of its rows that is
 // not the positive's gets a slot of its own. Every operand is a normalised row of the pre-pass
 // (norm_flag) or the table row itself.
-template <int NC, bool L2>
+template <int NC, bool L2, bool REG>
 __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __restrict__ nrm_e,
                                               const float* __restrict__ nrm_r, float* __restrict__ score,
                                               float* __restrict__ part, const NSSlots& S, int64_t n_ent, int64_t b,
@@ -1054,9 +1054,9 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     if (u < nj) {
       const int64_t h = readlane64u(my_h, u), t = readlane64u(my_t, u), r = readlane64u(my_r, u);
       const bool oh = h == ph, ot = t == pt, orr = r == pr;
-      if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], ent_n, h, d, lane); cnr[u] = nrm_e[h]; }
-      else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], ent_n, t, d, lane); cnr[u] = nrm_e[t]; }
-      else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], rel_n, r, d, lane); cnr[u] = nrm_r[r]; }
+      if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], ent_n, h, d, lane); cnr[u] = REG ? nrm_e[h] : 0.0f; }
+      else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], ent_n, t, d, lane); cnr[u] = REG ? nrm_e[t] : 0.0f; }
+      else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], rel_n, r, d, lane); cnr[u] = REG ? nrm_r[r] : 0.0f; }
       else if (!(oh && ot && orr)) {  // shares fewer than two rows: x = (h + r) - t, built here
         code[u] = 4;
         if (oh) C[u] = hn; else vload_row(C[u], ent_n, h, d, lane);
@@ -1075,9 +1075,12 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   Vec<NC> x, hr;
 #pragma unroll
   for (int q = 0; q < NC; ++q) hr.v[q] = hn.v[q] + rn.v[q];
-  float p_raw = wave_sum_u(code_x<NC, L2>(x, hr, hn, rn, tn, hn, 3));
-  if (L2) p_raw = sqrtf(p_raw);
+  const float p_sum = wave_sum_u(code_x<NC, L2>(x, hr, hn, rn, tn, hn, 3));
+  const float p_raw = L2 ? sqrtf(p_sum) : p_sum;
   const float p = A.use_model_margin ? A.model_margin - p_raw : p_raw;
+  // every x is kept from here on (the positive's in px, negative u's in C[u]): the gradient pass
+  // needs no row, so hn / rn / tn / hr die with the forward
+  const Vec<NC> px = x;
   const float psh = nph * nph, psr = npr * npr, pst = npt * npt;
   float qh = 0.f, qt = 0.f, qr = 0.f;
   if (w == 0) {
@@ -1103,6 +1106,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       ot += code[u] != 1 ? 1.0f : 0.0f;
     }
     float sv = wave_sum_u(code_x<NC, L2>(x, hr, hn, rn, tn, C[u], code[u]));
+    C[u] = x;
     if (L2) sv = sqrtf(sv);
     sraw[u] = sv;
     const float n = A.use_model_margin ? A.model_margin - sv : sv;
@@ -1214,11 +1218,11 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   const int place = filing ? atomicAdd(&S.counts[my_key], 1) : 0;
   if (w == 0) {
     const float g = sgn * s_gp;
-    p_raw = code_x<NC, L2>(x, hr, hn, rn, tn, hn, 3);  // x of the positive again (registers)
-    const float gs = L2 ? (p_raw > 0.0f ? g / sqrtf(wave_sum_u(p_raw)) : 0.0f) : g;
+    // a lane whose x is all zero gets gv = 0 whichever way gs is taken
+    const float gs = L2 ? (p_sum > 0.0f ? g / p_raw : 0.0f) : g;
 #pragma unroll
     for (int q = 0; q < NC; ++q) {
-      const float gv = L2 ? gs * x.v[q] : (x.v[q] > 0.0f ? g : (x.v[q] < 0.0f ? -g : 0.0f));
+      const float gv = L2 ? gs * px.v[q] : (px.v[q] > 0.0f ? g : (px.v[q] < 0.0f ? -g : 0.0f));
       Gh.v[q] += gv; Gr.v[q] += gv; Gt.v[q] -= gv;
     }
   }
@@ -1233,10 +1237,10 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
       own_r = readlane64u(my_r, u) == pr;
       own_t = readlane64u(my_t, u) == pt;
     }
-    code_x<NC, L2>(x, hr, hn, rn, tn, C[u], code[u]);  // C[u] normalised by the forward
+    const Vec<NC>& xu = C[u];  // its x, kept by the forward
     const float gs = L2 ? (sraw[u] > 0.0f ? g / sraw[u] : 0.0f) : g;
 #pragma unroll
-    for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * x.v[q] : (x.v[q] > 0.0f ? g : (x.v[q] < 0.0f ? -g : 0.0f));
+    for (int q = 0; q < NC; ++q) gx.v[q] = L2 ? gs * xu.v[q] : (xu.v[q] > 0.0f ? g : (xu.v[q] < 0.0f ? -g : 0.0f));
     if (own_h) vadd(Gh, gx, 1.0f);
     if (own_r) vadd(Gr, gx, 1.0f);
     if (own_t) vadd(Gt, gx, -1.0f);
@@ -1276,13 +1280,15 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   }
 }
 
-template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
+// REG: the regularization's squared norms of the corrupted rows are gathered (regul_rate != 0);
+// without it the instance holds no norms of them (fewer registers: 6 waves / SIMD)
+template <int NC, bool L2, bool REG>
+__global__ __launch_bounds__(256, NC > 4 ? 1 : (L2 ? 5 : 6)) void k_ns_transe_fused(NSArgs A, const float* __restrict__ nrm_e,
                                                          const float* __restrict__ nrm_r, float* __restrict__ score,
                                                          float* __restrict__ part, NSSlots S, int64_t n_ent,
                                                          const float* __restrict__ ent_n,
                                                          const float* __restrict__ rel_n) {
-  ns_fused_body<NC, L2>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, ent_n, rel_n);
+  ns_fused_body<NC, L2, REG>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, ent_n, rel_n);
 }
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -2200,8 +2206,14 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
   const bool l2 = model == MMRE_TRANSE_L2;
   const int nc = transe_fast_nc(A);
 #define MMRE_NS_FUSED(NC_, L2_)                                                                                    \
-  hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, n_ent,   \
-                     ent_u, rel_u)
+  do {                                                                                                             \
+    if (A.regul_rate != 0.0f)                                                                                      \
+      hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, \
+                         n_ent, ent_u, rel_u);                                                                     \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part,  \
+                         S, n_ent, ent_u, rel_u);                                                                  \
+  } while (0)
   if (nc == 1) { if (l2) MMRE_NS_FUSED(1, true); else MMRE_NS_FUSED(1, false); }
   else if (nc == 2) { if (l2) MMRE_NS_FUSED(2, true); else MMRE_NS_FUSED(2, false); }
   else if (nc == 4) { if (l2) MMRE_NS_FUSED(4, true); else MMRE_NS_FUSED(4, false); }
@@ -2389,8 +2401,14 @@ extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_to
   float* part = d_work + w.part;
   const dim3 grid((unsigned)batch), blk(256);
 #define MMRE_NS_FUSED(NC_, L2_)                                                                                    \
-  hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, n_ent,   \
-                     ent_u, rel_u)
+  do {                                                                                                             \
+    if (A.regul_rate != 0.0f)                                                                                      \
+      hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_, true>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part, S, \
+                         n_ent, ent_u, rel_u);                                                                     \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_ns_transe_fused<NC_, L2_, false>), grid, blk, 0, st, A, nrm_e, nrm_r, d_score, part,  \
+                         S, n_ent, ent_u, rel_u);                                                                  \
+  } while (0)
   if (nc == 1) { if (l2) MMRE_NS_FUSED(1, true); else MMRE_NS_FUSED(1, false); }
   else if (nc == 2) { if (l2) MMRE_NS_FUSED(2, true); else MMRE_NS_FUSED(2, false); }
   else if (nc == 4) { if (l2) MMRE_NS_FUSED(4, true); else MMRE_NS_FUSED(4, false); }
