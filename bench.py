@@ -598,7 +598,7 @@ def bench_ns(args, world, rank, dev, dist):
             grad_bytes = E * eb + R * rb
             slot_bytes = 2 * (B * (3 + 3 * k)) * 2 * 4 * (256 if d > 128 else 128)
         ach = (fwd_bytes + grad_bytes) / (fused_ms * 1e-3) / 1e9
-        step_kernels = (["k_ns_prepass(", "k_ns_transe_fused<4, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
+        step_kernels = (["k_ns_prepass(", "k_ns_transe_fused<4, false, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
                         if model == "transe" else
                         ["k_ns_gen_forward<4, ", "k_ns_reduce(", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"])
         traffic, tsrc, tper = (pmc_step_traffic("ns", step_kernels) if (model == "transe" and world == 1 and d == 200 and k == 25)
@@ -624,7 +624,7 @@ def bench_ns(args, world, rank, dev, dist):
                                             "2 x FETCH_SIZE + WRITE_SIZE)",
                             "traffic_source": tsrc, "traffic_per_kernel": tper,
                             "traffic_x_algorithmic": (traffic / (fwd_bytes + grad_bytes)) if traffic else None,
-                            "kernel": ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false> + "
+                            "kernel": ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false, false> + "
                                        "k_ns_reduce (the loss) + k_ns_row_owner<4, false>" if model == "transe" else
                                        "mmre_ns_forward_backward = k_ns_forward + k_ns_reduce + k_ns_gen_slots + "
                                        "k_ns_gen_owner") + ": events around hipGraph replays of the one-shot C-ABI call",
