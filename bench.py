@@ -601,7 +601,8 @@ def bench_ns(args, world, rank, dev, dist):
         step_kernels = (["k_ns_prepass(", "k_ns_transe_fused<4, false, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
                         if model == "transe" else
                         ["k_ns_gen_forward<4, ", "k_ns_reduce(", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"])
-        traffic, tsrc, tper = (pmc_step_traffic("ns", step_kernels) if (model == "transe" and world == 1 and d == 200 and k == 25)
+        pmc_cfg = "ns" if model == "transe" else f"ns_{model}"  # profiles/pmc_<pmc_cfg>.json
+        traffic, tsrc, tper = (pmc_step_traffic(pmc_cfg, step_kernels) if (world == 1 and d == 200 and k == 25)
                                else (None, None, None))
         out = {"metric": f"training triples/sec, {CONFIGS['ns']['workload']}",
                "value": n_rows * args.steps * world / elapsed, "unit": "training triples/s", "n_gpus": world,

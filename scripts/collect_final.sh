@@ -11,7 +11,7 @@ for d in $f/prof_*/; do
   [ -n "$s" ] && cp "$s" profiles/r3/${n}_kernel_stats.csv
 done
 [ -f $f/pytest_gpu.log ] && cp $f/pytest_gpu.log profiles/r3/pytest_gpu_final.log
-for c in c1 c2 c3 c4 c5 ns; do
+for c in c1 c2 c3 c4 c5 ns ns_distmult ns_complex ns_rotate; do
   [ -d gpurun_out/pmc_final_$c ] && python scripts/pmc_summary.py final_$c --json profiles/pmc_$c.json > /dev/null
 done
 ls -la profiles/r3 profiles/pmc_*.json

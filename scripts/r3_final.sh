@@ -3,8 +3,9 @@
 #   A: full -m gpu suite + smoke + C2 bench line + C2 kernel trace
 #   B: C1 / C3 / C4 / C5 bench lines (cpu_baseline + reference parity legs) + kernel traces
 #   C: NS bench lines (TransE k 25 / k 10 with the reference CPU leg; DistMult / ComplEx / RotatE) + traces
-#   D1 / D2: PMC passes (scripts/pmc.sh) of c2 c4 ns / c3 c5; E: C1 PMC + C2 bench again; F: C1 bench again
-# usage: scripts/r3_final.sh <A|B|C|D1|D2>
+#   D1 / D2: PMC passes (scripts/pmc.sh) of c1 c2 c4 ns / c3 c5; E: C1 PMC + C2 bench again; F: C1 bench again;
+#   G: PMC passes of the DistMult / ComplEx / RotatE NS steps; H: their bench lines again
+# usage: scripts/r3_final.sh <A|B|C|D1|D2|E|F|G|H>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -46,6 +47,14 @@ case $1 in
   E)  # C1's PMC passes, then the C2 bench line again (its PMC summary installed in profiles/ by now)
     bash scripts/pmc.sh final_c1 --config c1 || exit $?
     timeout -k 10 300 python bench.py > $o/bench_c2.json 2> $o/bench_c2.err || exit $?
+    ;;
+  G)  # PMC passes of the other models' NS steps (profiles/pmc_ns_<model>.json)
+    for m in distmult complex rotate; do bash scripts/pmc.sh final_ns_$m --config ns --ns-model $m || exit $?; done
+    ;;
+  H)  # the other models' NS lines again, with their PMC summaries installed
+    for m in distmult complex rotate; do
+      timeout -k 10 300 python bench.py --config ns --ns-model $m --no-cpu-baseline > $o/bench_ns_$m.json 2> $o/bench_ns_$m.err || exit $?
+    done
     ;;
   F)  # the C1 bench line with its PMC summary installed
     timeout -k 10 300 python bench.py --config c1 > $o/bench_c1.json 2> $o/bench_c1.err || exit $?
