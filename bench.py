@@ -1011,7 +1011,25 @@ def _with_build(out):
     cb = out.get("cpu_baseline")
     if isinstance(cb, dict):
         cb.setdefault("cpu_model", _cpu_model())
+        cb.setdefault("cores_note", _cores_note(int(cb.get("cores", 0))))
     return out
+
+
+def _cores_note(used: int) -> str:
+    """Why the CPU baseline ran on `used` threads (SURVEY 8(d) asks for the host's cores): the
+    GPU pool gives each GPU's process a share of the host -- OMP_NUM_THREADS / MAX_JOBS are set
+    to it (16 for one GPU of an 8-GPU node) -- while sched_getaffinity still lists every CPU of
+    the machine, which the other GPUs' processes share. The baseline uses the share: torch's
+    intra-op threads (= OMP_NUM_THREADS) for the reference's predict and as Base.so's
+    workThreads."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 0
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (f"{used} threads = this process's CPU share (OMP_NUM_THREADS={omp}, torch intra-op threads "
+            f"{torch.get_num_threads()}); sched_getaffinity lists {avail} CPUs, the whole host, shared with the other "
+            f"GPUs' processes")
 
 
 def _cpu_model():
@@ -1114,7 +1132,7 @@ def main():
     model, dim = cfg["model"], cfg["dim"]
     if model == "transe" and args.train_steps > 0:
         train_transe(w, dev, steps=args.train_steps)
-        if dist:  # every rank evaluates rank 0's tables (float atomics make training run-dependent)
+        if dist:  # every rank evaluates rank 0's tables (training is deterministic; one copy keeps it explicit)
             for k in ("ent", "rel"):
                 t = w[k].to(_coll_dev(dist, dev))
                 dist.broadcast(t, 0)
@@ -1182,6 +1200,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     _, counts = ev.run()  # one more evaluation outside the timed region: the counts the parity check reads
+    l1st = ev.l1q_stats() if hasattr(ev, "l1q_stats") else None  # the TransE L1 integer filter's record
     breakdown = None
     if world > 1:  # every rank's local / sweep / fixed / collective time, gathered (all ranks take part)
         breakdown = rank_breakdown(ev, dist, dev, sweep_ms, n_local, args.shard == "entity")
@@ -1246,6 +1265,14 @@ def main():
                            "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
                            "mr": metrics["filter"]["mr"]},
                "parity": None}
+        if l1st is not None:
+            pairs = int(n_local) * int(e_local)
+            out["l1_filter"] = {"undecided_pairs": l1st["undecided"],
+                                "undecided_frac": l1st["undecided"] / pairs if pairs else None,
+                                "fallback_to_f32": l1st["fallback"],
+                                "note": "pairs the 16-bit code bound left undecided, each rescored with the canonical "
+                                        "f32 chain (mmre_link_l1q_stats, rank 0's last evaluation); fallback_to_f32 = "
+                                        "the quantization pass found M > 128 x mean|x| and the sweep ran the f32 path"}
         if "trained" in w:
             out["config"]["tables"] = w["trained"]
         elif "tables" in w:

@@ -123,7 +123,9 @@ int mmre_link_truth_grouped(int model, int pred_kind, float margin, const float*
 /* The sweep (after mmre_link_truth[_grouped] on the same stream). For every query i and
  * every entity j != true(i):  raw += pred(j) < pred(true)   (Test.h:80-86, strict
  * <, ties favour the truth), added to the raw AND filtered columns (and the _tc
- * columns for allowed j when type masks are given, Test.h:88-98).
+ * columns for allowed j when type masks are given, Test.h:88-98). The kernel adds to the
+ * raw columns and a short pass after it adds them to the filtered ones, so every sweep
+ * call completes the count table the truth pass initialised (one sweep call per truth pass).
  * d_scores (nullable): (n_query, E) predicted values, for parity tests only. */
 int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
                     int64_t e_pad, const float* d_q_km, const int32_t* d_q_true, const int64_t* d_qr,
@@ -153,6 +155,14 @@ int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d
  * (mmre_link_prepare_queries). e_begin / e_end as for mmre_link_sweep_range (0, n_ent: whole
  * table). d_work: mmre_link_l1q_workspace(dim, e_pad, q_pad) bytes of device scratch. */
 int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
+/* The filter's own record of the last mmre_link_sweep_l1q on d_work (one tiny launch, no
+ * synchronisation): d_out[0] = pairs the code bound left undecided (each rescored with the
+ * canonical f32 chain), d_out[1] = 1 if the sweep ran the f32 fallback instead of the codes.
+ * The fallback is taken on the device, without a host round trip, when M (the largest |x|)
+ * exceeds 128 x the mean |x| of the two planes -- one outlier value stretching the 16-bit code
+ * range, which would leave most pairs undecided -- or is not finite. Counts are the same
+ * either way. */
+int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
 int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
                         int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,
                         const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query,
@@ -284,14 +294,20 @@ int mmre_ns_forward(int model, int norm_flag, float model_margin, int use_model_
                     const int64_t* d_h, const int64_t* d_t, const int64_t* d_r, int64_t batch, int64_t neg,
                     float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
                     float* d_work, void* stream);
-/* Backward of the forward above: accumulates d(loss)/d(table) * d_grad_loss[0]
- * into the dense gradient tables (float atomics); d_grad_loss NULL means 1. */
+/* Backward of the forward above: WRITES every row of the dense gradient tables with
+ * d(loss)/d(table) * d_grad_loss[0] (d_grad_loss NULL means 1). Deterministic, no float
+ * atomics: each scored row files its h / r / t gradient rows as slot records in its table
+ * rows' buckets and one wave per table row sums them in batch order (bit-identical run to
+ * run). d_work: >= mmre_rows_backward_workspace(model, batch * (1 + neg), n_ent, n_rel, dim)
+ * floats. dim <= 512. */
+int64_t mmre_rows_backward_workspace(int model, int64_t n_rows, int64_t n_ent, int64_t n_rel, int dim);
 int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model_margin, const float* d_ent,
                      const float* d_ent_im, const float* d_rel, const float* d_rel_im, int dim,
                      float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r, int64_t batch,
                      int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
                      const float* d_score, const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im,
-                     float* d_grad_rel, float* d_grad_rel_im, float* d_work, void* stream);
+                     float* d_grad_rel, float* d_grad_rel_im, int64_t n_ent, int64_t n_rel, float* d_work,
+                     int64_t work_floats, void* stream);
 
 /* Training: forward, loss and d(loss)/d(tables). mmre_ns_fused_forward computes the scores and
  * the loss and keeps what the gradient needs in d_work; mmre_ns_fused_grad then WRITES every
@@ -360,13 +376,18 @@ int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_total, const 
                         float* d_grad_ent, float* d_grad_rel, float* d_work, float lr, void* stream);
 
 /* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
- * batch = n_rows, neg = 0, d_loss = NULL. Its backward: accumulate
- * d_grad_score[i] * d(score_i)/d(tables) into the dense gradient tables. */
+ * batch = n_rows, neg = 0, d_loss = NULL. Its backward (OpenKE Model.forward under any loss,
+ * Model.py / SoftplusLoss.py:7-31 / SigmoidLoss.py:7-30; the repo's scoring_fn / _calc,
+ * module/NegativeSampling.py:69-82): WRITES every row of the dense gradient tables (n_ent /
+ * n_rel rows) with sum_i d_grad_score[i] * d(score_i)/d(tables), summed per table row in row
+ * order i (no float atomics: bit-identical run to run). d_work: >=
+ * mmre_rows_backward_workspace(model, n_rows, n_ent, n_rel, dim) floats. dim <= 512. */
 int mmre_score_rows_backward(int model, int norm_flag, float model_margin, int use_model_margin,
                              const float* d_ent, const float* d_ent_im, const float* d_rel, const float* d_rel_im,
                              int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t, const int64_t* d_r,
                              int64_t n_rows, const float* d_grad_score, float* d_grad_ent, float* d_grad_ent_im,
-                             float* d_grad_rel, float* d_grad_rel_im, void* stream);
+                             float* d_grad_rel, float* d_grad_rel_im, int64_t n_ent, int64_t n_rel, float* d_work,
+                             int64_t work_floats, void* stream);
 
 /* ====================================================================== *
  *  Zero-shot relation-embedding generator (module/model.py:674-686):     *

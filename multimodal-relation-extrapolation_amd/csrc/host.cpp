@@ -158,7 +158,9 @@ extern "C" int mmre_import_prob(const char* path, int64_t n_rel, float temperatu
     float* row = h_prob + i * (n_rel - 1);
     float sum = 0.0f;
     for (int64_t j = 0; j < n_rel - 1; ++j) {
-      const float e = expf(-row[j] / temperature);
+      // Reader.h:40 calls unqualified exp on a float with only <cmath> included and no `using
+      // namespace std`: libstdc++ resolves it to ::exp(double), so the value is (float)exp((double)x)
+      const float e = (float)exp((double)(-row[j] / temperature));
       sum += e;
       row[j] = e;
     }

@@ -325,10 +325,23 @@ __device__ __forceinline__ float rot_exact(const float* __restrict__ q_km, int64
 // undecided pairs as for RotatE (rot_bound), the undecided rescored exactly from the
 // row-major copies (l1_exact_rows: the canonical chain, acc + |q_k - e_k| in k order).
 // M non-finite (an inf / NaN anywhere in the planes): delta = inf, every pair is undecided.
+// Workspace header (L1Q_HDR bytes before the code planes): word 0 = bits of M, word 1 = the
+// fallback flag (k_l1q_quant), L1Q_SLOTS undecided-pair counters (uint64, L1Q_SLOT_STRIDE apart:
+// separate cache lines) from byte 256, the absmax blocks' partial sums of |x| from byte
+// L1Q_PART. Zeroed up to L1Q_PART by the launch sequence.
+constexpr int L1Q_HDR = 8192;
+constexpr int L1Q_SLOTS = 16;
+constexpr int L1Q_SLOT_STRIDE = 32;  // uint64 units = 256 B
+constexpr int L1Q_PART = 256 + L1Q_SLOTS * L1Q_SLOT_STRIDE * 8;
+constexpr int L1Q_MAX_BLOCKS = 512;
 struct L1Q {
   const float* q_rows;     // (queries, kt) row-major query vectors
   const float* ent_rows;   // (whole table, kt) row-major entity rows
-  const uint32_t* absmax;  // bits of M
+  const uint32_t* hdr;     // workspace header: hdr[0] bits of M, hdr[1] fallback flag
+  unsigned long long* undecided;  // counter slots
+  const float* q_f;        // fallback: the f32 k-major planes (query, entity slice) and their rows
+  const float* ent_f;
+  int kp_f;
   int kt;                  // floats per row (the canonical chain's length, padding rows are 0)
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax) {
@@ -723,24 +736,42 @@ struct UnitMap {
 // sequential k chain each (the canonical order). K is staged through LDS in
 // double-buffered steps of 8 rows (16 B per thread per plane per operand). Per-query
 // counts stay in registers until the workgroup moves to the next query tile.
-template <int OP, bool TC, bool STORE, int PK>
-__global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
-    const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
-    int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups, int pred_kind, float margin,
-    const float* __restrict__ thr, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,
-    const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
+// LDS of one VALU-sweep workgroup. A struct declared once in the kernel, so that the L1
+// filter's kernel and its f32 fallback path (the same kernel, one uniform branch) share it.
+template <int NPL, bool TC>
+struct ValuSmem {
+  float4 sq[2][NPL][KC][TQ / 4];
+  float4 se[2][NPL][KC][TE / 4];
+  float s_thr[2][TQ];
+  int32_t s_true[2][TQ];
+  int32_t s_rel[2][TC ? TQ : 1];
+  int8_t s_mode[2][TC ? TQ : 1];
+  int32_t s_cnt[TC ? 2 : 1][8][NT];  // per-thread counters (off the VGPR budget)
+  uint32_t s_unc[NT / 64];           // undecided pairs per wave (the L1 filter's counter)
+};
+
+// The sweep body. Counts go to the raw columns only (counts[0][q], counts[2][q]); the filtered
+// columns (initialised to minus the listed entities that beat the truth by the truth pass)
+// receive them in k_counts_finalize, one coalesced pass after the sweep (half the atomics).
+template <int OP, bool TC, bool STORE, int PK, int NPL>
+__device__ __forceinline__ void sweep_valu_body(
+    ValuSmem<NPL, TC>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
+    const float* __restrict__ q_km, int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups,
+    int pred_kind, float margin, const float* __restrict__ thr, const int32_t* __restrict__ qtrue,
+    const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
     const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
-    float* __restrict__ scores, L1Q l1) {
-  constexpr int NPL = (OP == 2) ? 2 : 1;
+    float* __restrict__ scores, const L1Q& l1) {
+  static_assert(NPL == ((OP == 2) ? 2 : 1), "planes");
   // filters: RotatE's raw-sqrt sum (rot_bound / rot_exact), TransE L1's 16-bit codes (L1Q)
   constexpr bool FAST = (OP == 2 || OP == 5) && !STORE;
-  __shared__ float4 sq[2][NPL][KC][TQ / 4];
-  __shared__ float4 se[2][NPL][KC][TE / 4];
-  __shared__ float s_thr[2][TQ];
-  __shared__ int32_t s_true[2][TQ];
-  __shared__ int32_t s_rel[2][TC ? TQ : 1];
-  __shared__ int8_t s_mode[2][TC ? TQ : 1];
-  __shared__ int32_t s_cnt[TC ? 2 : 1][8][NT];  // per-thread counters (off the VGPR budget)
+  auto& sq = sm.sq;
+  auto& se = sm.se;
+  auto& s_thr = sm.s_thr;
+  auto& s_true = sm.s_true;
+  auto& s_rel = sm.s_rel;
+  auto& s_mode = sm.s_mode;
+  auto& s_cnt = sm.s_cnt;
+  uint32_t n_unc = 0;  // undecided pairs of this thread (OP 5)
 
   const int tid = threadIdx.x;
   const int tq = tid >> 4, te = tid & 15;
@@ -816,7 +847,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
   // L1 filter constants (uniform): code step, bound slope and offset
   float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
   if constexpr (OP == 5) {
-    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.absmax))));
+    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr))));
     l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
     l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
   }
@@ -963,6 +994,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
             s_cnt[0][i][tid] += c;
             if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
           }
+          if constexpr (OP == 5) n_unc += __popc(unc[0]) + __popc(unc[1]);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             uint32_t m = unc[h];
@@ -1059,10 +1091,10 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
             }
             const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
             const int64_t q = q0 + ql;
-            if (te == 0 && q < n_query) {
-              if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
+            if (te == 0 && q < n_query) {  // raw columns only: k_counts_finalize adds them to the filtered ones
+              if (c) atomicAdd(&counts[q], c);
               if constexpr (TC) {
-                if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
+                if (cc) atomicAdd(&counts[2 * n_query + q], cc);
               }
             }
             s_cnt[0][i][tid] = 0;
@@ -1081,6 +1113,54 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
       buf ^= 1;
     }
   }
+  if constexpr (OP == 5) {  // the filter's undecided pairs: one atomic per workgroup, 16 slots
+    uint32_t u = n_unc;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
+    if ((tid & 63) == 0) sm.s_unc[tid >> 6] = u;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) t += sm.s_unc[w];
+      if (t) atomicAdd(l1.undecided + (blockIdx.x & (L1Q_SLOTS - 1)) * L1Q_SLOT_STRIDE, (unsigned long long)t);
+    }
+  }
+}
+
+template <int OP, bool TC, bool STORE, int PK>
+__global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
+    const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
+    int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups, int pred_kind, float margin,
+    const float* __restrict__ thr, const int32_t* __restrict__ qtrue, const int64_t* __restrict__ qr,
+    const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
+    const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
+    float* __restrict__ scores, L1Q l1) {
+  constexpr int NPL = (OP == 2) ? 2 : 1;
+  __shared__ ValuSmem<NPL, TC> sm;
+  if constexpr (OP == 5) {
+    // the L1 filter's fallback (k_l1q_quant decided that the codes are too coarse for these
+    // planes -- one outlier value sets the code step for everything): the exact f32 sweep of
+    // the float planes, as mmre_link_sweep would run it
+    if (__builtin_amdgcn_readfirstlane(l1.hdr[1]) != 0u) {
+      sweep_valu_body<0, TC, false, PK, NPL>(sm, l1.ent_f, e_pad, n_ent, l1.q_f, q_pad, n_query, l1.kp_f, n_et,
+                                             e_base, n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head,
+                                             type_tail, type_words, counts, nullptr, l1);
+      return;
+    }
+  }
+  sweep_valu_body<OP, TC, STORE, PK, NPL>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
+                                          n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head, type_tail,
+                                          type_words, counts, scores, l1);
+}
+
+// filtered columns += raw columns (after the sweep): counts[1] = counts[0] + (minus the listed
+// entities that beat the truth, written by the truth pass), likewise counts[3] from counts[2]
+__global__ __launch_bounds__(256) void k_counts_finalize(int32_t* __restrict__ counts, int64_t n_query, int tc) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n_query) return;
+  counts[n_query + q] += counts[q];
+  if (tc) counts[3 * n_query + q] += counts[2 * n_query + q];
 }
 
 // ------------------------------------------------------------ MFMA sweep ---
@@ -1176,9 +1256,9 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
     if constexpr (BAL) {  // each lane its row's count (both column waves add)
       const int64_t q = (int64_t)qtile * TQ + wq * 64 + lane;
       if (q < n_query) {
-        if (cntv) { atomicAdd(&counts[q], cntv); atomicAdd(&counts[n_query + q], cntv); }
+        if (cntv) atomicAdd(&counts[q], cntv);  // raw only (k_counts_finalize)
         if constexpr (TC) {
-          if (cntv_tc) { atomicAdd(&counts[2 * n_query + q], cntv_tc); atomicAdd(&counts[3 * n_query + q], cntv_tc); }
+          if (cntv_tc) atomicAdd(&counts[2 * n_query + q], cntv_tc);
         }
       }
     } else {
@@ -1198,9 +1278,9 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
           }
           const int64_t q = q0 + row_of(bi, r);
           if (lcol == 0 && q < n_query) {
-            if (c) { atomicAdd(&counts[q], c); atomicAdd(&counts[n_query + q], c); }
+            if (c) atomicAdd(&counts[q], c);  // raw only (k_counts_finalize)
             if constexpr (TC) {
-              if (cc) { atomicAdd(&counts[2 * n_query + q], cc); atomicAdd(&counts[3 * n_query + q], cc); }
+              if (cc) atomicAdd(&counts[2 * n_query + q], cc);
             }
           }
         }
@@ -1389,13 +1469,14 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
 
 // ------------------------------------------------------ L1 integer filter ---
 // M = max |x| over the query plane and the entity slice (non-finite values make M = inf),
-// as float bits in work[0] (zeroed by the caller's stream just before).
+// as float bits in hdr[0] (zeroed by the launch sequence just before), and per block the sum
+// of |x| (finite x) into the partials at byte L1Q_PART -- the fallback test's mean |x|.
 __global__ __launch_bounds__(256) void k_l1q_absmax(const float* __restrict__ q_km, int64_t q_pad,
                                                     const float* __restrict__ e_km, int64_t e_pad, int64_t e_cols,
                                                     int kp, uint32_t* __restrict__ work) {
   // work items (plane row r, column chunk y of 8) of both planes, strided over the blocks (no
   // index division per element); one atomic per block at most (same-address atomics serialize)
-  float m = 0.0f;
+  float m = 0.0f, sa = 0.0f;
   for (int it = blockIdx.x; it < kp * 8; it += gridDim.x) {
     const int r = it >> 3;
     const int64_t st = 8 * (int64_t)blockDim.x, c0 = (int64_t)(it & 7) * blockDim.x + threadIdx.x;
@@ -1403,24 +1484,35 @@ __global__ __launch_bounds__(256) void k_l1q_absmax(const float* __restrict__ q_
 #pragma unroll 4
     for (int64_t c = c0; c < q_pad / 4; c += st) {
       const float4 v = q4[c];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      const float a = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+      m = fmaxf(m, a);
       if (!(v.x - v.x == 0.0f && v.y - v.y == 0.0f && v.z - v.z == 0.0f && v.w - v.w == 0.0f)) m = INFINITY;
+      else sa += (fabsf(v.x) + fabsf(v.y)) + (fabsf(v.z) + fabsf(v.w));
     }
     const float4* e4 = reinterpret_cast<const float4*>(e_km + (int64_t)r * e_pad);
 #pragma unroll 4
     for (int64_t c = c0; c < e_cols / 4; c += st) {
       const float4 v = e4[c];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      const float a = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+      m = fmaxf(m, a);
       if (!(v.x - v.x == 0.0f && v.y - v.y == 0.0f && v.z - v.z == 0.0f && v.w - v.w == 0.0f)) m = INFINITY;
+      else sa += (fabsf(v.x) + fabsf(v.y)) + (fabsf(v.z) + fabsf(v.w));
     }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  __shared__ float s_m[4];
-  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  for (int o = 32; o > 0; o >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, o));
+    sa += __shfl_xor(sa, o);
+  }
+  __shared__ float s_m[4], s_s[4];
+  if ((threadIdx.x & 63) == 0) {
+    s_m[threadIdx.x >> 6] = m;
+    s_s[threadIdx.x >> 6] = sa;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     m = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    reinterpret_cast<float*>(reinterpret_cast<char*>(work) + L1Q_PART)[blockIdx.x] = (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]);
     // non-negative floats order as their bits; inf = no filter. Skip the atomic when the word
     // already holds at least m (a stale read only costs a redundant atomic).
     if (__float_as_uint(m) > __hip_atomic_load(work, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
@@ -1428,11 +1520,38 @@ __global__ __launch_bounds__(256) void k_l1q_absmax(const float* __restrict__ q_
   }
 }
 
+// The fallback test (every block of k_l1q_quant evaluates it identically; block 0 writes it):
+// the code step is 2M / 65535 and a pair stays undecided when its score lies within ~1.03 K
+// steps of its threshold, so the filter pays off while M is a modest multiple of the typical
+// magnitude. M > ratio x mean|x| (one outlier value stretching the code range: every other value
+// then lands in a few codes and most pairs would be rescored one at a time) or M non-finite
+// -> the sweep runs the f32 path instead (same counts either way).
+__device__ __forceinline__ bool l1q_fallback(const uint32_t* __restrict__ work, int n_part, double n_elem,
+                                             float ratio) {
+  __shared__ float s_p[4];
+  const float* part = reinterpret_cast<const float*>(reinterpret_cast<const char*>(work) + L1Q_PART);
+  float v = 0.0f;
+  for (int i = threadIdx.x; i < n_part; i += blockDim.x) v += part[i];  // fixed order per thread
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) s_p[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float sum = (s_p[0] + s_p[1]) + (s_p[2] + s_p[3]);
+  const float mx = __uint_as_float(work[0]);
+  if (!(mx < INFINITY)) return true;
+  return (double)mx > (double)ratio * ((double)sum / n_elem);
+}
+
 // Codes of columns [c0, c0 + n) of a k-major float plane (kp rows, stride pad) into dword rows
 // out[r][pad] = Q(x[2r]) | Q(x[2r + 1]) << 16, rows r < k2 (k >= kp: code 0 in both planes).
+// Skipped when the fallback test says the sweep will not read the codes.
 __global__ __launch_bounds__(256) void k_l1q_quant(const float* __restrict__ km, int64_t pad, int64_t c0, int64_t n,
                                                    int kp, int k2, uint32_t* __restrict__ out,
-                                                   const uint32_t* __restrict__ work) {
+                                                   uint32_t* __restrict__ work, int n_part, double n_elem,
+                                                   float ratio) {
+  const bool fb = l1q_fallback(work, n_part, n_elem, ratio);
+  if (blockIdx.x == 0 && threadIdx.x == 0) work[1] = fb ? 1u : 0u;
+  if (fb) return;
   const float mx = __uint_as_float(*work);
   const float inv = (mx > 0.0f && mx < INFINITY) ? 65535.0f / (2.0f * mx) : 0.0f;
   const float off = (mx < INFINITY) ? mx : 0.0f;
@@ -1453,6 +1572,17 @@ __global__ __launch_bounds__(256) void k_l1q_quant(const float* __restrict__ km,
   }
 }
 
+// Sum of the undecided-pair slots and the fallback flag -> out[0], out[1] (mmre_link_l1q_stats).
+__global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long* sl =
+      reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(work) + 256);
+  unsigned long long t = 0;
+  for (int i = 0; i < L1Q_SLOTS; ++i) t += sl[i * L1Q_SLOT_STRIDE];
+  out[0] = t;
+  out[1] = work[1];
+}
+
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
 
 // ---------------------------------------------------------------- launch ---
@@ -1467,6 +1597,13 @@ static int resident_groups(const void* kernel, int threads) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || per <= 0) per = 1;
   if (per > 4) per = 4;
   return cus * per;
+}
+
+static int launch_finalize(hipStream_t st, int32_t* counts, int64_t n_query, bool tc) {
+  hipLaunchKernelGGL(k_counts_finalize, dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, counts, n_query,
+                     tc ? 1 : 0);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
 }
 
 template <int OP, bool TCV, bool STV, int PK>
@@ -1520,7 +1657,7 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
   }
 #undef MMRE_LV1
   MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  return launch_finalize(st, counts, n_query, tc);
 }
 
 }  // namespace mmre
@@ -1765,7 +1902,7 @@ static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent
 #undef MMRE_MFMA
 #undef MMRE_MFMA_K
   MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  return launch_finalize(st, d_counts, n_query, tc);
 }
 
 extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
@@ -1780,7 +1917,15 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
 
 extern "C" int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
   if (dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
-  return 256 + 4 * (int64_t)l1q_rows(dim) * (e_pad + q_pad);
+  return L1Q_HDR + 4 * (int64_t)l1q_rows(dim) * (e_pad + q_pad);
+}
+
+extern "C" int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream) {
+  if (!d_work || !d_out || work_bytes < L1Q_HDR) return MMRE_ERR_ARG;
+  hipLaunchKernelGGL(k_l1q_stats, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint32_t*)d_work,
+                     (unsigned long long*)d_out);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
 }
 
 extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows,
@@ -1797,19 +1942,27 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   hipStream_t st = (hipStream_t)stream;
   const int kp = plane_rows(MMRE_TRANSE_L1, dim), k2 = l1q_rows(dim);
   uint32_t* hdr = (uint32_t*)d_work;
-  uint32_t* uq = (uint32_t*)((char*)d_work + 256);
+  uint32_t* uq = (uint32_t*)((char*)d_work + L1Q_HDR);
   uint32_t* ue = uq + (int64_t)k2 * q_pad;
   const int64_t e_cols = round_up(e_end, TE) - e_begin;  // the slice's whole tiles
-  MMRE_CHECK(hipMemsetAsync(hdr, 0, 4, st));
-  hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)std::min(kp * 8, 512)), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
+  // fallback ratio M / mean|x| (MMRE_L1Q_RATIO: experiments; <= 0 forces the fallback)
+  static const char* ratio_env = getenv("MMRE_L1Q_RATIO");
+  const float ratio = ratio_env ? (float)atof(ratio_env) : 128.0f;
+  const int n_abs = std::min(kp * 8, L1Q_MAX_BLOCKS);
+  const double n_elem = (double)kp * (double)(q_pad + e_cols);
+  MMRE_CHECK(hipMemsetAsync(hdr, 0, L1Q_PART, st));
+  hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)n_abs), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
                      kp, hdr);
-  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr);
-  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr);
+  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr,
+                     n_abs, n_elem, ratio);
+  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr,
+                     n_abs, n_elem, ratio);
   MMRE_CHECK_LAUNCH();
   const int64_t tw = (n_ent + 31) / 32;
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
-  const L1Q l1{d_q_rows, d_ent_rows, hdr, n_planes(MMRE_TRANSE_L1) * kp};
+  const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
+               n_planes(MMRE_TRANSE_L1) * kp};
   return launch_valu<5>(d_type_head != nullptr, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et,
                         (int)e_begin, (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr,
                         d_qmode, d_type_head, d_type_tail, tw, d_counts, nullptr, l1);

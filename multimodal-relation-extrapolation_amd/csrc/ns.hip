@@ -11,9 +11,11 @@
 // Layout: N = B * (1 + k) rows, positive b at row b, its negative j at row b + (j+1) B
 // (Base.cpp:109-145). One wavefront per positive scores its 1 + k rows (lanes over the
 // embedding dimension, shuffle reductions) and writes one partial loss; a single
-// workgroup reduces the partials in a fixed order (bit-reproducible loss). The backward
-// recomputes each row's intermediates and scatters d(loss)/d(row) into the dense
-// gradient tables with float atomics.
+// workgroup reduces the partials in a fixed order (bit-reproducible loss). No backward uses
+// float atomics: every gradient contribution is a SLOT record filed in its table row's bucket
+// (integer count atomics only) and one wave per table row sums its slots in slot order, so the
+// gradient tables are bit-identical run to run (the fused paths below; the rows backward of
+// mmre_score_rows_backward / mmre_ns_backward).
 #include "mmre_common.h"
 #include "sampler_openke.h"
 
@@ -83,96 +85,6 @@ __device__ float row_score(const NSArgs& A, int64_t row, int lane) {
       acc += sqrtf(re * re + im * im);
     }
     return A.model_margin - wave_sum(acc);
-  }
-}
-
-// g = d(loss)/d(forward score of this row) ; regw = regul_rate * d(loss)/dL scale for the
-// regularisation term applied to the raw gathered rows.
-__device__ void row_backward(const NSArgs& A, int64_t row, int lane, float g, float reg_ent, float reg_rel,
-                             float* gent, float* gent_im, float* grel, float* grel_im) {
-  const int d = A.dim;
-  const int64_t h = A.h[row], t = A.t[row], r = A.r[row];
-  if (A.model == MMRE_TRANSE_L1 || A.model == MMRE_TRANSE_L2) {
-    const float *hv = A.ent + h * d, *tv = A.ent + t * d, *rv = A.rel + r * d;
-    if (A.use_model_margin) g = -g;  // forward = m - s
-    float nh = 1.0f, nt = 1.0f, nr = 1.0f;
-    if (A.norm_flag) {
-      float a = 0.0f, b = 0.0f, c = 0.0f;
-      for (int k = lane; k < d; k += kWave) { a += hv[k] * hv[k]; b += tv[k] * tv[k]; c += rv[k] * rv[k]; }
-      nh = sqrtf(wave_sum(a)); nt = sqrtf(wave_sum(b)); nr = sqrtf(wave_sum(c));
-    }
-    const float ch = fmaxf(nh, 1e-12f), ct = fmaxf(nt, 1e-12f), cr = fmaxf(nr, 1e-12f);
-    float s = 0.0f;
-    if (A.model == MMRE_TRANSE_L2) {
-      for (int k = lane; k < d; k += kWave) {
-        const float x = (hv[k] / ch + rv[k] / cr) - tv[k] / ct;
-        s += x * x;
-      }
-      s = sqrtf(wave_sum(s));
-    }
-    // dL/dx_k = g * sign(x_k) (L1) or g * x_k / s (L2); x = h^ + r^ - t^
-    // through y = v / max(|v|, eps): dv = (dy - y (y . dy)) / |v|   (|v| > eps), dy / eps otherwise
-    float dh_dot = 0.0f, dt_dot = 0.0f, dr_dot = 0.0f;
-    if (A.norm_flag) {
-      for (int k = lane; k < d; k += kWave) {
-        const float x = (hv[k] / ch + rv[k] / cr) - tv[k] / ct;
-        const float gx = A.model == MMRE_TRANSE_L1 ? g * (float)((x > 0.0f) - (x < 0.0f)) : (s > 0.0f ? g * x / s : 0.0f);
-        dh_dot += (hv[k] / ch) * gx;
-        dr_dot += (rv[k] / cr) * gx;
-        dt_dot += (tv[k] / ct) * (-gx);
-      }
-      dh_dot = wave_sum(dh_dot); dr_dot = wave_sum(dr_dot); dt_dot = wave_sum(dt_dot);
-    }
-    for (int k = lane; k < d; k += kWave) {
-      const float x = (hv[k] / ch + rv[k] / cr) - tv[k] / ct;
-      const float gx = A.model == MMRE_TRANSE_L1 ? g * (float)((x > 0.0f) - (x < 0.0f)) : (s > 0.0f ? g * x / s : 0.0f);
-      float dh = gx, dr = gx, dt = -gx;
-      if (A.norm_flag) {
-        dh = nh > 1e-12f ? (dh - (hv[k] / ch) * dh_dot) / nh : dh / 1e-12f;
-        dr = nr > 1e-12f ? (dr - (rv[k] / cr) * dr_dot) / nr : dr / 1e-12f;
-        dt = nt > 1e-12f ? (dt - (tv[k] / ct) * dt_dot) / nt : dt / 1e-12f;
-      }
-      atomicAdd(&gent[h * d + k], dh + reg_ent * hv[k]);
-      atomicAdd(&gent[t * d + k], dt + reg_ent * tv[k]);
-      atomicAdd(&grel[r * d + k], dr + reg_rel * rv[k]);
-    }
-  } else if (A.model == MMRE_DISTMULT) {
-    const float *hv = A.ent + h * d, *tv = A.ent + t * d, *rv = A.rel + r * d;
-    for (int k = lane; k < d; k += kWave) {
-      atomicAdd(&gent[h * d + k], g * rv[k] * tv[k] + reg_ent * hv[k]);
-      atomicAdd(&gent[t * d + k], g * hv[k] * rv[k] + reg_ent * tv[k]);
-      atomicAdd(&grel[r * d + k], g * hv[k] * tv[k] + reg_rel * rv[k]);
-    }
-  } else if (A.model == MMRE_COMPLEX) {
-    const float *hr = A.ent + h * d, *hi = A.ent_im + h * d, *tr = A.ent + t * d, *ti = A.ent_im + t * d;
-    const float *rr = A.rel + r * d, *ri = A.rel_im + r * d;
-    for (int k = lane; k < d; k += kWave) {
-      atomicAdd(&gent[h * d + k], g * (tr[k] * rr[k] + ti[k] * ri[k]) + reg_ent * hr[k]);
-      atomicAdd(&gent_im[h * d + k], g * (ti[k] * rr[k] - tr[k] * ri[k]) + reg_ent * hi[k]);
-      atomicAdd(&gent[t * d + k], g * (hr[k] * rr[k] - hi[k] * ri[k]) + reg_ent * tr[k]);
-      atomicAdd(&gent_im[t * d + k], g * (hi[k] * rr[k] + hr[k] * ri[k]) + reg_ent * ti[k]);
-      atomicAdd(&grel[r * d + k], g * (hr[k] * tr[k] + hi[k] * ti[k]) + reg_rel * rr[k]);
-      atomicAdd(&grel_im[r * d + k], g * (hr[k] * ti[k] - hi[k] * tr[k]) + reg_rel * ri[k]);
-    }
-  } else {  // RotatE: forward = m - sum_k rho_k
-    const float *hv = A.ent + h * 2 * d, *tv = A.ent + t * 2 * d, *rv = A.rel + r * d;
-    for (int k = lane; k < d; k += kWave) {
-      float s, c;
-      const float th = rv[k] / A.phase_denom;
-      canon_sincos(th, &s, &c);
-      const float hre = hv[k], him = hv[d + k];
-      const float re = hre * c - him * s - tv[k];
-      const float im = hre * s + him * c - tv[d + k];
-      const float rho = sqrtf(re * re + im * im);
-      const float ga = rho > 0.0f ? -g * re / rho : 0.0f;  // dL/d re
-      const float gb = rho > 0.0f ? -g * im / rho : 0.0f;  // dL/d im
-      atomicAdd(&gent[h * 2 * d + k], ga * c + gb * s + reg_ent * hre);
-      atomicAdd(&gent[h * 2 * d + d + k], -ga * s + gb * c + reg_ent * him);
-      atomicAdd(&gent[t * 2 * d + k], -ga + reg_ent * tv[k]);
-      atomicAdd(&gent[t * 2 * d + d + k], -gb + reg_ent * tv[d + k]);
-      const float dth = ga * (-hre * s - him * c) + gb * (hre * c - him * s);
-      atomicAdd(&grel[r * d + k], dth / A.phase_denom + reg_rel * rv[k]);
-    }
   }
 }
 
@@ -299,47 +211,6 @@ __global__ __launch_bounds__(256) void k_ns_reduce(NSArgs A, const float* __rest
   ns_reduce_block(A, part, loss);
 }
 
-__global__ __launch_bounds__(256) void k_ns_backward(NSArgs A, const float* __restrict__ score,
-                                                      const float* __restrict__ grad_loss, float* gent, float* gent_im,
-                                                      float* grel, float* grel_im) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + (threadIdx.x >> 6);
-  if (b >= A.B) return;
-  const float G = grad_loss ? grad_loss[0] : 1.0f;
-  const float p = score[b];
-  float mx = -INFINITY, den = 0.0f;
-  if (A.adv_t > 0.0f) {
-    for (int64_t j = 0; j < A.K; ++j) mx = fmaxf(mx, -score[b + (j + 1) * A.B] * A.adv_t);
-    for (int64_t j = 0; j < A.K; ++j) den += expf(-score[b + (j + 1) * A.B] * A.adv_t - mx);
-  }
-  // regularization gradient scale: regul_rate * (1/3 or 1/6) * 2 v / (N * width)
-  const double N = (double)A.B * (1.0 + (double)A.K);
-  const int ew = A.model == MMRE_ROTATE ? 2 * A.dim : A.dim;
-  const float nterms = A.model == MMRE_COMPLEX ? 6.0f : 3.0f;
-  const float reg_ent = A.regul_rate != 0.0f ? (float)(G * A.regul_rate * 2.0 / (nterms * N * ew)) : 0.0f;
-  const float reg_rel = A.regul_rate != 0.0f ? (float)(G * A.regul_rate * 2.0 / (nterms * N * A.dim)) : 0.0f;
-  float gp = 0.0f;
-  for (int64_t j = 0; j < A.K; ++j) {
-    const float n = score[b + (j + 1) * A.B];
-    const float x = p - n, m = -A.loss_margin;
-    const float ind = x > m ? 1.0f : (x == m ? 0.5f : 0.0f);  // maximum(): ties split the gradient
-    const float c = A.adv_t > 0.0f ? G * (expf(-n * A.adv_t - mx) / den) / (float)A.B : G / (float)(A.B * A.K);
-    gp += c * ind;
-    row_backward(A, b + (j + 1) * A.B, lane, -c * ind, reg_ent, reg_rel, gent, gent_im, grel, grel_im);
-  }
-  row_backward(A, b, lane, gp, reg_ent, reg_rel, gent, gent_im, grel, grel_im);
-}
-
-// model(data) backward for arbitrary rows: dL/d(score of row i) = grad_score[i] (one wave per row).
-__global__ __launch_bounds__(256) void k_rows_backward(NSArgs A, const float* __restrict__ grad_score, float* gent,
-                                                       float* gent_im, float* grel, float* grel_im) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * NS_WAVES + (threadIdx.x >> 6);
-  if (row >= A.B) return;
-  const float g = grad_score[row];
-  if (g != 0.0f) row_backward(A, row, lane, g, 0.0f, 0.0f, gent, gent_im, grel, grel_im);
-}
-
 // ---------------------------------------------------------------------------------------
 // TransE fast path (L1 / L2, with or without norm_flag; dim <= 512).
 // One workgroup of NSW waves per positive: every wave loads the positive's h, r, t rows once
@@ -406,6 +277,12 @@ __device__ __forceinline__ float vsq(const Vec<NC>& a) {
 #pragma unroll
   for (int c = 0; c < NC; ++c) s += a.v[c] * a.v[c];
   return s;
+}
+
+template <int NC>
+__device__ __forceinline__ void vadd(Vec<NC>& a, const Vec<NC>& b, float s) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) a.v[c] += s * b.v[c];
 }
 
 // x = (h / nh + r / nr) - t / nt per element (the forward's association, TransE.py:55-58)
@@ -549,188 +426,6 @@ __global__ __launch_bounds__(256) void k_ns_transe_forward(NSArgs A, float* __re
   }
 }
 
-// dy (gradient w.r.t. the normalised row y = v / max(|v|, eps)) -> gradient w.r.t. v:
-// (dy - y (y . dy)) / |v| when |v| > eps, dy / eps otherwise; then + reg * v. Atomically
-// added, one instruction per 64 consecutive floats (256 contiguous bytes).
-template <int NC>
-__device__ __forceinline__ void scatter_row(float* g, int64_t id, int d, int lane, const Vec<NC>& v, float sq,
-                                            const Vec<NC>& dy, int norm_flag, float reg) {
-  float* o = g + id * d;
-  if (norm_flag) {
-    const float nv = sqrtf(sq);
-    const float cv = fmaxf(nv, 1e-12f);
-    float dot = 0.0f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) dot += (v.v[c] / cv) * dy.v[c];
-    dot = wave_sum(dot);
-    const float scale = nv > 1e-12f ? 1.0f / nv : 1.0f / 1e-12f;
-    const float proj = nv > 1e-12f ? dot : 0.0f;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + c * kWave;
-      if (i < d) atomicAdd(o + i, (dy.v[c] - (v.v[c] / cv) * proj) * scale + reg * v.v[c]);
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + c * kWave;
-      if (i < d) atomicAdd(o + i, dy.v[c] + reg * v.v[c]);
-    }
-  }
-}
-
-// gx = d(loss)/dx for one row (g = d(loss)/d(raw score s)): g sign(x) (L1), g x / |x| (L2)
-template <int NC, bool L2>
-__device__ __forceinline__ void row_gx(Vec<NC>& gx, const NSArgs& A, const RowCtx<NC>& R, float g, int lane) {
-  const float nh = norm_of(R.sh, A.norm_flag), nr = norm_of(R.sr, A.norm_flag), nt = norm_of(R.st, A.norm_flag);
-  float s = 0.0f;
-  if (L2) {
-    s = row_partial<NC, true>(R.h, R.r, R.t, nh, nr, nt);
-    s = sqrtf(wave_sum(s));
-  }
-  const float gs = L2 ? (s > 0.0f ? g / s : 0.0f) : g;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const float x = tx(R.h.v[c], R.r.v[c], R.t.v[c], nh, nr, nt);
-    gx.v[c] = L2 ? gs * x : g * (float)((x > 0.0f) - (x < 0.0f));
-  }
-}
-
-template <int NC>
-__device__ __forceinline__ void vadd(Vec<NC>& a, const Vec<NC>& b, float s) {
-#pragma unroll
-  for (int c = 0; c < NC; ++c) a.v[c] += s * b.v[c];
-}
-
-// one negative row's backward: shared rows accumulate in registers, the others are scattered
-template <int NC, bool L2>
-__device__ __forceinline__ void neg_backward(const NSArgs& A, const RowCtx<NC>& R, int64_t row, float g, int lane,
-                                             float reg_ent, float reg_rel, float* gent, float* grel, Vec<NC>& Gh,
-                                             Vec<NC>& Gr, Vec<NC>& Gt, float& oh, float& orr, float& ot) {
-  const int d = A.dim;
-  if (g == 0.0f && reg_ent == 0.0f && reg_rel == 0.0f) {  // inactive hinge, no regularization: nothing to add
-    oh += R.own_h ? 1.0f : 0.0f;
-    orr += R.own_r ? 1.0f : 0.0f;
-    ot += R.own_t ? 1.0f : 0.0f;
-    return;
-  }
-  Vec<NC> gx;
-  row_gx<NC, L2>(gx, A, R, g, lane);
-  if (R.own_h) { vadd(Gh, gx, 1.0f); oh += 1.0f; }
-  else scatter_row(gent, A.h[row], d, lane, R.h, R.sh, gx, A.norm_flag, reg_ent);
-  if (R.own_r) { vadd(Gr, gx, 1.0f); orr += 1.0f; }
-  else scatter_row(grel, A.r[row], d, lane, R.r, R.sr, gx, A.norm_flag, reg_rel);
-  if (R.own_t) { vadd(Gt, gx, -1.0f); ot += 1.0f; }
-  else {
-    Vec<NC> dt;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) dt.v[c] = -gx.v[c];
-    scatter_row(gent, A.t[row], d, lane, R.t, R.st, dt, A.norm_flag, reg_ent);
-  }
-}
-
-template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const float* __restrict__ score,
-                                                            const float* __restrict__ grad_loss, float* gent,
-                                                            float* grel) {
-  __shared__ float s_c[NS_MAXK];               // d(loss)/d(forward score) of each negative
-  __shared__ float s_gp;                       // ... of the positive
-  __shared__ float s_acc[NSW - 1][3][NC * kWave];
-  __shared__ float s_occ[NSW][3];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t b = blockIdx.x;
-  const int d = A.dim;
-  const float G = grad_loss ? grad_loss[0] : 1.0f;  // NULL: upstream gradient 1
-  const float p = score[b];
-  if (w == 0) {  // coefficients (same formulas as k_ns_backward)
-    float mx = -INFINITY, den = 0.0f;
-    if (A.adv_t > 0.0f) {
-      for (int64_t j = lane; j < A.K; j += kWave) mx = fmaxf(mx, -score[b + (j + 1) * A.B] * A.adv_t);
-#pragma unroll
-      for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
-      for (int64_t j = lane; j < A.K; j += kWave) den += expf(-score[b + (j + 1) * A.B] * A.adv_t - mx);
-      den = wave_sum(den);
-    }
-    float gp = 0.0f;
-    for (int64_t j = lane; j < A.K; j += kWave) {
-      const float n = score[b + (j + 1) * A.B];
-      const float x = p - n, m = -A.loss_margin;
-      const float ind = x > m ? 1.0f : (x == m ? 0.5f : 0.0f);
-      const float c = A.adv_t > 0.0f ? G * (expf(-n * A.adv_t - mx) / den) / (float)A.B : G / (float)(A.B * A.K);
-      s_c[j] = c * ind;
-      gp += c * ind;
-    }
-    gp = wave_sum(gp);
-    if (lane == 0) s_gp = gp;
-  }
-  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
-  RowCtx<NC> P;
-  vload(P.h, A.ent + ph * d, d, lane);
-  vload(P.r, A.rel + pr * d, d, lane);
-  vload(P.t, A.ent + pt * d, d, lane);
-  P.sh = vsq(P.h); P.sr = vsq(P.r); P.st = vsq(P.t);
-  wave_sum3(P.sh, P.sr, P.st);
-  P.own_h = P.own_r = P.own_t = true;
-  const double N = (double)A.B * (1.0 + (double)A.K);
-  const float reg_ent = A.regul_rate != 0.0f ? (float)(G * A.regul_rate * 2.0 / (3.0 * N * d)) : 0.0f;
-  const float reg_rel = reg_ent;
-  __syncthreads();
-  const float sgn = A.use_model_margin ? -1.0f : 1.0f;   // forward = m - s
-  Vec<NC> Gh, Gr, Gt, gx;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) Gh.v[c] = Gr.v[c] = Gt.v[c] = 0.0f;
-  float oh = 0.f, orr = 0.f, ot = 0.f;  // occurrences of the shared rows (regularization)
-  if (w == 0) {
-    row_gx<NC, L2>(gx, A, P, sgn * s_gp, lane);
-    vadd(Gh, gx, 1.0f); vadd(Gr, gx, 1.0f); vadd(Gt, gx, -1.0f);
-    oh = orr = ot = 1.0f;
-  }
-  int64_t j = w;
-  for (; j + NSW < A.K; j += 2 * NSW) {  // two negatives per step: both rows in flight together
-    const int64_t row0 = b + (j + 1) * A.B, row1 = row0 + NSW * A.B;
-    RowCtx<NC> R0, R1;
-    row_ctx_load(R0, A, row0, ph, pr, pt, P, lane);
-    row_ctx_load(R1, A, row1, ph, pr, pt, P, lane);
-    row_ctx_norms(R0, P);
-    row_ctx_norms(R1, P);
-    neg_backward<NC, L2>(A, R0, row0, -sgn * s_c[j], lane, reg_ent, reg_rel, gent, grel, Gh, Gr, Gt, oh, orr, ot);
-    neg_backward<NC, L2>(A, R1, row1, -sgn * s_c[j + NSW], lane, reg_ent, reg_rel, gent, grel, Gh, Gr, Gt, oh, orr,
-                         ot);
-  }
-  if (j < A.K) {
-    const int64_t row = b + (j + 1) * A.B;
-    RowCtx<NC> R;
-    row_ctx_load(R, A, row, ph, pr, pt, P, lane);
-    row_ctx_norms(R, P);
-    neg_backward<NC, L2>(A, R, row, -sgn * s_c[j], lane, reg_ent, reg_rel, gent, grel, Gh, Gr, Gt, oh, orr, ot);
-  }
-  // combine the shared-row accumulators of the waves, then one scatter per shared row
-  if (w > 0) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      s_acc[w - 1][0][c * kWave + lane] = Gh.v[c];
-      s_acc[w - 1][1][c * kWave + lane] = Gr.v[c];
-      s_acc[w - 1][2][c * kWave + lane] = Gt.v[c];
-    }
-  }
-  if (lane == 0) { s_occ[w][0] = oh; s_occ[w][1] = orr; s_occ[w][2] = ot; }
-  __syncthreads();
-  if (w != 0) return;
-  for (int i = 0; i < NSW - 1; ++i) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      Gh.v[c] += s_acc[i][0][c * kWave + lane];
-      Gr.v[c] += s_acc[i][1][c * kWave + lane];
-      Gt.v[c] += s_acc[i][2][c * kWave + lane];
-    }
-  }
-  float nh = 0.f, nr = 0.f, nt = 0.f;
-  for (int i = 0; i < NSW; ++i) { nh += s_occ[i][0]; nr += s_occ[i][1]; nt += s_occ[i][2]; }
-  scatter_row(gent, ph, d, lane, P.h, P.sh, Gh, A.norm_flag, reg_ent * nh);
-  scatter_row(grel, pr, d, lane, P.r, P.sr, Gr, A.norm_flag, reg_rel * nr);
-  scatter_row(gent, pt, d, lane, P.t, P.st, Gt, A.norm_flag, reg_ent * nt);
-}
-
 // ---------------------------------------------------------------------------------------
 // Fused forward + row-owner gradient (TransE fast path, K <= NSW * NSF_MAXJ).
 // The margin loss's d(loss)/d(score) of every row depends only on its own positive's scores
@@ -761,6 +456,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_backward(NSArgs A, const floa
 constexpr int NSF_MAXJ = 8;
 constexpr int NS_BUCKET = 64;   // slot ids kept in a table row's own bucket (one wave's width)
 constexpr int NS_HUB = 512;     // a row with more slots than a bucket orders them in LDS up to this many
+constexpr int NS_HUB_WG = 4;    // owner workgroups for the rows with more slots (HubOrder)
 
 struct NSSlots {        // the row-owner gradient's workspace
   float* shared;        // 3 B rows of dim floats: the positives' own rows (TransE)
@@ -1302,14 +998,15 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
   return v;
 }
 
-// The bucket entries of table row `row` (n = counts[row] of them) in increasing slot id, 64 at
-// a time. `pre` is the lane's entry of the row's bucket, loaded together with the count.
+// The bucket entries of table row `row` (n = counts[row] of them) in increasing slot id, up
+// to 64 at a time (next(take): lane u's entry = the next u-th smallest, INT64_MAX past take).
+// `pre` is the lane's entry of the row's bucket, loaded together with the count.
 //   n <= NS_BUCKET (nearly every row): ranked in registers -- lane l's rank = how many of the
 //     bucket's entries are smaller -- and a ds_permute sends each entry to the lane of its rank;
 //   NS_BUCKET < n <= NS_HUB (a hub row, e.g. a frequent relation): bucket + the row's overflow
-//     pairs collected into the wave's LDS list and bitonic-sorted there;
-//   n > NS_HUB: the next 64 by repeated wave minima over bucket + overflow (slow, rare).
-// chunk(c0) returns lane u's entry = the (c0 + u)-th smallest (INT64_MAX past n).
+//     pairs collected into the wave's LDS list and bitonic-sorted there.
+// Rows with n > NS_HUB are not ordered by their wave: the owner kernels hand them to extra
+// workgroups that order them cooperatively (HubOrder).
 struct SlotOrder {
   const int64_t* ovf;
   int n_ovf, n, lane;
@@ -1317,10 +1014,10 @@ struct SlotOrder {
   int64_t* hub;      // this wave's LDS list (NS_HUB entries)
   int64_t pre;       // lane's bucket entry
   int64_t regs;      // n <= 64: lane u's ordered entry
-  int64_t prev;      // selection path: the last entry taken
+  int pos;           // entries handed out so far
 
   __device__ void init() {
-    prev = -1;
+    pos = 0;
     if (n <= NS_BUCKET) {
       const int64_t mine = lane < n ? pre : INT64_MAX;
       int rank = 0;
@@ -1331,7 +1028,6 @@ struct SlotOrder {
       regs = (int64_t)(((uint64_t)hi << 32) | lo);
       return;
     }
-    if (n > NS_HUB) return;
     hub[lane] = pre;  // a full bucket
     int m = NS_BUCKET;
     for (int base = 0; base < n_ovf; base += kWave) {
@@ -1363,26 +1059,163 @@ struct SlotOrder {
     }
   }
 
-  __device__ int64_t chunk(int c0) {
+  __device__ int64_t next(int& take) {
+    take = (n - pos) < kWave ? (n - pos) : kWave;
+    const int c0 = pos;
+    pos += take;
     if (n <= NS_BUCKET) return regs;
-    if (n <= NS_HUB) return c0 + lane < n ? hub[c0 + lane] : INT64_MAX;
-    int64_t out = INT64_MAX;
-    const int take = n - c0 < kWave ? n - c0 : kWave;
-    for (int u = 0; u < take; ++u) {
-      int64_t v = pre > prev ? pre : INT64_MAX;
-      for (int e = lane; e < n_ovf; e += kWave) {
-        if (ovf[2 * (int64_t)e] == row) {
-          const int64_t sv = ovf[2 * (int64_t)e + 1];
-          if (sv > prev && sv < v) v = sv;
-        }
-      }
-      v = wave_min_i64(v);
-      if (lane == u) out = v;
-      prev = v;
-    }
-    return out;
+    return lane < take ? hub[c0 + lane] : INT64_MAX;
   }
 };
+
+// Hub rows (n > NS_HUB slots: a relation shared by thousands of the batch's rows) are ordered by
+// a whole workgroup in windows of slot ids: a histogram pass over the row's entries (bucket +
+// its pairs in the overflow list) picks the widest window [lo, hi) holding at most HUB_CAP of
+// them, a collect pass gathers those into LDS, a bitonic sort over 256 threads orders them,
+// and next() hands them out 64 at a time; then the next window. Linear in the row's entries
+// per window (the repeated wave minima it replaces were quadratic). Every member of the
+// workgroup calls next() the same number of times (it synchronises); LDS: 4 KB of histogram +
+// HUB_CAP entries, inside the owner kernels' 16-KB s_hub.
+constexpr int HUB_BINS = 1024;
+constexpr int HUB_CAP = 1024;
+struct HubOrder {
+  const int64_t* bucket;
+  const int64_t* ovf;
+  int n_ovf, n;
+  int64_t row, n_slots;  // slot ids are < n_slots
+  int32_t* hist;         // HUB_BINS counters
+  int64_t* buf;          // HUB_CAP entries
+  int32_t* s_cnt;        // LDS scalars: [0] collected, [1] bins taken
+  int64_t lo;            // the next window starts at this slot id
+  int wn, wi;            // entries in the window, handed out
+
+  __device__ void init() { lo = 0; wn = wi = 0; }
+
+  template <class F>
+  __device__ __forceinline__ void for_entries(F&& f) {  // every entry of the row, any order
+    const int tid = threadIdx.x;
+    if (tid < NS_BUCKET) f(bucket[row * NS_BUCKET + tid]);
+    for (int e = tid; e < n_ovf; e += blockDim.x)
+      if (ovf[2 * (int64_t)e] == row) f(ovf[2 * (int64_t)e + 1]);
+  }
+
+  __device__ void build() {
+    const int tid = threadIdx.x;
+    int64_t span = n_slots - lo;
+    int64_t hi = n_slots;
+    for (;;) {
+      const int64_t binw = (span + HUB_BINS - 1) / HUB_BINS;
+      __syncthreads();
+      for (int i = tid; i < HUB_BINS; i += blockDim.x) hist[i] = 0;
+      __syncthreads();
+      for_entries([&](int64_t e) {
+        const int64_t sl = entry_slot(e);
+        if (sl >= lo && sl < lo + span) atomicAdd(&hist[(int)((sl - lo) / binw)], 1);
+      });
+      __syncthreads();
+      if (tid < kWave) {  // wave 0: the longest run of leading bins holding <= HUB_CAP entries
+        constexpr int PER = HUB_BINS / kWave;
+        int loc = 0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) loc += hist[tid * PER + i];
+        int inc = loc;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+          const int v = __shfl_up(inc, o);
+          if (tid >= o) inc += v;
+        }
+        const int before = inc - loc;
+        // the first lane whose run passes the cap finds the exact bin; all lanes within: every bin
+        const uint64_t over = __ballot(inc > HUB_CAP);
+        int taken = HUB_BINS;
+        if (over) {
+          const int L = __builtin_ctzll(over);
+          if (tid == L) {
+            int c = before, b = 0;
+            while (b < PER && c + hist[tid * PER + b] <= HUB_CAP) c += hist[tid * PER + b++];
+            s_cnt[1] = L * PER + b;
+          }
+        } else if (tid == 0) {
+          s_cnt[1] = taken;
+        }
+      }
+      __syncthreads();
+      const int nb = s_cnt[1];
+      if (nb > 0) {
+        hi = nb == HUB_BINS ? lo + span : lo + (int64_t)nb * binw;
+        break;
+      }
+      span = binw;  // the first bin alone holds more than HUB_CAP: narrow to it (binw >= 1 id -> <= 1 entry)
+    }
+    if (tid == 0) s_cnt[0] = 0;
+    __syncthreads();
+    for_entries([&](int64_t e) {
+      const int64_t sl = entry_slot(e);
+      if (sl >= lo && sl < hi) buf[atomicAdd(&s_cnt[0], 1)] = e;
+    });
+    __syncthreads();
+    wn = s_cnt[0];
+    int M = 2;
+    while (M < wn) M <<= 1;
+    for (int i = wn + tid; i < M; i += blockDim.x) buf[i] = INT64_MAX;
+    __syncthreads();
+    for (int k = 2; k <= M; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < M; i += blockDim.x) {
+          const int x = i ^ j;
+          if (x > i) {
+            const int64_t a = buf[i], b = buf[x];
+            const bool up = (i & k) == 0;
+            if ((a > b) == up) { buf[i] = b; buf[x] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    lo = hi;
+    wi = 0;
+  }
+
+  __device__ int64_t next(int& take) {
+    while (wi == wn) build();  // uniform over the workgroup (wn, wi come from LDS after a barrier)
+    take = (wn - wi) < kWave ? (wn - wi) : kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int64_t e = lane < take ? buf[wi + lane] : INT64_MAX;
+    wi += take;
+    return e;
+  }
+};
+
+// The hub rows of the table (n > NS_HUB), in row order, dealt round-robin to the kernel's
+// n_hub_wg extra workgroups: hb-th of them calls f(row, n) for the rows k = hb, hb + n_hub_wg, ...
+// (the whole workgroup together).
+template <class F>
+__device__ __forceinline__ void for_hub_rows(const int32_t* __restrict__ counts, int64_t n_rows, int hb, int n_hub_wg,
+                                             uint64_t* s_masks, F&& f) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int64_t k = 0;
+  for (int64_t base = 0; base < n_rows; base += 256) {
+    const int64_t row = base + tid;
+    const bool hub = row < n_rows && counts[row] > NS_HUB;
+    const uint64_t m = __ballot(hub);
+    if (lane == 0) s_masks[w] = m;
+    __syncthreads();
+    uint64_t mk[4] = {s_masks[0], s_masks[1], s_masks[2], s_masks[3]};
+    __syncthreads();
+    for (int ww = 0; ww < 4; ++ww) {
+      uint64_t mm = mk[ww];
+      while (mm) {
+        const int b = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        if (k % n_hub_wg == hb) {
+          const int64_t r = base + ww * 64 + b;
+          f(r, counts[r]);
+        }
+        ++k;
+      }
+    }
+  }
+}
 
 // One wave per table row (entities, then relations): the row's slots summed in batch order,
 // d(loss)/d(raw row) = (dy - y (y . dy)) / |v| with y = v / max(|v|, eps) when the model
@@ -1390,53 +1223,28 @@ struct SlotOrder {
 // written to every row of the gradient table. sgd_lr > 0 (the optimizer's plain SGD step fused
 // in, mmre_ns_fused_grad_sgd): the row's parameters also become fma(-lr, g, v), torch's SGD
 // arithmetic; rows without slots keep theirs (p - lr * 0 = p).
-template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ ent, const float* __restrict__ rel,
-                                                      int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
-                                                      const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
-                                                      const float* __restrict__ shared, const float* __restrict__ rec,
-                                                      const int32_t* __restrict__ counts,
-                                                      const int64_t* __restrict__ bucket, const int64_t* __restrict__ ovf,
-                                                      const int32_t* __restrict__ ovf_n, int64_t K,
-                                                      const float* __restrict__ grad_loss, float* __restrict__ gent,
-                                                      float* __restrict__ grel, float sgd_lr, float* __restrict__ pent,
-                                                      float* __restrict__ prel, NSArgs RA, const float* __restrict__ part,
-                                                      float* __restrict__ loss, int64_t reduce_block) {
-  __shared__ int64_t s_hub[4][NS_HUB];
-  if ((int64_t)blockIdx.x == reduce_block) {  // the training step's loss (mmre_ns_step_openke): one extra workgroup
-    ns_reduce_block(RA, part, loss);
-    return;
-  }
+// One table row's gradient from its ordered slots (Ord: SlotOrder for a wave, HubOrder for a
+// workgroup; with a HubOrder every wave of the workgroup calls this for the same row -- next()
+// synchronises -- and only the `active` one loads, sums and writes). v / nv: the row and its norm.
+template <int NC, bool L2, class Ord>
+__device__ __forceinline__ void transe_owner_row(Ord& ord, bool active, int64_t row, int n, const Vec<NC>& v,
+                                                 float nv, int64_t n_ent, int d, int norm_flag, float reg,
+                                                 const float* __restrict__ shared, const float* __restrict__ rec,
+                                                 int64_t K, const float* __restrict__ grad_loss, float* gent,
+                                                 float* grel, float sgd_lr, float* pent, float* prel) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
-  float* o = (is_ent ? gent : grel) + id * d;
-  // the count, the lane's bucket entry (meaningful below the count), the row itself and its
-  // norm: one round trip, all in flight together
-  const int n = counts[row];
-  const int64_t pre = bucket[row * NS_BUCKET + lane];
-  Vec<NC> v;
-  vload_row(v, is_ent ? ent : rel, id, d, lane);
-  const float nv = (is_ent ? nrm_e : nrm_r)[id];
-  if (n == 0) {  // not in the batch: zero gradient (and an unchanged parameter row)
-    Vec<NC> z;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) z.v[c] = 0.0f;
-    vstore_row(o, 0, z, d, lane);
-    return;
-  }
   const int64_t spp = 3 + 3 * K;
   Vec<NC> dy;
 #pragma unroll
   for (int c = 0; c < NC; ++c) dy.v[c] = 0.0f;
   float cnt = 0.0f;
-  SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, -1};
-  ord.init();
-  for (int c0 = 0; c0 < n; c0 += kWave) {
-    const int take = (n - c0) < kWave ? (n - c0) : kWave;
-    const int64_t ordered = ord.chunk(c0);
+  for (int c0 = 0; c0 < n;) {
+    int take;
+    const int64_t ordered = ord.next(take);
+    c0 += take;
+    if (!active) continue;
     int64_t src = 0;  // shared row index, or -(record index + 1) for a negative's record
     float sg = 0.0f, m = 0.0f;
     if (lane < take) {  // lane u decodes its slot: where its contribution lives, and its sign
@@ -1477,6 +1285,7 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
       for (int c = 0; c < NC; ++c) dy.v[c] += g0 * v0.v[c];
     }
   }
+  if (!active) return;
   const float G = grad_loss ? grad_loss[0] : 1.0f;
   const float rr = reg * cnt;
   if (norm_flag) {
@@ -1493,12 +1302,92 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* __restrict__ 
 #pragma unroll
     for (int c = 0; c < NC; ++c) dy.v[c] = (dy.v[c] + rr * v.v[c]) * G;
   }
+  float* o = (is_ent ? gent : grel) + id * d;
   vstore_row(o, 0, dy, d, lane);
   if (sgd_lr != 0.0f) {
+    Vec<NC> p;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) v.v[c] = __builtin_fmaf(-sgd_lr, dy.v[c], v.v[c]);
-    vstore_row(is_ent ? pent : prel, id, v, d, lane);
+    for (int c = 0; c < NC; ++c) p.v[c] = __builtin_fmaf(-sgd_lr, dy.v[c], v.v[c]);
+    vstore_row(is_ent ? pent : prel, id, p, d, lane);
   }
+}
+
+// The hub workgroups' LDS view of an owner kernel's s_hub (16 KB): histogram, then entries.
+__device__ __forceinline__ HubOrder hub_order(int64_t (*s_hub)[NS_HUB], int32_t* s_hc, const int64_t* bucket,
+                                              const int64_t* ovf, int n_ovf, int n, int64_t row, int64_t n_slots) {
+  int64_t* flat = &s_hub[0][0];
+  static_assert(4 * NS_HUB >= HUB_BINS / 2 + HUB_CAP, "hub LDS");
+  HubOrder o{bucket, ovf, n_ovf, n, row, n_slots, reinterpret_cast<int32_t*>(flat), flat + HUB_BINS / 2, s_hc, 0, 0, 0};
+  o.init();
+  return o;
+}
+
+// One wave per table row (entities, then relations): the row's slots summed in batch order,
+// d(loss)/d(raw row) = (dy - y (y . dy)) / |v| with y = v / max(|v|, eps) when the model
+// normalises (dy / eps below eps), + reg * (occurrences) * v, times the upstream gradient;
+// written to every row of the gradient table. sgd_lr > 0 (the optimizer's plain SGD step fused
+// in, mmre_ns_fused_grad_sgd): the row's parameters also become fma(-lr, g, v), torch's SGD
+// arithmetic; rows without slots keep theirs (p - lr * 0 = p). Rows with more than NS_HUB slots
+// go to the n_hub_wg workgroups from hub_block0 on (HubOrder). With SGD the parameter tables
+// ent / rel are also pent / prel (read, then written, by the row's own wave): not __restrict__.
+template <int NC, bool L2>
+__global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const float* rel,
+                                                      int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
+                                                      const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
+                                                      const float* __restrict__ shared, const float* __restrict__ rec,
+                                                      const int32_t* __restrict__ counts,
+                                                      const int64_t* __restrict__ bucket, const int64_t* __restrict__ ovf,
+                                                      const int32_t* __restrict__ ovf_n, int64_t K,
+                                                      const float* __restrict__ grad_loss, float* __restrict__ gent,
+                                                      float* __restrict__ grel, float sgd_lr, float* pent,
+                                                      float* prel, NSArgs RA, const float* __restrict__ part,
+                                                      float* __restrict__ loss, int64_t reduce_block,
+                                                      int64_t hub_block0, int n_hub_wg, int64_t n_slots) {
+  __shared__ int64_t s_hub[4][NS_HUB];
+  __shared__ uint64_t s_masks[4];
+  __shared__ int32_t s_hc[2];
+  if ((int64_t)blockIdx.x == reduce_block) {  // the training step's loss (mmre_ns_step_openke): one extra workgroup
+    ns_reduce_block(RA, part, loss);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  if ((int64_t)blockIdx.x >= hub_block0) {  // hub rows, a workgroup each
+    for_hub_rows(counts, n_ent + n_rel, (int)((int64_t)blockIdx.x - hub_block0), n_hub_wg, s_masks,
+                 [&](int64_t row, int n) {
+                   const bool is_ent = row < n_ent;
+                   const int64_t id = is_ent ? row : row - n_ent;
+                   Vec<NC> v;
+                   vload_row(v, is_ent ? ent : rel, id, d, lane);
+                   const float nv = (is_ent ? nrm_e : nrm_r)[id];
+                   HubOrder ord = hub_order(s_hub, s_hc, bucket, ovf, ovf_n[0], n, row, n_slots);
+                   transe_owner_row<NC, L2>(ord, threadIdx.x < 64, row, n, v, nv, n_ent, d, norm_flag, reg, shared,
+                                            rec, K, grad_loss, gent, grel, sgd_lr, pent, prel);
+                 });
+    return;
+  }
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_ent + n_rel) return;  // wave-uniform
+  const bool is_ent = row < n_ent;
+  const int64_t id = is_ent ? row : row - n_ent;
+  // the count, the lane's bucket entry (meaningful below the count), the row itself and its
+  // norm: one round trip, all in flight together
+  const int n = counts[row];
+  const int64_t pre = bucket[row * NS_BUCKET + lane];
+  Vec<NC> v;
+  vload_row(v, is_ent ? ent : rel, id, d, lane);
+  const float nv = (is_ent ? nrm_e : nrm_r)[id];
+  if (n > NS_HUB) return;  // a hub workgroup's row
+  if (n == 0) {  // not in the batch: zero gradient (and an unchanged parameter row)
+    Vec<NC> z;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) z.v[c] = 0.0f;
+    vstore_row((is_ent ? gent : grel) + id * d, 0, z, d, lane);
+    return;
+  }
+  SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, 0};
+  ord.init();
+  transe_owner_row<NC, L2>(ord, true, row, n, v, nv, n_ent, d, norm_flag, reg, shared, rec, K, grad_loss, gent, grel,
+                           sgd_lr, pent, prel);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1740,7 +1629,7 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
   }
 }
 
-// One wave per positive: the loss's d/d(score) coefficients of its rows (k_ns_backward's
+// One wave per positive: the loss's d/d(score) coefficients of its rows (k_ns_row_coef's
 // formulas, unit upstream gradient), each row's gradient; what a negative adds to a row it
 // shares with its positive (same role, same id) is summed in registers, every other row gets
 // a slot of its own. Inactive rows (zero coefficient, no regularization) add nothing.
@@ -1878,56 +1767,26 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
   }
 }
 
-// One wave per table row: its slots' records summed in slot order, + reg (occurrences) v, times
-// the upstream gradient, written to every row of the gradient tables (and, with sgd_lr, the
-// parameter rows updated by fma(-lr, g, v)).
-template <int NC>
-__global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, int64_t n_rel, float reg_ent,
-                                                      float reg_rel, const float* __restrict__ rec,
-                                                      const int32_t* __restrict__ counts,
-                                                      const int64_t* __restrict__ bucket,
-                                                      const int64_t* __restrict__ ovf, const int32_t* __restrict__ ovf_n,
-                                                      int dpad, const float* __restrict__ grad_loss, float* gent,
-                                                      float* gent_im, float* grel, float* grel_im, float sgd_lr,
-                                                      float* pent, float* pent_im, float* prel, float* prel_im) {
-  __shared__ int64_t s_hub[4][NS_HUB];
+// One table row of the generic owner from its ordered slots (Ord as for transe_owner_row).
+template <int NC, class Ord>
+__device__ __forceinline__ void gen_owner_row(Ord& ord, bool active, const NSArgs& A, int64_t row, int n,
+                                              const Row2<NC>& v, int64_t n_ent, float reg_ent, float reg_rel,
+                                              const float* __restrict__ rec, const float* __restrict__ grad_loss,
+                                              float* oa, float* ob, float* pa, float* pb, float sgd_lr) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
-  const int64_t id = is_ent ? row : row - n_ent;
   const int d = A.dim;
-  const int64_t pre = bucket[row * NS_BUCKET + lane];
   const bool two = A.model == MMRE_COMPLEX || (A.model == MMRE_ROTATE && is_ent);
-  const bool s2 = A.model != MMRE_DISTMULT;  // record stride (rec_store)
-  // output rows of the two halves
-  float *oa, *ob = nullptr, *pa = nullptr, *pb = nullptr;
-  if (is_ent) {
-    if (A.model == MMRE_COMPLEX) { oa = gent + id * d; ob = gent_im + id * d; pa = pent ? pent + id * d : nullptr; pb = pent_im ? pent_im + id * d : nullptr; }
-    else if (A.model == MMRE_ROTATE) { oa = gent + id * 2 * d; ob = oa + d; pa = pent ? pent + id * 2 * d : nullptr; pb = pa ? pa + d : nullptr; }
-    else { oa = gent + id * d; pa = pent ? pent + id * d : nullptr; }
-  } else {
-    oa = grel + id * d;
-    pa = prel ? prel + id * d : nullptr;
-    if (A.model == MMRE_COMPLEX) { ob = grel_im + id * d; pb = prel_im ? prel_im + id * d : nullptr; }
-  }
-  const int n = counts[row];
+  const bool s2 = A.model == MMRE_COMPLEX || A.model == MMRE_ROTATE;  // record stride (rec_store); TransE: d
   Row2<NC> dy;
   vzero(dy.a);
   vzero(dy.b);
-  if (n == 0) {
-    vstore(oa, dy.a, d, lane);
-    if (two) vstore(ob, dy.b, d, lane);
-    return;
-  }
-  Row2<NC> v;
-  gen_load(v, A, is_ent, id, lane);
   float cnt = 0.0f;
-  SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, -1};
-  ord.init();
-  for (int c0 = 0; c0 < n; c0 += kWave) {
-    const int take = (n - c0) < kWave ? (n - c0) : kWave;
-    const int64_t ordered = ord.chunk(c0);
+  for (int c0 = 0; c0 < n;) {
+    int take;
+    const int64_t ordered = ord.next(take);
+    c0 += take;
+    if (!active) continue;
     const int sl = lane < take ? (int)entry_slot(ordered) : 0;
     cnt += wave_sum(lane < take ? entry_mult(ordered) : 0.0f);  // integer-valued: exact in any order
     int u = 0;
@@ -1944,6 +1803,7 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
       row2_add(dy, r0);
     }
   }
+  if (!active) return;
   const float G = grad_loss ? grad_loss[0] : 1.0f;
   const float rr = (is_ent ? reg_ent : reg_rel) * cnt;
 #pragma unroll
@@ -1954,13 +1814,207 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
   vstore(oa, dy.a, d, lane);
   if (two) vstore(ob, dy.b, d, lane);
   if (sgd_lr != 0.0f) {
+    Row2<NC> p;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      v.a.v[c] = __builtin_fmaf(-sgd_lr, dy.a.v[c], v.a.v[c]);
-      v.b.v[c] = __builtin_fmaf(-sgd_lr, dy.b.v[c], v.b.v[c]);
+      p.a.v[c] = __builtin_fmaf(-sgd_lr, dy.a.v[c], v.a.v[c]);
+      p.b.v[c] = __builtin_fmaf(-sgd_lr, dy.b.v[c], v.b.v[c]);
     }
-    vstore(pa, v.a, d, lane);
-    if (two) vstore(pb, v.b, d, lane);
+    vstore(pa, p.a, d, lane);
+    if (two) vstore(pb, p.b, d, lane);
+  }
+}
+
+// One wave per table row: its slots' records summed in slot order, + reg (occurrences) v, times
+// the upstream gradient, written to every row of the gradient tables (and, with sgd_lr, the
+// parameter rows updated by fma(-lr, g, v)). Rows with more than NS_HUB slots go to the
+// n_hub_wg workgroups from hub_block0 on (HubOrder).
+template <int NC>
+__global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, int64_t n_rel, float reg_ent,
+                                                      float reg_rel, const float* __restrict__ rec,
+                                                      const int32_t* __restrict__ counts,
+                                                      const int64_t* __restrict__ bucket,
+                                                      const int64_t* __restrict__ ovf, const int32_t* __restrict__ ovf_n,
+                                                      int dpad, const float* __restrict__ grad_loss, float* gent,
+                                                      float* gent_im, float* grel, float* grel_im, float sgd_lr,
+                                                      float* pent, float* pent_im, float* prel, float* prel_im,
+                                                      int64_t hub_block0, int n_hub_wg, int64_t n_slots) {
+  __shared__ int64_t s_hub[4][NS_HUB];
+  __shared__ uint64_t s_masks[4];
+  __shared__ int32_t s_hc[2];
+  (void)dpad;
+  const int lane = threadIdx.x & 63;
+  const int d = A.dim;
+  // output rows of the two halves of table row `row`
+  auto outs = [&](int64_t row, float*& oa, float*& ob, float*& pa, float*& pb) {
+    const bool is_ent = row < n_ent;
+    const int64_t id = is_ent ? row : row - n_ent;
+    ob = pa = pb = nullptr;
+    if (is_ent) {
+      if (A.model == MMRE_COMPLEX) { oa = gent + id * d; ob = gent_im + id * d; pa = pent ? pent + id * d : nullptr; pb = pent_im ? pent_im + id * d : nullptr; }
+      else if (A.model == MMRE_ROTATE) { oa = gent + id * 2 * d; ob = oa + d; pa = pent ? pent + id * 2 * d : nullptr; pb = pa ? pa + d : nullptr; }
+      else { oa = gent + id * d; pa = pent ? pent + id * d : nullptr; }
+    } else {
+      oa = grel + id * d;
+      pa = prel ? prel + id * d : nullptr;
+      if (A.model == MMRE_COMPLEX) { ob = grel_im + id * d; pb = prel_im ? prel_im + id * d : nullptr; }
+    }
+  };
+  if ((int64_t)blockIdx.x >= hub_block0) {  // hub rows, a workgroup each
+    for_hub_rows(counts, n_ent + n_rel, (int)((int64_t)blockIdx.x - hub_block0), n_hub_wg, s_masks,
+                 [&](int64_t row, int n) {
+                   const bool is_ent = row < n_ent;
+                   float *oa, *ob, *pa, *pb;
+                   outs(row, oa, ob, pa, pb);
+                   Row2<NC> v;
+                   gen_load(v, A, is_ent, is_ent ? row : row - n_ent, lane);
+                   HubOrder ord = hub_order(s_hub, s_hc, bucket, ovf, ovf_n[0], n, row, n_slots);
+                   gen_owner_row<NC>(ord, threadIdx.x < 64, A, row, n, v, n_ent, reg_ent, reg_rel, rec, grad_loss, oa,
+                                     ob, pa, pb, sgd_lr);
+                 });
+    return;
+  }
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= n_ent + n_rel) return;  // wave-uniform
+  const bool is_ent = row < n_ent;
+  const int64_t id = is_ent ? row : row - n_ent;
+  const int64_t pre = bucket[row * NS_BUCKET + lane];
+  const bool two = A.model == MMRE_COMPLEX || (A.model == MMRE_ROTATE && is_ent);
+  float *oa, *ob, *pa, *pb;
+  outs(row, oa, ob, pa, pb);
+  const int n = counts[row];
+  if (n > NS_HUB) return;  // a hub workgroup's row
+  if (n == 0) {
+    Row2<NC> z;
+    vzero(z.a);
+    vzero(z.b);
+    vstore(oa, z.a, d, lane);
+    if (two) vstore(ob, z.b, d, lane);
+    return;
+  }
+  Row2<NC> v;
+  gen_load(v, A, is_ent, id, lane);
+  SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, 0};
+  ord.init();
+  gen_owner_row<NC>(ord, true, A, row, n, v, n_ent, reg_ent, reg_rel, rec, grad_loss, oa, ob, pa, pb, sgd_lr);
+}
+
+// ---------------------------------------------------------------------------------------
+// Deterministic backward of model(data) over ARBITRARY rows (mmre_score_rows_backward: OpenKE
+// Model.forward in 'normal' mode under any loss -- SoftplusLoss, SigmoidLoss, cross modes -- and
+// the repo's scoring_fn / _calc) and of the non-fused margin loss (mmre_ns_backward). No float
+// atomics: scored row i files three slots 3i + q (its h / r / t gradient row, raw space) into
+// the buckets of their table rows, and k_ns_gen_owner sums each table row's slots in slot order
+// (= batch order), so the gradient tables are bit-identical run to run.
+// ---------------------------------------------------------------------------------------
+
+// TransE (L1 / L2, optional norm_flag) gradient of one row in RAW space: the per-element
+// expressions of the TransE forward's derivative (x = (h/|h| + r/|r|) - t/|t|, TransE.py:46-74;
+// gx = g sign(x) or g x / |x|; the normalisation's Jacobian (dy - y (y . dy)) / |v|), on rows held
+// in registers.
+template <int NC>
+__device__ __forceinline__ void transe_row_grad(const NSArgs& A, const Row2<NC>& H, const Row2<NC>& R,
+                                                const Row2<NC>& T, float g, Row2<NC>& dH, Row2<NC>& dR,
+                                                Row2<NC>& dT) {
+  const bool l2 = A.model == MMRE_TRANSE_L2;
+  if (A.use_model_margin) g = -g;  // forward = m - s
+  float nh = 1.0f, nt = 1.0f, nr = 1.0f;
+  if (A.norm_flag) {
+    float a = vsq(H.a), b = vsq(T.a), c = vsq(R.a);
+    wave_sum3(a, b, c);
+    nh = sqrtf(a); nt = sqrtf(b); nr = sqrtf(c);
+  }
+  const float ch = fmaxf(nh, 1e-12f), ct = fmaxf(nt, 1e-12f), cr = fmaxf(nr, 1e-12f);
+  float s = 0.0f;
+  if (l2) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float x = (H.a.v[c] / ch + R.a.v[c] / cr) - T.a.v[c] / ct;
+      s += x * x;
+    }
+    s = sqrtf(wave_sum(s));
+  }
+  Vec<NC> gx;
+  float dh_dot = 0.0f, dt_dot = 0.0f, dr_dot = 0.0f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float x = (H.a.v[c] / ch + R.a.v[c] / cr) - T.a.v[c] / ct;
+    gx.v[c] = !l2 ? g * (float)((x > 0.0f) - (x < 0.0f)) : (s > 0.0f ? g * x / s : 0.0f);
+    dh_dot += (H.a.v[c] / ch) * gx.v[c];
+    dr_dot += (R.a.v[c] / cr) * gx.v[c];
+    dt_dot += (T.a.v[c] / ct) * (-gx.v[c]);
+  }
+  if (A.norm_flag) wave_sum3(dh_dot, dr_dot, dt_dot);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float dh = gx.v[c], dr = gx.v[c], dt = -gx.v[c];
+    if (A.norm_flag) {
+      dh = nh > 1e-12f ? (dh - (H.a.v[c] / ch) * dh_dot) / nh : dh / 1e-12f;
+      dr = nr > 1e-12f ? (dr - (R.a.v[c] / cr) * dr_dot) / nr : dr / 1e-12f;
+      dt = nt > 1e-12f ? (dt - (T.a.v[c] / ct) * dt_dot) / nt : dt / 1e-12f;
+    }
+    dH.a.v[c] = dh; dR.a.v[c] = dr; dT.a.v[c] = dt;
+    dH.b.v[c] = dR.b.v[c] = dT.b.v[c] = 0.0f;
+  }
+}
+
+// d(loss)/d(score) of every row of the margin loss (MarginLoss.py:24-28 with the detached
+// self-adversarial weights of :19-22 through NegativeSampling.py:23-32; unit upstream
+// gradient): coef[b] = sum_j c_j ind_j for positive b, coef[b + (j + 1) B] = -c_j ind_j.
+__global__ __launch_bounds__(256) void k_ns_row_coef(NSArgs A, const float* __restrict__ score,
+                                                      float* __restrict__ coef) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (b >= A.B) return;
+  const float p = score[b];
+  float mx = -INFINITY, den = 0.0f;
+  if (A.adv_t > 0.0f) {
+    for (int64_t j = lane; j < A.K; j += kWave) mx = fmaxf(mx, -score[b + (j + 1) * A.B] * A.adv_t);
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) mx = fmaxf(mx, __shfl_xor(mx, s));
+    for (int64_t j = lane; j < A.K; j += kWave) den += expf(-score[b + (j + 1) * A.B] * A.adv_t - mx);
+    den = wave_sum(den);
+  }
+  float gp = 0.0f;
+  for (int64_t j = lane; j < A.K; j += kWave) {
+    const float n = score[b + (j + 1) * A.B];
+    const float x = p - n, m = -A.loss_margin;
+    const float ind = x > m ? 1.0f : (x == m ? 0.5f : 0.0f);  // maximum(): ties split the gradient
+    const float c = A.adv_t > 0.0f ? (expf(-n * A.adv_t - mx) / den) / (float)A.B : 1.0f / (float)(A.B * A.K);
+    coef[b + (j + 1) * A.B] = -(c * ind);
+    gp += c * ind;
+  }
+  gp = wave_sum(gp);
+  if (lane == 0) coef[b] = gp;
+}
+
+// One wave per scored row: its three gradient rows as slot records 3i + q (q = h, r, t) and the
+// slots filed in their table rows' buckets (occurrence weight 1: the regularization counts every
+// gathered row). Rows adding nothing (zero coefficient, no regularization) file nothing.
+template <int NC>
+__global__ __launch_bounds__(256) void k_rows_slots(NSArgs A, const float* __restrict__ coef, int64_t n_rows,
+                                                    NSSlots S, int64_t n_ent, int with_reg) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * NS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (i >= n_rows) return;  // wave-uniform
+  const float g = coef[i];
+  if (g == 0.0f && !with_reg) return;
+  const int d = A.dim;
+  const int64_t h = A.h[i], t = A.t[i], r = A.r[i];
+  Row2<NC> H, R, T, dH, dR, dT;
+  gen_load(H, A, true, h, lane);
+  gen_load(R, A, false, r, lane);
+  gen_load(T, A, true, t, lane);
+  if (A.model == MMRE_TRANSE_L1 || A.model == MMRE_TRANSE_L2) transe_row_grad(A, H, R, T, g, dH, dR, dT);
+  else gen_row_grad(A, H, R, T, g, dH, dR, dT);
+  const bool s2 = A.model == MMRE_COMPLEX || A.model == MMRE_ROTATE;  // k_ns_gen_owner's record layout
+  const bool e2 = s2, r2 = A.model == MMRE_COMPLEX;
+  rec_store(S.rec, 3 * i, d, s2, e2, dH, lane);
+  rec_store(S.rec, 3 * i + 1, d, s2, r2, dR, lane);
+  rec_store(S.rec, 3 * i + 2, d, s2, e2, dT, lane);
+  if (lane < 3) {
+    const uint32_t key = lane == 0 ? (uint32_t)h : (lane == 1 ? (uint32_t)(n_ent + r) : (uint32_t)t);
+    put_slot(S, key, 3 * i + lane, 1.0f);
   }
 }
 
@@ -2037,42 +2091,98 @@ extern "C" int mmre_ns_forward(int model, int norm_flag, float model_margin, int
   return MMRE_OK;
 }
 
+// Workspace of the rows backward (floats): per-row coefficients, 3 slot records per row,
+// per-table-row slot counts (+ the overflow count), buckets, overflow pairs.
+struct RowsWs {
+  int64_t coef, rec, counts, bucket, ovf, total;
+};
+static int64_t al64r(int64_t x) { return (x + 63) & ~(int64_t)63; }
+static void rows_ws(int model, int64_t n_rows, int64_t E, int64_t R, int d, RowsWs& w) {
+  const int64_t width = (model == MMRE_COMPLEX || model == MMRE_ROTATE) ? 2 * (int64_t)d : d;
+  int64_t o = 0;
+  w.coef = o;   o = al64r(o + n_rows);
+  w.rec = o;    o = al64r(o + 3 * n_rows * width);
+  w.counts = o; o = al64r(o + E + R + 1);
+  w.bucket = o; o = al64r(o + 2 * (E + R) * NS_BUCKET);
+  w.ovf = o;    o = al64r(o + 4 * 3 * n_rows);
+  w.total = o;
+}
+
+extern "C" int64_t mmre_rows_backward_workspace(int model, int64_t n_rows, int64_t n_ent, int64_t n_rel, int dim) {
+  if (n_rows <= 0 || n_ent <= 0 || n_rel <= 0 || dim <= 0) return 0;
+  RowsWs w;
+  rows_ws(model, n_rows, n_ent, n_rel, dim, w);
+  return w.total;
+}
+
+static int gen_nc_rows(int dim) { return dim <= 64 ? 1 : dim <= 128 ? 2 : dim <= 256 ? 4 : dim <= 512 ? 8 : 0; }
+
+// coefficients in w.coef already (or to be read from d_coef): slots, then the owner pass
+static int rows_backward_impl(const NSArgs& A, const float* d_coef, int64_t n_rows, int64_t n_ent, int64_t n_rel,
+                              float reg_ent, float reg_rel, const float* d_grad_loss, float* d_grad_ent,
+                              float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work,
+                              const RowsWs& w, hipStream_t st) {
+  const int nc = gen_nc_rows(A.dim);
+  if (nc == 0) return MMRE_ERR_SHAPE;
+  if (n_ent + n_rel >= (int64_t)UINT32_MAX || 3 * n_rows >= (int64_t)INT32_MAX) return MMRE_ERR_SHAPE;
+  int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
+  NSSlots S{nullptr, d_work + w.rec, counts, reinterpret_cast<int64_t*>(d_work + w.bucket),
+            reinterpret_cast<int64_t*>(d_work + w.ovf), counts + n_ent + n_rel, (uint32_t)(n_ent + n_rel)};
+  MMRE_CHECK(hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)(n_ent + n_rel + 1), st));
+  const dim3 sgrid((unsigned)((n_rows + NS_WAVES - 1) / NS_WAVES)), ogrid((unsigned)((n_ent + n_rel + 3) / 4)),
+      hgrid(ogrid.x + NS_HUB_WG), blk(256);
+  const int with_reg = (reg_ent != 0.0f || reg_rel != 0.0f) ? 1 : 0;
+#define MMRE_ROWS(NC_)                                                                                              \
+  do {                                                                                                              \
+    hipLaunchKernelGGL((k_rows_slots<NC_>), sgrid, blk, 0, st, A, d_coef, n_rows, S, n_ent, with_reg);              \
+    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), hgrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec, S.counts, \
+                       S.bucket, S.ovf, S.ovf_n, 0, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel,             \
+                       d_grad_rel_im, 0.0f, nullptr, nullptr, nullptr, nullptr, (int64_t)ogrid.x, NS_HUB_WG,        \
+                       3 * n_rows);                                                                                 \
+  } while (0)
+  if (nc == 1) MMRE_ROWS(1);
+  else if (nc == 2) MMRE_ROWS(2);
+  else if (nc == 4) MMRE_ROWS(4);
+  else MMRE_ROWS(8);
+#undef MMRE_ROWS
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
 extern "C" int mmre_ns_backward(int model, int norm_flag, float model_margin, int use_model_margin,
                                 const float* d_ent, const float* d_ent_im, const float* d_rel, const float* d_rel_im,
                                 int dim, float phase_denom, const int64_t* d_h, const int64_t* d_t,
                                 const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin,
                                 float adv_temperature, float regul_rate, const float* d_score,
                                 const float* d_grad_loss, float* d_grad_ent, float* d_grad_ent_im, float* d_grad_rel,
-                                float* d_grad_rel_im, float* d_work, void* stream) {
-  (void)d_work;
+                                float* d_grad_rel_im, int64_t n_ent, int64_t n_rel, float* d_work,
+                                int64_t work_floats, void* stream) {
   NSArgs A;
   int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                    phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
   if (rc) return rc;
-  if (!d_score || !d_grad_ent || !d_grad_rel) return MMRE_ERR_ARG;  // d_grad_loss NULL: upstream gradient 1
+  if (!d_score || !d_grad_ent || !d_grad_rel || !d_work || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
   if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
+  const int64_t n_rows = batch * (1 + neg);
+  RowsWs w;
+  rows_ws(model, n_rows, n_ent, n_rel, dim, w);
+  if (work_floats < w.total) return MMRE_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  const int nc = transe_fast_nc(A);
-  const dim3 grid((unsigned)batch), blk(256);
-  const bool l2 = model == MMRE_TRANSE_L2;
-#define MMRE_NS_BWD(NC_, L2_)                                                                               \
-  hipLaunchKernelGGL((k_ns_transe_backward<NC_, L2_>), grid, blk, 0, st, A, d_score, d_grad_loss, d_grad_ent, \
-                     d_grad_rel)
-  if (nc == 1) {
-    if (l2) MMRE_NS_BWD(1, true); else MMRE_NS_BWD(1, false);
-  } else if (nc == 2) {
-    if (l2) MMRE_NS_BWD(2, true); else MMRE_NS_BWD(2, false);
-  } else if (nc == 4) {
-    if (l2) MMRE_NS_BWD(4, true); else MMRE_NS_BWD(4, false);
-  } else if (nc == 8) {
-    if (l2) MMRE_NS_BWD(8, true); else MMRE_NS_BWD(8, false);
-  } else {
-    hipLaunchKernelGGL(k_ns_backward, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
-                       d_score, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
-  }
-#undef MMRE_NS_BWD
+  hipLaunchKernelGGL(k_ns_row_coef, dim3((unsigned)((batch + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A, d_score,
+                     d_work + w.coef);
   MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  // regularization scale per gathered row (TransE.py:92-102 and its kin, without the upstream gradient: the
+  // owner pass multiplies by it)
+  const double N = (double)batch * (1.0 + (double)neg);
+  const double nterms = model == MMRE_COMPLEX ? 6.0 : 3.0;
+  const double ew = model == MMRE_ROTATE ? 2.0 * dim : (double)dim;
+  const float reg_ent = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * ew)) : 0.0f;
+  const float reg_rel = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * dim)) : 0.0f;
+  NSArgs R = A;
+  R.B = n_rows;
+  R.K = 0;
+  return rows_backward_impl(R, d_work + w.coef, n_rows, n_ent, n_rel, reg_ent, reg_rel, d_grad_loss, d_grad_ent,
+                            d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, w, st);
 }
 
 extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_margin, int use_model_margin,
@@ -2080,18 +2190,19 @@ extern "C" int mmre_score_rows_backward(int model, int norm_flag, float model_ma
                                         const float* d_rel_im, int dim, float phase_denom, const int64_t* d_h,
                                         const int64_t* d_t, const int64_t* d_r, int64_t n_rows,
                                         const float* d_grad_score, float* d_grad_ent, float* d_grad_ent_im,
-                                        float* d_grad_rel, float* d_grad_rel_im, void* stream) {
+                                        float* d_grad_rel, float* d_grad_rel_im, int64_t n_ent, int64_t n_rel,
+                                        float* d_work, int64_t work_floats, void* stream) {
   NSArgs A;
   int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                    phase_denom, d_h, d_t, d_r, n_rows, 0, 0.0f, 0.0f, 0.0f);
   if (rc) return rc;
-  if (!d_grad_score || !d_grad_ent || !d_grad_rel) return MMRE_ERR_ARG;
+  if (!d_grad_score || !d_grad_ent || !d_grad_rel || !d_work || n_ent <= 0 || n_rel <= 0) return MMRE_ERR_ARG;
   if (model == MMRE_COMPLEX && (!d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_rows_backward, dim3((unsigned)((n_rows + NS_WAVES - 1) / NS_WAVES)), dim3(256), 0, st, A,
-                     d_grad_score, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im);
-  MMRE_CHECK_LAUNCH();
-  return MMRE_OK;
+  RowsWs w;
+  rows_ws(model, n_rows, n_ent, n_rel, dim, w);
+  if (work_floats < w.total) return MMRE_ERR_WORKSPACE;
+  return rows_backward_impl(A, d_grad_score, n_rows, n_ent, n_rel, 0.0f, 0.0f, nullptr, d_grad_ent, d_grad_ent_im,
+                            d_grad_rel, d_grad_rel_im, d_work, w, (hipStream_t)stream);
 }
 
 // Workspace of the fused path, in 4-byte words, 256-B aligned pieces: loss partials, row
@@ -2265,9 +2376,10 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     else                                                                                                            \
       hipLaunchKernelGGL((k_ns_gen_slots<NC_, MMRE_ROTATE>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,       \
                          (int)(regul_rate != 0.0f));                                                                \
-    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), ogrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec,         \
-                       S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, \
-                       d_grad_rel_im, lr, pe, pei, pr, pri);                                                        \
+    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), dim3(ogrid.x + NS_HUB_WG), blk, 0, st, A, n_ent, n_rel, reg_ent,       \
+                       reg_rel, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent,          \
+                       d_grad_ent_im, d_grad_rel, d_grad_rel_im, lr, pe, pei, pr, pri, (int64_t)ogrid.x, NS_HUB_WG,  \
+                       w.slots);                                                                                    \
   } while (0)
     if (nc == 1) MMRE_NS_GEN(1);
     else if (nc == 2) MMRE_NS_GEN(2);
@@ -2280,12 +2392,14 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
   const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
   // the training step (d_loss_out): one more workgroup reduces the forward's loss partials
   const int64_t reduce_block = d_loss_out ? (int64_t)ogrid.x : -1;
-  const dim3 ogrid2((unsigned)(ogrid.x + (d_loss_out ? 1 : 0)));
+  // after the row workgroups: the loss reduction (the training step), then the hub workgroups
+  const int64_t hub_block0 = (int64_t)ogrid.x + (d_loss_out ? 1 : 0);
+  const dim3 ogrid2((unsigned)(hub_block0 + NS_HUB_WG));
 #define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
   hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid2, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
                      d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n,         \
                      neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr, A, d_work + w.part, d_loss_out,           \
-                     reduce_block)
+                     reduce_block, hub_block0, NS_HUB_WG, w.slots)
   const int nc = transe_fast_nc(A);
   const bool l2 = model == MMRE_TRANSE_L2;
   if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }

@@ -31,6 +31,7 @@ SIGNATURES = {
     "mmre_link_sweep": (I32, [I32, I32, F32, P, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P, P]),
     "mmre_link_sweep_range": (I32, [I32, I32, F32, P, I64, I64, I64, I64, P, P, P, P, I64, I64, I32, P, P, P, P, P]),
     "mmre_link_l1q_workspace": (I64, [I32, I64, I64]),
+    "mmre_link_l1q_stats": (I32, [P, I64, P, P]),
     "mmre_link_sweep_l1q": (I32, [I32, F32, P, P, I64, I64, I64, I64, P, P, P, P, P, I64, I64, I32, P, P, P, P, P,
                                   I64, P]),
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
@@ -55,7 +56,8 @@ SIGNATURES = {
     "mmre_ns_forward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
                               P]),
     "mmre_ns_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, I64, F32, F32, F32, P, P, P,
-                               P, P, P, P, P]),
+                               P, P, P, I64, I64, P, I64, P]),
+    "mmre_rows_backward_workspace": (I64, [I32, I64, I64, I64, I32]),
     "mmre_ns_fused_workspace": (I64, [I32, I32, I64, I64, I64, I64, I32]),
     "mmre_ns_fused_forward": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
                                     F32, P, P, P, P]),
@@ -67,7 +69,8 @@ SIGNATURES = {
                                   P, P, I64, I64, I32, I64, I64, F32, F32, F32, P, P, P, P, P, F32, P]),
     "mmre_ns_forward_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I64, I64, I32, F32, P, P, P, I64, I64, F32, F32,
                                        F32, P, P, P, P, P, P, P, P]),
-    "mmre_score_rows_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, P, P, P, P, P, P]),
+    "mmre_score_rows_backward": (I32, [I32, I32, F32, I32, P, P, P, P, I32, F32, P, P, P, I64, P, P, P, P, P, I64, I64,
+                                       P, I64, P]),
     "mmre_generator_workspace": (I64, [I64, I32, I32, I32, I32]),
     "mmre_generator_forward": (I32, [P, I32, P, I32, I64, P, P, P, P, I32, P, P, P, P, I32, P, P, P, P, I32, P, P,
                                      F32, I32, F32, P, P, P]),

@@ -38,12 +38,16 @@ SIGNATURES = {
 _base = None
 
 
-def load(latch_errors: bool = True):
+def load(latch_errors: bool | None = None):
     """Load libmmre_base.so once (after libmmre_hip.so, which it links). This binding checks
-    for errors (check()), so it switches the library to the latched error mode; a caller that
-    never checks -- the reference's own Tester over ctypes.CDLL -- keeps the default, abort."""
+    for errors (check()), so its FIRST load switches the library to the latched error mode; later
+    calls leave the mode alone unless latch_errors is given explicitly. The mode is global to the
+    process: a reference Tester that opens the same libmmre_base.so over ctypes.CDLL in a process
+    where mmre.base was loaded sees latched errors too -- load(latch_errors=False) restores abort
+    (INTEGRATION.md §C)."""
     global _base
-    if _base is None:
+    first = _base is None
+    if first:
         if not os.path.exists(BASE_PATH):
             raise MMREError(f"{BASE_PATH} is missing: build it with __graft_entry__.build()")
         from ._lib import lib
@@ -54,7 +58,8 @@ def load(latch_errors: bool = True):
             fn.restype = res
             fn.argtypes = args
         _base = L
-    _base.mmre_base_set_error_mode(1 if latch_errors else 0)
+    if latch_errors is not None or first:
+        _base.mmre_base_set_error_mode(1 if (latch_errors is None or latch_errors) else 0)
     return _base
 
 

@@ -267,7 +267,23 @@ class LinkSweep:
                  ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(scores), st)
         if sweep_events is not None:
             sweep_events[1].record()
+        b["l1q_used"] = l1q
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
+
+    def l1q_stats(self, buffers):
+        """The integer filter's record of the last run() on `buffers` (mmre_link_l1q_stats):
+        dict(undecided=pairs rescored with the canonical chain, fallback=True if the sweep ran
+        the f32 path because the codes were too coarse), or None if that run did not use the
+        filter (not TransE L1, score-storing, MMRE_L1_FILTER=0). Synchronises the stream."""
+        if not buffers.get("l1q_used"):
+            return None
+        wk = buffers["l1q_work"]
+        out = buffers.get("l1q_stats")
+        if out is None:
+            out = buffers["l1q_stats"] = torch.zeros(2, dtype=torch.int64, device=self.device)
+        call("mmre_link_l1q_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
+        u, f = (int(x) for x in out.cpu())
+        return dict(undecided=u, fallback=bool(f))
 
 
 def _rows_view(c):

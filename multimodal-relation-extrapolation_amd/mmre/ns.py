@@ -43,8 +43,8 @@ class _FusedNS(torch.autograd.Function):
     """Training (the tables need gradients): mmre_ns_fused_forward in the forward (loss,
     scores, and the gradient's slot contributions kept in the workspace), mmre_ns_fused_grad
     in the backward (every row of the gradient tables written, scaled by the upstream
-    gradient; for TransE a row-owner pass with no float atomics). Otherwise mmre_ns_forward,
-    with mmre_ns_backward as the backward."""
+    gradient; a row-owner pass with no float atomics). Otherwise mmre_ns_forward, with
+    mmre_ns_backward (slots + row owner, no float atomics either) as the backward."""
 
     @staticmethod
     def forward(ctx, ent, rel, ent_im, rel_im, h, t, r, spec, batch, neg, loss_margin, adv_t, regul_rate, events,
@@ -114,14 +114,17 @@ class _FusedNS(torch.autograd.Function):
                 ev[3].record()
             ctx.work = ctx.events = ctx.sgd = None
             return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None, None
-        ge = torch.zeros_like(ent)
-        gr = torch.zeros_like(rel)
-        gei = torch.zeros_like(ent_im) if ent_im is not None else None
-        gri = torch.zeros_like(rel_im) if rel_im is not None else None
+        # deterministic rows backward (slots + row owner): writes every row, no fills
+        E, R = int(ent.shape[0]), int(rel.shape[0])
+        ge, gr = torch.empty_like(ent), torch.empty_like(rel)
+        gei = torch.empty_like(ent_im) if ent_im is not None else None
+        gri = torch.empty_like(rel_im) if rel_im is not None else None
+        nw = int(lib().mmre_rows_backward_workspace(spec.model_id, batch * (1 + neg), E, R, spec.dim))
+        work = torch.empty(nw, dtype=torch.float32, device=dev)
         call("mmre_ns_backward", spec.model_id, int(spec.norm_flag), spec.model_margin, int(spec.use_model_margin),
              ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom, ptr(h), ptr(t), ptr(r),
              batch, neg, float(loss_margin), float(adv_t), float(regul_rate), ptr(score), ptr(gl), ptr(ge), ptr(gei),
-             ptr(gr), ptr(gri), None, stream_ptr(dev))
+             ptr(gr), ptr(gri), E, R, ptr(work), nw, stream_ptr(dev))
         return ge, gr, gei, gri, None, None, None, None, None, None, None, None, None, None, None
 
 
@@ -175,12 +178,17 @@ class _ScoreRows(torch.autograd.Function):
         if not ctx.has_im:
             ent_im = rel_im = None
         g = g_score.to(torch.float32).contiguous()
-        ge, gr = torch.zeros_like(ent), torch.zeros_like(rel)
-        gei = torch.zeros_like(ent_im) if ent_im is not None else None
-        gri = torch.zeros_like(rel_im) if rel_im is not None else None
+        # deterministic rows backward (slots + row owner, no float atomics): writes every row
+        E, R = int(ent.shape[0]), int(rel.shape[0])
+        ge, gr = torch.empty_like(ent), torch.empty_like(rel)
+        gei = torch.empty_like(ent_im) if ent_im is not None else None
+        gri = torch.empty_like(rel_im) if rel_im is not None else None
+        n = int(h.shape[0])
+        nw = int(lib().mmre_rows_backward_workspace(spec.model_id, n, E, R, spec.dim))
+        work = torch.empty(nw, dtype=torch.float32, device=ent.device)
         call("mmre_score_rows_backward", spec.model_id, int(spec.norm_flag), spec.model_margin,
              int(spec.use_model_margin), ptr(ent), ptr(ent_im), ptr(rel), ptr(rel_im), spec.dim, spec.phase_denom,
-             ptr(h), ptr(t), ptr(r), int(h.shape[0]), ptr(g), ptr(ge), ptr(gei), ptr(gr), ptr(gri),
+             ptr(h), ptr(t), ptr(r), n, ptr(g), ptr(ge), ptr(gei), ptr(gr), ptr(gri), E, R, ptr(work), nw,
              stream_ptr(ent.device))
         return ge, gr, gei, gri, None, None, None, None
 

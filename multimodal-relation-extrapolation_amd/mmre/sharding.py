@@ -141,6 +141,7 @@ class ShardedLinkEvaluation:
             def local_runner(qh_, qr_, qt_, qm_, filt, masks_tc, events=None):
                 return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs,
                               sweep_events=events)["counts"]
+            self.sweep, self.sweep_buffers = sw, bufs
         self.local_runner = local_runner
         self._graph_wanted = bool(graph) and dev.type == "cuda" and self._default_runner
         self._graph = None
@@ -213,6 +214,12 @@ class ShardedLinkEvaluation:
     def run(self, events=None, copy_counts=True):
         """(metrics, counts (4, 2n) int32) of one evaluation, synchronously."""
         return self.finish(self.launch(events), copy_counts)
+
+    def l1q_stats(self):
+        """The TransE L1 integer filter's record of this rank's last local sweep (undecided pairs,
+        fallback), or None (another model / runner)."""
+        sw = getattr(self, "sweep", None)
+        return None if sw is None else sw.l1q_stats(self.sweep_buffers)
 
 
 def entity_slices(n_ent: int, world: int, tile: int = 128):

@@ -67,9 +67,18 @@ class Trainer(object):
             self.model.cuda()
         if self.optimizer is None:
             self.optimizer = self.make_optimizer()
-        if hasattr(self.model, "fuse_optimizer") and hasattr(self.optimizer, "fusable_lr"):
-            # the fused negative-sampling backward applies the plain SGD step itself (bit-identical)
+        fusing = hasattr(self.model, "fuse_optimizer") and hasattr(self.optimizer, "fusable_lr")
+        if fusing:
+            # the fused negative-sampling backward applies the plain SGD step itself (bit-identical);
+            # only for the duration of this run (train_one_step: zero_grad, ONE backward, step)
             self.model.fuse_optimizer(self.optimizer)
+        try:
+            self._run_epochs()
+        finally:
+            if fusing:
+                self.model.fuse_optimizer(None)
+
+    def _run_epochs(self):
         fast = self._one_call_step() if self.one_call_step else None
         self.used_one_call_step = fast is not None
         for epoch in range(self.train_times):

@@ -424,7 +424,8 @@ int orc_import_prob(const char *path, int64_t n_rel, float temp, float *prob) {
     float sum = 0.0f;
     for (int64_t i = 0; i < n_rel; ++i) {
         for (int64_t j = 0; j < n_rel - 1; ++j) {
-            float e = expf(-prob[i * (n_rel - 1) + j] / temp);
+            /* Reader.h:40: unqualified exp(float) with <cmath> only = (float)exp((double)x) */
+            float e = (float)exp((double)(-prob[i * (n_rel - 1) + j] / temp));
             sum += e;
             prob[i * (n_rel - 1) + j] = e;
         }

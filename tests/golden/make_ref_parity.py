@@ -10,9 +10,12 @@ STRUCTURED tables (mmre.workloads.structured_tables: deterministic, bit-identica
 host, truths ranked near the top -- hit@10 ~0.5-0.8, not the ~0 of OpenKE-initialised tables)
 and a seeded test sample:
 
+    C2  FB15K-237-ZS TransE d=200   all 17,596 test triples -> 35,192 sweeps x 14,208 entities
+        (norm_flag; the bench's TRAINED tables: 300 steps of this build's HIP trainer, written by
+        scripts/dump_trained_tables.py on a GPU box, sha256 checked here and in the GPU test)
     C3  DB15K-ZS ComplEx d=200      all 5,653 test triples  -> 11,306 sweeps x 12,741 entities
-    C4  FB15K-237-ZS RotatE d=512   500 test triples        ->  1,000 sweeps x 14,208 entities
-    C5  synthetic DistMult d=256    256 test triples        ->    512 sweeps x 1,000,000 entities
+    C4  FB15K-237-ZS RotatE d=512   1,000 test triples      ->  2,000 sweeps x 14,208 entities
+    C5  synthetic DistMult d=256    all 4,096 test triples  ->  8,192 sweeps x 1,000,000 entities
 
 The REFERENCE's CPU path ranks the sample: the OpenKE Tester loop (Tester.py:70-91) over the
 reference's own Base.so (getHeadBatch / testHead / getTailBatch / testTail /
@@ -31,7 +34,8 @@ tests/test_oracle_golden.py). Stored per fixture:
 
 tests/test_ref_parity_gpu.py holds the HIP sweep to these exactly (see there).
 
-Usage:  python tests/golden/make_ref_parity.py [c3 c4 c5]   (C4 takes ~15 min on 8 cores)
+Usage:  python tests/golden/make_ref_parity.py [c2 c3 c4 c5]   (C4 takes ~15 min on 8 cores)
+        (c2 reads gpurun_out/trained_c2.npz)
 """
 from __future__ import annotations
 
@@ -53,12 +57,17 @@ for p in (os.path.join(REPO, "multimodal-relation-extrapolation_amd"), os.path.j
 NEAR_REL = 1e-5
 
 
-def make(config: str, threads: int = 8):
+def make(config: str, threads: int = 8, tables_path: str | None = None):
     import ref_tester
-    from mmre.workloads import ref_parity_workload, tables_sha256
+    from mmre.workloads import TRAINED_TABLES, ref_parity_workload, tables_sha256
     t0 = time.time()
-    w = ref_parity_workload(config)
+    if config in TRAINED_TABLES and tables_path is None:
+        tables_path = os.path.join(REPO, "gpurun_out", f"trained_{config}.npz")
+    w = ref_parity_workload(config, tables_path=tables_path)
     sha = tables_sha256(w)
+    if tables_path is not None:
+        with np.load(tables_path, allow_pickle=False) as z:
+            assert str(z["sha256"]) == sha, "trained tables' sha256 differs from the one the GPU run recorded"
     print(f"{config}: workload + structured tables in {time.time() - t0:.1f} s, sha256 {sha[:16]}", flush=True)
     tmp = tempfile.mkdtemp(prefix=f"mmre_refpar_{config}_")
     try:

@@ -56,6 +56,31 @@ def write_dataset(path, n_ent=40, n_rel=9, seed=3):
         f.write(" ".join(f"{x:.6f}" for x in kl) + "\n")
 
 
+WIDE_REL, WIDE_SEED, WIDE_TEMPS = 200, 11, (0.1, 0.5, 1.0, 2.0)
+
+
+def wide_kl_text(n_rel=WIDE_REL, seed=WIDE_SEED):
+    """kl_prob.txt of a 200-relation table with a wide value range (exp of -x / T spans many
+    binades, so a float-vs-double exp would show), regenerated identically by the CPU test."""
+    kl = np.random.default_rng(seed).uniform(0.0, 20.0, n_rel * (n_rel - 1))
+    return " ".join(f"{x:.6f}" for x in kl) + "\n"
+
+
+def write_wide(path, n_rel=WIDE_REL):
+    """Minimal OpenKE directory with n_rel relations (importProb reads relationTotal and
+    kl_prob.txt only)."""
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, "entity2id.txt"), "w") as f:
+        f.write("2\ne0\t0\ne1\t1\n")
+    with open(os.path.join(path, "relation2id.txt"), "w") as f:
+        f.write(f"{n_rel}\n" + "".join(f"r{i}\t{i}\n" for i in range(n_rel)))
+    for name in ("train2id.txt", "valid2id.txt", "test2id.txt"):
+        with open(os.path.join(path, name), "w") as f:
+            f.write("1\n0 1 0\n")
+    with open(os.path.join(path, "kl_prob.txt"), "w") as f:
+        f.write(wide_kl_text(n_rel))
+
+
 def load_base():
     subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     lib = ctypes.CDLL(os.path.join(REPO, "oracle", "_ref", "Base.so"))
@@ -109,6 +134,20 @@ def main():
         R = int(lib.getRelationTotal())
         p = ctypes.c_void_p.in_dll(lib, "prob").value
         res[f"{name}_prob"] = np.ctypeslib.as_array((ctypes.c_float * (R * (R - 1))).from_address(p)).copy()
+    # the prob table alone over 200 relations and a wide KL range (Reader.h:40's
+    # unqualified exp(float) is (float)exp((double)x) under libstdc++)
+    import tempfile
+    wide = tempfile.mkdtemp(prefix="mmre_prel200_")
+    write_wide(wide)
+    lib.setInPath((wide.rstrip("/") + "/").encode())
+    lib.setWorkThreads(1)
+    lib.importTrainFiles()
+    R = int(lib.getRelationTotal())
+    assert R == WIDE_REL
+    for T in WIDE_TEMPS:
+        lib.importProb(T)
+        p = ctypes.c_void_p.in_dll(lib, "prob").value
+        res[f"wide_prob_T{T}"] = np.ctypeslib.as_array((ctypes.c_float * (R * (R - 1))).from_address(p)).copy()
     np.savez_compressed(os.path.join(HERE, "sampler_p.npz"), **res)
     neg1 = sum(int((res[k][2] == -1).sum()) for k in res if "_step" in k)
     print("sampler_p fixture:", len(cases), "cases; relation negatives equal to -1 (empty list):", neg1)

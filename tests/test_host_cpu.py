@@ -3,6 +3,7 @@ host-side parts (metric reduction, glibc seeds, LCG bookkeeping, dataset/filter/
 relation sharding) agree with the oracle and the reference's golden vectors. No GPU needed."""
 import ctypes
 import os
+import sys
 import re
 
 import numpy as np
@@ -304,6 +305,26 @@ def test_import_prob_is_the_reference(golden):
         assert np.array_equal(out.ravel(), g[f"{name}_prob"]), name
     with pytest.raises(Exception):
         call("mmre_import_prob", b"/nonexistent/kl_prob.txt", n_rel, 1.0, out.ctypes.data_as(ctypes.c_void_p))
+
+
+def test_import_prob_wide_table_is_the_reference(golden, tmp_path):
+    """200 relations, KL values over [0, 20), temperatures 0.1-2: exp(-x / T) spans many binades,
+    so evaluating Reader.h:40's unqualified exp(float) as expf instead of libstdc++'s
+    (float)exp((double)x) would differ by an ulp somewhere. Bit-equal to the
+    reference Base.so's `prob` table, and so is the oracle's restatement."""
+    import oracle as oracle_mod
+    from mmre._lib import call
+    sys.path.insert(0, os.path.join(GOLDEN))
+    from make_sampler_p import WIDE_REL, WIDE_TEMPS, wide_kl_text
+    g = golden("sampler_p")
+    path = tmp_path / "kl_prob.txt"
+    path.write_text(wide_kl_text())
+    for T in WIDE_TEMPS:
+        want = g[f"wide_prob_T{T}"]
+        out = np.zeros((WIDE_REL, WIDE_REL - 1), np.float32)
+        call("mmre_import_prob", str(path).encode(), WIDE_REL, float(T), out.ctypes.data_as(ctypes.c_void_p))
+        assert np.array_equal(out.ravel(), want), T
+        assert np.array_equal(np.asarray(oracle_mod.import_prob(str(path), WIDE_REL, T)).ravel(), want), T
 
 
 def test_bench_quotes_pmc_traffic_only_for_this_build(tmp_path, monkeypatch):

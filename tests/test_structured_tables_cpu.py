@@ -18,13 +18,20 @@ import pytest
 from conftest import GOLDEN
 
 
-@pytest.mark.parametrize("config", ["c3", "c4", "c5"])
+@pytest.mark.parametrize("config", ["c2", "c3", "c4", "c5"])
 def test_ref_parity_fixture(config, golden):
     from mmre.link import link_metrics
-    from mmre.workloads import REF_PARITY, ref_parity_workload, tables_sha256
+    from mmre.workloads import REF_PARITY, TRAINED_TABLES, ref_parity_workload, tables_sha256, zs_workload
     fx = golden(f"ref_parity_{config}")
-    w = ref_parity_workload(config)
-    assert tables_sha256(w) == str(fx["tables_sha256"])
+    if config in TRAINED_TABLES:
+        # trained tables (C2): rebuilt only on a GPU (tests/test_ref_fixture_gpu.py checks their
+        # sha256 there); here the workload's queries and the fixture itself
+        (dataset, model, dim), _, _ = REF_PARITY[config]
+        w = zs_workload(dataset, model, dim)
+        assert len(str(fx["tables_sha256"])) == 64
+    else:
+        w = ref_parity_workload(config)
+        assert tables_sha256(w) == str(fx["tables_sha256"])
     n = len(w["test_h"])
     assert REF_PARITY[config][1] in (None, n)
     assert np.array_equal(fx["q"], np.stack([w["test_h"], w["test_r"], w["test_t"]], 1))

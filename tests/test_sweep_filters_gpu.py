@@ -110,3 +110,58 @@ def test_l1_filter_on_and_off_and_entity_slices(oracle_mod, monkeypatch):
             res = sw.run(tq(qh), tq(qr), tq(qt), tq(qm, np.int8), filt=filt, entity_range=(e0, e1))
             total += res["counts"].cpu().numpy()
         assert np.array_equal(total, on["counts"])
+
+
+def _c2_eval(w, dev, norm_flag):
+    from mmre.link import FilterIndex, HEAD, TAIL, LinkSweep, ScoreSpec
+    import torch
+    n = len(w["test_h"])
+    to = lambda a, dt=np.int64: torch.from_numpy(np.asarray(a, dt)).to(dev)
+    qh, qr, qt = (np.r_[w[k], w[k]] for k in ("test_h", "test_r", "test_t"))
+    qm = np.r_[np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)]
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], w["n_ent"], w["n_rel"])
+    filt = tuple(to(a, a.dtype) for a in index.groups(qh, qr, qt, qm))
+    spec = ScoreSpec(model="transe", ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=int(w["dim"]),
+                     norm_flag=norm_flag, pred_kind=0)
+    sw = LinkSweep(spec)
+    bufs = sw.alloc_queries(2 * n)
+    args = (to(qh), to(qr), to(qt), to(qm, np.int8))
+
+    def run(reps=5):
+        ts = []
+        for _ in range(reps):
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            sw.run(*args, filt=filt, buffers=bufs, sweep_events=ev)
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]))
+        return bufs["counts"].cpu().numpy().copy(), float(np.median(ts)), sw.l1q_stats(bufs)
+    return sw, run
+
+
+def test_l1_filter_outlier_row_falls_back_to_f32(monkeypatch):
+    """the 16-bit codes span M = max |x| of both planes, so ONE outlier row
+    (a drifted norm_flag=False table) would stretch the code step for every pair and leave most
+    of them to the one-at-a-time rescoring. The quantization pass detects it (M > 128 x mean|x|)
+    on the device and the sweep runs the f32 path instead: counts unchanged, time within 1.1x of
+    the f32 sweep (MMRE_L1_FILTER=0). The ordinary table keeps the filter, with its undecided
+    pairs counted."""
+    import torch
+    from mmre.workloads import zs_workload
+    dev = torch.device("cuda:0")
+    w = zs_workload("FB15K-237-ZS", "transe", 200)
+    _, run = _c2_eval(w, dev, norm_flag=False)
+    c_plain, t_plain, st_plain = run()
+    assert st_plain is not None and not st_plain["fallback"], st_plain
+    w["ent"] = w["ent"].clone()
+    w["ent"][123] *= 1000.0                               # one drifted entity row
+    _, run = _c2_eval(w, dev, norm_flag=False)
+    c_out, t_out, st_out = run()
+    assert st_out["fallback"] and st_out["undecided"] == 0, st_out
+    monkeypatch.setenv("MMRE_L1_FILTER", "0")
+    _, run32 = _c2_eval(w, dev, norm_flag=False)
+    c_32, t_32, st_32 = run32()
+    assert st_32 is None
+    assert np.array_equal(c_out, c_32)
+    print(f"L1 filter: plain table {t_plain:.3f} ms ({st_plain['undecided']} undecided pairs); outlier table "
+          f"{t_out:.3f} ms (fallback) vs f32 sweep {t_32:.3f} ms")
+    assert t_out <= 1.1 * t_32
