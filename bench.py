@@ -62,6 +62,8 @@ CONFIGS = {
                           "generator + LayerNormalization (SURVEY 8(f) rank 4)"),
 }
 MFMA_F32_PEAK = 157.3e12  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+MFMA_BF16_PEAK = 16 * MFMA_F32_PEAK  # dense bf16 MFMA: 16x the f32 rate (MI355X_MICROARCH.md, ~2.5 PF)
+MFMA_FILTER = os.environ.get("MMRE_MFMA_FILTER", "1") != "0"
 
 
 def bytes_per_triple(model, dim):
@@ -86,7 +88,8 @@ def valu_ops_per_triple(model, dim):
 
 KERNEL_NAMES = {"transe": "k_sweep_valu<5, false, false, 0>" if os.environ.get("MMRE_L1_FILTER", "1") != "0"
                 else "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
-                "distmult": "k_sweep_mfma<false, false, 2", "complex": "k_sweep_mfma<false, false, 2"}
+                "distmult": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2",
+                "complex": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2"}
 
 
 def pmc_traffic(config: str, model: str):
@@ -1200,7 +1203,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     _, counts = ev.run()  # one more evaluation outside the timed region: the counts the parity check reads
-    l1st = ev.l1q_stats() if hasattr(ev, "l1q_stats") else None  # the TransE L1 integer filter's record
+    fst = ev.filter_stats() if hasattr(ev, "filter_stats") else None  # the count-only filter's record (l1q / bf3)
     breakdown = None
     if world > 1:  # every rank's local / sweep / fixed / collective time, gathered (all ranks take part)
         breakdown = rank_breakdown(ev, dist, dev, sweep_ms, n_local, args.shard == "entity")
@@ -1212,7 +1215,19 @@ def main():
         triples_launch = n_local * e_local
         tps = triples_launch / (sweep_ms * 1e-3) if sweep_ms > 0 else 0.0
         traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
-        if model in ("distmult", "complex"):
+        if model in ("distmult", "complex") and fst is not None and fst["kind"] == "bf3" and not fst["fallback"]:
+            # the split-bf16 filter: three bf16 products of K = dim x planes per triple on the bf16
+            # MFMA (kernel_ms brackets the whole filtered sweep: split, sweep, rescoring)
+            flops = 2.0 * dim * (2 if model == "complex" else 1)
+            ach = tps * 3.0 * flops / 1e12
+            roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_BF16_PEAK / 1e12, "unit": "TFLOP/s (bf16 MFMA)",
+                    "frac": ach * 1e12 / MFMA_BF16_PEAK, "flops_per_triple": 3.0 * flops,
+                    "f32_equiv_TFLOPs": tps * flops / 1e12,
+                    "f32_equiv_frac": tps * flops / MFMA_F32_PEAK,
+                    "mfma_note": "executed flops = 3 bf16 products (hi.hi, hi.lo, lo.hi) x 2K per triple against the "
+                                 "dense bf16 MFMA peak; f32_equiv = the triple's 2K algorithmic flops against the f32 "
+                                 "MFMA peak (the exact sweep's roof, which the filter passes)"}
+        elif model in ("distmult", "complex"):
             flops = 2.0 * dim * (2 if model == "complex" else 1)
             ach = tps * flops / 1e12
             roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
@@ -1265,14 +1280,23 @@ def main():
                            "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
                            "mr": metrics["filter"]["mr"]},
                "parity": None}
-        if l1st is not None:
+        if fst is not None and fst["kind"] == "l1q":
             pairs = int(n_local) * int(e_local)
-            out["l1_filter"] = {"undecided_pairs": l1st["undecided"],
-                                "undecided_frac": l1st["undecided"] / pairs if pairs else None,
-                                "fallback_to_f32": l1st["fallback"],
+            out["l1_filter"] = {"undecided_pairs": fst["undecided"],
+                                "undecided_frac": fst["undecided"] / pairs if pairs else None,
+                                "fallback_to_f32": fst["fallback"],
                                 "note": "pairs the 16-bit code bound left undecided, each rescored with the canonical "
                                         "f32 chain (mmre_link_l1q_stats, rank 0's last evaluation); fallback_to_f32 = "
                                         "the quantization pass found M > 128 x mean|x| and the sweep ran the f32 path"}
+        elif fst is not None and fst["kind"] == "bf3":
+            pairs = int(n_local) * int(e_local)
+            out["mfma_filter"] = {"undecided_pairs": fst["undecided"],
+                                  "undecided_frac": fst["undecided"] / pairs if pairs else None,
+                                  "fallback_to_f32": fst["fallback"],
+                                  "note": "pairs the split-bf16 bound left undecided (truths included), each rescored "
+                                          "with the canonical f32 chain (mmre_link_bf3_stats, rank 0's last "
+                                          "evaluation); fallback_to_f32 = the pair list overflowed and the exact f32 "
+                                          "MFMA sweep counted"}
         if "trained" in w:
             out["config"]["tables"] = w["trained"]
         elif "tables" in w:

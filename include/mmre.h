@@ -169,6 +169,29 @@ int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, cons
                         int64_t q_pad, int dim, const uint32_t* d_type_head, const uint32_t* d_type_tail,
                         int32_t* d_counts, const float* d_truth, void* d_work, int64_t work_bytes, void* stream);
 
+/* DistMult / ComplEx (MMRE_DISTMULT, MMRE_COMPLEX) count-only sweep through a split-bf16 MFMA
+ * filter: same counts as mmre_link_sweep / mmre_link_sweep_range without type constraints (bit
+ * for bit; replaces the same Test.h:65-192 scan), faster. Each f32 plane value x is split into
+ * hi = bf16(x) and lo = bf16(x - hi); the sweep computes Qhi.Ehi + Qhi.Elo + Qlo.Ehi on the bf16
+ * MFMA (16 k per instruction against the f32 MFMA's 2) and decides a pair only when its
+ * prediction is on one side of the query's threshold over the whole error bound
+ * cb |q|_2 |e|_2; the rest (the truth, near ties, non-finite values) are listed and rescored
+ * with the canonical f32 chain from the row-major copies d_ent_rows (whole table) and d_q_rows.
+ * If the list overflows, the device resets the raw counts and runs the exact f32 sweep instead
+ * (no host round trip). e_begin / e_end as for mmre_link_sweep_range (0, n_ent: whole table).
+ * d_work: mmre_link_bf3_workspace(model, dim, e_pad, q_pad) bytes of device scratch (0 for a
+ * model without the filter). */
+int64_t mmre_link_bf3_workspace(int model, int dim, int64_t e_pad, int64_t q_pad);
+/* The filter's record of the last mmre_link_sweep_bf3 on d_work (one tiny launch, no
+ * synchronisation): d_out[0] = pairs listed for exact rescoring, d_out[1] = 1 if the list
+ * overflowed and the exact f32 sweep counted instead. */
+int mmre_link_bf3_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
+int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows,
+                        int64_t n_ent, int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km,
+                        const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
+                        int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts, const float* d_truth,
+                        void* d_work, int64_t work_bytes, void* stream);
+
 /* Test.h:232-327 test_link_prediction + getTestLink* (Test.h:356-390), host side,
  * with the reference's float accumulation order (P14). Counts: int32, column c of
  * query i at counts[c*stride + i] (c = raw, filt, raw_tc, filt_tc).

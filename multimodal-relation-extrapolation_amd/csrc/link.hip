@@ -23,6 +23,8 @@
 
 namespace mmre {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // a v_pk_*_f32 operand pair
+
 constexpr int TQ = 128;   // queries per workgroup tile
 constexpr int TE = 128;   // entities per workgroup tile
 constexpr int KC = 8;     // K rows per LDS stage
@@ -834,6 +836,11 @@ __device__ __forceinline__ void sweep_valu_body(
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = 0.0f;
+  f32x2 accp[4][8];  // RotatE filter: the packed accumulators (pair layout at the inner loop)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) accp[i][j] = f32x2{0.0f, 0.0f};
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     s_cnt[0][i][tid] = 0;
@@ -868,16 +875,29 @@ __device__ __forceinline__ void sweep_valu_body(
         const float qa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
         if constexpr (OP == 2 && FAST) {
+          // packed f32: every v_pk_* computes two pairs' IEEE-identical results (the scalar
+          // chain's sub, sub, mul, fma, add per half), so one full-rate issue covers two
+          // elements and only the two v_sqrt_f32 stay per-element. Pair (ip, jp) of query rows
+          // (2ip, 2ip+1) and entity columns (2jp, 2jp+1): the straight product takes
+          // (2ip, 2jp) | (2ip+1, 2jp+1), the swapped one (op_sel) (2ip, 2jp+1) | (2ip+1, 2jp).
           float4 b0 = sq[buf][NPL - 1][kk][tq], b1 = sq[buf][NPL - 1][kk][16 + tq];
           float4 y0 = se[buf][NPL - 1][kk][te], y1 = se[buf][NPL - 1][kk][16 + te];
-          const float qb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-          const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+          const f32x2 qa2[4] = {{a0.x, a0.y}, {a0.z, a0.w}, {a1.x, a1.y}, {a1.z, a1.w}};
+          const f32x2 qb2[4] = {{b0.x, b0.y}, {b0.z, b0.w}, {b1.x, b1.y}, {b1.z, b1.w}};
+          const f32x2 xv2[4] = {{x0.x, x0.y}, {x0.z, x0.w}, {x1.x, x1.y}, {x1.z, x1.w}};
+          const f32x2 yv2[4] = {{y0.x, y0.y}, {y0.z, y0.w}, {y1.x, y1.y}, {y1.z, y1.w}};
 #pragma unroll
-          for (int i = 0; i < 8; ++i)
+          for (int ip = 0; ip < 4; ++ip)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float dr = qa[i] - xv[j], di = qb[i] - yv[j];
-              acc[i][j] = acc[i][j] + __builtin_amdgcn_sqrtf(__builtin_fmaf(di, di, dr * dr));
+            for (int jp = 0; jp < 4; ++jp) {  // the straight and swapped chains issued side by side
+              const f32x2 dr0 = qa2[ip] - xv2[jp], dr1 = qa2[ip] - xv2[jp].yx;
+              const f32x2 di0 = qb2[ip] - yv2[jp], di1 = qb2[ip] - yv2[jp].yx;
+              const f32x2 p0 = dr0 * dr0, p1 = dr1 * dr1;
+              const f32x2 v0 = __builtin_elementwise_fma(di0, di0, p0), v1 = __builtin_elementwise_fma(di1, di1, p1);
+              const f32x2 m0 = {__builtin_amdgcn_sqrtf(v0.x), __builtin_amdgcn_sqrtf(v0.y)};
+              const f32x2 m1 = {__builtin_amdgcn_sqrtf(v1.x), __builtin_amdgcn_sqrtf(v1.y)};
+              accp[ip][2 * jp] = accp[ip][2 * jp] + m0;
+              accp[ip][2 * jp + 1] = accp[ip][2 * jp + 1] + m1;
             }
         } else if constexpr (OP == 2) {
           float4 b0 = sq[buf][NPL - 1][kk][tq], b1 = sq[buf][NPL - 1][kk][16 + tq];
@@ -928,6 +948,19 @@ __device__ __forceinline__ void sweep_valu_body(
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE;
         if constexpr (FAST) {
+          if constexpr (OP == 2) {  // unpack the pair layout (register renames) and restart it
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const f32x2 p = accp[i >> 1][(j & ~1) + ((i ^ j) & 1)];
+                acc[i][j] = (i & 1) ? p.y : p.x;
+              }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) accp[i][j] = f32x2{0.0f, 0.0f};
+          }
           uint32_t unc[2] = {0u, 0u};  // undecided pairs, bit i * 8 + j (rows 0-3 / 4-7)
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
@@ -1188,8 +1221,9 @@ __global__ __launch_bounds__(NT, KS == 16 && !TC && !STORE ? 4 : 2) void k_sweep
     int64_t q_pad, int64_t n_query, int ktot, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode,
     const uint32_t* __restrict__ type_head, const uint32_t* __restrict__ type_tail, int64_t type_words,
-    int32_t* __restrict__ counts, float* __restrict__ scores, int emajor) {
+    int32_t* __restrict__ counts, float* __restrict__ scores, int emajor, const uint32_t* __restrict__ gate) {
   static_assert(KS == 16 || KS == 32, "stage of 16 or 32 K rows");
+  if (gate != nullptr && *gate == 0u) return;  // the split-bf16 filter's fallback: runs only on its overflow
   // 16-row stages (33 KB of LDS) run 4 workgroups per CU: the row counters then live one row
   // per lane (ballot counts), which frees the 32 registers of per-lane row counters
   constexpr bool BAL = KS == 16;
@@ -1585,6 +1619,310 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
 
+// ------------------------------------------------- split-bf16 MFMA filter ---
+// DistMult / ComplEx count-only sweeps through a filter with exact rescoring, as the VALU
+// sweeps' (rot_bound, L1Q): every f32 plane value x is split into two bf16 values hi = bf16(x)
+// and lo = bf16(x - hi) (round to nearest even), and the sweep computes
+//     S' = Qhi . Ehi + Qhi . Elo + Qlo . Ehi
+// on v_mfma_f32_32x32x16_bf16: three MFMAs of 16 k each per 32 x 32 block where the exact
+// sweep issues eight v_mfma_f32_32x32x2_f32 of 2 k (16x the f32 rate per MFMA cycle,
+// 5.3x per scored element). Bound on |S' - S|, S the canonical f32 fma chain (what the exact
+// sweep and the truth kernels compute), P the exact dot product, with Sigma = sum |q_k||e_k|
+// <= |q|_2 |e|_2 (Cauchy-Schwarz):
+//   |P - T|  <= 3.02 x 2^-16 Sigma      T = the three products' exact sum; the dropped terms
+//                                       are lo.lo + (hi+lo).r_e + r_q.e with |lo| <= 2^-8 (1+2^-8) |x|
+//                                       and |r| = |x - hi - lo| <= 2^-16 |x| (bf16: 8-bit significand)
+//   |T - S'| <= 3K x 2u (1 + 2^-7) Sigma   any order / grouping of the 3K exact bf16 products
+//                                       summed with at most one rounding (RN or toward zero,
+//                                       2u) per addition -- MFMA's internal summation order is
+//                                       not documented, so no more is assumed
+//   |S - P|  <= K u (1 + small) Sigma      the canonical chain (u = 2^-24)
+// plus 2^-29 sqrt(K) |q||e| for the values |x| < 2^-60 the split sets to zero (norms are
+// clamped to >= 2^-30). So B = cb |q|_2 |e|_2, cb = 1.02 (7K 2^-24 (1 + 2^-7) + 3.02 2^-16 +
+// 2^-29 sqrt K) (computed on the host, the norms' own rounding inside the 2 %). A pair whose
+// prediction is on the same side of its query's threshold at both ends of [S' - B, S' + B]
+// is decided (apply_pred is monotone); every other valid pair -- the truth itself, near ties,
+// any non-finite S' (an inf / NaN operand is split into a NaN hi) -- is appended to a pair
+// list and rescored with the canonical chain from the row-major copies (k_bf3_rescore), so
+// the counts are the exact sweep's bit for bit. ~2e-4 of the C3 pairs and 2e-5 of C5's land
+// in the list. A list that overflows its capacity sets a flag on the device: the raw counts
+// are reset and the exact f32 sweep runs instead (gated launches, no host round trip).
+// Workspace: header (BF3_HDR bytes: word 0 appended pairs, word 1 overflow flag) | pair list
+// (bf3_cap int2) | |q| (q_pad floats) | |e| (e_pad floats) | split query planes (K/16 blocks
+// x q_pad rows x 64 B: hi[16] | lo[16]) | split entity planes (K/16 x e_pad x 64 B).
+constexpr int BF3_HDR = 256;
+#ifndef BF3_WG_PER_CU
+#define BF3_WG_PER_CU 3  // workgroups per CU the sweep is compiled for (168 VGPRs)
+#endif
+inline int64_t bf3_cap(int64_t q_pad, int64_t e_pad) {
+  const char* cap_env = getenv("MMRE_BF3_CAP");  // tests: a tiny list forces the overflow fallback
+  if (cap_env && atoll(cap_env) > 0) return atoll(cap_env);
+  int64_t c = q_pad * e_pad / 512;
+  c = c < (1 << 16) ? (1 << 16) : c;
+  return c > (1 << 26) ? (1 << 26) : c;
+}
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t bf16_rn_bits(float x) {  // finite x: round to nearest even
+  const uint32_t u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+// One thread per column c of a k-major plane (K rows x pad, columns col0 + c): the column's
+// split blocks out[kb][c] = {hi[16], lo[16]} (4 x 16 B) and its 2-norm (>= 2^-30).
+__global__ __launch_bounds__(256) void k_bf3_split(const float* __restrict__ km, int64_t pad, int64_t col0,
+                                                   int64_t n_cols, int ktot, uint4* __restrict__ out,
+                                                   int64_t out_pad, float* __restrict__ norms) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cols) return;
+  const float* src = km + col0 + c;
+  float ss = 0.0f;
+  for (int kb = 0; kb < ktot / 16; ++kb) {
+    uint32_t hw[8], lw[8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float x = src[(int64_t)(kb * 16 + j) * pad];
+      ss = __builtin_fmaf(x, x, ss);
+      uint32_t hb = 0u, lb = 0u;
+      if (!(fabsf(x) < INFINITY)) {
+        hb = 0x7FC0u;  // inf / NaN: a NaN operand, every product NaN: the pair is undecided
+      } else if (fabsf(x) >= 0x1p-60f) {
+        hb = bf16_rn_bits(x);
+        lb = bf16_rn_bits(x - __uint_as_float(hb << 16));  // x - hi is exact (Sterbenz)
+      }
+      if (j & 1) { hw[j >> 1] |= hb << 16; lw[j >> 1] |= lb << 16; }
+      else { hw[j >> 1] = hb; lw[j >> 1] = lb; }
+    }
+    uint4* o = out + ((int64_t)kb * out_pad + c) * 4;
+    o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    o[1] = make_uint4(hw[4], hw[5], hw[6], hw[7]);
+    o[2] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    o[3] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
+  }
+  norms[c] = fmaxf(sqrtf(ss), 0x1p-30f);  // inf stays inf (bound inf: undecided); NaN: the hi is NaN
+}
+
+// The sweep: units, grid and staging as k_sweep_mfma's 16-row plain variant (4 workgroups per
+// CU, ballot row counters), one split block (16 k) per stage: 8 KB per operand tile, read into
+// LDS as 16-B chunks at position chunk ^ ((row >> 2) & 3) of the row's 64 B (the 32 lanes of
+// an MFMA operand read hit 32 different 16-B bank groups: conflict-free).
+template <int PK>
+__global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
+    const uint4* __restrict__ ent_b, int64_t e_pad, int64_t n_ent, const uint4* __restrict__ q_b, int64_t q_pad,
+    int64_t n_query, int nkb, int n_et, int e_base, int n_groups, int pred_kind, float margin,
+    const float* __restrict__ thr, const float* __restrict__ qn, const float* __restrict__ en, float cb,
+    int32_t* __restrict__ counts, uint32_t* __restrict__ hdr, int2* __restrict__ pairs, int64_t cap, int emajor) {
+  __shared__ uint4 sq[2][TQ * 4];
+  __shared__ uint4 se[2][TE * 4];
+  __shared__ __attribute__((aligned(16))) float s_th[2][TQ];
+  __shared__ __attribute__((aligned(16))) float s_qb[2][TQ];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const PredSel<PK> pred(pred_kind, margin);
+  const int wq = wave >> 1, we = wave & 1;
+  const int lrow = lane >> 5, lcol = lane & 31;
+  const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
+  const int per_grp = gridDim.x / n_groups;
+  const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et, emajor != 0);
+  const int u0 = (int)((int64_t)gmem * um.count / per_grp);
+  const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
+  if (u0 >= u1) return;  // uniform over the workgroup
+
+  int tpar = 0;
+  int cntv = 0;  // lane L: the count of wave row L (tile row wq * 64 + L) in the current query tile
+  auto row_of = [&](int bi, int r) { return wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * lrow; };
+  auto load_rows = [&](int qtile) {
+    const int64_t q0 = (int64_t)qtile * TQ;
+    tpar ^= 1;
+    if (tid < TQ) {
+      const int64_t q = q0 + tid;
+      s_th[tpar][tid] = q < n_query ? thr[q] : -INFINITY;  // -inf: nothing beats a padded row
+      s_qb[tpar][tid] = q < n_query ? cb * qn[q] : 0.0f;
+    }
+    cntv = 0;
+  };
+  auto flush_rows = [&](int qtile) {
+    const int64_t q = (int64_t)qtile * TQ + wq * 64 + lane;
+    if (q < n_query && cntv) atomicAdd(&counts[q], cntv);  // raw only (k_counts_finalize)
+  };
+  auto sidx = [](int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); };
+
+  uint4 rq0, rq1, re0, re1;
+  int ld_unit = u0, ld_kb = 0, ld_qt, ld_et;
+  um.at(u0, ld_qt, ld_et);
+  auto gload = [&]() {
+    const uint4* qp = q_b + ((int64_t)ld_kb * q_pad + (int64_t)ld_qt * TQ) * 4;
+    const uint4* ep = ent_b + ((int64_t)ld_kb * e_pad + (int64_t)ld_et * TE) * 4;
+    rq0 = qp[tid];
+    rq1 = qp[tid + NT];
+    re0 = ep[tid];
+    re1 = ep[tid + NT];
+    if (++ld_kb == nkb) {
+      ld_kb = 0;
+      if (++ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
+    }
+  };
+  auto swrite = [&](int buf) {
+    const int r0 = tid >> 2, c = tid & 3;
+    sq[buf][sidx(r0, c)] = rq0;
+    sq[buf][sidx(r0 + 64, c)] = rq1;
+    se[buf][sidx(r0, c)] = re0;
+    se[buf][sidx(r0 + 64, c)] = re1;
+  };
+
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  int cur_qt, cur_et;
+  um.at(u0, cur_qt, cur_et);
+  load_rows(cur_qt);
+  gload();
+  swrite(0);
+  __syncthreads();
+
+  int buf = 0;
+  for (int unit = u0; unit < u1; ++unit) {
+    for (int kb = 0; kb < nkb; ++kb) {
+      const bool more = ld_unit < u1;
+      if (more) gload();
+      __builtin_amdgcn_sched_barrier(0);  // the next stage's loads stay at the top (k_sweep_mfma)
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int qrow = wq * 64 + i * 32 + lcol, ecol = we * 64 + i * 32 + lcol;
+        ah[i] = __builtin_bit_cast(bf16x8, sq[buf][sidx(qrow, lrow)]);
+        al[i] = __builtin_bit_cast(bf16x8, sq[buf][sidx(qrow, 2 + lrow)]);
+        bh[i] = __builtin_bit_cast(bf16x8, se[buf][sidx(ecol, lrow)]);
+        bl[i] = __builtin_bit_cast(bf16x8, se[buf][sidx(ecol, 2 + lrow)]);
+      }
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) {
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+        }
+      if (kb == nkb - 1) {  // unit finished: decide, count, list the undecided
+        const int64_t q0 = (int64_t)cur_qt * TQ;
+        const int64_t ebase = (int64_t)cur_et * TE + we * 64;
+        const int64_t e0 = ebase + lcol, e1 = ebase + 32 + lcol;
+        const bool ev0 = e0 < n_ent, ev1 = e1 < n_ent;
+        const float ne0 = ev0 ? en[e0] : 0.0f, ne1 = ev1 ? en[e1] : 0.0f;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r4 = 0; r4 < 16; r4 += 4) {  // four rows' thresholds and bound factors per LDS read pair
+            const float4 t4 = *reinterpret_cast<const float4*>(&s_th[tpar][row_of(bi, r4)]);
+            const float4 b4 = *reinterpret_cast<const float4*>(&s_qb[tpar][row_of(bi, r4)]);
+            const float tv[4] = {t4.x, t4.y, t4.z, t4.w}, qb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+          for (int r = r4; r < r4 + 4; ++r) {
+            bool better[2], und[2];
+#pragma unroll
+            for (int bj = 0; bj < 2; ++bj) {
+              const float s = acc[bi][bj][r];
+              const float bnd = qb[r - r4] * (bj ? ne1 : ne0);
+              const float p1 = pred(s - bnd), p2 = pred(s + bnd);
+              const bool fin = fabsf(s) < INFINITY;  // false for inf and NaN
+              const bool sure = fin & (fmaxf(p1, p2) < tv[r - r4]);
+              const bool out = (fin & (fminf(p1, p2) >= tv[r - r4])) | (tv[r - r4] != tv[r - r4]);
+              const bool ev = bj ? ev1 : ev0;
+              better[bj] = sure & ev;
+              und[bj] = !sure & !out & ev;
+            }
+            const uint64_t m0 = __ballot(better[0]), m1 = __ballot(better[1]);
+            const int L0 = bi * 32 + (r & 3) + 8 * (r >> 2);
+            const int c_lo = __popcll(m0 & 0xffffffffull) + __popcll(m1 & 0xffffffffull);
+            const int c_hi = __popcll(m0 >> 32) + __popcll(m1 >> 32);
+            cntv += lane == L0 ? c_lo : (lane == L0 + 4 ? c_hi : 0);
+            if (__builtin_expect(und[0] | und[1], 0)) {  // rare: list the pair(s) for exact rescoring
+              const int64_t q = q0 + row_of(bi, r);
+              if (q < n_query) {
+#pragma unroll
+                for (int bj = 0; bj < 2; ++bj) {
+                  if (!und[bj]) continue;
+                  const uint32_t i = atomicAdd(&hdr[0], 1u);
+                  if (i < (uint64_t)cap) pairs[i] = make_int2((int)q, (int)((bj ? e1 : e0) + e_base));
+                  else hdr[1] = 1u;
+                }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.0f;
+        const bool last = unit + 1 >= u1;
+        int next_qt = cur_qt, next_et = cur_et;
+        if (!last) um.at(unit + 1, next_qt, next_et);
+        if (last || next_qt != cur_qt) {  // uniform: leave this query tile
+          flush_rows(cur_qt);
+          if (!last) load_rows(next_qt);
+        }
+        cur_qt = next_qt;
+        cur_et = next_et;
+      }
+      if (more) swrite(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+}
+
+// Overflowed list: reset the raw counts the filter sweep added (the truth pass left them 0);
+// the gated f32 sweep that follows recounts them.
+__global__ __launch_bounds__(256) void k_bf3_fallback_zero(const uint32_t* __restrict__ hdr,
+                                                           int32_t* __restrict__ counts, int64_t n_query) {
+  if (hdr[1] == 0u) return;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n_query) counts[q] = 0;
+}
+
+// The listed pairs, one thread each: the canonical chain (acc = fma(e_k, q_k, acc), k in
+// order -- the truth kernels' and the f32 MFMA's arithmetic) from the row-major copies, and
+// the strict Test.h compare against the query's threshold.
+template <int PK>
+__global__ __launch_bounds__(256) void k_bf3_rescore(const uint32_t* __restrict__ hdr, const int2* __restrict__ pairs,
+                                                     int64_t cap, const float* __restrict__ q_rows,
+                                                     const float* __restrict__ ent_rows, int ktot, int pred_kind,
+                                                     float margin, const float* __restrict__ thr,
+                                                     int32_t* __restrict__ counts) {
+  if (hdr[1] != 0u) return;  // overflow: the exact sweep counted everything
+  const PredSel<PK> pred(pred_kind, margin);
+  const int64_t n = (int64_t)hdr[0] < cap ? (int64_t)hdr[0] : cap;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int2 p = pairs[i];
+    const float4* a = reinterpret_cast<const float4*>(q_rows + (int64_t)p.x * ktot);
+    const float4* b = reinterpret_cast<const float4*>(ent_rows + (int64_t)p.y * ktot);
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int k = 0; k < ktot / 4; ++k) {
+      const float4 x = b[k], y = a[k];
+      acc = __builtin_fmaf(x.x, y.x, acc);
+      acc = __builtin_fmaf(x.y, y.y, acc);
+      acc = __builtin_fmaf(x.z, y.z, acc);
+      acc = __builtin_fmaf(x.w, y.w, acc);
+    }
+    if (pred(acc) < thr[p.x]) atomicAdd(&counts[p.x], 1);
+  }
+}
+
+__global__ void k_bf3_stats(const uint32_t* __restrict__ hdr, unsigned long long* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    out[0] = hdr[0];
+    out[1] = hdr[1];
+  }
+}
+
 // ---------------------------------------------------------------- launch ---
 // Resident workgroups of a persistent sweep: the occupancy API's blocks per CU (capped at 4,
 // the VGPR-limited residency of a 256-thread group at <= 128 VGPRs) x the device's CUs.
@@ -1820,37 +2158,14 @@ extern "C" int mmre_link_truth(int model, int pred_kind, float margin, const flo
 #undef MMRE_TF
 }
 
-// The sweep over entities [e_begin, e_end) of the table (e_begin a multiple of TE): the kernels
-// see the slice (pointer offset by e_begin columns, row stride e_pad, n_ent_local ids) and add
-// e_begin back wherever an absolute id matters (truth exclusion, type-constraint bits).
-static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent, int64_t e_pad,
-                      int64_t e_begin, int64_t e_end, const float* d_q_km, const int32_t* d_q_true,
-                      const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
-                      const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
-                      const float* d_truth, float* d_scores, hipStream_t st) {
-  int rc = check_link_args(model, pred_kind, d_ent_km, n_ent, e_pad, d_q_km, d_q_true, d_qr, d_qmode, n_query, q_pad,
-                           d_type_head, d_type_tail, d_counts, d_truth);
-  if (rc) return rc;
-  if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
-  if (d_scores && (e_begin != 0 || e_end != n_ent)) return MMRE_ERR_ARG;  // score rows are whole-table
-  const int64_t tw = (n_ent + 31) / 32;  // type bitsets span the whole table
-  const int e_base = (int)e_begin;
-  d_ent_km += e_begin;
-  n_ent = e_end - e_begin;
-  const int n_et = (int)((n_ent + TE - 1) / TE);
-  const int kp = plane_rows(model, dim);
-  const bool tc = d_type_head != nullptr;
-  const bool store = d_scores != nullptr;
-  const int op = op_of_model(model);
-  if (op <= 2) {
-#define MMRE_LV(OPV) launch_valu<OPV>(tc, store, st, d_ent_km, e_pad, n_ent, n_et, e_base, d_q_km, q_pad, n_query, kp, pred_kind, \
-                                      margin, d_truth, d_q_true, d_qr, d_qmode, d_type_head, d_type_tail, tw, d_counts, d_scores)
-    if (op == 0) return MMRE_LV(0);
-    if (op == 1) return MMRE_LV(1);
-    return MMRE_LV(2);
-#undef MMRE_LV
-  }
-  const int ktot = n_planes(model) * kp;
+// The f32 MFMA sweep's launch (DistMult / ComplEx; d_ent_km already at the slice's first
+// column). gate != NULL: every workgroup returns at once unless *gate != 0 (the split-bf16
+// filter's overflow fallback, mmre_link_sweep_bf3).
+static void launch_mfma(bool tc, bool store, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,
+                        int64_t e_pad, int n_et, int e_base, const float* d_q_km, int64_t q_pad, int64_t n_query,
+                        int ktot, const float* d_truth, const int64_t* d_qr, const int8_t* d_qmode,
+                        const uint32_t* d_type_head, const uint32_t* d_type_tail, int64_t tw, int32_t* d_counts,
+                        float* d_scores, hipStream_t st, const uint32_t* gate) {
   // persistent XCD-grouped grid as for the VALU sweep, 2 workgroups per resident slot (MI355X,
   // KCM = 16: C3 1.20 / 1.24 / 1.22 / 1.24 ms and C5 36.5 / 36.5 / 36.5 / 36.6 ms at 1/2/3/4x)
   // K stages of 32 rows (a unit's last one 16 when K = 32 n + 16: C3 ComplEx 2 x 200): half the
@@ -1886,7 +2201,7 @@ static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL(KERNEL, dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,       \
                        n_query, ktot, n_et, e_base, ng, pred_kind, margin, d_truth, d_qr, d_qmode, d_type_head,  \
-                       d_type_tail, tw, d_counts, d_scores, emajor);                                              \
+                       d_type_tail, tw, d_counts, d_scores, emajor, gate);                                              \
   } while (0)
 #define MMRE_MFMA(TCV, STV, PKV)                                                                           \
   do {                                                                                                 \
@@ -1901,6 +2216,41 @@ static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent
   else MMRE_MFMA(false, false, -1);
 #undef MMRE_MFMA
 #undef MMRE_MFMA_K
+}
+
+// The sweep over entities [e_begin, e_end) of the table (e_begin a multiple of TE): the kernels
+// see the slice (pointer offset by e_begin columns, row stride e_pad, n_ent_local ids) and add
+// e_begin back wherever an absolute id matters (truth exclusion, type-constraint bits).
+static int sweep_impl(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent, int64_t e_pad,
+                      int64_t e_begin, int64_t e_end, const float* d_q_km, const int32_t* d_q_true,
+                      const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim,
+                      const uint32_t* d_type_head, const uint32_t* d_type_tail, int32_t* d_counts,
+                      const float* d_truth, float* d_scores, hipStream_t st) {
+  int rc = check_link_args(model, pred_kind, d_ent_km, n_ent, e_pad, d_q_km, d_q_true, d_qr, d_qmode, n_query, q_pad,
+                           d_type_head, d_type_tail, d_counts, d_truth);
+  if (rc) return rc;
+  if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
+  if (d_scores && (e_begin != 0 || e_end != n_ent)) return MMRE_ERR_ARG;  // score rows are whole-table
+  const int64_t tw = (n_ent + 31) / 32;  // type bitsets span the whole table
+  const int e_base = (int)e_begin;
+  d_ent_km += e_begin;
+  n_ent = e_end - e_begin;
+  const int n_et = (int)((n_ent + TE - 1) / TE);
+  const int kp = plane_rows(model, dim);
+  const bool tc = d_type_head != nullptr;
+  const bool store = d_scores != nullptr;
+  const int op = op_of_model(model);
+  if (op <= 2) {
+#define MMRE_LV(OPV) launch_valu<OPV>(tc, store, st, d_ent_km, e_pad, n_ent, n_et, e_base, d_q_km, q_pad, n_query, kp, pred_kind, \
+                                      margin, d_truth, d_q_true, d_qr, d_qmode, d_type_head, d_type_tail, tw, d_counts, d_scores)
+    if (op == 0) return MMRE_LV(0);
+    if (op == 1) return MMRE_LV(1);
+    return MMRE_LV(2);
+#undef MMRE_LV
+  }
+  const int ktot = n_planes(model) * kp;
+  launch_mfma(tc, store, pred_kind, margin, d_ent_km, n_ent, e_pad, n_et, e_base, d_q_km, q_pad, n_query, ktot,
+              d_truth, d_qr, d_qmode, d_type_head, d_type_tail, tw, d_counts, d_scores, st, nullptr);
   MMRE_CHECK_LAUNCH();
   return launch_finalize(st, d_counts, n_query, tc);
 }
@@ -1966,6 +2316,87 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   return launch_valu<5>(d_type_head != nullptr, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et,
                         (int)e_begin, (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr,
                         d_qmode, d_type_head, d_type_tail, tw, d_counts, nullptr, l1);
+}
+
+extern "C" int64_t mmre_link_bf3_workspace(int model, int dim, int64_t e_pad, int64_t q_pad) {
+  if (!mfma_model(model) || dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
+  const int64_t ktot = (int64_t)n_planes(model) * plane_rows(model, dim);
+  return BF3_HDR + 8 * bf3_cap(q_pad, e_pad) + 4 * (q_pad + e_pad) + 4 * ktot * (q_pad + e_pad);
+}
+
+extern "C" int mmre_link_bf3_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream) {
+  if (!d_work || !d_out || work_bytes < BF3_HDR) return MMRE_ERR_ARG;
+  hipLaunchKernelGGL(k_bf3_stats, dim3(1), dim3(64), 0, (hipStream_t)stream, (const uint32_t*)d_work,
+                     (unsigned long long*)d_out);
+  MMRE_CHECK_LAUNCH();
+  return MMRE_OK;
+}
+
+extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const float* d_ent_km,
+                                   const float* d_ent_rows, int64_t n_ent, int64_t e_pad, int64_t e_begin,
+                                   int64_t e_end, const float* d_q_km, const float* d_q_rows,
+                                   const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
+                                   int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts, const float* d_truth,
+                                   void* d_work, int64_t work_bytes, void* stream) {
+  if (!mfma_model(model)) return MMRE_ERR_MODEL;
+  int rc = check_link_args(model, pred_kind, d_ent_km, n_ent, e_pad, d_q_km, d_q_true, d_qr, d_qmode, n_query,
+                           q_pad, nullptr, nullptr, d_counts, d_truth);
+  if (rc) return rc;
+  if (!d_ent_rows || !d_q_rows || !d_work || work_bytes < mmre_link_bf3_workspace(model, dim, e_pad, q_pad))
+    return MMRE_ERR_WORKSPACE;
+  if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int kp = plane_rows(model, dim);
+  const int ktot = n_planes(model) * kp;  // a multiple of 16 (plane_rows)
+  const int64_t cap = bf3_cap(q_pad, e_pad);
+  char* w = (char*)d_work;
+  uint32_t* hdr = (uint32_t*)w;
+  int2* pairs = (int2*)(w + BF3_HDR);
+  float* qn = (float*)(w + BF3_HDR + 8 * cap);
+  float* en = qn + q_pad;
+  uint4* qb = (uint4*)(en + e_pad);
+  uint4* eb = qb + (int64_t)ktot * q_pad / 4;
+  const int64_t e_cols = round_up(e_end, TE) - e_begin;  // the slice's whole tiles
+  const int64_t n_slice = e_end - e_begin;
+  const int n_et = (int)((n_slice + TE - 1) / TE);
+  // bound coefficient (see k_sweep_bf3's header): 1.02 (7K 2^-24 (1 + 2^-7) + 3.02 2^-16 + 2^-29 sqrt K)
+  const double K = (double)ktot;
+  const float cb = (float)(1.02 * (7.0 * K * std::ldexp(1.0, -24) * (1.0 + std::ldexp(1.0, -7)) +
+                                   3.02 * std::ldexp(1.0, -16) + std::ldexp(1.0, -29) * std::sqrt(K)));
+  MMRE_CHECK(hipMemsetAsync(hdr, 0, 8, st));
+  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0,
+                     q_pad, ktot, qb, q_pad, qn);
+  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((e_cols + 255) / 256)), dim3(256), 0, st, d_ent_km, e_pad, e_begin,
+                     e_cols, ktot, eb, e_pad, en);
+  MMRE_CHECK_LAUNCH();
+  static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
+  static const char* order_env = getenv("MMRE_MFMA_EMAJOR");
+  const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
+#define MMRE_BF3(PKV)                                                                                           \
+  do {                                                                                                          \
+    const int res = resident_groups((const void*)k_sweep_bf3<PKV>, NT);                                        \
+    const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                        \
+    int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;              \
+    if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                           \
+    const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                          \
+    hipLaunchKernelGGL((k_sweep_bf3<PKV>), dim3((unsigned)g), dim3(NT), 0, st, eb, e_pad, n_slice, qb, q_pad,   \
+                       n_query, ktot / 16, n_et, (int)e_begin, ng, pred_kind, margin, d_truth, qn, en, cb,     \
+                       d_counts, hdr, pairs, cap, emajor);                                                     \
+    MMRE_CHECK_LAUNCH();                                                                                       \
+    hipLaunchKernelGGL((k_bf3_fallback_zero), dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, hdr,  \
+                       d_counts, n_query);                                                                     \
+    launch_mfma(false, false, pred_kind, margin, d_ent_km + e_begin, n_slice, e_pad, n_et, (int)e_begin,       \
+                d_q_km, q_pad, n_query, ktot, d_truth, nullptr, nullptr, nullptr, nullptr, 0, d_counts,        \
+                nullptr, st, hdr + 1);                                                                         \
+    MMRE_CHECK_LAUNCH();                                                                                       \
+    hipLaunchKernelGGL((k_bf3_rescore<PKV>), dim3(1024), dim3(256), 0, st, hdr, pairs, cap, d_q_rows,          \
+                       d_ent_rows, ktot, pred_kind, margin, d_truth, d_counts);                               \
+    MMRE_CHECK_LAUNCH();                                                                                       \
+  } while (0)
+  if (pred_kind == 2) MMRE_BF3(2);
+  else MMRE_BF3(-1);
+#undef MMRE_BF3
+  return launch_finalize(st, d_counts, n_query, false);
 }
 
 extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,

@@ -455,6 +455,7 @@ __global__ __launch_bounds__(256) void k_ns_transe_forward(NSArgs A, float* __re
 // ---------------------------------------------------------------------------------------
 constexpr int NSF_MAXJ = 8;
 constexpr int NS_BUCKET = 64;   // slot ids kept in a table row's own bucket (one wave's width)
+constexpr int NS_BUCKET_HEAD = 16;  // bucket entries the owner reads with the count (128 B)
 constexpr int NS_HUB = 512;     // a row with more slots than a bucket orders them in LDS up to this many
 constexpr int NS_HUB_WG = 4;    // owner workgroups for the rows with more slots (HubOrder)
 
@@ -1369,14 +1370,16 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const fl
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
-  // the count, the lane's bucket entry (meaningful below the count), the row itself and its
-  // norm: one round trip, all in flight together
+  // the count, the bucket's first NS_BUCKET_HEAD entries (one 128-B line: every slot of most
+  // rows), the row itself and its norm: one round trip, all in flight together; the rest of the
+  // bucket only for a row holding more, and only its live entries (below the count)
   const int n = counts[row];
-  const int64_t pre = bucket[row * NS_BUCKET + lane];
+  int64_t pre = lane < NS_BUCKET_HEAD ? bucket[row * NS_BUCKET + lane] : 0;
   Vec<NC> v;
   vload_row(v, is_ent ? ent : rel, id, d, lane);
   const float nv = (is_ent ? nrm_e : nrm_r)[id];
   if (n > NS_HUB) return;  // a hub workgroup's row
+  if (n > NS_BUCKET_HEAD && lane >= NS_BUCKET_HEAD && lane < n) pre = bucket[row * NS_BUCKET + lane];
   if (n == 0) {  // not in the batch: zero gradient (and an unchanged parameter row)
     Vec<NC> z;
 #pragma unroll
@@ -1647,10 +1650,14 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
   (void)dpad;
   NSArgs A = A_;
   A.model = MODEL;  // compile-time model
+  constexpr int NH = MODEL == MMRE_DISTMULT ? 1 : 2;  // row halves carried by the own-row partials
+  __shared__ float s_own[NS_WAVES - 1][3][NH][NC][kWave];  // waves 1-3's own-row partial sums
+  __shared__ float s_occ[NS_WAVES - 1][3];
   const int d = A.dim;
   const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (b >= A.B) return;  // wave-uniform
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t b = blockIdx.x;  // one workgroup per positive, its negatives split over the waves
+  if (b >= A.B) return;  // workgroup-uniform
   const float p = score[b];
   float mx = -INFINITY, den = 0.0f;
   if (A.adv_t > 0.0f) {
@@ -1677,11 +1684,20 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
   gen_load(T, A, true, pt, lane);
   Vec<NC> psn, pcs;
   rot_sincos(A, R, psn, pcs);
-  gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt, &psn, &pcs);
-  float kh = 1.0f, kr = 1.0f, kt = 1.0f;  // occurrences of the positive's rows (regularization)
+  // wave 0 starts the own-row sums with the positive's gradient, waves 1-3 from zero; each wave
+  // takes a contiguous range of the negatives; the partials are combined in wave order below
+  if (w == 0) {
+    gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt, &psn, &pcs);
+  } else {
+    vzero(Gh.a); vzero(Gh.b); vzero(Gr.a); vzero(Gr.b); vzero(Gt.a); vzero(Gt.b);
+  }
+  const float k0 = w == 0 ? 1.0f : 0.0f;
+  float kh = k0, kr = k0, kt = k0;  // occurrences of the positive's rows (regularization)
   const int64_t sb = b * (3 + 3 * A.K);
-  for (int64_t j0 = 0; j0 < A.K; j0 += CH) {
-    const int nch = (int)(A.K - j0 < CH ? A.K - j0 : CH);
+  const int64_t per = (A.K + NS_WAVES - 1) / NS_WAVES;
+  const int64_t jlo = (int64_t)w * per, jhi = jlo + per < A.K ? jlo + per : A.K;
+  for (int64_t j0 = jlo; j0 < jhi; j0 += CH) {
+    const int nch = (int)(jhi - j0 < CH ? jhi - j0 : CH);
     int64_t mh = 0, mt = 0, mr = 0;
     float mg = 0.0f;
     if (lane < nch) {
@@ -1757,6 +1773,35 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
         S.ovf[2 * (int64_t)o + 1] = e;
       }
     }
+  }
+  // own rows: wave 0 adds waves 1, 2, 3's partials in that order (a fixed order: bit-reproducible)
+  auto park = [&](int k, const Row2<NC>& g) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      s_own[w - 1][k][0][c][lane] = g.a.v[c];
+      if constexpr (NH == 2) s_own[w - 1][k][NH - 1][c][lane] = g.b.v[c];
+    }
+  };
+  auto gather = [&](int v, int k, Row2<NC>& g) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      g.a.v[c] += s_own[v][k][0][c][lane];
+      if constexpr (NH == 2) g.b.v[c] += s_own[v][k][NH - 1][c][lane];
+    }
+  };
+  if (w > 0) {
+    park(0, Gh);
+    park(1, Gr);
+    park(2, Gt);
+    if (lane == 0) { s_occ[w - 1][0] = kh; s_occ[w - 1][1] = kr; s_occ[w - 1][2] = kt; }
+  }
+  __syncthreads();
+  if (w > 0) return;
+  for (int v = 0; v < NS_WAVES - 1; ++v) {
+    gather(v, 0, Gh);
+    gather(v, 1, Gr);
+    gather(v, 2, Gt);
+    kh += s_occ[v][0]; kr += s_occ[v][1]; kt += s_occ[v][2];  // integer-valued
   }
   rec_store(S.rec, sb, d, S2, E2, Gh, lane);
   rec_store(S.rec, sb + 1, d, S2, R2, Gr, lane);
@@ -2364,7 +2409,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     const double ew = model == MMRE_ROTATE ? 2.0 * dim : (double)dim;
     const float reg_ent = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * ew)) : 0.0f;
     const float reg_rel = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * dim)) : 0.0f;
-    const dim3 sgrid((unsigned)((batch + NS_WAVES - 1) / NS_WAVES));
+    const dim3 sgrid((unsigned)batch);  // a workgroup per positive
 #define MMRE_NS_GEN(NC_)                                                                                            \
   do {                                                                                                              \
     if (model == MMRE_DISTMULT)                                                                                     \

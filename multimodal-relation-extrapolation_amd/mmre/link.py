@@ -175,6 +175,9 @@ class LinkSweep:
         # TransE L1 count-only sweeps through the integer filter (mmre_link_sweep_l1q);
         # MMRE_L1_FILTER=0 keeps the f32 sweep (A/B measurements)
         self.l1_filter = os.environ.get("MMRE_L1_FILTER", "1") != "0"
+        # DistMult / ComplEx count-only sweeps without type constraints through the split-bf16
+        # MFMA filter (mmre_link_sweep_bf3); MMRE_MFMA_FILTER=0 keeps the f32 MFMA sweep
+        self.mfma_filter = os.environ.get("MMRE_MFMA_FILTER", "1") != "0"
 
     def prepare_entities(self):
         s = self.spec
@@ -242,11 +245,18 @@ class LinkSweep:
                  self.e_pad, ptr(self.ent_rows), ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n,
                  b["q_pad"], s.dim, ptr(off), ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
         l1q = (self.model_id == MODEL_IDS["transe"] and not return_scores and q_rows and self.l1_filter)
+        bf3 = (self.model_id in (MODEL_IDS["distmult"], MODEL_IDS["complex"]) and not return_scores and q_rows
+               and type_masks is None and self.mfma_filter)
         if l1q:
             need = int(_lib.lib().mmre_link_l1q_workspace(s.dim, self.e_pad, b["q_pad"]))
             wk = b.get("l1q_work")
             if wk is None or wk.numel() < need:
                 wk = b["l1q_work"] = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if bf3:
+            need = int(_lib.lib().mmre_link_bf3_workspace(self.model_id, s.dim, self.e_pad, b["q_pad"]))
+            wk = b.get("bf3_work")
+            if wk is None or wk.numel() < need:
+                wk = b["bf3_work"] = torch.empty(need, dtype=torch.uint8, device=self.device)
         if sweep_events is not None:
             sweep_events[0].record()
         if l1q:  # TransE L1 count-only: the integer filter (same counts, bit for bit)
@@ -255,6 +265,12 @@ class LinkSweep:
                  self.n_ent, self.e_pad, e0, e1, ptr(b["q_km"]), ptr(b["q_rows"]), ptr(b["q_true"]), ptr(qr),
                  ptr(qmode), n, b["q_pad"], s.dim, ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(wk),
                  int(wk.numel()), st)
+        elif bf3:  # DistMult / ComplEx count-only: the split-bf16 MFMA filter (same counts, bit for bit)
+            e0, e1 = (0, self.n_ent) if entity_range is None else (int(entity_range[0]), int(entity_range[1]))
+            call("mmre_link_sweep_bf3", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km),
+                 ptr(self.ent_rows), self.n_ent, self.e_pad, e0, e1, ptr(b["q_km"]), ptr(b["q_rows"]),
+                 ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(b["counts"]), ptr(b["truth"]),
+                 ptr(wk), int(wk.numel()), st)
         elif entity_range is not None:
             if return_scores:
                 raise ValueError("entity_range sweeps keep no score rows")
@@ -268,7 +284,32 @@ class LinkSweep:
         if sweep_events is not None:
             sweep_events[1].record()
         b["l1q_used"] = l1q
+        b["bf3_used"] = bf3
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
+
+    def bf3_stats(self, buffers):
+        """The split-bf16 MFMA filter's record of the last run() on `buffers` (mmre_link_bf3_stats):
+        dict(undecided=pairs rescored with the canonical chain, fallback=True if the pair list
+        overflowed and the exact f32 sweep counted instead), or None if that run did not use the
+        filter. Synchronises the stream."""
+        if not buffers.get("bf3_used"):
+            return None
+        wk = buffers["bf3_work"]
+        out = buffers.get("bf3_stats")
+        if out is None:
+            out = buffers["bf3_stats"] = torch.zeros(2, dtype=torch.int64, device=self.device)
+        call("mmre_link_bf3_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
+        u, f = (int(x) for x in out.cpu())
+        return dict(undecided=u, fallback=bool(f))
+
+    def filter_stats(self, buffers):
+        """Whichever count-only filter the last run() on `buffers` used: dict(kind="l1q" | "bf3",
+        undecided=..., fallback=...), or None (the exact sweep ran)."""
+        st = self.l1q_stats(buffers)
+        if st is not None:
+            return dict(kind="l1q", **st)
+        st = self.bf3_stats(buffers)
+        return None if st is None else dict(kind="bf3", **st)
 
     def l1q_stats(self, buffers):
         """The integer filter's record of the last run() on `buffers` (mmre_link_l1q_stats):

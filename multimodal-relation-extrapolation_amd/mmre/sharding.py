@@ -221,6 +221,12 @@ class ShardedLinkEvaluation:
         sw = getattr(self, "sweep", None)
         return None if sw is None else sw.l1q_stats(self.sweep_buffers)
 
+    def filter_stats(self):
+        """The count-only filter's record of this rank's last local sweep (LinkSweep.filter_stats:
+        kind l1q / bf3, undecided pairs, fallback), or None."""
+        sw = getattr(self, "sweep", None)
+        return None if sw is None else sw.filter_stats(self.sweep_buffers)
+
 
 def entity_slices(n_ent: int, world: int, tile: int = 128):
     """Contiguous entity slices [e0, e1) per rank, cut at multiples of the sweep's entity tile:

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 4, GPU call B: bench lines of every config touched this round
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/r4b
+T="timeout -k 10"
+for c in c3 c5 c4; do
+  $T 300 python -u bench.py --config $c --steps 20 --no-cpu-baseline > gpurun_out/r4b/bench_$c.json 2> gpurun_out/r4b/bench_$c.err || exit 1
+done
+for m in transe distmult complex rotate; do
+  $T 300 python -u bench.py --config ns --ns-model $m --steps 200 --no-cpu-baseline > gpurun_out/r4b/bench_ns_$m.json 2> gpurun_out/r4b/bench_ns_$m.err || exit 1
+done
+$T 300 python -u bench.py --steps 100 --no-cpu-baseline > gpurun_out/r4b/bench_c2.json 2> gpurun_out/r4b/bench_c2.err || exit 1
+echo done

@@ -165,3 +165,105 @@ def test_l1_filter_outlier_row_falls_back_to_f32(monkeypatch):
     print(f"L1 filter: plain table {t_plain:.3f} ms ({st_plain['undecided']} undecided pairs); outlier table "
           f"{t_out:.3f} ms (fallback) vs f32 sweep {t_32:.3f} ms")
     assert t_out <= 1.1 * t_32
+
+
+def _adversarial_dot(model, E=2300, R=5, d=48, Q=300, seed=0, nonfinite=True):
+    """DistMult / ComplEx tables that put many pairs inside the split-bf16 bound: exact copies of
+    the truth row (exact ties), copies a few ulps away, zero rows, rows below the split's 2^-60
+    cut, subnormal values, and (nonfinite) a row whose products overflow and a NaN."""
+    rng = np.random.default_rng(seed)
+    two = model == "complex"
+    ent = rng.normal(0, 0.3, (E, d)).astype(np.float32)
+    ent_im = rng.normal(0, 0.3, (E, d)).astype(np.float32) if two else None
+    rel = rng.normal(0, 0.5, (R, d)).astype(np.float32)
+    rel_im = rng.normal(0, 0.5, (R, d)).astype(np.float32) if two else None
+    rel[0] = 1.0                                        # DistMult r = 1: scores are plain dot products
+    qh, qr, qt = rng.integers(0, E, Q), rng.integers(0, R, Q), rng.integers(0, E, Q)
+    qm = rng.integers(0, 2, Q).astype(np.int8)
+    free = iter(rng.permutation(np.arange(E)))
+    used = set(qh.tolist()) | set(qt.tolist())
+    nxt = lambda: next(e for e in free if e not in used)
+    tabs = [ent] + ([ent_im] if two else [])
+    for i in range(0, Q, 3):
+        truth = qh[i] if qm[i] == 0 else qt[i]
+        for _ in range(3):                              # exact ties with the truth
+            e = nxt()
+            for t in tabs:
+                t[e] = t[truth]
+        for k in range(4):                              # a few ulps away
+            e = nxt()
+            for t in tabs:
+                t[e] = t[truth]
+            cols = rng.choice(d, 1 + k, replace=False)
+            bump = np.where(rng.random(len(cols)) < 0.5, -np.inf, np.inf).astype(np.float32)
+            ent[e, cols] = np.nextafter(ent[e, cols], bump)
+    for _ in range(4):
+        e = nxt()
+        for t in tabs:
+            t[e] = 0.0
+    e = nxt(); ent[e] = 1e-20                           # below the split's 2^-60 cut (hi = lo = 0)
+    e = nxt(); ent[e] = ent[qt[0]]; ent[e, ::3] = np.float32(1e-40)   # subnormal values
+    if nonfinite:
+        e = nxt(); ent[e] = 1e38                        # products overflow: S' = inf, rescored
+        e = nxt(); ent[e, 5] = np.nan
+    return ent, rel, ent_im, rel_im, qh, qr, qt, qm
+
+
+@pytest.mark.parametrize("model,seed,nonfinite", [("distmult", 0, True), ("distmult", 1, False),
+                                                  ("complex", 0, True), ("complex", 2, False)])
+def test_mfma_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, monkeypatch, model, seed, nonfinite):
+    """The split-bf16 MFMA filter (mmre_link_sweep_bf3): raw / filtered counts bit-equal to the
+    score-storing exact sweep, to the exact count-only f32 MFMA sweep (MMRE_MFMA_FILTER=0) and to
+    the oracle's Test.h restatement; the undecided list holds every truth and tie; entity slices
+    sum to the whole table; a list too small for the undecided pairs (MMRE_BF3_CAP) takes the
+    device-side fallback to the exact sweep with the same counts."""
+    import torch
+    from mmre.link import FilterIndex, LinkSweep
+    ent, rel, ent_im, rel_im, qh, qr, qt, qm = _adversarial_dot(model, seed=seed, nonfinite=nonfinite)
+    E, R, d = ent.shape[0], rel.shape[0], rel.shape[1]
+    rng = np.random.default_rng(seed + 10)
+    fh, fr, ft = rng.integers(0, E, 3 * E), rng.integers(0, R, 3 * E), rng.integers(0, E, 3 * E)
+    fh, fr, ft = np.concatenate([fh, qh]), np.concatenate([fr, qr]), np.concatenate([ft, qt])
+    index = FilterIndex(fh, fr, ft, E, R)
+    spec = _spec_from(model, ent, rel, ent_im, rel_im, dim=d)
+    exact = _run(spec, qh, qr, qt, qm, index=index, scores=True)
+    dev = spec.ent.device
+    tq = lambda a, dt=np.int64: torch.from_numpy(np.asarray(a, dt)).to(dev)
+    args = (tq(qh), tq(qr), tq(qt), tq(qm, np.int8))
+    filt = tuple(torch.from_numpy(a).to(dev) for a in index.groups(qh, qr, qt, qm))
+
+    def run(entity_range=None):
+        sw = LinkSweep(spec)
+        bufs = sw.alloc_queries(len(qh))
+        f = filt if entity_range is None else tuple(
+            torch.from_numpy(a).to(dev) for a in index.groups(qh, qr, qt, qm, entity_range=entity_range))
+        res = sw.run(*args, filt=f, buffers=bufs, entity_range=entity_range)
+        torch.cuda.synchronize()
+        return res["counts"].cpu().numpy().copy(), sw.bf3_stats(bufs)
+
+    fast, st = run()
+    assert st is not None and not st["fallback"], st
+    assert st["undecided"] >= len(qh), st               # every truth is listed (its S' is within the bound)
+    assert np.array_equal(fast[:2], exact["counts"][:2])
+    monkeypatch.setenv("MMRE_MFMA_FILTER", "0")
+    f32, st32 = run()
+    monkeypatch.delenv("MMRE_MFMA_FILTER")
+    assert st32 is None and np.array_equal(fast, f32)
+    total = np.zeros_like(fast)
+    for e0, e1 in ((0, 768), (768, 1664), (1664, E)):
+        c, _ = run((e0, e1))
+        total += c
+    assert np.array_equal(total[:2], fast[:2])
+    monkeypatch.setenv("MMRE_BF3_CAP", "64")
+    small, st_small = run()
+    monkeypatch.delenv("MMRE_BF3_CAP")
+    assert st_small["fallback"], st_small
+    assert np.array_equal(small, fast)
+    hrt = oracle_mod.sorted_hrt(fh, fr, ft)
+    for mode_id, mode in ((0, "head_batch"), (1, "tail_batch")):
+        sel = qm == mode_id
+        o_pred = oracle_mod.link_predict(model, mode, ent, rel, qh[sel], qr[sel], qt[sel], ent_im=ent_im,
+                                         rel_im=rel_im)
+        o_c = oracle_mod.test_rank(mode, o_pred, qh[sel], qr[sel], qt[sel], hrt)
+        assert np.array_equal(fast[:2, sel].T, o_c[:, :2])
+    print(f"{model}: {st['undecided']} of {len(qh) * E} pairs rescored")
