@@ -1550,13 +1550,14 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
                                                         int32_t* __restrict__ zero, int64_t n_zero) {
   NSArgs A = A_;
   A.model = MODEL;  // compile-time model: the other models' registers and branches fold away
-  __shared__ float s_n[NS_WAVES][NS_MAXK];
+  __shared__ float s_n[NS_MAXK];             // the positive's negative scores (loss, after the barrier)
+  __shared__ float s_sq[NS_WAVES][6], s_mx[NS_WAVES];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; zero && i < n_zero;
        i += (int64_t)gridDim.x * blockDim.x)
     zero[i] = 0;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = (int64_t)blockIdx.x * NS_WAVES + w;
-  if (b >= A.B) return;  // whole wave exits together
+  const int64_t b = blockIdx.x;  // one workgroup per positive, its negatives split over the waves
+  if (b >= A.B) return;  // workgroup-uniform
   const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
   Row2<NC> H, R, T;
   gen_load(H, A, true, ph, lane);
@@ -1565,12 +1566,14 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
   Vec<NC> psn, pcs;
   rot_sincos(A, R, psn, pcs);
   const float p = gen_score(A, H, R, T, psn, pcs);
-  if (lane == 0) score[b] = p;
+  if (w == 0 && lane == 0) score[b] = p;
   float sq[6] = {0, 0, 0, 0, 0, 0};
-  if (A.regul_rate != 0.0f) row_sq(A, b, lane, sq);
+  if (w == 0 && A.regul_rate != 0.0f) row_sq(A, b, lane, sq);
   float mx = -INFINITY;
-  for (int64_t j0 = 0; j0 < A.K; j0 += kWave) {
-    const int nch = (int)(A.K - j0 < kWave ? A.K - j0 : kWave);
+  const int64_t per = (A.K + NS_WAVES - 1) / NS_WAVES;
+  const int64_t jlo = (int64_t)w * per, jhi = jlo + per < A.K ? jlo + per : A.K;
+  for (int64_t j0 = jlo; j0 < jhi; j0 += kWave) {
+    const int nch = (int)(jhi - j0 < kWave ? jhi - j0 : kWave);
     int64_t mh = 0, mt = 0, mr = 0;
     if (lane < nch) {
       const int64_t row = b + (j0 + lane + 1) * A.B;
@@ -1604,31 +1607,37 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
           n = gen_score(A, H, X[i], T, sn, cs);
         } else if (code[i] == 3) n = p;
         else n = row_score(A, row, lane);
-        if (lane == 0) { score[row] = n; s_n[w][j] = n; }
+        if (lane == 0) { score[row] = n; s_n[j] = n; }
         if (A.regul_rate != 0.0f) row_sq(A, row, lane, sq);
         if (A.adv_t > 0.0f) mx = fmaxf(mx, -n * A.adv_t);
       }
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  float loss = 0.0f;
-  if (lane == 0) {
-    if (A.adv_t > 0.0f) {
-      float den = 0.0f;
-      for (int64_t j = 0; j < A.K; ++j) den += expf(-s_n[w][j] * A.adv_t - mx);
-      for (int64_t j = 0; j < A.K; ++j) {
-        const float n = s_n[w][j];
-        loss += expf(-n * A.adv_t - mx) / den * fmaxf(p - n, -A.loss_margin);
-      }
-    } else {
-      for (int64_t j = 0; j < A.K; ++j) loss += fmaxf(p - s_n[w][j], -A.loss_margin);
-    }
-    part[b * 7] = loss;
-  }
+  // the waves' regularization partials and maxima, combined by wave 0 in wave order
   for (int i = 0; i < 6; ++i) {
     const float v = A.regul_rate != 0.0f ? wave_sum(sq[i]) : 0.0f;
-    if (lane == 0) part[b * 7 + 1 + i] = v;
+    if (lane == 0) s_sq[w][i] = v;
+  }
+  if (lane == 0) s_mx[w] = mx;
+  __syncthreads();
+  if (w != 0 || lane != 0) return;
+  float loss = 0.0f;
+  for (int v = 1; v < NS_WAVES; ++v) mx = fmaxf(mx, s_mx[v]);
+  if (A.adv_t > 0.0f) {
+    float den = 0.0f;
+    for (int64_t j = 0; j < A.K; ++j) den += expf(-s_n[j] * A.adv_t - mx);
+    for (int64_t j = 0; j < A.K; ++j) {
+      const float n = s_n[j];
+      loss += expf(-n * A.adv_t - mx) / den * fmaxf(p - n, -A.loss_margin);
+    }
+  } else {
+    for (int64_t j = 0; j < A.K; ++j) loss += fmaxf(p - s_n[j], -A.loss_margin);
+  }
+  part[b * 7] = loss;
+  for (int i = 0; i < 6; ++i) {
+    float v = s_sq[0][i];
+    for (int ww = 1; ww < NS_WAVES; ++ww) v += s_sq[ww][i];
+    part[b * 7 + 1 + i] = v;
   }
 }
 
@@ -2327,6 +2336,7 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
     if (is_transe(model)) {
       hipLaunchKernelGGL(k_ns_forward, fgrid, dim3(256), 0, st, A, d_score, part, S.counts, n_ent + n_rel + 1);
     } else {
+      const dim3 fgrid((unsigned)batch);  // k_ns_gen_forward: a workgroup per positive
 #define MMRE_NS_GF(NC_, M_)                                                                                        \
   hipLaunchKernelGGL((k_ns_gen_forward<NC_, M_>), fgrid, dim3(256), 0, st, A, d_score, part, S.counts,             \
                      n_ent + n_rel + 1)

@@ -10,4 +10,9 @@ for m in transe distmult complex rotate; do
   $T 300 python -u bench.py --config ns --ns-model $m --steps 200 --no-cpu-baseline > gpurun_out/r4b/bench_ns_$m.json 2> gpurun_out/r4b/bench_ns_$m.err || exit 1
 done
 $T 300 python -u bench.py --steps 100 --no-cpu-baseline > gpurun_out/r4b/bench_c2.json 2> gpurun_out/r4b/bench_c2.err || exit 1
+for W in 2 4 8; do
+  $T 300 python -u scripts/step_breakdown.py --emulate-world $W --graph --config c2 >> gpurun_out/r4b/c2_shard_emulation.txt 2>&1 || exit 1
+done
+$T 300 python -u scripts/step_breakdown.py --emulate-world 8 --entity --config c2 >> gpurun_out/r4b/c2_shard_emulation.txt 2>&1 || exit 1
+$T 300 python -u scripts/step_breakdown.py --emulate-world 8 --graph --config c4 >> gpurun_out/r4b/c4_shard_emulation.txt 2>&1 || exit 1
 echo done

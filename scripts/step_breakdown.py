@@ -34,6 +34,9 @@ def main():
                     "against 1/W of the entity tiles) instead of query-sharded")
     ap.add_argument("--graph", action="store_true", help="--emulate-world: replay each rank's local evaluation "
                     "from a hipGraph")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
+                    help="--emulate-world: workload (c2: the bench's trained TransE tables; c3-c5: the "
+                         "structured tables of the reference fixtures)")
     a = ap.parse_args()
     if a.emulate_world:
         return emulate(a)
@@ -81,10 +84,17 @@ def emulate(a):
     swept and reduced alone (the all-gather is not included)."""
     from mmre.link import HEAD, TAIL, LinkSweep
     from mmre.sharding import lpt_partition
+    from mmre.workloads import REF_PARITY, structured_tables, synthetic_large, train_transe, workload_spec
     dev = torch.device("cuda:0")
-    w = zs_workload()
+    (dataset, model, dim), _, _ = REF_PARITY[a.config]
+    w = synthetic_large(dim=dim) if dataset == "synthetic-1M" else zs_workload(dataset, model, dim)
+    if a.config == "c2":
+        w["norm_flag"] = True
+        train_transe(w, dev, steps=300)  # the bench's tables
+    else:
+        structured_tables(w)
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], w["n_ent"], w["n_rel"])
-    spec = ScoreSpec(model="transe", ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=200, norm_flag=True)
+    spec = workload_spec(w, dev)
     th, tr, tt = (np.asarray(x, np.int64) for x in (w["test_h"], w["test_r"], w["test_t"]))
     n = len(th)
     qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
@@ -96,6 +106,10 @@ def emulate(a):
         masks = [np.ones(2 * n, bool)] * a.emulate_world
     to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
     worst = 0.0
+    if a.emulate_world > 1:  # N = 1 under the same harness, for the ratio
+        masks = [np.ones(2 * n, bool)] + list(masks)
+        slices = [(0, w["n_ent"])] + list(slices)
+    one = None
     for k, m in enumerate(masks):
         er = slices[k] if a.entity else None
         q = [to(x[m]) for x in (qh, qr, qt, qm)]
@@ -123,11 +137,17 @@ def emulate(a):
             for _ in range(3):
                 step()
         ms = timeit(step, a.reps)
+        sweep = ev[0].elapsed_time(ev[1]) if not a.graph else float("nan")
+        if a.emulate_world > 1 and k == 0:
+            one = ms
+            print(f"N=1: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms")
+            continue
         worst = max(worst, ms)
-        print(f"rank {k}: {int(m.sum())} sweeps, step {ms:.3f} ms, sweep kernel {ev[0].elapsed_time(ev[1]):.3f} ms")
-    print(f"world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "
-          f"slowest rank {worst:.3f} ms "
-          f"(+ all-gather + metric reduction)")
+        print(f"rank {k - (1 if one is not None else 0)}: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms, "
+              f"sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms")
+    ratio = f", N=1 / slowest = {one / worst:.2f}x" if one else ""
+    print(f"{a.config} world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "
+          f"slowest rank {worst:.3f} ms (+ all-gather + metric reduction){ratio}")
 
 
 if __name__ == "__main__":
