@@ -398,27 +398,6 @@ int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_total, const 
                         float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
                         float* d_grad_ent, float* d_grad_rel, float* d_work, float lr, void* stream);
 
-/* The same training step as TWO launches (same batches, losses, scores, gradients, parameters
- * and LCG states, bit for bit): the sampler and the row norms run inside the fused loss kernel
- * (each positive's workgroup draws its own rows; norms with the pre-pass's arithmetic where the
- * rows are used), then the row owner (gradient + SGD + the loss). The slot counts are
- * double-buffered by step parity in d_state -- mmre_ns_step_state_bytes(n_ent, n_rel) bytes,
- * ZEROED by the caller before the first step and kept (not shared, not modified) between steps:
- * step i files into one buffer and zeroes the other, which step i - 1's row owner has read. */
-int64_t mmre_ns_step_state_bytes(int64_t n_ent, int64_t n_rel);
-int mmre_ns_step_openke_persistent(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
-                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
-                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
-                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
-                                   const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads,
-                                   int64_t mode, const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h,
-                                   int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
-                                   int model, int norm_flag, float* d_ent, float* d_rel, int64_t n_ent,
-                                   int64_t n_rel, int dim, int64_t batch, int64_t neg, float loss_margin,
-                                   float adv_temperature, float regul_rate, float* d_score, float* d_loss,
-                                   float* d_grad_ent, float* d_grad_rel, float* d_work, int32_t* d_state, float lr,
-                                   void* stream);
-
 /* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
  * batch = n_rows, neg = 0, d_loss = NULL. Its backward (OpenKE Model.forward under any loss,
  * Model.py / SoftplusLoss.py:7-31 / SigmoidLoss.py:7-30; the repo's scoring_fn / _calc,

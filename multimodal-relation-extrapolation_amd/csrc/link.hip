@@ -1668,38 +1668,58 @@ __device__ __forceinline__ uint32_t bf16_rn_bits(float x) {  // finite x: round 
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 
-// One thread per column c of a k-major plane (K rows x pad, columns col0 + c): the column's
-// split blocks out[kb][c] = {hi[16], lo[16]} (4 x 16 B) and its 2-norm (>= 2^-30).
+// One thread per (column c, 16-k block kb) of a k-major plane (K rows x pad, columns col0 + c):
+// the split block out[kb][c] = {hi[16], lo[16]} (4 x 16 B). Consecutive threads take
+// consecutive columns of one block: coalesced 64-B-per-thread reads and writes.
 __global__ __launch_bounds__(256) void k_bf3_split(const float* __restrict__ km, int64_t pad, int64_t col0,
-                                                   int64_t n_cols, int ktot, uint4* __restrict__ out,
-                                                   int64_t out_pad, float* __restrict__ norms) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n_cols) return;
-  const float* src = km + col0 + c;
-  float ss = 0.0f;
-  for (int kb = 0; kb < ktot / 16; ++kb) {
-    uint32_t hw[8], lw[8];
+                                                   int64_t n_cols, int nkb, uint4* __restrict__ out,
+                                                   int64_t out_pad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_cols * nkb) return;
+  const int kb = (int)(i / n_cols);
+  const int64_t c = i - (int64_t)kb * n_cols;
+  const float* src = km + col0 + c + (int64_t)kb * 16 * pad;
+  float x[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float x = src[(int64_t)(kb * 16 + j) * pad];
-      ss = __builtin_fmaf(x, x, ss);
-      uint32_t hb = 0u, lb = 0u;
-      if (!(fabsf(x) < INFINITY)) {
-        hb = 0x7FC0u;  // inf / NaN: a NaN operand, every product NaN: the pair is undecided
-      } else if (fabsf(x) >= 0x1p-60f) {
-        hb = bf16_rn_bits(x);
-        lb = bf16_rn_bits(x - __uint_as_float(hb << 16));  // x - hi is exact (Sterbenz)
-      }
-      if (j & 1) { hw[j >> 1] |= hb << 16; lw[j >> 1] |= lb << 16; }
-      else { hw[j >> 1] = hb; lw[j >> 1] = lb; }
+  for (int j = 0; j < 16; ++j) x[j] = src[(int64_t)j * pad];  // all in flight together
+  uint32_t hw[8], lw[8];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t hb = 0u, lb = 0u;
+    if (!(fabsf(x[j]) < INFINITY)) {
+      hb = 0x7FC0u;  // inf / NaN: a NaN operand, every product NaN: the pair is undecided
+    } else if (fabsf(x[j]) >= 0x1p-60f) {
+      hb = bf16_rn_bits(x[j]);
+      lb = bf16_rn_bits(x[j] - __uint_as_float(hb << 16));  // x - hi is exact (Sterbenz)
     }
-    uint4* o = out + ((int64_t)kb * out_pad + c) * 4;
-    o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-    o[1] = make_uint4(hw[4], hw[5], hw[6], hw[7]);
-    o[2] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-    o[3] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
+    if (j & 1) { hw[j >> 1] |= hb << 16; lw[j >> 1] |= lb << 16; }
+    else { hw[j >> 1] = hb; lw[j >> 1] = lb; }
   }
-  norms[c] = fmaxf(sqrtf(ss), 0x1p-30f);  // inf stays inf (bound inf: undecided); NaN: the hi is NaN
+  uint4* o = out + ((int64_t)kb * out_pad + c) * 4;
+  o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  o[1] = make_uint4(hw[4], hw[5], hw[6], hw[7]);
+  o[2] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  o[3] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
+}
+
+// The bound's 2-norms, one wave per row of a row-major copy (rows r0 .. r0 + n_out - 1, K
+// floats each; rows >= n_rows get 0 -- padding the sweep never counts): |x|_2 clamped to
+// >= 2^-30, inf / NaN kept (the bound is then inf / NaN: undecided). Any summation order
+// serves -- the bound's 2 % slack covers the norm's rounding.
+__global__ __launch_bounds__(256) void k_bf3_norms(const float* __restrict__ rows, int64_t n_rows, int64_t r0,
+                                                   int64_t n_out, int ktot, float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n_out) return;
+  const int64_t r = r0 + i;
+  float ss = 0.0f;
+  if (r < n_rows) {
+    const float* x = rows + r * (int64_t)ktot;
+    for (int k = lane; k < ktot; k += 64) ss = __builtin_fmaf(x[k], x[k], ss);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  if (lane == 0) norms[i] = r < n_rows ? fmaxf(sqrtf(ss), 0x1p-30f) : 0.0f;
 }
 
 // The sweep: units, grid and staging as k_sweep_mfma's 16-row plain variant (4 workgroups per
@@ -2364,10 +2384,15 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   const float cb = (float)(1.02 * (7.0 * K * std::ldexp(1.0, -24) * (1.0 + std::ldexp(1.0, -7)) +
                                    3.02 * std::ldexp(1.0, -16) + std::ldexp(1.0, -29) * std::sqrt(K)));
   MMRE_CHECK(hipMemsetAsync(hdr, 0, 8, st));
-  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0,
-                     q_pad, ktot, qb, q_pad, qn);
-  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((e_cols + 255) / 256)), dim3(256), 0, st, d_ent_km, e_pad, e_begin,
-                     e_cols, ktot, eb, e_pad, en);
+  const int nkb = ktot / 16;
+  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad * nkb + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad,
+                     (int64_t)0, q_pad, nkb, qb, q_pad);
+  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((e_cols * nkb + 255) / 256)), dim3(256), 0, st, d_ent_km, e_pad,
+                     e_begin, e_cols, nkb, eb, e_pad);
+  hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((q_pad + 3) / 4)), dim3(256), 0, st, d_q_rows, n_query, (int64_t)0,
+                     q_pad, ktot, qn);
+  hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((e_cols + 3) / 4)), dim3(256), 0, st, d_ent_rows, n_ent, e_begin,
+                     e_cols, ktot, en);
   MMRE_CHECK_LAUNCH();
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
   static const char* order_env = getenv("MMRE_MFMA_EMAJOR");

@@ -713,46 +713,11 @@ __device__ __forceinline__ float wave_sum_u(float v) {
 // (h + r) - t in the corrupted-row registers as its rows arrive, and each of its rows that is
 // not the positive's gets a slot of its own. Every operand is a normalised row of the pre-pass
 // (norm_flag) or the table row itself.
-// The two-launch training step (mmre_ns_step_openke_persistent): the sampler runs inside the
-// fused kernel (each positive's workgroup draws its own rows) and the row norms are computed
-// where the rows are used (the pre-pass's arithmetic: vsq, wave_sum, sqrtf, x / max(|x|, eps):
-// the same floats), so the step has no first launch. The slot counts and the overflow count are
-// double-buffered by step parity (ctr, advanced by the fused kernel's last workgroup): step i's
-// fused kernel files into buffer ctr & 1 and zeroes the other one, which step i - 1's row owner
-// has finished reading; step i's row owner reads buffer (ctr - 1) & 1.
-#ifndef NS_STEP2_WAVES
-#define NS_STEP2_WAVES 5  // waves per SIMD the two-launch fused kernel is compiled for
-#endif
-struct NSStep2 {
-  OpenKESamplerArgs sa;      // the sampler (its ticket: the fused kernel's workgroups)
-  int32_t* counts2;          // [2][n_rows] slot counts
-  int32_t* ovf2;             // [2] overflow counts
-  int32_t* ctr;              // steps run (parity)
-  int64_t n_rows;
-  const float *ent, *rel;    // the raw tables
-  int norm_flag;
-};
-
-// raw table row -> the operand the model uses (normalised under norm_flag) and the raw row's 2-norm
-template <int NC>
-__device__ __forceinline__ float load_operand(Vec<NC>& o, const float* table, int64_t row, int d, int lane,
-                                              int norm_flag) {
-  vload_row(o, table, row, d, lane);
-  const float nr = sqrtf(wave_sum(vsq(o)));  // ns_prepass_block's arithmetic, bit for bit
-  if (norm_flag) {
-    const float cn = fmaxf(nr, 1e-12f);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) o.v[c] = o.v[c] / cn;
-  }
-  return nr;
-}
-
-template <int NC, bool L2, bool REG, bool S2>
+template <int NC, bool L2, bool REG>
 __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __restrict__ nrm_e,
                                               const float* __restrict__ nrm_r, float* __restrict__ score,
-                                              float* __restrict__ part, const NSSlots& S_, int64_t n_ent, int64_t b,
-                                              const float* __restrict__ ent_n, const float* __restrict__ rel_n,
-                                              const NSStep2* __restrict__ s2 = nullptr) {
+                                              float* __restrict__ part, const NSSlots& S, int64_t n_ent, int64_t b,
+                                              const float* __restrict__ ent_n, const float* __restrict__ rel_n) {
   __shared__ float s_n[NSW * NSF_MAXJ];
   __shared__ float s_c[NSW * NSF_MAXJ];
   __shared__ float s_gp;
@@ -761,68 +726,20 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
   __shared__ float s_occ[NSW][3];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   const int d = A.dim;
+  const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
   // this wave's negatives j = w + NSW u, u < nj; lane u holds negative u's row ids
   const int nj = w < A.K ? (int)((A.K - w + NSW - 1) / NSW) : 0;
-  NSSlots S = S_;
-  int64_t ph, pr, pt;
   int64_t my_h = 0, my_t = 0, my_r = 0;
-  if constexpr (S2) {
-    const int par = __builtin_amdgcn_readfirstlane(s2->ctr[0]) & 1;
-    S.counts = s2->counts2 + par * s2->n_rows;
-    S.ovf_n = s2->ovf2 + par;
-    if (w == NSW - 1) {  // zero the other parity's counts (step i - 1's owner is done with them)
-      int32_t* z = s2->counts2 + (par ^ 1) * s2->n_rows;
-      const int64_t per = (s2->n_rows + A.B - 1) / A.B;
-      for (int64_t i = b * per + lane; i < (b + 1) * per && i < s2->n_rows; i += kWave) z[i] = 0;
-      if (b == 0 && lane == 0) s2->ovf2[par ^ 1] = 0;
-    }
-    // the sampler: lane u < nj draws this wave's negative u, lane 63 the positive (every wave:
-    // the same draws, so nothing waits on another wave); wave 0 writes the positive's batch row
-    const OpenKESamplerArgs& sa = s2->sa;
-    const bool neg = lane < nj, pos = lane == kWave - 1;
-    int64_t sh = 0, stt = 0, sr = 0;
-    if (neg || pos) {
-      const int64_t row = pos ? b : b + (w + NSW * (int64_t)lane + 1) * A.B;
-      float sy;
-      sampler_openke_value(row, sa.train_list, sa.train_total, sa.head_hrt, sa.tail_hrt, sa.rel_hrt, sa.lef_head,
-                           sa.rig_head, sa.lef_tail, sa.rig_tail, sa.lef_rel, sa.rig_rel, sa.left_mean,
-                           sa.right_mean, sa.n_ent, sa.n_rel, sa.seeds, sa.work_threads, sa.B, sa.neg, sa.neg_rel,
-                           sa.mode, sa.blk, sa.n_blk, sa.rel_prob, sh, stt, sr, sy);
-      if (neg || w == 0) { sa.bh[row] = sh; sa.bt[row] = stt; sa.br[row] = sr; sa.by[row] = sy; }
-    }
-    ph = readlane64u(sh, kWave - 1);
-    pr = readlane64u(sr, kWave - 1);
-    pt = readlane64u(stt, kWave - 1);
-    my_h = sh; my_t = stt; my_r = sr;
-  } else {
-    ph = A.h[b]; pr = A.r[b]; pt = A.t[b];
-    if (lane < nj) {
-      const int64_t row = b + (w + NSW * (int64_t)lane + 1) * A.B;
-      my_h = A.h[row]; my_t = A.t[row]; my_r = A.r[row];
-    }
+  if (lane < nj) {
+    const int64_t row = b + (w + NSW * (int64_t)lane + 1) * A.B;
+    my_h = A.h[row]; my_t = A.t[row]; my_r = A.r[row];
   }
-  // the rows as the model uses them: normalised by the pre-pass (norm_flag), else the tables;
-  // S2: loaded raw and normalised here
-  const int nf = S2 ? s2->norm_flag : 0;
-  const float* ent_u = S2 ? s2->ent : ent_n;
-  const float* rel_u = S2 ? s2->rel : rel_n;
-  auto ld = [&](Vec<NC>& o, bool is_ent, int64_t id) -> float {
-    if constexpr (S2) return load_operand(o, is_ent ? ent_u : rel_u, id, d, lane, nf);
-    vload_row(o, is_ent ? ent_n : rel_n, id, d, lane);
-    return 0.0f;
-  };
+  // the rows as the model uses them: normalised by the pre-pass (norm_flag), else the tables
   Vec<NC> hn, rn, tn;
-  float nph, npr, npt;
-  if constexpr (S2) {
-    nph = ld(hn, true, ph);
-    npr = ld(rn, false, pr);
-    npt = ld(tn, true, pt);
-  } else {
-    ld(hn, true, ph);
-    ld(rn, false, pr);
-    ld(tn, true, pt);
-    nph = nrm_e[ph]; npr = nrm_r[pr]; npt = nrm_e[pt];
-  }
+  vload_row(hn, ent_n, ph, d, lane);
+  vload_row(rn, rel_n, pr, d, lane);
+  vload_row(tn, ent_n, pt, d, lane);
+  const float nph = nrm_e[ph], npr = nrm_r[pr], npt = nrm_e[pt];
   // issue every corrupted-row load of the wave before any arithmetic
   Vec<NC> C[NSF_MAXJ];
   float cnr[NSF_MAXJ];
@@ -834,17 +751,17 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     if (u < nj) {
       const int64_t h = readlane64u(my_h, u), t = readlane64u(my_t, u), r = readlane64u(my_r, u);
       const bool oh = h == ph, ot = t == pt, orr = r == pr;
-      if (orr && ot && !oh) { code[u] = 0; const float nr = ld(C[u], true, h); cnr[u] = REG ? (S2 ? nr : nrm_e[h]) : 0.0f; }
-      else if (orr && oh && !ot) { code[u] = 1; const float nr = ld(C[u], true, t); cnr[u] = REG ? (S2 ? nr : nrm_e[t]) : 0.0f; }
-      else if (oh && ot && !orr) { code[u] = 2; const float nr = ld(C[u], false, r); cnr[u] = REG ? (S2 ? nr : nrm_r[r]) : 0.0f; }
+      if (orr && ot && !oh) { code[u] = 0; vload_row(C[u], ent_n, h, d, lane); cnr[u] = REG ? nrm_e[h] : 0.0f; }
+      else if (orr && oh && !ot) { code[u] = 1; vload_row(C[u], ent_n, t, d, lane); cnr[u] = REG ? nrm_e[t] : 0.0f; }
+      else if (oh && ot && !orr) { code[u] = 2; vload_row(C[u], rel_n, r, d, lane); cnr[u] = REG ? nrm_r[r] : 0.0f; }
       else if (!(oh && ot && orr)) {  // shares fewer than two rows: x = (h + r) - t, built here
         code[u] = 4;
-        if (oh) C[u] = hn; else ld(C[u], true, h);
+        if (oh) C[u] = hn; else vload_row(C[u], ent_n, h, d, lane);
         Vec<NC> o;
-        if (orr) o = rn; else ld(o, false, r);
+        if (orr) o = rn; else vload_row(o, rel_n, r, d, lane);
 #pragma unroll
         for (int q = 0; q < NC; ++q) C[u].v[q] = C[u].v[q] + o.v[q];
-        if (ot) o = tn; else ld(o, true, t);
+        if (ot) o = tn; else vload_row(o, ent_n, t, d, lane);
 #pragma unroll
         for (int q = 0; q < NC; ++q) C[u].v[q] = C[u].v[q] - o.v[q];
       }
@@ -892,15 +809,7 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     const float n = A.use_model_margin ? A.model_margin - sv : sv;
     if (code[u] == 4) {  // rare: its raw norms read here (the regularization's squared norms)
       const int64_t h = readlane64u(my_h, u), r = readlane64u(my_r, u), t = readlane64u(my_t, u);
-      float a, c, e;
-      if constexpr (S2) {  // no norm tables: the rows again (rare path)
-        Vec<NC> o;
-        a = h == ph ? nph : load_operand(o, ent_u, h, d, lane, 0);
-        c = r == pr ? npr : load_operand(o, rel_u, r, d, lane, 0);
-        e = t == pt ? npt : load_operand(o, ent_u, t, d, lane, 0);
-      } else {
-        a = h == ph ? nph : nrm_e[h]; c = r == pr ? npr : nrm_r[r]; e = t == pt ? npt : nrm_e[t];
-      }
+      const float a = h == ph ? nph : nrm_e[h], c = r == pr ? npr : nrm_r[r], e = t == pt ? npt : nrm_e[t];
       qh += a * a; qr += c * c; qt += e * e;
     } else {
       const float sq = cnr[u] * cnr[u];
@@ -1065,19 +974,6 @@ __device__ __forceinline__ void ns_fused_body(const NSArgs& A, const float* __re
     vstore_row(S.shared, 3 * b + 0, Gh, d, lane);
     vstore_row(S.shared, 3 * b + 1, Gr, d, lane);
     vstore_row(S.shared, 3 * b + 2, Gt, d, lane);
-    if constexpr (S2) {
-      // the sampler's seed ticket (every wave read its seeds long before): the last workgroup
-      // advances the per-pthread seeds for the next step, resets the ticket and counts the step
-      int last = 0;
-      if (lane == 0) last = atomicAdd(s2->sa.ticket, 1) == (int)gridDim.x - 1;
-      last = __builtin_amdgcn_readfirstlane(last);
-      if (last) {
-        const OpenKESamplerArgs& sa = s2->sa;
-        for (int64_t id = lane; id < sa.work_threads; id += kWave)
-          sa.seeds[id] = advanced_seed(sa.seeds[id], id, sa.work_threads, sa.B, sa.adv_per);
-        if (lane == 0) { *sa.ticket = 0; s2->ctr[0] = s2->ctr[0] + 1; }
-      }
-    }
   }
 }
 
@@ -1089,15 +985,7 @@ __global__ __launch_bounds__(256, NC > 4 ? 1 : (L2 ? 5 : 6)) void k_ns_transe_fu
                                                          float* __restrict__ part, NSSlots S, int64_t n_ent,
                                                          const float* __restrict__ ent_n,
                                                          const float* __restrict__ rel_n) {
-  ns_fused_body<NC, L2, REG, false>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, ent_n, rel_n);
-}
-
-// The two-launch step's fused kernel (NSStep2): sampler, norms and the fused loss in one launch.
-template <int NC, bool L2, bool REG>
-__global__ __launch_bounds__(256, NC > 4 ? 1 : NS_STEP2_WAVES) void k_ns_transe_step2(NSArgs A, float* __restrict__ score,
-                                                                              float* __restrict__ part, NSSlots S,
-                                                                              int64_t n_ent, NSStep2 s2) {
-  ns_fused_body<NC, L2, REG, true>(A, nullptr, nullptr, score, part, S, n_ent, blockIdx.x, nullptr, nullptr, &s2);
+  ns_fused_body<NC, L2, REG>(A, nrm_e, nrm_r, score, part, S, n_ent, blockIdx.x, ent_n, rel_n);
 }
 
 __device__ __forceinline__ uint64_t lanes_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
@@ -1301,30 +1189,45 @@ struct HubOrder {
 
 // The hub rows of the table (n > NS_HUB), in row order, dealt round-robin to the kernel's
 // n_hub_wg extra workgroups: hb-th of them calls f(row, n) for the rows k = hb, hb + n_hub_wg, ...
-// (the whole workgroup together).
+// (the whole workgroup together). The counts are scanned HUB_SCAN rows per pass, each thread
+// loading HUB_SCAN / 256 consecutive counts at once (one round trip per pass, not one per 256
+// rows: the per-256 scan serialised ~57 load latencies and two barriers each at C2 and kept the
+// owner kernel alive for ~70 us); a pass's hub rows are found through one 16-bit mask per
+// thread in LDS and four wave ballots.
+constexpr int HUB_SCAN = 4096;
 template <class F>
 __device__ __forceinline__ void for_hub_rows(const int32_t* __restrict__ counts, int64_t n_rows, int hb, int n_hub_wg,
-                                             uint64_t* s_masks, F&& f) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+                                             uint16_t* s_bits, F&& f) {
+  constexpr int PER = HUB_SCAN / 256;  // 16 consecutive rows per thread
+  const int tid = threadIdx.x, lane = tid & 63;
   int64_t k = 0;
-  for (int64_t base = 0; base < n_rows; base += 256) {
-    const int64_t row = base + tid;
-    const bool hub = row < n_rows && counts[row] > NS_HUB;
-    const uint64_t m = __ballot(hub);
-    if (lane == 0) s_masks[w] = m;
+  for (int64_t base = 0; base < n_rows; base += HUB_SCAN) {
+    const int64_t r0 = base + (int64_t)tid * PER;
+    int c[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) c[i] = r0 + i < n_rows ? counts[r0 + i] : 0;  // all in flight together
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) bits |= (uint32_t)(c[i] > NS_HUB) << i;
+    __syncthreads();  // the previous pass's readers of s_bits are done
+    s_bits[tid] = (uint16_t)bits;
     __syncthreads();
-    uint64_t mk[4] = {s_masks[0], s_masks[1], s_masks[2], s_masks[3]};
-    __syncthreads();
-    for (int ww = 0; ww < 4; ++ww) {
-      uint64_t mm = mk[ww];
-      while (mm) {
-        const int b = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        if (k % n_hub_wg == hb) {
-          const int64_t r = base + ww * 64 + b;
-          f(r, counts[r]);
+    for (int q = 0; q < 4; ++q) {  // threads 64q .. 64q + 63, in order
+      const uint32_t mine = s_bits[q * 64 + lane];
+      uint64_t nz = __ballot(mine != 0u);
+      while (nz) {
+        const int t = __builtin_ctzll(nz);
+        nz &= nz - 1;
+        uint32_t m = s_bits[q * 64 + t];
+        while (m) {
+          const int i = __builtin_ctz(m);
+          m &= m - 1u;
+          if (k % n_hub_wg == hb) {
+            const int64_t r = base + (int64_t)(q * 64 + t) * PER + i;
+            f(r, counts[r]);
+          }
+          ++k;
         }
-        ++k;
       }
     }
   }
@@ -1441,7 +1344,7 @@ __device__ __forceinline__ HubOrder hub_order(int64_t (*s_hub)[NS_HUB], int32_t*
 // written to every row of the gradient table. sgd_lr > 0 (the optimizer's plain SGD step fused
 // in, mmre_ns_fused_grad_sgd): the row's parameters also become fma(-lr, g, v), torch's SGD
 // arithmetic; rows without slots keep theirs (p - lr * 0 = p). Rows with more than NS_HUB slots
-// go to the n_hub_wg workgroups from hub_block0 on (HubOrder). With SGD the parameter tables
+// go to the first n_hub_wg workgroups (HubOrder); rows start at workgroup row_block0. With SGD the parameter tables
 // ent / rel are also pent / prel (read, then written, by the row's own wave): not __restrict__.
 template <int NC, bool L2>
 __global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const float* rel,
@@ -1455,41 +1358,30 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const fl
                                                       float* __restrict__ grel, float sgd_lr, float* pent,
                                                       float* prel, NSArgs RA, const float* __restrict__ part,
                                                       float* __restrict__ loss, int64_t reduce_block,
-                                                      int64_t hub_block0, int n_hub_wg, int64_t n_slots,
-                                                      const int32_t* __restrict__ step_ctr, int64_t count_stride) {
+                                                      int64_t row_block0, int n_hub_wg, int64_t n_slots) {
   __shared__ int64_t s_hub[4][NS_HUB];
-  __shared__ uint64_t s_masks[4];
+  __shared__ uint16_t s_bits[256];
   __shared__ int32_t s_hc[2];
   if ((int64_t)blockIdx.x == reduce_block) {  // the training step's loss (mmre_ns_step_openke): one extra workgroup
     ns_reduce_block(RA, part, loss);
     return;
   }
-  if (step_ctr != nullptr) {  // the two-launch step (NSStep2): this step's parity of the counts
-    const int par = (__builtin_amdgcn_readfirstlane(step_ctr[0]) - 1) & 1;
-    counts += par * count_stride;
-    ovf_n += par;
-  }
-  // no norm tables (the two-launch step): each row's norm from the row itself, the pre-pass's arithmetic
-  auto norm_of = [&](const Vec<NC>& v, bool is_ent, int64_t id) -> float {
-    if (nrm_e == nullptr) return sqrtf(wave_sum(vsq(v)));
-    return (is_ent ? nrm_e : nrm_r)[id];
-  };
   const int lane = threadIdx.x & 63;
-  if ((int64_t)blockIdx.x >= hub_block0) {  // hub rows, a workgroup each
-    for_hub_rows(counts, n_ent + n_rel, (int)((int64_t)blockIdx.x - hub_block0), n_hub_wg, s_masks,
+  if ((int64_t)blockIdx.x < n_hub_wg) {  // hub rows: the first n_hub_wg workgroups (they start first)
+    for_hub_rows(counts, n_ent + n_rel, (int)blockIdx.x, n_hub_wg, s_bits,
                  [&](int64_t row, int n) {
                    const bool is_ent = row < n_ent;
                    const int64_t id = is_ent ? row : row - n_ent;
                    Vec<NC> v;
                    vload_row(v, is_ent ? ent : rel, id, d, lane);
-                   const float nv = norm_of(v, is_ent, id);
+                   const float nv = (is_ent ? nrm_e : nrm_r)[id];
                    HubOrder ord = hub_order(s_hub, s_hc, bucket, ovf, ovf_n[0], n, row, n_slots);
                    transe_owner_row<NC, L2>(ord, threadIdx.x < 64, row, n, v, nv, n_ent, d, norm_flag, reg, shared,
                                             rec, K, grad_loss, gent, grel, sgd_lr, pent, prel);
                  });
     return;
   }
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = ((int64_t)blockIdx.x - row_block0) * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
@@ -1500,7 +1392,7 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const fl
   int64_t pre = lane < NS_BUCKET_HEAD ? bucket[row * NS_BUCKET + lane] : 0;
   Vec<NC> v;
   vload_row(v, is_ent ? ent : rel, id, d, lane);
-  const float nv_tab = nrm_e ? (is_ent ? nrm_e : nrm_r)[id] : 0.0f;  // in flight with the row
+  const float nv = (is_ent ? nrm_e : nrm_r)[id];
   if (n > NS_HUB) return;  // a hub workgroup's row
   if (n > NS_BUCKET_HEAD && lane >= NS_BUCKET_HEAD && lane < n) pre = bucket[row * NS_BUCKET + lane];
   if (n == 0) {  // not in the batch: zero gradient (and an unchanged parameter row)
@@ -1510,7 +1402,6 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const fl
     vstore_row((is_ent ? gent : grel) + id * d, 0, z, d, lane);
     return;
   }
-  const float nv = nrm_e ? nv_tab : sqrtf(wave_sum(vsq(v)));
   SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, 0};
   ord.init();
   transe_owner_row<NC, L2>(ord, true, row, n, v, nv, n_ent, d, norm_flag, reg, shared, rec, K, grad_loss, gent, grel,
@@ -2006,7 +1897,7 @@ __device__ __forceinline__ void gen_owner_row(Ord& ord, bool active, const NSArg
 // One wave per table row: its slots' records summed in slot order, + reg (occurrences) v, times
 // the upstream gradient, written to every row of the gradient tables (and, with sgd_lr, the
 // parameter rows updated by fma(-lr, g, v)). Rows with more than NS_HUB slots go to the
-// n_hub_wg workgroups from hub_block0 on (HubOrder).
+// first n_hub_wg workgroups (HubOrder); rows start at workgroup row_block0.
 template <int NC>
 __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, int64_t n_rel, float reg_ent,
                                                       float reg_rel, const float* __restrict__ rec,
@@ -2016,9 +1907,9 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
                                                       int dpad, const float* __restrict__ grad_loss, float* gent,
                                                       float* gent_im, float* grel, float* grel_im, float sgd_lr,
                                                       float* pent, float* pent_im, float* prel, float* prel_im,
-                                                      int64_t hub_block0, int n_hub_wg, int64_t n_slots) {
+                                                      int64_t row_block0, int n_hub_wg, int64_t n_slots) {
   __shared__ int64_t s_hub[4][NS_HUB];
-  __shared__ uint64_t s_masks[4];
+  __shared__ uint16_t s_bits[256];
   __shared__ int32_t s_hc[2];
   (void)dpad;
   const int lane = threadIdx.x & 63;
@@ -2038,8 +1929,8 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
       if (A.model == MMRE_COMPLEX) { ob = grel_im + id * d; pb = prel_im ? prel_im + id * d : nullptr; }
     }
   };
-  if ((int64_t)blockIdx.x >= hub_block0) {  // hub rows, a workgroup each
-    for_hub_rows(counts, n_ent + n_rel, (int)((int64_t)blockIdx.x - hub_block0), n_hub_wg, s_masks,
+  if ((int64_t)blockIdx.x < n_hub_wg) {  // hub rows: the first n_hub_wg workgroups (they start first)
+    for_hub_rows(counts, n_ent + n_rel, (int)blockIdx.x, n_hub_wg, s_bits,
                  [&](int64_t row, int n) {
                    const bool is_ent = row < n_ent;
                    float *oa, *ob, *pa, *pb;
@@ -2052,7 +1943,7 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
                  });
     return;
   }
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = ((int64_t)blockIdx.x - row_block0) * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
@@ -2315,7 +2206,7 @@ static int rows_backward_impl(const NSArgs& A, const float* d_coef, int64_t n_ro
     hipLaunchKernelGGL((k_rows_slots<NC_>), sgrid, blk, 0, st, A, d_coef, n_rows, S, n_ent, with_reg);              \
     hipLaunchKernelGGL((k_ns_gen_owner<NC_>), hgrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec, S.counts, \
                        S.bucket, S.ovf, S.ovf_n, 0, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel,             \
-                       d_grad_rel_im, 0.0f, nullptr, nullptr, nullptr, nullptr, (int64_t)ogrid.x, NS_HUB_WG,        \
+                       d_grad_rel_im, 0.0f, nullptr, nullptr, nullptr, nullptr, (int64_t)NS_HUB_WG, NS_HUB_WG,        \
                        3 * n_rows);                                                                                 \
   } while (0)
   if (nc == 1) MMRE_ROWS(1);
@@ -2521,9 +2412,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
                            const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
                            float regul_rate, const float* d_score, const float* d_grad_loss, float* d_grad_ent,
                            float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work, float lr,
-                           float* pe, float* pei, float* pr, float* pri, void* stream, float* d_loss_out = nullptr,
-                           const int32_t* step_ctr = nullptr, int32_t* step_counts = nullptr,
-                           int32_t* step_ovf = nullptr) {
+                           float* pe, float* pei, float* pr, float* pri, void* stream, float* d_loss_out = nullptr) {
   NSArgs A;
   int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                    phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
@@ -2559,7 +2448,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
                          (int)(regul_rate != 0.0f));                                                                \
     hipLaunchKernelGGL((k_ns_gen_owner<NC_>), dim3(ogrid.x + NS_HUB_WG), blk, 0, st, A, n_ent, n_rel, reg_ent,       \
                        reg_rel, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent,          \
-                       d_grad_ent_im, d_grad_rel, d_grad_rel_im, lr, pe, pei, pr, pri, (int64_t)ogrid.x, NS_HUB_WG,  \
+                       d_grad_ent_im, d_grad_rel, d_grad_rel_im, lr, pe, pei, pr, pri, (int64_t)NS_HUB_WG, NS_HUB_WG,  \
                        w.slots);                                                                                    \
   } while (0)
     if (nc == 1) MMRE_NS_GEN(1);
@@ -2572,20 +2461,16 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
   }
   const float reg = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (3.0 * N * dim)) : 0.0f;
   // the training step (d_loss_out): one more workgroup reduces the forward's loss partials
-  const int64_t reduce_block = d_loss_out ? (int64_t)ogrid.x : -1;
-  // after the row workgroups: the loss reduction (the training step), then the hub workgroups
-  const int64_t hub_block0 = (int64_t)ogrid.x + (d_loss_out ? 1 : 0);
-  const dim3 ogrid2((unsigned)(hub_block0 + NS_HUB_WG));
-  // the two-launch step (step_ctr): parity-buffered counts, norms computed by the owner itself
-  const float* nrm_e_o = step_ctr ? nullptr : d_work + w.nrm_e;
-  const float* nrm_r_o = step_ctr ? nullptr : d_work + w.nrm_r;
-  const int32_t* cnt_o = step_ctr ? step_counts : S.counts;
-  const int32_t* ovf_n_o = step_ctr ? step_ovf : S.ovf_n;
+  // the hub workgroups first (their count scan starts with the kernel), then (the training
+  // step) the loss reduction's workgroup, then one workgroup per 4 table rows
+  const int64_t reduce_block = d_loss_out ? (int64_t)NS_HUB_WG : -1;
+  const int64_t row_block0 = (int64_t)NS_HUB_WG + (d_loss_out ? 1 : 0);
+  const dim3 ogrid2((unsigned)(row_block0 + ogrid.x));
 #define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
   hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid2, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
-                     nrm_e_o, nrm_r_o, S.shared, S.rec, cnt_o, S.bucket, S.ovf, ovf_n_o,                              \
+                     d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n,         \
                      neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr, A, d_work + w.part, d_loss_out,           \
-                     reduce_block, hub_block0, NS_HUB_WG, w.slots, step_ctr, n_ent + n_rel)
+                     reduce_block, row_block0, NS_HUB_WG, w.slots)
   const int nc = transe_fast_nc(A);
   const bool l2 = model == MMRE_TRANSE_L2;
   if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }
@@ -2720,68 +2605,4 @@ extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_to
                          d_batch_h, d_batch_t, d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
                          nullptr, d_grad_ent, nullptr, d_grad_rel, nullptr, d_work, lr, d_ent, nullptr, d_rel, nullptr,
                          stream, d_loss);
-}
-
-extern "C" int64_t mmre_ns_step_state_bytes(int64_t n_ent, int64_t n_rel) {
-  if (n_ent <= 0 || n_rel <= 0) return 0;
-  return (int64_t)sizeof(int32_t) * (2 * (n_ent + n_rel) + 3);
-}
-
-extern "C" int mmre_ns_step_openke_persistent(
-    const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt, const int64_t* d_tail_hrt,
-    const int64_t* d_rel_hrt, const int64_t* d_lef_head, const int64_t* d_rig_head, const int64_t* d_lef_tail,
-    const int64_t* d_rig_tail, const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
-    const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode, const int32_t* d_blocks,
-    int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
-    int model, int norm_flag, float* d_ent, float* d_rel, int64_t n_ent, int64_t n_rel, int dim, int64_t batch,
-    int64_t neg, float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
-    float* d_grad_ent, float* d_grad_rel, float* d_work, int32_t* d_state, float lr, void* stream) {
-  if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
-      !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y || !d_ticket || !d_state)
-    return MMRE_ERR_ARG;
-  if ((d_left_mean == nullptr) != (d_right_mean == nullptr)) return MMRE_ERR_ARG;
-  if (train_total <= 0 || n_ent <= 1 || work_threads <= 0 || batch <= 0 || neg <= 0 || mode < -1 || mode > 1)
-    return MMRE_ERR_ARG;
-  if (n_blocks < 0 || (n_blocks > 0 && !d_blocks)) return MMRE_ERR_ARG;
-  if (!d_score || !d_loss || !d_grad_ent || !d_grad_rel || !d_work || n_rel <= 0 || !(lr != 0.0f))
-    return MMRE_ERR_ARG;
-  NSArgs A;
-  int rc = ns_args(A, model, norm_flag, 0.0f, 0, d_ent, nullptr, d_rel, nullptr, dim, 0.0f, d_batch_h, d_batch_t,
-                   d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate);
-  if (rc) return rc;
-  if (!is_transe(model) || !fused_fast(A)) return MMRE_ERR_SHAPE;  // the fused TransE path's shapes only
-  if (n_ent + n_rel >= (int64_t)INT32_MAX / 2) return MMRE_ERR_SHAPE;
-  hipStream_t st = (hipStream_t)stream;
-  FusedWs w;
-  fused_ws(model, norm_flag, batch, neg, n_ent, n_rel, dim, w);
-  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
-  const int64_t n_rows = n_ent + n_rel;
-  NSStep2 s2{OpenKESamplerArgs{d_train_list, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head, d_lef_tail,
-                               d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, train_total, n_ent, n_rel,
-                               d_seeds, work_threads, batch, neg, 0, mode, d_blocks, n_blocks, d_batch_h, d_batch_t,
-                               d_batch_r, d_batch_y, d_ticket, mmre_sampler_draws_per_positive(neg, 0, mode), nullptr},
-             d_state, d_state + 2 * n_rows, d_state + 2 * n_rows + 2, n_rows, d_ent, d_rel, norm_flag};
-  const bool l2 = model == MMRE_TRANSE_L2;
-  const int nc = transe_fast_nc(A);
-  float* part = d_work + w.part;
-  const dim3 grid((unsigned)batch), blk(256);
-  // 1. sampler + norms + the fused loss kernel (scores, loss partials, slots)
-#define MMRE_NS_STEP2(NC_, L2_)                                                                                     \
-  do {                                                                                                             \
-    if (A.regul_rate != 0.0f)                                                                                      \
-      hipLaunchKernelGGL((k_ns_transe_step2<NC_, L2_, true>), grid, blk, 0, st, A, d_score, part, S, n_ent, s2);   \
-    else                                                                                                           \
-      hipLaunchKernelGGL((k_ns_transe_step2<NC_, L2_, false>), grid, blk, 0, st, A, d_score, part, S, n_ent, s2);  \
-  } while (0)
-  if (nc == 1) { if (l2) MMRE_NS_STEP2(1, true); else MMRE_NS_STEP2(1, false); }
-  else if (nc == 2) { if (l2) MMRE_NS_STEP2(2, true); else MMRE_NS_STEP2(2, false); }
-  else if (nc == 4) { if (l2) MMRE_NS_STEP2(4, true); else MMRE_NS_STEP2(4, false); }
-  else { if (l2) MMRE_NS_STEP2(8, true); else MMRE_NS_STEP2(8, false); }
-#undef MMRE_NS_STEP2
-  MMRE_CHECK_LAUNCH();
-  // 2. gradient + SGD (row owner, its own norms, this step's parity of the counts), and the loss
-  return fused_grad_impl(model, norm_flag, 0.0f, 0, d_ent, nullptr, d_rel, nullptr, n_ent, n_rel, dim, 0.0f,
-                         d_batch_h, d_batch_t, d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
-                         nullptr, d_grad_ent, nullptr, d_grad_rel, nullptr, d_work, lr, d_ent, nullptr, d_rel, nullptr,
-                         stream, d_loss, s2.ctr, s2.counts2, s2.ovf2);
 }

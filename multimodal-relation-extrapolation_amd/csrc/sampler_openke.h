@@ -145,16 +145,16 @@ static __device__ int64_t corrupt_rel(const int64_t* __restrict__ T, const int64
 // One GPU thread per output ROW (positive or negative): the state before any draw is the
 // pthread's seed advanced by an affine jump, so the rows of one positive -- a chain of up to
 // 1 + 2 neg dependent draws and binary searches in the reference -- are produced in parallel
-// (B (1 + neg + neg_rel) threads instead of B). sampler_openke_value returns the row's
-// (h, t, r, y); sampler_openke_row stores it into the batch.
-static __device__ __forceinline__ void sampler_openke_value(int64_t row,
+// (B (1 + neg + neg_rel) threads instead of B).
+static __device__ __forceinline__ void sampler_openke_row(int64_t row, 
     const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
     const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
     const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
     const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
     const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* __restrict__ seeds,
     int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk,
-    int64_t n_blk, const float* __restrict__ rel_prob, int64_t& oh, int64_t& ot, int64_t& orl, float& oy) {
+    int64_t n_blk, int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br,
+    float* __restrict__ by, const float* __restrict__ rel_prob) {
   const int64_t b = row % B, j = row / B;  // j = 0: the positive; 1..neg: entity negatives; then relation ones
   // slice of the reference's pthread `id` that owns position b (Base.cpp:93-100)
   const int64_t per = B % work_threads == 0 ? B / work_threads : B / work_threads + 1;
@@ -166,10 +166,9 @@ static __device__ __forceinline__ void sampler_openke_value(int64_t row,
   const int64_t i = rand_max(&st, train_total);  // Base.cpp:104
   const int64_t h = train_list[3 * i], r = train_list[3 * i + 1], t = train_list[3 * i + 2];
   if (j == 0) {
-    oh = h; ot = t; orl = r; oy = 1.0f;
+    bh[row] = h; bt[row] = t; br[row] = r; by[row] = 1.0f;
     return;
   }
-  oy = -1.0f;
   if (j <= neg) {
     const int64_t k = j - 1;
     st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * k));
@@ -186,36 +185,20 @@ static __device__ __forceinline__ void sampler_openke_value(int64_t row,
     int4 kb = make_int4(0, 0, 0, 0);
     if (pre) kb = reinterpret_cast<const int4*>(blk + 8 * i)[replace_tail ? 0 : 1];
     if (replace_tail) {  // corrupt_head returns a replacement TAIL (Base.cpp:116)
-      oh = h; orl = r;
-      ot = pre ? corrupt_in_block(head_hrt, 2, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
-               : corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r);
+      bh[row] = h; br[row] = r;
+      bt[row] = pre ? corrupt_in_block(head_hrt, 2, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
+                    : corrupt_head(head_hrt, lef_head, rig_head, n_ent, &st, h, r);
     } else {
-      ot = t; orl = r;
-      oh = pre ? corrupt_in_block(tail_hrt, 0, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
-               : corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r);
+      bt[row] = t; br[row] = r;
+      bh[row] = pre ? corrupt_in_block(tail_hrt, 0, n_ent, &st, kb.x, kb.y, kb.z, kb.w)
+                    : corrupt_tail(tail_hrt, lef_tail, rig_tail, n_ent, &st, t, r);
     }
   } else {
     const int64_t k = j - 1 - neg;
     st = lcg_jump(seeds[id], base + 1 + (uint64_t)(per_neg * neg + k));
-    oh = h; ot = t; orl = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r, rel_prob);
+    bh[row] = h; bt[row] = t; br[row] = corrupt_rel(rel_hrt, lef_rel, rig_rel, n_rel, &st, h, t, r, rel_prob);
   }
-}
-
-static __device__ __forceinline__ void sampler_openke_row(int64_t row,
-    const int64_t* __restrict__ train_list, int64_t train_total, const int64_t* __restrict__ head_hrt,
-    const int64_t* __restrict__ tail_hrt, const int64_t* __restrict__ rel_hrt, const int64_t* __restrict__ lef_head,
-    const int64_t* __restrict__ rig_head, const int64_t* __restrict__ lef_tail, const int64_t* __restrict__ rig_tail,
-    const int64_t* __restrict__ lef_rel, const int64_t* __restrict__ rig_rel, const float* __restrict__ left_mean,
-    const float* __restrict__ right_mean, int64_t n_ent, int64_t n_rel, const uint64_t* __restrict__ seeds,
-    int64_t work_threads, int64_t B, int64_t neg, int64_t neg_rel, int64_t mode, const int32_t* __restrict__ blk,
-    int64_t n_blk, int64_t* __restrict__ bh, int64_t* __restrict__ bt, int64_t* __restrict__ br,
-    float* __restrict__ by, const float* __restrict__ rel_prob) {
-  int64_t h, t, r;
-  float y;
-  sampler_openke_value(row, train_list, train_total, head_hrt, tail_hrt, rel_hrt, lef_head, rig_head, lef_tail,
-                       rig_tail, lef_rel, rig_rel, left_mean, right_mean, n_ent, n_rel, seeds, work_threads, B, neg,
-                       neg_rel, mode, blk, n_blk, rel_prob, h, t, r, y);
-  bh[row] = h; bt[row] = t; br[row] = r; by[row] = y;
+  by[row] = -1.0f;
 }
 
 

@@ -14,8 +14,6 @@ backward = d(loss)/d(embedding tables) into dense gradient tables: for every mod
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from ._lib import call, lib, ptr, require_cuda, stream_ptr
@@ -206,18 +204,13 @@ def score_rows(spec: NSSpec, ent, rel, h, t, r, ent_im=None, rel_im=None):
 class OpenKETrainStep:
     """One OpenKE training step for TransE -- Trainer.train_one_step (Trainer.py:43-54) over the
     loader's Base.cpp sampling, strategy/NegativeSampling + MarginLoss, optim.SGD -- as ONE C-ABI
-    call: the values of sampler.sample(B, neg, 0, mode) + fused_ns_loss(...).backward() +
-    SGD.step(), bit for bit (tests/test_ns_full_gpu.py). The parameters are updated in place;
-    ent.grad / rel.grad hold the step's gradient tables, `batch` the sampled batch, `score` the
-    row scores. Calling it returns the loss tensor (device).
-    two_launch (default; MMRE_NS_STEP2=0 turns it off): mmre_ns_step_openke_persistent -- the
-    sampler and the row norms inside the fused loss kernel, the slot counts double-buffered in a
-    step-state buffer this object owns (zeroed here, advanced by every step): two launches per
-    step. Otherwise mmre_ns_step_openke: sampler + pre-pass, fused loss, row owner (three)."""
+    call (mmre_ns_step_openke, three launches): the values of sampler.sample(B, neg, 0, mode) +
+    fused_ns_loss(...).backward() + SGD.step(), bit for bit (tests/test_ns_full_gpu.py). The
+    parameters are updated in place; ent.grad / rel.grad hold the step's gradient tables, `batch`
+    the sampled batch, `score` the row scores. Calling it returns the loss tensor (device)."""
 
     def __init__(self, sampler, spec: NSSpec, ent, rel, batch: int, neg: int, loss_margin: float, lr: float,
-                 adv_temperature: float | None = None, regul_rate: float = 0.0, mode: int = 0,
-                 two_launch: bool | None = None):
+                 adv_temperature: float | None = None, regul_rate: float = 0.0, mode: int = 0):
         if spec.model not in ("transe", "transe_l2") or spec.use_model_margin:
             raise ValueError("OpenKETrainStep: TransE without a model margin (the fused path)")
         require_cuda(ent, rel)
@@ -237,23 +230,13 @@ class OpenKETrainStep:
                           batch_r=torch.empty(n, dtype=torch.int64, device=dev),
                           batch_y=torch.empty(n, dtype=torch.float32, device=dev))
         self.ge, self.gr = torch.empty_like(ent), torch.empty_like(rel)  # the step's gradient tables
-        if two_launch is None:
-            two_launch = os.environ.get("MMRE_NS_STEP2", "1") != "0"
-        self.two_launch = bool(two_launch)
-        self.state = None
-        if self.two_launch:  # the step-state buffer: parity-buffered slot counts + the step counter, zeroed
-            nb = int(lib().mmre_ns_step_state_bytes(E, R))
-            self.state = torch.zeros((nb + 3) // 4, dtype=torch.int32, device=dev)
 
     def __call__(self):
         s = self.spec
         E, R = int(self.ent.shape[0]), int(self.rel.shape[0])
-        args = (*self.sampler.step_args(self.B, self.K, self.mode, self.batch), s.model_id, int(s.norm_flag),
-                ptr(self.ent), ptr(self.rel), E, R, s.dim, self.B, self.K, self.margin, self.adv, self.regul,
-                ptr(self.score), ptr(self.loss), ptr(self.ge), ptr(self.gr), ptr(self.work))
-        if self.two_launch:
-            call("mmre_ns_step_openke_persistent", *args, ptr(self.state), self.lr, stream_ptr(self.ent.device))
-        else:
-            call("mmre_ns_step_openke", *args, self.lr, stream_ptr(self.ent.device))
+        call("mmre_ns_step_openke", *self.sampler.step_args(self.B, self.K, self.mode, self.batch), s.model_id,
+             int(s.norm_flag), ptr(self.ent), ptr(self.rel), E, R, s.dim, self.B, self.K, self.margin, self.adv,
+             self.regul, ptr(self.score), ptr(self.loss), ptr(self.ge), ptr(self.gr), ptr(self.work),
+             self.lr, stream_ptr(self.ent.device))
         self.ent.grad, self.rel.grad = self.ge, self.gr  # as backward() leaves them
         return self.loss[0]

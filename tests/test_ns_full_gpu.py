@@ -315,16 +315,12 @@ def test_hub_rows_ordered_deterministically(c2_training, model, n_pos):
         assert np.linalg.norm(gg - gw) <= 1e-4 * np.linalg.norm(gw), (n, np.linalg.norm(gg - gw), np.linalg.norm(gw))
 
 
-@pytest.mark.parametrize("two_launch", [True, False])
 @pytest.mark.parametrize("regul,adv", [(0.0, None), (0.5, None), (0.0, 1.0)])
-def test_train_step_equals_the_autograd_path(c2_training, regul, adv, two_launch):
-    """The one-call training step (mmre.ns.OpenKETrainStep) against the drop-in path
+def test_train_step_equals_the_autograd_path(c2_training, regul, adv):
+    """mmre_ns_step_openke (mmre.ns.OpenKETrainStep: sampler + pre-pass in one launch, the fused
+    loss kernel, the row owner with SGD and the loss reduction) against the drop-in path
     (OpenKESampler.sample + fused_ns_loss + backward + mmre.optim.SGD.step) over four steps at the
-    C2 training shape: batches, losses, scores, gradients, parameters and LCG states bit-identical.
-    two_launch: mmre_ns_step_openke_persistent (sampler and row norms inside the fused loss kernel,
-    parity-buffered slot counts: four steps flip the parity twice); else mmre_ns_step_openke
-    (sampler + pre-pass in one launch, the fused loss kernel, the row owner with SGD and the loss
-    reduction)."""
+    C2 training shape: batches, losses, scores, gradients, parameters and LCG states bit-identical."""
     from mmre.ns import NSSpec, OpenKETrainStep, fused_ns_loss
     from mmre.optim import SGD
     from mmre.sampler import OpenKESampler
@@ -338,8 +334,7 @@ def test_train_step_equals_the_autograd_path(c2_training, regul, adv, two_launch
     sa = OpenKESampler(idx, DEV, bern=True)
     sb = OpenKESampler(idx, DEV, bern=True)
     opt = SGD([ea, ra], lr=lr)
-    step = OpenKETrainStep(sb, spec, eb, rb, B, k, margin, lr, adv_temperature=adv, regul_rate=regul,
-                           two_launch=two_launch)
+    step = OpenKETrainStep(sb, spec, eb, rb, B, k, margin, lr, adv_temperature=adv, regul_rate=regul)
     for i in range(4):
         ba = sa.sample(B, k)
         opt.zero_grad(set_to_none=True)
