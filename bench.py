@@ -88,8 +88,8 @@ def valu_ops_per_triple(model, dim):
 
 KERNEL_NAMES = {"transe": "k_sweep_valu<5, false, false, 0>" if os.environ.get("MMRE_L1_FILTER", "1") != "0"
                 else "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
-                "distmult": "k_sweep_bf3<2, " if MFMA_FILTER else "k_sweep_mfma<false, false, 2",
-                "complex": "k_sweep_bf3<2, " if MFMA_FILTER else "k_sweep_mfma<false, false, 2"}
+                "distmult": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2",
+                "complex": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2"}
 
 
 def pmc_traffic(config: str, model: str):

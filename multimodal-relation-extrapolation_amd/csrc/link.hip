@@ -1726,17 +1726,16 @@ __global__ __launch_bounds__(256) void k_bf3_norms(const float* __restrict__ row
 // CU, ballot row counters), one split block (16 k) per stage: 8 KB per operand tile, read into
 // LDS as 16-B chunks at position chunk ^ ((row >> 2) & 3) of the row's 64 B (the 32 lanes of
 // an MFMA operand read hit 32 different 16-B bank groups: conflict-free).
-template <int PK, int KB>
-__global__ __launch_bounds__(NT, KB == 1 ? BF3_WG_PER_CU : 2) void k_sweep_bf3(
+template <int PK>
+__global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
     const uint4* __restrict__ ent_b, int64_t e_pad, int64_t n_ent, const uint4* __restrict__ q_b, int64_t q_pad,
     int64_t n_query, int nkb, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const float* __restrict__ qn, const float* __restrict__ en, float cb,
     int32_t* __restrict__ counts, uint32_t* __restrict__ hdr, int2* __restrict__ pairs, int64_t cap, int emajor) {
-  __shared__ uint4 sq[2][KB][TQ * 4];  // KB split blocks (16 k each) per stage
-  __shared__ uint4 se[2][KB][TE * 4];
+  __shared__ uint4 sq[2][TQ * 4];
+  __shared__ uint4 se[2][TE * 4];
   __shared__ __attribute__((aligned(16))) float s_th[2][TQ];
   __shared__ __attribute__((aligned(16))) float s_qb[2][TQ];
-  const int nst = (nkb + KB - 1) / KB;  // stages per unit (the last one may hold fewer blocks)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const PredSel<PK> pred(pred_kind, margin);
@@ -1768,35 +1767,27 @@ __global__ __launch_bounds__(NT, KB == 1 ? BF3_WG_PER_CU : 2) void k_sweep_bf3(
   };
   auto sidx = [](int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); };
 
-  uint4 rq[KB][2], re[KB][2];
-  int ld_unit = u0, ld_st = 0, ld_qt, ld_et;
+  uint4 rq0, rq1, re0, re1;
+  int ld_unit = u0, ld_kb = 0, ld_qt, ld_et;
   um.at(u0, ld_qt, ld_et);
   auto gload = [&]() {
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk) {
-      const int kb = ld_st * KB + kk;
-      if (kk > 0 && kb >= nkb) break;  // uniform: the unit's short last stage
-      const uint4* qp = q_b + ((int64_t)kb * q_pad + (int64_t)ld_qt * TQ) * 4;
-      const uint4* ep = ent_b + ((int64_t)kb * e_pad + (int64_t)ld_et * TE) * 4;
-      rq[kk][0] = qp[tid];
-      rq[kk][1] = qp[tid + NT];
-      re[kk][0] = ep[tid];
-      re[kk][1] = ep[tid + NT];
-    }
-    if (++ld_st == nst) {
-      ld_st = 0;
+    const uint4* qp = q_b + ((int64_t)ld_kb * q_pad + (int64_t)ld_qt * TQ) * 4;
+    const uint4* ep = ent_b + ((int64_t)ld_kb * e_pad + (int64_t)ld_et * TE) * 4;
+    rq0 = qp[tid];
+    rq1 = qp[tid + NT];
+    re0 = ep[tid];
+    re1 = ep[tid + NT];
+    if (++ld_kb == nkb) {
+      ld_kb = 0;
       if (++ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
     }
   };
   auto swrite = [&](int buf) {
     const int r0 = tid >> 2, c = tid & 3;
-#pragma unroll
-    for (int kk = 0; kk < KB; ++kk) {  // a short stage's missing block: never read
-      sq[buf][kk][sidx(r0, c)] = rq[kk][0];
-      sq[buf][kk][sidx(r0 + 64, c)] = rq[kk][1];
-      se[buf][kk][sidx(r0, c)] = re[kk][0];
-      se[buf][kk][sidx(r0 + 64, c)] = re[kk][1];
-    }
+    sq[buf][sidx(r0, c)] = rq0;
+    sq[buf][sidx(r0 + 64, c)] = rq1;
+    se[buf][sidx(r0, c)] = re0;
+    se[buf][sidx(r0 + 64, c)] = re1;
   };
 
   floatx16 acc[2][2];
@@ -1816,32 +1807,28 @@ __global__ __launch_bounds__(NT, KB == 1 ? BF3_WG_PER_CU : 2) void k_sweep_bf3(
 
   int buf = 0;
   for (int unit = u0; unit < u1; ++unit) {
-    for (int st = 0; st < nst; ++st) {
+    for (int kb = 0; kb < nkb; ++kb) {
       const bool more = ld_unit < u1;
       if (more) gload();
       __builtin_amdgcn_sched_barrier(0);  // the next stage's loads stay at the top (k_sweep_mfma)
+      bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
-      for (int kk = 0; kk < KB; ++kk) {
-        if (kk > 0 && st * KB + kk >= nkb) break;  // uniform: the unit's short last stage
-        bf16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int qrow = wq * 64 + i * 32 + lcol, ecol = we * 64 + i * 32 + lcol;
-          ah[i] = __builtin_bit_cast(bf16x8, sq[buf][kk][sidx(qrow, lrow)]);
-          al[i] = __builtin_bit_cast(bf16x8, sq[buf][kk][sidx(qrow, 2 + lrow)]);
-          bh[i] = __builtin_bit_cast(bf16x8, se[buf][kk][sidx(ecol, lrow)]);
-          bl[i] = __builtin_bit_cast(bf16x8, se[buf][kk][sidx(ecol, 2 + lrow)]);
-        }
-#pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-          for (int bj = 0; bj < 2; ++bj) {
-            acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
-            acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
-            acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
-          }
+      for (int i = 0; i < 2; ++i) {
+        const int qrow = wq * 64 + i * 32 + lcol, ecol = we * 64 + i * 32 + lcol;
+        ah[i] = __builtin_bit_cast(bf16x8, sq[buf][sidx(qrow, lrow)]);
+        al[i] = __builtin_bit_cast(bf16x8, sq[buf][sidx(qrow, 2 + lrow)]);
+        bh[i] = __builtin_bit_cast(bf16x8, se[buf][sidx(ecol, lrow)]);
+        bl[i] = __builtin_bit_cast(bf16x8, se[buf][sidx(ecol, 2 + lrow)]);
       }
-      if (st == nst - 1) {  // unit finished: decide, count, list the undecided
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) {
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[bi], bl[bj], acc[bi][bj], 0, 0, 0);
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[bi], bh[bj], acc[bi][bj], 0, 0, 0);
+        }
+      if (kb == nkb - 1) {  // unit finished: decide, count, list the undecided
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE + we * 64;
         const int64_t e0 = ebase + lcol, e1 = ebase + 32 + lcol;
@@ -2410,14 +2397,14 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
   static const char* order_env = getenv("MMRE_MFMA_EMAJOR");
   const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
-#define MMRE_BF3(PKV, KBV)                                                                                      \
+#define MMRE_BF3(PKV)                                                                                           \
   do {                                                                                                          \
-    const int res = resident_groups((const void*)k_sweep_bf3<PKV, KBV>, NT);                                   \
+    const int res = resident_groups((const void*)k_sweep_bf3<PKV>, NT);                                        \
     const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                        \
     int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;              \
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                           \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                          \
-    hipLaunchKernelGGL((k_sweep_bf3<PKV, KBV>), dim3((unsigned)g), dim3(NT), 0, st, eb, e_pad, n_slice, qb, q_pad, \
+    hipLaunchKernelGGL((k_sweep_bf3<PKV>), dim3((unsigned)g), dim3(NT), 0, st, eb, e_pad, n_slice, qb, q_pad,   \
                        n_query, ktot / 16, n_et, (int)e_begin, ng, pred_kind, margin, d_truth, qn, en, cb,     \
                        d_counts, hdr, pairs, cap, emajor);                                                     \
     MMRE_CHECK_LAUNCH();                                                                                       \
@@ -2431,10 +2418,8 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
                        d_ent_rows, ktot, pred_kind, margin, d_truth, d_counts);                               \
     MMRE_CHECK_LAUNCH();                                                                                       \
   } while (0)
-  static const char* kb_env = getenv("MMRE_BF3_KB"); /* experiments: split blocks per LDS stage (1 / 2) */
-  const int kbs = kb_env ? atoi(kb_env) : 1;
-  if (kbs == 2) { if (pred_kind == 2) MMRE_BF3(2, 2); else MMRE_BF3(-1, 2); }
-  else { if (pred_kind == 2) MMRE_BF3(2, 1); else MMRE_BF3(-1, 1); }
+  if (pred_kind == 2) MMRE_BF3(2);
+  else MMRE_BF3(-1);
 #undef MMRE_BF3
   return launch_finalize(st, d_counts, n_query, false);
 }
