@@ -1156,7 +1156,8 @@ __device__ __forceinline__ void sweep_valu_body(
       uint32_t t = 0;
 #pragma unroll
       for (int w = 0; w < NT / 64; ++w) t += sm.s_unc[w];
-      if (t) atomicAdd(l1.undecided + (blockIdx.x & (L1Q_SLOTS - 1)) * L1Q_SLOT_STRIDE, (unsigned long long)t);
+      // 32-bit counter in the slot's low word (the stats kernel reads only that word)
+      if (t) atomicAdd(reinterpret_cast<uint32_t*>(l1.undecided + (blockIdx.x & (L1Q_SLOTS - 1)) * L1Q_SLOT_STRIDE), t);
     }
   }
 }
@@ -1612,7 +1613,7 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
   const unsigned long long* sl =
       reinterpret_cast<const unsigned long long*>(reinterpret_cast<const char*>(work) + 256);
   unsigned long long t = 0;
-  for (int i = 0; i < L1Q_SLOTS; ++i) t += sl[i * L1Q_SLOT_STRIDE];
+  for (int i = 0; i < L1Q_SLOTS; ++i) t += *reinterpret_cast<const uint32_t*>(sl + i * L1Q_SLOT_STRIDE);
   out[0] = t;
   out[1] = work[1];
 }

@@ -1385,16 +1385,18 @@ __global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const fl
   if (row >= n_ent + n_rel) return;  // wave-uniform
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
-  // the count, the bucket's first NS_BUCKET_HEAD entries (one 128-B line: every slot of most
-  // rows), the row itself and its norm: one round trip, all in flight together; the rest of the
-  // bucket only for a row holding more, and only its live entries (below the count)
+  // the count, the bucket's first entries, the row itself and its norm: one round trip, all in
+  // flight together. Entity rows read NS_BUCKET_HEAD entries (one 128-B line: every slot of
+  // nearly every entity row) and the rest only when they hold more (only the live ones);
+  // relation rows -- few, and the kernel's longest chains -- read the whole bucket at once.
   const int n = counts[row];
-  int64_t pre = lane < NS_BUCKET_HEAD ? bucket[row * NS_BUCKET + lane] : 0;
+  const int head = is_ent ? NS_BUCKET_HEAD : NS_BUCKET;
+  int64_t pre = lane < head ? bucket[row * NS_BUCKET + lane] : 0;
   Vec<NC> v;
   vload_row(v, is_ent ? ent : rel, id, d, lane);
   const float nv = (is_ent ? nrm_e : nrm_r)[id];
   if (n > NS_HUB) return;  // a hub workgroup's row
-  if (n > NS_BUCKET_HEAD && lane >= NS_BUCKET_HEAD && lane < n) pre = bucket[row * NS_BUCKET + lane];
+  if (n > head && lane >= head && lane < n) pre = bucket[row * NS_BUCKET + lane];
   if (n == 0) {  // not in the batch: zero gradient (and an unchanged parameter row)
     Vec<NC> z;
 #pragma unroll
@@ -1565,14 +1567,20 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
                                                         int32_t* __restrict__ zero, int64_t n_zero) {
   NSArgs A = A_;
   A.model = MODEL;  // compile-time model: the other models' registers and branches fold away
-  __shared__ float s_n[NS_MAXK];             // the positive's negative scores (loss, after the barrier)
+  // SPLIT (DistMult): one workgroup per positive, its negatives split over the waves; the
+  // two-half models keep one wave per positive (their per-wave positive rows, sin / cos and
+  // gradient make the split's redundant work cost more than its parallelism gains)
+  constexpr bool SPLIT = MODEL == MMRE_DISTMULT;
+  __shared__ float s_n[SPLIT ? NS_MAXK : NS_WAVES * NS_MAXK];  // the negative scores (loss)
   __shared__ float s_sq[NS_WAVES][6], s_mx[NS_WAVES];
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; zero && i < n_zero;
        i += (int64_t)gridDim.x * blockDim.x)
     zero[i] = 0;
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = blockIdx.x;  // one workgroup per positive, its negatives split over the waves
-  if (b >= A.B) return;  // workgroup-uniform
+  const int64_t b = SPLIT ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * NS_WAVES + w;
+  if (b >= A.B) return;  // workgroup- (SPLIT) or wave-uniform
+  float* sn = s_n + (SPLIT ? 0 : w * NS_MAXK);
+  const bool lead = SPLIT ? w == 0 : true;  // the wave that owns the positive's own terms
   const int64_t ph = A.h[b], pr = A.r[b], pt = A.t[b];
   Row2<NC> H, R, T;
   gen_load(H, A, true, ph, lane);
@@ -1581,12 +1589,12 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
   Vec<NC> psn, pcs;
   rot_sincos(A, R, psn, pcs);
   const float p = gen_score(A, H, R, T, psn, pcs);
-  if (w == 0 && lane == 0) score[b] = p;
+  if (lead && lane == 0) score[b] = p;
   float sq[6] = {0, 0, 0, 0, 0, 0};
-  if (w == 0 && A.regul_rate != 0.0f) row_sq(A, b, lane, sq);
+  if (lead && A.regul_rate != 0.0f) row_sq(A, b, lane, sq);
   float mx = -INFINITY;
-  const int64_t per = (A.K + NS_WAVES - 1) / NS_WAVES;
-  const int64_t jlo = (int64_t)w * per, jhi = jlo + per < A.K ? jlo + per : A.K;
+  const int64_t per = SPLIT ? (A.K + NS_WAVES - 1) / NS_WAVES : A.K;
+  const int64_t jlo = SPLIT ? (int64_t)w * per : 0, jhi = jlo + per < A.K ? jlo + per : A.K;
   for (int64_t j0 = jlo; j0 < jhi; j0 += kWave) {
     const int nch = (int)(jhi - j0 < kWave ? jhi - j0 : kWave);
     int64_t mh = 0, mt = 0, mr = 0;
@@ -1622,38 +1630,45 @@ __global__ __launch_bounds__(256) void k_ns_gen_forward(NSArgs A_, float* __rest
           n = gen_score(A, H, X[i], T, sn, cs);
         } else if (code[i] == 3) n = p;
         else n = row_score(A, row, lane);
-        if (lane == 0) { score[row] = n; s_n[j] = n; }
+        if (lane == 0) { score[row] = n; sn[j] = n; }
         if (A.regul_rate != 0.0f) row_sq(A, row, lane, sq);
         if (A.adv_t > 0.0f) mx = fmaxf(mx, -n * A.adv_t);
       }
     }
   }
-  // the waves' regularization partials and maxima, combined by wave 0 in wave order
-  for (int i = 0; i < 6; ++i) {
-    const float v = A.regul_rate != 0.0f ? wave_sum(sq[i]) : 0.0f;
-    if (lane == 0) s_sq[w][i] = v;
+  float sqv[6];
+  for (int i = 0; i < 6; ++i) sqv[i] = A.regul_rate != 0.0f ? wave_sum(sq[i]) : 0.0f;
+  if constexpr (SPLIT) {  // the waves' regularization partials and maxima, combined by wave 0 in wave order
+    if (lane == 0) {
+      for (int i = 0; i < 6; ++i) s_sq[w][i] = sqv[i];
+      s_mx[w] = mx;
+    }
+    __syncthreads();
+    if (w != 0 || lane != 0) return;
+    for (int v = 1; v < NS_WAVES; ++v) mx = fmaxf(mx, s_mx[v]);
+    for (int i = 0; i < 6; ++i) {
+      float v = s_sq[0][i];
+      for (int ww = 1; ww < NS_WAVES; ++ww) v += s_sq[ww][i];
+      sqv[i] = v;
+    }
+  } else {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane != 0) return;
   }
-  if (lane == 0) s_mx[w] = mx;
-  __syncthreads();
-  if (w != 0 || lane != 0) return;
   float loss = 0.0f;
-  for (int v = 1; v < NS_WAVES; ++v) mx = fmaxf(mx, s_mx[v]);
   if (A.adv_t > 0.0f) {
     float den = 0.0f;
-    for (int64_t j = 0; j < A.K; ++j) den += expf(-s_n[j] * A.adv_t - mx);
+    for (int64_t j = 0; j < A.K; ++j) den += expf(-sn[j] * A.adv_t - mx);
     for (int64_t j = 0; j < A.K; ++j) {
-      const float n = s_n[j];
+      const float n = sn[j];
       loss += expf(-n * A.adv_t - mx) / den * fmaxf(p - n, -A.loss_margin);
     }
   } else {
-    for (int64_t j = 0; j < A.K; ++j) loss += fmaxf(p - s_n[j], -A.loss_margin);
+    for (int64_t j = 0; j < A.K; ++j) loss += fmaxf(p - sn[j], -A.loss_margin);
   }
   part[b * 7] = loss;
-  for (int i = 0; i < 6; ++i) {
-    float v = s_sq[0][i];
-    for (int ww = 1; ww < NS_WAVES; ++ww) v += s_sq[ww][i];
-    part[b * 7 + 1 + i] = v;
-  }
+  for (int i = 0; i < 6; ++i) part[b * 7 + 1 + i] = sqv[i];
 }
 
 // One wave per positive: the loss's d/d(score) coefficients of its rows (k_ns_row_coef's
@@ -1675,13 +1690,17 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
   NSArgs A = A_;
   A.model = MODEL;  // compile-time model
   constexpr int NH = MODEL == MMRE_DISTMULT ? 1 : 2;  // row halves carried by the own-row partials
-  __shared__ float s_own[NS_WAVES - 1][3][NH][NC][kWave];  // waves 1-3's own-row partial sums
+  // SPLIT (DistMult): one workgroup per positive, its negatives split over the waves, own-row
+  // partials combined in wave order; the two-half models: one wave per positive (k_ns_gen_forward)
+  constexpr bool SPLIT = MODEL == MMRE_DISTMULT;
+  __shared__ float s_own[SPLIT ? NS_WAVES - 1 : 1][3][NH][NC][kWave];  // waves 1-3's own-row partial sums
   __shared__ float s_occ[NS_WAVES - 1][3];
   const int d = A.dim;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t b = blockIdx.x;  // one workgroup per positive, its negatives split over the waves
-  if (b >= A.B) return;  // workgroup-uniform
+  const int64_t b = SPLIT ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * NS_WAVES + w;
+  if (b >= A.B) return;  // workgroup- (SPLIT) or wave-uniform
+  const bool lead = SPLIT ? w == 0 : true;
   const float p = score[b];
   float mx = -INFINITY, den = 0.0f;
   if (A.adv_t > 0.0f) {
@@ -1710,16 +1729,16 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
   rot_sincos(A, R, psn, pcs);
   // wave 0 starts the own-row sums with the positive's gradient, waves 1-3 from zero; each wave
   // takes a contiguous range of the negatives; the partials are combined in wave order below
-  if (w == 0) {
+  if (lead) {
     gen_row_grad(A, H, R, T, gp, Gh, Gr, Gt, &psn, &pcs);
   } else {
     vzero(Gh.a); vzero(Gh.b); vzero(Gr.a); vzero(Gr.b); vzero(Gt.a); vzero(Gt.b);
   }
-  const float k0 = w == 0 ? 1.0f : 0.0f;
+  const float k0 = lead ? 1.0f : 0.0f;
   float kh = k0, kr = k0, kt = k0;  // occurrences of the positive's rows (regularization)
   const int64_t sb = b * (3 + 3 * A.K);
-  const int64_t per = (A.K + NS_WAVES - 1) / NS_WAVES;
-  const int64_t jlo = (int64_t)w * per, jhi = jlo + per < A.K ? jlo + per : A.K;
+  const int64_t per = SPLIT ? (A.K + NS_WAVES - 1) / NS_WAVES : A.K;
+  const int64_t jlo = SPLIT ? (int64_t)w * per : 0, jhi = jlo + per < A.K ? jlo + per : A.K;
   for (int64_t j0 = jlo; j0 < jhi; j0 += CH) {
     const int nch = (int)(jhi - j0 < CH ? jhi - j0 : CH);
     int64_t mh = 0, mt = 0, mr = 0;
@@ -1813,19 +1832,21 @@ __global__ __launch_bounds__(256) void k_ns_gen_slots(NSArgs A_, const float* __
       if constexpr (NH == 2) g.b.v[c] += s_own[v][k][NH - 1][c][lane];
     }
   };
-  if (w > 0) {
-    park(0, Gh);
-    park(1, Gr);
-    park(2, Gt);
-    if (lane == 0) { s_occ[w - 1][0] = kh; s_occ[w - 1][1] = kr; s_occ[w - 1][2] = kt; }
-  }
-  __syncthreads();
-  if (w > 0) return;
-  for (int v = 0; v < NS_WAVES - 1; ++v) {
-    gather(v, 0, Gh);
-    gather(v, 1, Gr);
-    gather(v, 2, Gt);
-    kh += s_occ[v][0]; kr += s_occ[v][1]; kt += s_occ[v][2];  // integer-valued
+  if constexpr (SPLIT) {
+    if (w > 0) {
+      park(0, Gh);
+      park(1, Gr);
+      park(2, Gt);
+      if (lane == 0) { s_occ[w - 1][0] = kh; s_occ[w - 1][1] = kr; s_occ[w - 1][2] = kt; }
+    }
+    __syncthreads();
+    if (w > 0) return;
+    for (int v = 0; v < NS_WAVES - 1; ++v) {
+      gather(v, 0, Gh);
+      gather(v, 1, Gr);
+      gather(v, 2, Gt);
+      kh += s_occ[v][0]; kr += s_occ[v][1]; kt += s_occ[v][2];  // integer-valued
+    }
   }
   rec_store(S.rec, sb, d, S2, E2, Gh, lane);
   rec_store(S.rec, sb + 1, d, S2, R2, Gr, lane);
@@ -2351,7 +2372,8 @@ extern "C" int mmre_ns_fused_forward(int model, int norm_flag, float model_margi
     if (is_transe(model)) {
       hipLaunchKernelGGL(k_ns_forward, fgrid, dim3(256), 0, st, A, d_score, part, S.counts, n_ent + n_rel + 1);
     } else {
-      const dim3 fgrid((unsigned)batch);  // k_ns_gen_forward: a workgroup per positive
+      // k_ns_gen_forward: DistMult a workgroup per positive, the two-half models a wave per positive
+      const dim3 fgrid((unsigned)(model == MMRE_DISTMULT ? batch : (batch + NS_WAVES - 1) / NS_WAVES));
 #define MMRE_NS_GF(NC_, M_)                                                                                        \
   hipLaunchKernelGGL((k_ns_gen_forward<NC_, M_>), fgrid, dim3(256), 0, st, A, d_score, part, S.counts,             \
                      n_ent + n_rel + 1)
@@ -2434,7 +2456,8 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     const double ew = model == MMRE_ROTATE ? 2.0 * dim : (double)dim;
     const float reg_ent = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * ew)) : 0.0f;
     const float reg_rel = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * dim)) : 0.0f;
-    const dim3 sgrid((unsigned)batch);  // a workgroup per positive
+    // DistMult: a workgroup per positive; the two-half models: a wave per positive
+    const dim3 sgrid((unsigned)(model == MMRE_DISTMULT ? batch : (batch + NS_WAVES - 1) / NS_WAVES));
 #define MMRE_NS_GEN(NC_)                                                                                            \
   do {                                                                                                              \
     if (model == MMRE_DISTMULT)                                                                                     \
