@@ -1849,10 +1849,20 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
             for (int bj = 0; bj < 2; ++bj) {
               const float s = acc[bi][bj][r];
               const float bnd = qb[r - r4] * (bj ? ne1 : ne0);
-              const float p1 = pred(s - bnd), p2 = pred(s + bnd);
               const bool fin = fabsf(s) < INFINITY;  // false for inf and NaN
-              const bool sure = fin & (fmaxf(p1, p2) < tv[r - r4]);
-              const bool out = (fin & (fminf(p1, p2) >= tv[r - r4])) | (tv[r - r4] != tv[r - r4]);
+              bool sure, out;
+              if constexpr (PK == 2) {
+                // predict = -s: better iff S > -th. Rounding is monotone, so fl(s - B) > -th
+                // implies s - B > -th (every S of the bracket beats the truth) and
+                // fl(s + B) < -th implies s + B < -th (none does); a NaN S' or bound decides nothing
+                const float nt = -tv[r - r4];
+                sure = fin & (s - bnd > nt);
+                out = (fin & (s + bnd < nt)) | (nt != nt);  // a NaN threshold: nothing beats it
+              } else {
+                const float p1 = pred(s - bnd), p2 = pred(s + bnd);
+                sure = fin & (fmaxf(p1, p2) < tv[r - r4]);
+                out = (fin & (fminf(p1, p2) >= tv[r - r4])) | (tv[r - r4] != tv[r - r4]);
+              }
               const bool ev = bj ? ev1 : ev0;
               better[bj] = sure & ev;
               und[bj] = !sure & !out & ev;

@@ -1347,7 +1347,7 @@ __device__ __forceinline__ HubOrder hub_order(int64_t (*s_hub)[NS_HUB], int32_t*
 // go to the first n_hub_wg workgroups (HubOrder); rows start at workgroup row_block0. With SGD the parameter tables
 // ent / rel are also pent / prel (read, then written, by the row's own wave): not __restrict__.
 template <int NC, bool L2>
-__global__ __launch_bounds__(256) void k_ns_row_owner(const float* ent, const float* rel,
+__global__ __launch_bounds__(256, NC > 4 ? 5 : 7) void k_ns_row_owner(const float* ent, const float* rel,
                                                       int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
                                                       const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
                                                       const float* __restrict__ shared, const float* __restrict__ rec,
