@@ -345,6 +345,7 @@ struct L1Q {
   const float* ent_f;
   int kp_f;
   int kt;                  // floats per row (the canonical chain's length, padding rows are 0)
+  const uint32_t* gate;    // non-OP-5 sweeps: run only if *gate != 0 (the filter's fallback launch)
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax) {
   const float m = __uint_as_float(*absmax);
@@ -1174,14 +1175,13 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
   __shared__ ValuSmem<NPL, TC> sm;
   if constexpr (OP == 5) {
     // the L1 filter's fallback (k_l1q_quant decided that the codes are too coarse for these
-    // planes -- one outlier value sets the code step for everything): the exact f32 sweep of
-    // the float planes, as mmre_link_sweep would run it
-    if (__builtin_amdgcn_readfirstlane(l1.hdr[1]) != 0u) {
-      sweep_valu_body<0, TC, false, PK, NPL>(sm, l1.ent_f, e_pad, n_ent, l1.q_f, q_pad, n_query, l1.kp_f, n_et,
-                                             e_base, n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head,
-                                             type_tail, type_words, counts, nullptr, l1);
-      return;
-    }
+    // planes -- one outlier value sets the code step for everything): this launch does nothing
+    // and the exact f32 sweep launched after it (gated on the same flag) counts. A separate
+    // launch, not a branch here: inlining the f32 body beside the filter's grew the kernel by
+    // half and its register spills (18 -> 23)
+    if (__builtin_amdgcn_readfirstlane(l1.hdr[1]) != 0u) return;
+  } else {
+    if (l1.gate != nullptr && __builtin_amdgcn_readfirstlane(*l1.gate) == 0u) return;
   }
   sweep_valu_body<OP, TC, STORE, PK, NPL>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
                                           n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head, type_tail,
@@ -2007,7 +2007,8 @@ template <int OP>
 static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km, int64_t e_pad, int64_t n_ent,
                        int n_et, int e_base, const float* q_km, int64_t q_pad, int64_t n_query, int kp, int pk, float m, const float* thr,
                        const int32_t* qtrue, const int64_t* qr, const int8_t* qmode, const uint32_t* th,
-                       const uint32_t* tt, int64_t tw, int32_t* counts, float* scores, L1Q l1 = {}) {
+                       const uint32_t* tt, int64_t tw, int32_t* counts, float* scores, L1Q l1 = {},
+                       bool finalize = true) {
 #define MMRE_LV1(TCV, STV, PKV) \
   launch_valu_one<OP, TCV, STV, PKV>(st, ent_km, e_pad, n_ent, n_et, e_base, q_km, q_pad, n_query, kp, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1)
   // the model's usual prediction kind is compiled into the epilogue of the plain sweep
@@ -2026,7 +2027,7 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
   }
 #undef MMRE_LV1
   MMRE_CHECK_LAUNCH();
-  return launch_finalize(st, counts, n_query, tc);
+  return finalize ? launch_finalize(st, counts, n_query, tc) : MMRE_OK;
 }
 
 }  // namespace mmre
@@ -2343,10 +2344,19 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               n_planes(MMRE_TRANSE_L1) * kp};
-  return launch_valu<5>(d_type_head != nullptr, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et,
-                        (int)e_begin, (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr,
-                        d_qmode, d_type_head, d_type_tail, tw, d_counts, nullptr, l1);
+               n_planes(MMRE_TRANSE_L1) * kp, nullptr};
+  const bool tc = d_type_head != nullptr;
+  rc = launch_valu<5>(tc, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et, (int)e_begin,
+                      (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr, d_qmode,
+                      d_type_head, d_type_tail, tw, d_counts, nullptr, l1, false);
+  if (rc) return rc;
+  // the fallback: the exact f32 sweep of the float planes, gated on the flag k_l1q_quant wrote
+  // (its workgroups return at once when the codes were used)
+  L1Q gate{};
+  gate.gate = hdr + 1;
+  return launch_valu<0>(tc, false, st, d_ent_km + e_begin, e_pad, n_slice, n_et, (int)e_begin, d_q_km, q_pad, n_query,
+                        kp, pred_kind, margin, d_truth, d_q_true, d_qr, d_qmode, d_type_head, d_type_tail, tw,
+                        d_counts, nullptr, gate, true);
 }
 
 extern "C" int64_t mmre_link_bf3_workspace(int model, int dim, int64_t e_pad, int64_t q_pad) {
