@@ -859,10 +859,12 @@ __device__ __forceinline__ void sweep_valu_body(
     l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
     l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
   }
+  const uint32_t fb_flag = OP == 5 ? l1.hdr[1] : 0u;  // the L1 filter's fallback flag, in flight with the stage
   load_meta(cur_qt, 0);
   gload();
   swrite(0);
   __syncthreads();
+  if (OP == 5 && __builtin_amdgcn_readfirstlane(fb_flag) != 0u) return;  // uniform: the f32 launch counts
 
   int buf = 0;
   for (int unit = u0; unit < u1; ++unit) {
@@ -1173,14 +1175,13 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     float* __restrict__ scores, L1Q l1) {
   constexpr int NPL = (OP == 2) ? 2 : 1;
   __shared__ ValuSmem<NPL, TC> sm;
-  if constexpr (OP == 5) {
-    // the L1 filter's fallback (k_l1q_quant decided that the codes are too coarse for these
-    // planes -- one outlier value sets the code step for everything): this launch does nothing
-    // and the exact f32 sweep launched after it (gated on the same flag) counts. A separate
-    // launch, not a branch here: inlining the f32 body beside the filter's grew the kernel by
-    // half and its register spills (18 -> 23)
-    if (__builtin_amdgcn_readfirstlane(l1.hdr[1]) != 0u) return;
-  } else {
+  // the L1 filter's fallback (k_l1q_quant decided that the codes are too coarse for these
+  // planes -- one outlier value sets the code step for everything): the filter launch does
+  // nothing (sweep_valu_body tests the flag once its first stage is loaded, so the flag's load
+  // latency hides under the stage's) and the exact f32 sweep launched after it, gated on the
+  // same flag, counts. A separate launch, not a branch here: inlining the f32 body beside the
+  // filter's grew the kernel by half and its register spills (18 -> 23)
+  if constexpr (OP != 5) {
     if (l1.gate != nullptr && __builtin_amdgcn_readfirstlane(*l1.gate) == 0u) return;
   }
   sweep_valu_body<OP, TC, STORE, PK, NPL>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
@@ -1985,6 +1986,11 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   // CUs that run at different speeds (C2 on MI355X: 1,024 groups 4.0 ms, 8,192 3.43 ms,
   // 16,384 3.30 ms, 30,528 (one unit each) 3.36 ms).
   int g = 16 * resident_groups((const void*)k_sweep_valu<OP, TCV, STV, PK>, NT);
+  // a gated launch (the L1 filter's f32 fallback, l1.gate) runs one persistent workgroup per
+  // resident slot: when the gate is shut -- every time but the rare fallback -- its workgroups
+  // only read the flag and leave, one residency round instead of 16 (a 16x grid of such
+  // workgroups cost 77 us per evaluation at C2)
+  if (l1.gate != nullptr) g /= 16;
   // Small sweeps (a rank's share under relation sharding): no more workgroups than the
   // busiest XCD group has units, so every workgroup gets at most one unit and no empty
   // workgroups are dispatched (C2 at 8-way: 4,380 sweeps 0.52 -> 0.47 ms; 4-way 0.89 -> 0.85).
@@ -2229,6 +2235,7 @@ static void launch_mfma(bool tc, bool store, int pred_kind, float margin, const 
     const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                           \
     const int64_t lo = ks32 ? 2LL * res : (int64_t)res;                                                           \
     int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>(lo, units / 16)) & ~7;                            \
+    if (gate != nullptr) g = (int)lo & ~7; /* gated (the bf3 fallback): one residency round when shut */          \
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                              \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                             \
     hipLaunchKernelGGL(KERNEL, dim3((unsigned)g), dim3(NT), 0, st, d_ent_km, e_pad, n_ent, d_q_km, q_pad,       \
