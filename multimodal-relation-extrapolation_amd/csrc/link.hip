@@ -1986,11 +1986,15 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   // CUs that run at different speeds (C2 on MI355X: 1,024 groups 4.0 ms, 8,192 3.43 ms,
   // 16,384 3.30 ms, 30,528 (one unit each) 3.36 ms).
   int g = 16 * resident_groups((const void*)k_sweep_valu<OP, TCV, STV, PK>, NT);
-  // a gated launch (the L1 filter's f32 fallback, l1.gate) runs one persistent workgroup per
-  // resident slot: when the gate is shut -- every time but the rare fallback -- its workgroups
-  // only read the flag and leave, one residency round instead of 16 (a 16x grid of such
-  // workgroups cost 77 us per evaluation at C2)
-  if (l1.gate != nullptr) g /= 16;
+  // a gated launch (the L1 filter's f32 fallback, l1.gate) runs 4 workgroups per resident
+  // slot: when the gate is shut -- every time but the rare fallback -- its workgroups only
+  // read the flag and leave, and a 16x grid of such workgroups cost 77 us per evaluation at
+  // C2; one per slot (1x) made the open-gate sweep 15% slower than the plain f32 sweep
+  static const char* fbdiv = getenv("MMRE_L1_FB_DIV");
+  if (l1.gate != nullptr) {
+    const int div = fbdiv ? atoi(fbdiv) : 4;
+    g /= div > 1 ? div : 1;
+  }
   // Small sweeps (a rank's share under relation sharding): no more workgroups than the
   // busiest XCD group has units, so every workgroup gets at most one unit and no empty
   // workgroups are dispatched (C2 at 8-way: 4,380 sweeps 0.52 -> 0.47 ms; 4-way 0.89 -> 0.85).

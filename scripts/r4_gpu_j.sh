@@ -2,7 +2,7 @@
 # round 4, GPU call J: fallback-flag latency hidden, gated launches one residency round
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-o=gpurun_out/r4j
+o=gpurun_out/r4${R4TAG:-j}
 mkdir -p $o
 T="timeout -k 10"
 $T 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu -s tests/test_sweep_filters_gpu.py \
