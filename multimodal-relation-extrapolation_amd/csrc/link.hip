@@ -751,6 +751,8 @@ struct ValuSmem {
   int8_t s_mode[2][TC ? TQ : 1];
   int32_t s_cnt[TC ? 2 : 1][8][NT];  // per-thread counters (off the VGPR budget)
   uint32_t s_unc[NT / 64];           // undecided pairs per wave (the L1 filter's counter)
+  uint32_t s_ts[2][TQ];              // L1 filter, prediction = score: per query row, the integer
+  uint32_t s_tw[2][TQ];              // thresholds t_sure and t_out - t_sure (load_meta)
 };
 
 // The sweep body. Counts go to the raw columns only (counts[0][q], counts[2][q]); the filtered
@@ -774,7 +776,6 @@ __device__ __forceinline__ void sweep_valu_body(
   auto& s_rel = sm.s_rel;
   auto& s_mode = sm.s_mode;
   auto& s_cnt = sm.s_cnt;
-  uint32_t n_unc = 0;  // undecided pairs of this thread (OP 5)
 
   const int tid = threadIdx.x;
   const int tq = tid >> 4, te = tid & 15;
@@ -789,12 +790,37 @@ __device__ __forceinline__ void sweep_valu_body(
   if (u0 >= u1) return;  // uniform over the workgroup
   const int nkc = kp / KC;
 
+  // L1 filter constants (uniform): code step, bound slope and offset
+  float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
+  if constexpr (OP == 5) {
+    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr))));
+    l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+    l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
+  }
+
   auto load_meta = [&](int qtile, int slot) {
     if (tid < TQ) {
       const int64_t q = (int64_t)qtile * TQ + tid;
       const bool v = q < n_query;
-      s_thr[slot][tid] = v ? thr[q] : -INFINITY;
+      const float th = v ? thr[q] : -INFINITY;
+      s_thr[slot][tid] = th;
       s_true[slot][tid] = v ? qtrue[q] : -1;
+      if constexpr (OP == 5 && PK == 0) {
+        // prediction = the score: the filter decides in the integer domain. With a = delta *
+        // S_int, |S - a| <= l1f a + l1c, so S_int < x = (th - l1c) / (delta (1 + l1f)) gives
+        // S < th and S_int >= y = (th + l1c) / (delta (1 - l1f)) gives S >= th; x, y are shrunk /
+        // grown by 2^-18 against the float rounding of their own computation. Once per query
+        // row and query tile, not per unit.
+        uint32_t t_sure = 0u, t_out = 0xFFFFFFFFu;
+        if (l1d < INFINITY) {
+          const float x = (th - l1c) / (l1d * (1.0f + l1f)) * (1.0f - 0x1p-18f);
+          const float y = (th + l1c) / (l1d * (1.0f - l1f)) * (1.0f + 0x1p-18f);
+          t_sure = x > 0.0f ? (uint32_t)floorf(fminf(x, 0x1p31f)) : 0u;
+          t_out = y > 0.0f ? (uint32_t)ceilf(fminf(y, 0x1p31f)) : 0u;
+        }
+        sm.s_ts[slot][tid] = t_sure;
+        sm.s_tw[slot][tid] = t_out > t_sure ? t_out - t_sure : 0u;
+      }
       if constexpr (TC) {
         s_rel[slot][tid] = v ? (int32_t)qr[q] : 0;
         s_mode[slot][tid] = v ? qmode[q] : 0;
@@ -847,18 +873,15 @@ __device__ __forceinline__ void sweep_valu_body(
     s_cnt[0][i][tid] = 0;
     if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] = 0;
   }
+  if (OP == 5 && tid < NT / 64) sm.s_unc[tid] = 0u;
 
   int cur_qt, cur_et;
   um.at(u0, cur_qt, cur_et);
   int slot = 0;
   uint32_t lo = 0xFFFFFFFFu;  // RotatE: min of the sqrt inputs' bits over this unit (see rot_mag)
-  // L1 filter constants (uniform): code step, bound slope and offset
-  float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
-  if constexpr (OP == 5) {
-    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr))));
-    l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
-    l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
-  }
+  // L1 filter: the code rows actually used in the last stage (the plane is padded to whole
+  // stages; 100 of 104 rows at d = 200: the pad rows' zeros are not swept)
+  const int kk_last = (OP == 5) ? ((((l1.kt + 1) >> 1) + 1) & ~1) - (nkc - 1) * KC : KC;
   const uint32_t fb_flag = OP == 5 ? l1.hdr[1] : 0u;  // the L1 filter's fallback flag, in flight with the stage
   load_meta(cur_qt, 0);
   gload();
@@ -871,8 +894,9 @@ __device__ __forceinline__ void sweep_valu_body(
     for (int kc = 0; kc < nkc; ++kc) {
       const bool more = ld_unit < u1;
       if (more) gload();
+      const int kk_n = (OP == 5 && kc == nkc - 1) ? kk_last : KC;
 #pragma unroll 2
-      for (int kk = 0; kk < KC; ++kk) {
+      for (int kk = 0; kk < kk_n; ++kk) {
         float4 a0 = sq[buf][0][kk][tq], a1 = sq[buf][0][kk][16 + tq];
         float4 x0 = se[buf][0][kk][te], x1 = se[buf][0][kk][16 + te];
         const float qa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -965,24 +989,63 @@ __device__ __forceinline__ void sweep_valu_body(
               for (int j = 0; j < 8; ++j) accp[i][j] = f32x2{0.0f, 0.0f};
           }
           uint32_t unc[2] = {0u, 0u};  // undecided pairs, bit i * 8 + j (rows 0-3 / 4-7)
+          bool whole = false;
+          if constexpr (OP == 5 && PK == 0 && !TC) {
+            // L1 filter, a whole entity tile (every tile but the last, uniform): per pair one
+            // compare + carry-add for the count and one subtract + compare for the undecided
+            // band [t_sure, t_out), its wave-wide ballot OR-ed into one scalar mask. The count
+            // needs no truth test: the truth's S is th itself, which no pair below t_sure
+            // reaches (S_int < t_sure proves S < th). The per-pair bits of the rescoring loop
+            // are built only when a wave holds an undecided pair (~7 % of waves at C2), with
+            // the truth excluded there.
+            if (ebase + TE <= n_ent) {
+              whole = true;
+              const int32_t ecol = (int32_t)(e_base + ebase) + te * 4;  // entity id of column 0
+              uint64_t any = 0;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
+                const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
+                int c = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const uint32_t si = __float_as_uint(acc[i][j]);
+                  c += si < t_sure;
+                  any |= __ballot(si - t_sure < t_span);
+                }
+                s_cnt[0][i][tid] += c;
+              }
+              if (any) {  // rare: per-pair bits (thresholds re-read: no register held across)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                  const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
+                  const uint32_t t_sure = *(volatile uint32_t*)&sm.s_ts[slot][ql];
+                  const uint32_t t_span = *(volatile uint32_t*)&sm.s_tw[slot][ql];
+                  const int32_t toff = *(volatile int32_t*)&s_true[slot][ql] - ecol;
+#pragma unroll
+                  for (int j = 0; j < 8; ++j) {
+                    const uint32_t si = __float_as_uint(acc[i][j]);
+                    const bool u = (si - t_sure < t_span) & (toff != ((j < 4) ? j : 60 + j));
+                    unc[i >> 2] |= (uint32_t)u << ((i & 3) * 8 + j);
+                  }
+                }
+              }
+#pragma unroll
+              for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[i][j] = 0.0f;
+            }
+          }
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
+            if (whole) break;
             const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
             const float th = s_thr[slot][ql];
             const int32_t tr = s_true[slot][ql];
             int c = 0, cc = 0;
             if constexpr (OP == 5 && PK == 0) {
-              // prediction = the score: decide in the integer domain. With a = delta * S_int,
-              // |S - a| <= l1f a + l1c, so S_int < x = (th - l1c) / (delta (1 + l1f)) gives S < th
-              // and S_int >= y = (th + l1c) / (delta (1 - l1f)) gives S >= th; x, y are shrunk /
-              // grown by 2^-18 against the float rounding of their own computation.
-              uint32_t t_sure = 0u, t_out = 0xFFFFFFFFu;
-              if (l1d < INFINITY) {
-                const float x = (th - l1c) / (l1d * (1.0f + l1f)) * (1.0f - 0x1p-18f);
-                const float y = (th + l1c) / (l1d * (1.0f - l1f)) * (1.0f + 0x1p-18f);
-                t_sure = x > 0.0f ? (uint32_t)floorf(fminf(x, 0x1p31f)) : 0u;
-                t_out = y > 0.0f ? (uint32_t)ceilf(fminf(y, 0x1p31f)) : 0u;
-              }
+              // prediction = the score: the integer thresholds of load_meta
+              const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
@@ -995,7 +1058,7 @@ __device__ __forceinline__ void sweep_valu_body(
                   const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
                   cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
                 }
-                unc[i >> 2] |= (uint32_t)(!sure & (si < t_out) & valid) << ((i & 3) * 8 + j);
+                unc[i >> 2] |= (uint32_t)((si - t_sure < t_span) & valid) << ((i & 3) * 8 + j);
                 acc[i][j] = 0.0f;
               }
               s_cnt[0][i][tid] += c;
@@ -1030,7 +1093,6 @@ __device__ __forceinline__ void sweep_valu_body(
             s_cnt[0][i][tid] += c;
             if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
           }
-          if constexpr (OP == 5) n_unc += __popc(unc[0]) + __popc(unc[1]);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             uint32_t m = unc[h];
@@ -1041,6 +1103,7 @@ __device__ __forceinline__ void sweep_valu_body(
               const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
               const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
               float sx;
+              if constexpr (OP == 5) atomicAdd(&sm.s_unc[tid >> 6], 1u);  // the wave's undecided pairs (LDS)
               if constexpr (OP == 5)
                 sx = l1_exact_rows(l1.q_rows + (q0 + ql) * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt,
                                    l1.kt);
@@ -1150,10 +1213,6 @@ __device__ __forceinline__ void sweep_valu_body(
     }
   }
   if constexpr (OP == 5) {  // the filter's undecided pairs: one atomic per workgroup, 16 slots
-    uint32_t u = n_unc;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
-    if ((tid & 63) == 0) sm.s_unc[tid >> 6] = u;
     __syncthreads();
     if (tid == 0) {
       uint32_t t = 0;
