@@ -38,8 +38,9 @@ def main():
     M = max(float(Q.abs().max()), float(ent.abs().max()))
     S = torch.cdist(Q, ent, p=1)                                    # (2n, E)
     th = S[torch.arange(len(ths)), torch.tensor(ths)]
-    for name, m in (("M = data max", M), ("M = 2 (fixed bound)", 2.0)):
-        delta = 2 * m / 65535
+    for name, m, levels in (("16-bit, M = data max", M, 65535), ("16-bit, M = 2 (fixed bound)", 2.0, 65535),
+                            ("8-bit, M = data max", M, 255), ("10-bit, M = data max", M, 1023)):
+        delta = 2 * m / levels
         B = K * delta + 2.0 ** -22 * K * th
         und = ((S - th[:, None]).abs() <= B[:, None]).double()
         p = float(und.mean())
