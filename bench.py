@@ -1196,6 +1196,8 @@ def main():
         for e2 in evs:
             sw.run(*ev.q, filt=ev.filt, type_masks=ev.masks_tc, buffers=bufs, sweep_events=e2)
         torch.cuda.synchronize()
+        twin_fst = sw.filter_stats(bufs)
+        print(f"eager twin filter record: {twin_fst}", file=sys.stderr)
         del sw, bufs
     sweep_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if n_local else 0.0
     if dist:
@@ -1204,6 +1206,7 @@ def main():
         elapsed = float(t.item())
     _, counts = ev.run()  # one more evaluation outside the timed region: the counts the parity check reads
     fst = ev.filter_stats() if hasattr(ev, "filter_stats") else None  # the count-only filter's record (l1q / bf3)
+    print(f"evaluation filter record: {fst}", file=sys.stderr)
     breakdown = None
     if world > 1:  # every rank's local / sweep / fixed / collective time, gathered (all ranks take part)
         breakdown = rank_breakdown(ev, dist, dev, sweep_ms, n_local, args.shard == "entity")

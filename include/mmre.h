@@ -147,21 +147,24 @@ int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d
 
 /* TransE L1 (model MMRE_TRANSE_L1) count-only sweep through an integer filter: same counts as
  * mmre_link_sweep / mmre_link_sweep_range (bit for bit; replaces the same Test.h:65-192 scan),
- * faster. The k-major planes are quantized to 16-bit codes over the largest |x| of both (three
- * short launches on the stream), the sweep sums |code differences| with v_sad_u16 (one issue
- * slot per element against two), and every pair the quantization error bound leaves on both
- * sides of its query's threshold is rescored with the canonical f32 chain from the row-major
- * copies d_ent_rows (whole table, mmre_link_prepare_entities) and d_q_rows
+ * faster. The k-major planes are quantized over the largest |x| of both to 8-bit codes (four k
+ * per dword, summed with one v_sad_u8 per four elements) or, when a fixed sample of pairs
+ * scored with those codes leaves more than 1 % undecided, to 16-bit codes (v_sad_u16, two
+ * elements per instruction); the choice is made on the device (short launches on the stream,
+ * no host round trip). Every pair the quantization error bound leaves on both sides of its
+ * query's threshold is rescored with the canonical f32 chain from the row-major copies
+ * d_ent_rows (whole table, mmre_link_prepare_entities) and d_q_rows
  * (mmre_link_prepare_queries). e_begin / e_end as for mmre_link_sweep_range (0, n_ent: whole
- * table). d_work: mmre_link_l1q_workspace(dim, e_pad, q_pad) bytes of device scratch. */
+ * table). d_work: mmre_link_l1q_workspace(dim, e_pad, q_pad) bytes of device scratch.
+ * Environment MMRE_L1_BITS=8 / 16 forces a code width (tests, experiments). */
 int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
 /* The filter's own record of the last mmre_link_sweep_l1q on d_work (one tiny launch, no
  * synchronisation): d_out[0] = pairs the code bound left undecided (each rescored with the
- * canonical f32 chain), d_out[1] = 1 if the sweep ran the f32 fallback instead of the codes.
- * The fallback is taken on the device, without a host round trip, when M (the largest |x|)
- * exceeds 128 x the mean |x| of the two planes -- one outlier value stretching the 16-bit code
- * range, which would leave most pairs undecided -- or is not finite. Counts are the same
- * either way. */
+ * canonical f32 chain), d_out[1] = the code width the sweep used: 0 = 8-bit codes, 2 = 16-bit
+ * codes, 1 = the f32 fallback instead of the codes. The fallback is taken on the device when M
+ * (the largest |x|) exceeds 128 x the mean |x| of the two planes -- one outlier value stretching
+ * the code range, which would leave most pairs undecided -- or is not finite. Counts are the
+ * same either way. */
 int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
 int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
                         int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,

@@ -254,8 +254,8 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
 }
 
 // ------------------------------------------------------------ score ops ----
-// OP: 0 TransE L1, 1 TransE L2, 2 RotatE, 3 DistMult, 4 ComplEx, 5 TransE L1 on 16-bit codes
-// (the integer filter; acc carries a uint32 in float bits). One k step.
+// OP: 0 TransE L1, 1 TransE L2, 2 RotatE, 3 DistMult, 4 ComplEx, 5 / 6 TransE L1 on 16-bit /
+// 8-bit codes (the integer filter; acc carries a uint32 in float bits). One k step.
 template <int OP>
 __device__ __forceinline__ float op_step(float acc, float qa, float qb, float x, float y) {
   if constexpr (OP == 0) {
@@ -268,6 +268,8 @@ __device__ __forceinline__ float op_step(float acc, float qa, float qb, float x,
     return acc + sqrtf(__builtin_fmaf(di, di, dr * dr));
   } else if constexpr (OP == 5) {  // TransE L1 integer filter: two 16-bit codes per dword
     return __uint_as_float(__builtin_amdgcn_sad_u16(__float_as_uint(qa), __float_as_uint(x), __float_as_uint(acc)));
+  } else if constexpr (OP == 6) {  // TransE L1 integer filter: four 8-bit codes per dword
+    return __uint_as_float(__builtin_amdgcn_sad_u8(__float_as_uint(qa), __float_as_uint(x), __float_as_uint(acc)));
   } else {
     return __builtin_fmaf(x, qa, acc);
   }
@@ -327,10 +329,22 @@ __device__ __forceinline__ float rot_exact(const float* __restrict__ q_km, int64
 // undecided pairs as for RotatE (rot_bound), the undecided rescored exactly from the
 // row-major copies (l1_exact_rows: the canonical chain, acc + |q_k - e_k| in k order).
 // M non-finite (an inf / NaN anywhere in the planes): delta = inf, every pair is undecided.
+// Round 4: the default code width is 8 bits -- four k per dword, ONE v_sad_u8 per four elements
+// at the issue cost of one v_sad_u16 (scripts/probes/sad8_rate.hip: 4.4 vs 4.7 SIMD-cycles per
+// wave-instruction), i.e. half the inner loop -- with the same bound at delta = 2M / 255 (a band
+// 257x wider: 0.38 % of the trained C2 pairs undecided, scripts/probes/transe_quant_frac.py).
+// Whether that band pays depends on the data (how many scores sit that close to the
+// thresholds: xavier-init tables, whose truths rank mid-table, put tens of percent there), so
+// k_l1q_probe counts the undecided pairs of a fixed sample with the 8-bit codes and, over
+// L1Q_PROBE_FRAC of it, the 16-bit codes are made and swept instead. The choice is one device
+// word (hdr[1]); the three sweeps (8-bit, 16-bit, f32) are launched gated on it, and the one it
+// names counts -- no host round trip.
 // Workspace header (L1Q_HDR bytes before the code planes): word 0 = bits of M, word 1 = the
-// fallback flag (k_l1q_quant), L1Q_SLOTS undecided-pair counters (uint64, L1Q_SLOT_STRIDE apart:
-// separate cache lines) from byte 256, the absmax blocks' partial sums of |x| from byte
-// L1Q_PART. Zeroed up to L1Q_PART by the launch sequence.
+// code-width word (L1Q_CODES8 / L1Q_F32 / L1Q_CODES16), word 2 = the probe's undecided pairs,
+// L1Q_SLOTS undecided-pair counters (uint64, L1Q_SLOT_STRIDE apart: separate cache lines) from
+// byte 256, the absmax blocks' partial sums of |x| from byte L1Q_PART. Zeroed up to L1Q_PART by
+// the launch sequence. The 16-bit planes follow the header, then the 8-bit planes.
+constexpr uint32_t L1Q_CODES8 = 0u, L1Q_F32 = 1u, L1Q_CODES16 = 2u;
 constexpr int L1Q_HDR = 8192;
 constexpr int L1Q_SLOTS = 16;
 constexpr int L1Q_SLOT_STRIDE = 32;  // uint64 units = 256 B
@@ -339,23 +353,23 @@ constexpr int L1Q_MAX_BLOCKS = 512;
 struct L1Q {
   const float* q_rows;     // (queries, kt) row-major query vectors
   const float* ent_rows;   // (whole table, kt) row-major entity rows
-  const uint32_t* hdr;     // workspace header: hdr[0] bits of M, hdr[1] fallback flag
+  const uint32_t* hdr;     // workspace header: hdr[0] bits of M, hdr[1] code-width word, hdr[2] probe count
   unsigned long long* undecided;  // counter slots
   const float* q_f;        // fallback: the f32 k-major planes (query, entity slice) and their rows
   const float* ent_f;
   int kp_f;
   int kt;                  // floats per row (the canonical chain's length, padding rows are 0)
-  const uint32_t* gate;    // non-OP-5 sweeps: run only if *gate != 0 (the filter's fallback launch)
+  const uint32_t* gate;    // gated launches: run only if *gate is the sweep's code-width word (L1Q_F32 for the f32 sweep)
 };
-__device__ __forceinline__ float l1q_delta(const uint32_t* absmax) {
+__device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
-  return m == 0.0f ? 0.0f : (m < INFINITY ? (2.0f * m) / 65535.0f : INFINITY);
+  return m == 0.0f ? 0.0f : (m < INFINITY ? (2.0f * m) / levels : INFINITY);
 }
 __device__ __forceinline__ float l1_exact_rows(const float* __restrict__ q, const float* __restrict__ e, int kt) {
   const float4* q4 = reinterpret_cast<const float4*>(q);
   const float4* e4 = reinterpret_cast<const float4*>(e);
   float acc = 0.0f;
-#pragma unroll 10
+#pragma unroll 5
   for (int k = 0; k < kt / 4; ++k) {
     const float4 a = q4[k], b = e4[k];
     acc = acc + fabsf(a.x - b.x);
@@ -741,7 +755,7 @@ struct UnitMap {
 // counts stay in registers until the workgroup moves to the next query tile.
 // LDS of one VALU-sweep workgroup. A struct declared once in the kernel, so that the L1
 // filter's kernel and its f32 fallback path (the same kernel, one uniform branch) share it.
-template <int NPL, bool TC>
+template <int NPL, bool TC, bool LIST>
 struct ValuSmem {
   float4 sq[2][NPL][KC][TQ / 4];
   float4 se[2][NPL][KC][TE / 4];
@@ -753,6 +767,7 @@ struct ValuSmem {
   uint32_t s_unc[NT / 64];           // undecided pairs per wave (the L1 filter's counter)
   uint32_t s_ts[2][TQ];              // L1 filter, prediction = score: per query row, the integer
   uint32_t s_tw[2][TQ];              // thresholds t_sure and t_out - t_sure (load_meta)
+  int2 s_pairs[LIST ? NT / 64 : 1][LIST ? 128 : 1];  // L1 filter: each wave's undecided (query, entity) pairs
 };
 
 // The sweep body. Counts go to the raw columns only (counts[0][q], counts[2][q]); the filtered
@@ -760,7 +775,7 @@ struct ValuSmem {
 // receive them in k_counts_finalize, one coalesced pass after the sweep (half the atomics).
 template <int OP, bool TC, bool STORE, int PK, int NPL>
 __device__ __forceinline__ void sweep_valu_body(
-    ValuSmem<NPL, TC>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
+    ValuSmem<NPL, TC, (OP == 5 || OP == 6) && !TC>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
     const float* __restrict__ q_km, int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups,
     int pred_kind, float margin, const float* __restrict__ thr, const int32_t* __restrict__ qtrue,
     const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
@@ -768,7 +783,8 @@ __device__ __forceinline__ void sweep_valu_body(
     float* __restrict__ scores, const L1Q& l1) {
   static_assert(NPL == ((OP == 2) ? 2 : 1), "planes");
   // filters: RotatE's raw-sqrt sum (rot_bound / rot_exact), TransE L1's 16-bit codes (L1Q)
-  constexpr bool FAST = (OP == 2 || OP == 5) && !STORE;
+  constexpr bool L1F = OP == 5 || OP == 6;  // TransE L1's integer filter (16- / 8-bit codes)
+  constexpr bool FAST = (OP == 2 || L1F) && !STORE;
   auto& sq = sm.sq;
   auto& se = sm.se;
   auto& s_thr = sm.s_thr;
@@ -792,8 +808,8 @@ __device__ __forceinline__ void sweep_valu_body(
 
   // L1 filter constants (uniform): code step, bound slope and offset
   float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
-  if constexpr (OP == 5) {
-    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr))));
+  if constexpr (L1F) {
+    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr, OP == 6 ? 255.0f : 65535.0f))));
     l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
     l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
   }
@@ -805,7 +821,7 @@ __device__ __forceinline__ void sweep_valu_body(
       const float th = v ? thr[q] : -INFINITY;
       s_thr[slot][tid] = th;
       s_true[slot][tid] = v ? qtrue[q] : -1;
-      if constexpr (OP == 5 && PK == 0) {
+      if constexpr (L1F && PK == 0) {
         // prediction = the score: the filter decides in the integer domain. With a = delta *
         // S_int, |S - a| <= l1f a + l1c, so S_int < x = (th - l1c) / (delta (1 + l1f)) gives
         // S < th and S_int >= y = (th + l1c) / (delta (1 - l1f)) gives S >= th; x, y are shrunk /
@@ -873,7 +889,30 @@ __device__ __forceinline__ void sweep_valu_body(
     s_cnt[0][i][tid] = 0;
     if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] = 0;
   }
-  if (OP == 5 && tid < NT / 64) sm.s_unc[tid] = 0u;
+  if (L1F && tid < NT / 64) sm.s_unc[tid] = 0u;
+  // L1 filter: the wave's undecided pairs are appended to its LDS list (ballot order, no
+  // atomics) and rescored 64 at a time, one pair per lane, whenever the list holds a full
+  // batch -- the dependent row loads of the canonical chain are paid once per 64 pairs, not once
+  // per lane-pair with the wave waiting on its busiest lane (which made the 8-bit codes' 0.4 %
+  // of undecided pairs cost 0.8 ms at C2). Rescored pairs that beat their threshold go straight
+  // to the raw count columns (the query tile's counts may have been flushed already).
+  // (Type-constrained sweeps keep the per-lane loop: the list's 4 KB would push their LDS past
+  // four workgroups per CU.)
+  constexpr bool LIST = L1F && !TC;
+  int list_n = 0;         // wave-uniform
+  uint32_t n_listed = 0;  // the wave's undecided pairs (the filter's counter; per lane without the list)
+  auto rescore = [&](int2 p) {
+    const int64_t q = p.x;
+    const int e = p.y;
+    const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
+    if (pred(sx) < thr[q]) {
+      atomicAdd(&counts[q], 1);
+      if constexpr (TC) {
+        const uint32_t* tm = qmode[q] == MMRE_HEAD_BATCH ? type_head : type_tail;
+        if (type_bit(tm, type_words, qr[q], e + e_base)) atomicAdd(&counts[2 * n_query + q], 1);
+      }
+    }
+  };
 
   int cur_qt, cur_et;
   um.at(u0, cur_qt, cur_et);
@@ -881,20 +920,22 @@ __device__ __forceinline__ void sweep_valu_body(
   uint32_t lo = 0xFFFFFFFFu;  // RotatE: min of the sqrt inputs' bits over this unit (see rot_mag)
   // L1 filter: the code rows actually used in the last stage (the plane is padded to whole
   // stages; 100 of 104 rows at d = 200: the pad rows' zeros are not swept)
-  const int kk_last = (OP == 5) ? ((((l1.kt + 1) >> 1) + 1) & ~1) - (nkc - 1) * KC : KC;
-  const uint32_t fb_flag = OP == 5 ? l1.hdr[1] : 0u;  // the L1 filter's fallback flag, in flight with the stage
+  const int kk_last = L1F ? ((((l1.kt + (OP == 6 ? 3 : 1)) >> (OP == 6 ? 2 : 1)) + 1) & ~1) - (nkc - 1) * KC : KC;
+  // the L1 filter's code-width word (L1Q_CODES8 / _CODES16 / _F32: which of the gated sweeps
+  // counts), in flight with the stage
+  const uint32_t fb_flag = L1F ? l1.hdr[1] : 0u;
   load_meta(cur_qt, 0);
   gload();
   swrite(0);
   __syncthreads();
-  if (OP == 5 && __builtin_amdgcn_readfirstlane(fb_flag) != 0u) return;  // uniform: the f32 launch counts
+  if (L1F && __builtin_amdgcn_readfirstlane(fb_flag) != (OP == 6 ? L1Q_CODES8 : L1Q_CODES16)) return;  // uniform
 
   int buf = 0;
   for (int unit = u0; unit < u1; ++unit) {
     for (int kc = 0; kc < nkc; ++kc) {
       const bool more = ld_unit < u1;
       if (more) gload();
-      const int kk_n = (OP == 5 && kc == nkc - 1) ? kk_last : KC;
+      const int kk_n = (L1F && kc == nkc - 1) ? kk_last : KC;
 #pragma unroll 2
       for (int kk = 0; kk < kk_n; ++kk) {
         float4 a0 = sq[buf][0][kk][tq], a1 = sq[buf][0][kk][16 + tq];
@@ -990,7 +1031,7 @@ __device__ __forceinline__ void sweep_valu_body(
           }
           uint32_t unc[2] = {0u, 0u};  // undecided pairs, bit i * 8 + j (rows 0-3 / 4-7)
           bool whole = false;
-          if constexpr (OP == 5 && PK == 0 && !TC) {
+          if constexpr (L1F && PK == 0 && !TC) {
             // L1 filter, a whole entity tile (every tile but the last, uniform): per pair one
             // compare + carry-add for the count and one subtract + compare for the undecided
             // band [t_sure, t_out), its wave-wide ballot OR-ed into one scalar mask. The count
@@ -1030,10 +1071,6 @@ __device__ __forceinline__ void sweep_valu_body(
                   }
                 }
               }
-#pragma unroll
-              for (int i = 0; i < 8; ++i)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[i][j] = 0.0f;
             }
           }
 #pragma unroll
@@ -1043,7 +1080,7 @@ __device__ __forceinline__ void sweep_valu_body(
             const float th = s_thr[slot][ql];
             const int32_t tr = s_true[slot][ql];
             int c = 0, cc = 0;
-            if constexpr (OP == 5 && PK == 0) {
+            if constexpr (L1F && PK == 0) {
               // prediction = the score: the integer thresholds of load_meta
               const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
 #pragma unroll
@@ -1059,7 +1096,6 @@ __device__ __forceinline__ void sweep_valu_body(
                   cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
                 }
                 unc[i >> 2] |= (uint32_t)((si - t_sure < t_span) & valid) << ((i & 3) * 8 + j);
-                acc[i][j] = 0.0f;
               }
               s_cnt[0][i][tid] += c;
               if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
@@ -1070,7 +1106,7 @@ __device__ __forceinline__ void sweep_valu_body(
               const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
               const bool valid = (e + e_base != tr) & (e < n_ent);
               float a, bnd;
-              if constexpr (OP == 5) {
+              if constexpr (L1F) {
                 a = (float)__float_as_uint(acc[i][j]) * l1d;
                 bnd = __builtin_fmaf(a, l1f, l1c);
               } else {
@@ -1088,14 +1124,40 @@ __device__ __forceinline__ void sweep_valu_body(
                 cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
               }
               unc[i >> 2] |= (uint32_t)(!sure & !out & valid) << ((i & 3) * 8 + j);
-              acc[i][j] = 0.0f;
             }
             s_cnt[0][i][tid] += c;
             if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
           }
+          if constexpr (LIST) {
+            int2* wl = sm.s_pairs[tid >> 6];
+            const int lane = tid & 63;
+            for (;;) {  // uniform: one undecided pair per lane and round into the list
+              const bool has = (unc[0] | unc[1]) != 0u;
+              const uint64_t bal = __ballot(has);
+              if (bal == 0) break;
+              if (has) {
+                const int h = unc[0] ? 0 : 1;
+                const int b = __builtin_ctz(unc[h]);
+                unc[h] &= unc[h] - 1u;
+                const int i = h * 4 + (b >> 3), j = b & 7;
+                const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
+                const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
+                const int pos = list_n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                wl[pos] = make_int2((int)(q0 + ql), e);
+              }
+              const int nb = __builtin_popcountll(bal);
+              list_n += nb;
+              n_listed += (uint32_t)nb;
+              if (list_n >= 64) {  // a full batch (the list holds < 128: < 64 before this round)
+                list_n -= 64;
+                rescore(wl[list_n + lane]);
+              }
+            }
+          }
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            uint32_t m = unc[h];
+            uint32_t m = LIST ? 0u : unc[h];  // (the L1 filter's pairs went to the wave's list)
             while (m) {  // rare: exact rescoring, one pair at a time
               const int b = __builtin_ctz(m);
               m &= m - 1u;
@@ -1103,12 +1165,13 @@ __device__ __forceinline__ void sweep_valu_body(
               const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
               const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
               float sx;
-              if constexpr (OP == 5) atomicAdd(&sm.s_unc[tid >> 6], 1u);  // the wave's undecided pairs (LDS)
-              if constexpr (OP == 5)
+              if constexpr (L1F) {
+                ++n_listed;
                 sx = l1_exact_rows(l1.q_rows + (q0 + ql) * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt,
                                    l1.kt);
-              else
+              } else {
                 sx = rot_exact(q_km, q_pad, q0 + ql, ent_km, e_pad, e, kp);
+              }
               const float v = pred(sx);
               if (v < s_thr[slot][ql]) {
                 s_cnt[0][i][tid] += 1;
@@ -1119,6 +1182,12 @@ __device__ __forceinline__ void sweep_valu_body(
               }
             }
           }
+          // the accumulators restart here, after the rescoring: dead while it runs, so its row
+          // loads have the registers
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][j] = 0.0f;
         } else {
         if constexpr (OP == 2) {
           bool bad = lo < __float_as_uint(kRotMin);  // v = 0 or v < 2^-96
@@ -1212,7 +1281,13 @@ __device__ __forceinline__ void sweep_valu_body(
       buf ^= 1;
     }
   }
-  if constexpr (OP == 5) {  // the filter's undecided pairs: one atomic per workgroup, 16 slots
+  if constexpr (L1F) {  // the filter's undecided pairs: one atomic per workgroup, 16 slots
+    if constexpr (LIST) {
+      if (list_n > 0 && (tid & 63) < list_n) rescore(sm.s_pairs[tid >> 6][tid & 63]);  // the last partial batch
+      if ((tid & 63) == 0) sm.s_unc[tid >> 6] = n_listed;
+    } else {
+      if (n_listed) atomicAdd(&sm.s_unc[tid >> 6], n_listed);
+    }
     __syncthreads();
     if (tid == 0) {
       uint32_t t = 0;
@@ -1233,15 +1308,16 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
     float* __restrict__ scores, L1Q l1) {
   constexpr int NPL = (OP == 2) ? 2 : 1;
-  __shared__ ValuSmem<NPL, TC> sm;
+  __shared__ ValuSmem<NPL, TC, (OP == 5 || OP == 6) && !TC> sm;
   // the L1 filter's fallback (k_l1q_quant decided that the codes are too coarse for these
   // planes -- one outlier value sets the code step for everything): the filter launch does
   // nothing (sweep_valu_body tests the flag once its first stage is loaded, so the flag's load
   // latency hides under the stage's) and the exact f32 sweep launched after it, gated on the
   // same flag, counts. A separate launch, not a branch here: inlining the f32 body beside the
   // filter's grew the kernel by half and its register spills (18 -> 23)
-  if constexpr (OP != 5) {
-    if (l1.gate != nullptr && __builtin_amdgcn_readfirstlane(*l1.gate) == 0u) return;
+  if (l1.gate != nullptr) {
+    const uint32_t want = OP == 6 ? L1Q_CODES8 : OP == 5 ? L1Q_CODES16 : L1Q_F32;
+    if (__builtin_amdgcn_readfirstlane(*l1.gate) != want) return;
   }
   sweep_valu_body<OP, TC, STORE, PK, NPL>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
                                           n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head, type_tail,
@@ -1638,36 +1714,97 @@ __device__ __forceinline__ bool l1q_fallback(const uint32_t* __restrict__ work, 
 }
 
 // Codes of columns [c0, c0 + n) of a k-major float plane (kp rows, stride pad) into dword rows
-// out[r][pad] = Q(x[2r]) | Q(x[2r + 1]) << 16, rows r < k2 (k >= kp: code 0 in both planes).
-// Skipped when the fallback test says the sweep will not read the codes.
+// r < kw, Q(x) = rint((x + M) (2^BITS - 1) / 2M): BITS 16 packs Q(x[2r]) | Q(x[2r + 1]) << 16,
+// BITS 8 the four codes Q(x[4r + h]) << 8h (k >= kp: code 0 in both planes).
+// mode 0 (the first codes made): the fallback test decides between these codes and the f32
+// sweep and writes the code-width word. mode 1 (the 16-bit codes after k_l1q_probe): made only
+// while the f32 fallback is off and the probe counted more than probe_max undecided pairs; the
+// first block writes L1Q_CODES16 (the other blocks read the word before or after that store
+// and reach the same decision either way).
+template <int BITS>
 __global__ __launch_bounds__(256) void k_l1q_quant(const float* __restrict__ km, int64_t pad, int64_t c0, int64_t n,
-                                                   int kp, int k2, uint32_t* __restrict__ out,
+                                                   int kp, int kw, uint32_t* __restrict__ out,
                                                    uint32_t* __restrict__ work, int n_part, double n_elem,
-                                                   float ratio) {
-  const bool fb = l1q_fallback(work, n_part, n_elem, ratio);
-  if (blockIdx.x == 0 && threadIdx.x == 0) work[1] = fb ? 1u : 0u;
-  if (fb) return;
+                                                   float ratio, int mode, uint32_t probe_max) {
+  if (mode == 1) {
+    const uint32_t w = __builtin_amdgcn_readfirstlane(work[1]);
+    if (w == L1Q_F32) return;
+    if (w != L1Q_CODES16 && __builtin_amdgcn_readfirstlane(work[2]) <= probe_max) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) work[1] = L1Q_CODES16;
+  } else {
+    const bool fb = l1q_fallback(work, n_part, n_elem, ratio);
+    if (blockIdx.x == 0 && threadIdx.x == 0) work[1] = fb ? L1Q_F32 : (BITS == 8 ? L1Q_CODES8 : L1Q_CODES16);
+    if (fb) return;
+  }
+  constexpr int PER = 32 / BITS;
+  constexpr float LEVELS = BITS == 8 ? 255.0f : 65535.0f;
   const float mx = __uint_as_float(*work);
-  const float inv = (mx > 0.0f && mx < INFINITY) ? 65535.0f / (2.0f * mx) : 0.0f;
+  const float inv = (mx > 0.0f && mx < INFINITY) ? LEVELS / (2.0f * mx) : 0.0f;
   const float off = (mx < INFINITY) ? mx : 0.0f;
-  const int64_t total = (int64_t)k2 * n;
+  const int64_t total = (int64_t)kw * n;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int r = (int)(i / n);
     const int64_t c = c0 + i % n;
-    uint32_t code[2];
+    uint32_t word = 0u;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int k = 2 * r + h;
+    for (int h = 0; h < PER; ++h) {
+      const int k = PER * r + h;
       float t = k < kp ? (km[(int64_t)k * pad + c] + off) * inv : 0.0f;
-      t = t == t ? fminf(fmaxf(t, 0.0f), 65535.0f) : 0.0f;
-      code[h] = (uint32_t)rintf(t);
+      t = t == t ? fminf(fmaxf(t, 0.0f), LEVELS) : 0.0f;
+      word |= (uint32_t)rintf(t) << (BITS * h);
     }
-    out[(int64_t)r * pad + c] = code[0] | (code[1] << 16);
+    out[(int64_t)r * pad + c] = word;
   }
 }
 
-// Sum of the undecided-pair slots and the fallback flag -> out[0], out[1] (mmre_link_l1q_stats).
+// The code-width probe (runs when the 8-bit codes were made): L1Q_PROBE_Q workgroups, each one
+// query column (evenly spaced over the queries) against L1Q_PROBE_E consecutive entity columns
+// of the slice (the start spread over the slice), scored with the 8-bit codes; the pairs inside
+// their query's undecided band (the epilogue's test in its float form) are counted into hdr[2].
+constexpr int L1Q_PROBE_Q = 64, L1Q_PROBE_E = 1024;
+constexpr double L1Q_PROBE_FRAC = 0.01;  // undecided fraction of the sample above which 16-bit codes
+__global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ uq, int64_t q_pad, int64_t n_query,
+                                                   const uint32_t* __restrict__ ue, int64_t e_pad, int64_t n_slice,
+                                                   int kw, int kt, const float* __restrict__ thr, int pred_kind,
+                                                   float margin, uint32_t* __restrict__ work) {
+  if (__builtin_amdgcn_readfirstlane(work[1]) != L1Q_CODES8) return;
+  const PredSel<-1> pred(pred_kind, margin);
+  const int64_t q = (int64_t)blockIdx.x * n_query / gridDim.x;
+  const int64_t span = n_slice > L1Q_PROBE_E ? n_slice - L1Q_PROBE_E : 0;
+  const int64_t c = (((int64_t)blockIdx.x * span / gridDim.x) & ~(int64_t)3) + 4 * threadIdx.x;
+  const float l1d = l1q_delta(work, 255.0f);
+  const float l1f = (float)(kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+  const float l1c = __builtin_fmaf((float)kt * 1.03f, l1d, 0x1p-120f);
+  uint32_t acc[4] = {0u, 0u, 0u, 0u};
+  if (c < n_slice) {  // columns c .. c + 3 lie inside the slice's whole tiles
+    for (int r = 0; r < kw; ++r) {
+      const uint32_t a = uq[(int64_t)r * q_pad + q];
+      const uint4 e = *reinterpret_cast<const uint4*>(ue + (int64_t)r * e_pad + c);
+      acc[0] = __builtin_amdgcn_sad_u8(a, e.x, acc[0]);
+      acc[1] = __builtin_amdgcn_sad_u8(a, e.y, acc[1]);
+      acc[2] = __builtin_amdgcn_sad_u8(a, e.z, acc[2]);
+      acc[3] = __builtin_amdgcn_sad_u8(a, e.w, acc[3]);
+    }
+  }
+  const float th = thr[q];
+  uint32_t und = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = (float)acc[j] * l1d;
+    const float bnd = __builtin_fmaf(a, l1f, l1c);
+    const float p1 = pred(a - bnd), p2 = pred(a + bnd);
+    const bool fin = a < INFINITY;
+    const bool sure = fin & (fmaxf(p1, p2) < th);
+    const bool out = (fin & (fminf(p1, p2) >= th)) | (th != th);
+    und += (uint32_t)(!sure & !out & (c + j < n_slice));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) und += __shfl_xor(und, o);
+  if ((threadIdx.x & 63) == 0 && und) atomicAdd(work + 2, und);
+}
+
+// Sum of the undecided-pair slots and the code-width word -> out[0], out[1] (mmre_link_l1q_stats).
 __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
   const unsigned long long* sl =
@@ -1679,6 +1816,7 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
 }
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
+static int l1q_rows8(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 3) / 4, KC); }
 
 // ------------------------------------------------- split-bf16 MFMA filter ---
 // DistMult / ComplEx count-only sweeps through a filter with exact rescoring, as the VALU
@@ -2082,7 +2220,7 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
   launch_valu_one<OP, TCV, STV, PKV>(st, ent_km, e_pad, n_ent, n_et, e_base, q_km, q_pad, n_query, kp, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1)
   // the model's usual prediction kind is compiled into the epilogue of the plain sweep
   constexpr int fast = (OP == 2) ? 3 : 0;  // RotatE -(m - s), TransE s
-  if constexpr (OP == 5) {  // the integer filter: count-only sweeps
+  if constexpr (OP == 5 || OP == 6) {  // the integer filter: count-only sweeps
     if (store) return MMRE_ERR_ARG;
     if (tc) MMRE_LV1(true, false, -1);
     else if (pk == fast) MMRE_LV1(false, false, fast);
@@ -2369,7 +2507,7 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
 
 extern "C" int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
   if (dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
-  return L1Q_HDR + 4 * (int64_t)l1q_rows(dim) * (e_pad + q_pad);
+  return L1Q_HDR + 4 * (int64_t)(l1q_rows(dim) + l1q_rows8(dim)) * (e_pad + q_pad);
 }
 
 extern "C" int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream) {
@@ -2392,34 +2530,70 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   if (!d_ent_rows || !d_q_rows || !d_work || work_bytes < mmre_link_l1q_workspace(dim, e_pad, q_pad)) return MMRE_ERR_WORKSPACE;
   if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  const int kp = plane_rows(MMRE_TRANSE_L1, dim), k2 = l1q_rows(dim);
+  const int kp = plane_rows(MMRE_TRANSE_L1, dim), k2 = l1q_rows(dim), k4 = l1q_rows8(dim);
   uint32_t* hdr = (uint32_t*)d_work;
-  uint32_t* uq = (uint32_t*)((char*)d_work + L1Q_HDR);
+  uint32_t* uq = (uint32_t*)((char*)d_work + L1Q_HDR);  // 16-bit planes
   uint32_t* ue = uq + (int64_t)k2 * q_pad;
+  uint32_t* vq = ue + (int64_t)k2 * e_pad;              // 8-bit planes
+  uint32_t* ve = vq + (int64_t)k4 * q_pad;
   const int64_t e_cols = round_up(e_end, TE) - e_begin;  // the slice's whole tiles
   // fallback ratio M / mean|x| (MMRE_L1Q_RATIO: experiments; <= 0 forces the fallback)
   static const char* ratio_env = getenv("MMRE_L1Q_RATIO");
   const float ratio = ratio_env ? (float)atof(ratio_env) : 128.0f;
   const int n_abs = std::min(kp * 8, L1Q_MAX_BLOCKS);
   const double n_elem = (double)kp * (double)(q_pad + e_cols);
-  MMRE_CHECK(hipMemsetAsync(hdr, 0, L1Q_PART, st));
-  hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)n_abs), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
-                     kp, hdr);
-  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr,
-                     n_abs, n_elem, ratio);
-  hipLaunchKernelGGL(k_l1q_quant, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr,
-                     n_abs, n_elem, ratio);
-  MMRE_CHECK_LAUNCH();
+  // code width (MMRE_L1_BITS: experiments and tests): 8 / 16 forces it, otherwise the 8-bit
+  // codes unless k_l1q_probe finds their band too wide for this data
+  const char* bits_env = getenv("MMRE_L1_BITS");
+  const int bits = bits_env ? atoi(bits_env) : 0;
   const int64_t tw = (n_ent + 31) / 32;
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
+  MMRE_CHECK(hipMemsetAsync(hdr, 0, L1Q_PART, st));
+  hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)n_abs), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
+                     kp, hdr);
+  if (bits != 16) {
+    hipLaunchKernelGGL(k_l1q_quant<8>, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k4, vq, hdr,
+                       n_abs, n_elem, ratio, 0, 0u);
+    hipLaunchKernelGGL(k_l1q_quant<8>, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k4, ve, hdr,
+                       n_abs, n_elem, ratio, 0, 0u);
+  }
+  if (bits == 0) {
+    hipLaunchKernelGGL(k_l1q_probe, dim3(L1Q_PROBE_Q), dim3(256), 0, st, vq, q_pad, n_query, ve + e_begin, e_pad,
+                       n_slice, k4, n_planes(MMRE_TRANSE_L1) * kp, d_truth, pred_kind, margin, hdr);
+    const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
+    const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);
+    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr,
+                       n_abs, n_elem, ratio, 1, probe_max);
+    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr,
+                       n_abs, n_elem, ratio, 1, probe_max);
+  } else if (bits == 16) {
+    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr,
+                       n_abs, n_elem, ratio, 0, 0u);
+    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr,
+                       n_abs, n_elem, ratio, 0, 0u);
+  }
+  MMRE_CHECK_LAUNCH();
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
                n_planes(MMRE_TRANSE_L1) * kp, nullptr};
   const bool tc = d_type_head != nullptr;
-  rc = launch_valu<5>(tc, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et, (int)e_begin,
-                      (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr, d_qmode,
-                      d_type_head, d_type_tail, tw, d_counts, nullptr, l1, false);
-  if (rc) return rc;
+  // the gated sweeps: the one the code-width word names counts, the others' workgroups leave
+  if (bits != 16) {
+    rc = launch_valu<6>(tc, false, st, (const float*)(ve + e_begin), e_pad, n_slice, n_et, (int)e_begin,
+                        (const float*)vq, q_pad, n_query, k4, pred_kind, margin, d_truth, d_q_true, d_qr, d_qmode,
+                        d_type_head, d_type_tail, tw, d_counts, nullptr, l1, false);
+    if (rc) return rc;
+  }
+  if (bits != 8) {
+    // after the 8-bit sweep the 16-bit one rarely counts: gated at its top (one flag load per
+    // workgroup, 4 workgroups per resident slot) like the f32 fallback below
+    L1Q l16 = l1;
+    if (bits == 0) l16.gate = hdr + 1;
+    rc = launch_valu<5>(tc, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et, (int)e_begin,
+                        (const float*)uq, q_pad, n_query, k2, pred_kind, margin, d_truth, d_q_true, d_qr, d_qmode,
+                        d_type_head, d_type_tail, tw, d_counts, nullptr, l16, false);
+    if (rc) return rc;
+  }
   // the fallback: the exact f32 sweep of the float planes, gated on the flag k_l1q_quant wrote
   // (its workgroups return at once when the codes were used)
   L1Q gate{};

@@ -314,8 +314,9 @@ class LinkSweep:
     def l1q_stats(self, buffers):
         """The integer filter's record of the last run() on `buffers` (mmre_link_l1q_stats):
         dict(undecided=pairs rescored with the canonical chain, fallback=True if the sweep ran
-        the f32 path because the codes were too coarse), or None if that run did not use the
-        filter (not TransE L1, score-storing, MMRE_L1_FILTER=0). Synchronises the stream."""
+        the f32 path because the codes were too coarse, bits=8 | 16 the code width the sweep
+        used -- None on the fallback), or None if that run did not use the filter (not TransE
+        L1, score-storing, MMRE_L1_FILTER=0). Synchronises the stream."""
         if not buffers.get("l1q_used"):
             return None
         wk = buffers["l1q_work"]
@@ -323,8 +324,9 @@ class LinkSweep:
         if out is None:
             out = buffers["l1q_stats"] = torch.zeros(2, dtype=torch.int64, device=self.device)
         call("mmre_link_l1q_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
-        u, f = (int(x) for x in out.cpu())
-        return dict(undecided=u, fallback=bool(f))
+        u, w = (int(x) for x in out.cpu())
+        # the code-width word: 0 = 8-bit codes, 1 = the f32 fallback, 2 = 16-bit codes
+        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w))
 
 
 def _rows_view(c):

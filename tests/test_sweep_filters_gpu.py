@@ -1,7 +1,8 @@
 """GPU parity of the sweep's filters (csrc/link.hip): the count-only RotatE sweeps sum the raw
 v_sqrt_f32 -- within 1 ulp of sqrtf (scripts/probes/sqrt_ulp.hip, exhaustive) -- and the
-count-only TransE L1 sweeps sum |code differences| of 16-bit quantized planes with v_sad_u16
-(mmre_link_sweep_l1q); both rescore with the canonical chain every pair whose prediction the
+count-only TransE L1 sweeps sum |code differences| of 8-bit (v_sad_u8) or 16-bit (v_sad_u16)
+quantized planes (mmre_link_sweep_l1q; the width picked on the device by a sampled probe, or
+forced with MMRE_L1_BITS); both rescore with the canonical chain every pair whose prediction the
 error bound cannot place on one side of the threshold.
 
 Bar: raw / filtered / type-constrained counts bit-equal to the score-storing (exact) sweep's
@@ -51,9 +52,19 @@ def _adversarial(E=1500, R=6, d=48, Q=257, seed=0, margin=6.0, model="rotate", h
 
 @pytest.mark.parametrize("model,seed,huge", [("rotate", 0, True), ("rotate", 1, True), ("transe", 0, False),
                                              ("transe", 1, False), ("transe", 2, True)])
-def test_fast_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, model, seed, huge):
+def test_fast_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, monkeypatch, model, seed, huge):
     """huge: a row of 3e19 and a NaN -- for TransE these make the quantization scale
-    non-finite, so every pair is rescored (slow, exact)."""
+    non-finite, so every pair is rescored (slow, exact). TransE runs every code width: 8-bit,
+    16-bit and the probe's choice."""
+    for bits in (("8", "16", None) if model == "transe" else (None,)):
+        if bits is None:
+            monkeypatch.delenv("MMRE_L1_BITS", raising=False)
+        else:
+            monkeypatch.setenv("MMRE_L1_BITS", bits)
+        _fast_filter_case(oracle_mod, model, seed, huge)
+
+
+def _fast_filter_case(oracle_mod, model, seed, huge):
     from mmre.link import FilterIndex
     margin = 6.0 if model == "rotate" else None
     ent, rel, qh, qr, qt, qm = _adversarial(seed=seed, margin=margin or 6.0, model=model, huge=huge)
@@ -88,10 +99,15 @@ def test_fast_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, model, seed
 def test_l1_filter_on_and_off_and_entity_slices(oracle_mod, monkeypatch):
     """TransE L1: the integer-filter sweep equals the f32 sweep (MMRE_L1_FILTER=0) on the whole
     table and on entity slices (mmre_link_sweep_l1q with e_begin / e_end), whose counts sum to
-    the whole-table ones; the margin prediction kind takes the generic epilogue."""
+    the whole-table ones; the margin prediction kind takes the generic epilogue. Every code
+    width (MMRE_L1_BITS 8, 16, the probe's choice)."""
     import torch
     from mmre.link import FilterIndex, LinkSweep
-    for margin in (None, 4.0):
+    for margin, bits in ((None, "8"), (None, "16"), (None, None), (4.0, "8"), (4.0, "16"), (4.0, None)):
+        if bits is None:
+            monkeypatch.delenv("MMRE_L1_BITS", raising=False)
+        else:
+            monkeypatch.setenv("MMRE_L1_BITS", bits)
         ent, rel, qh, qr, qt, qm = _adversarial(E=2100, d=40, Q=200, seed=5, model="transe", huge=False)
         E, R = ent.shape[0], rel.shape[0]
         index = FilterIndex(qh, qr, qt, E, R)
@@ -165,6 +181,34 @@ def test_l1_filter_outlier_row_falls_back_to_f32(monkeypatch):
     print(f"L1 filter: plain table {t_plain:.3f} ms ({st_plain['undecided']} undecided pairs); outlier table "
           f"{t_out:.3f} ms (fallback) vs f32 sweep {t_32:.3f} ms")
     assert t_out <= 1.1 * t_32
+
+
+def test_l1_code_width_probe_picks_16_bit_on_untrained_tables(monkeypatch):
+    """The 8-bit codes' band (257x the 16-bit one) holds tens of percent of the pairs when the
+    truths rank mid-table (xavier-init C2 tables): the probe sees it and the 16-bit codes run,
+    counts equal to both forced widths and the f32 sweep, time within 1.15x of the forced 16-bit
+    sweep (the probe, the 16-bit quantization and the 8-bit launch's early exit are the extra)."""
+    from mmre.workloads import zs_workload
+    import torch
+    dev = torch.device("cuda:0")
+    w = zs_workload("FB15K-237-ZS", "transe", 200)
+    res = {}
+    for bits in (None, "8", "16"):
+        if bits is None:
+            monkeypatch.delenv("MMRE_L1_BITS", raising=False)
+        else:
+            monkeypatch.setenv("MMRE_L1_BITS", bits)
+        _, run = _c2_eval(w, dev, norm_flag=True)
+        res[bits] = run()
+    monkeypatch.delenv("MMRE_L1_BITS", raising=False)
+    monkeypatch.setenv("MMRE_L1_FILTER", "0")
+    _, run32 = _c2_eval(w, dev, norm_flag=True)
+    c32, t32, _ = run32()
+    (ca, ta, sa), (c8, t8, s8), (c16, t16, s16) = res[None], res["8"], res["16"]
+    print(f"xavier C2: auto {ta:.3f} ms ({sa}), 8-bit {t8:.3f} ms ({s8}), 16-bit {t16:.3f} ms ({s16}), f32 {t32:.3f} ms")
+    assert sa["bits"] == 16 and s8["bits"] == 8 and s16["bits"] == 16
+    assert np.array_equal(ca, c32) and np.array_equal(c8, c32) and np.array_equal(c16, c32)
+    assert ta <= 1.15 * t16
 
 
 def _adversarial_dot(model, E=2300, R=5, d=48, Q=300, seed=0, nonfinite=True):
