@@ -72,21 +72,23 @@ def bytes_per_triple(model, dim):
             "rotate": 8 * dim}[model]
 
 
-def valu_ops_per_triple(model, dim):
+def valu_ops_per_triple(model, dim, l1_bits=16):
     """VALU issue slots per scored triple in the sweep's inner loop, counted from
     the instruction stream and checked against SQ_INSTS_VALU (profiles/pmc_*.json): TransE L1
     sub + add per element; RotatE 9 per complex element: 5 full-rate f32 ops (dr, di, dr*dr,
     fma(di, di, .), the accumulate) + the raw v_sqrt_f32 of the fast filter at quarter rate =
     4 slots (scripts/probes/trans_rate.hip, rot_rate.hip). The rare exact rescoring of
     undecided pairs is not counted (it is work the filter adds, not the triple's)."""
-    if model == "transe" and os.environ.get("MMRE_L1_FILTER", "1") != "0":
+    if model == "transe" and os.environ.get("MMRE_L1_FILTER", "1") != "0" and l1_bits:
         # the integer filter (mmre_link_sweep_l1q): one v_sad_u16 per two elements at half rate
-        # (scripts/probes/sad_rate.hip: 4.64 vs 2.36 cycles per wave-instruction) = 1 slot each
-        return 1 * dim
+        # (scripts/probes/sad_rate.hip: 4.64 vs 2.36 cycles per wave-instruction) = 1 slot each;
+        # with the 8-bit codes one v_sad_u8 (the same issue cost, scripts/probes/sad8_rate.hip)
+        # per four elements = half a slot each
+        return dim // 2 if l1_bits == 8 else dim
     return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 9 * dim}.get(model)
 
 
-KERNEL_NAMES = {"transe": "k_sweep_valu<5, false, false, 0>" if os.environ.get("MMRE_L1_FILTER", "1") != "0"
+KERNEL_NAMES = {"transe": "k_sweep_valu<6, false, false, 0>" if os.environ.get("MMRE_L1_FILTER", "1") != "0"
                 else "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
                 "distmult": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2",
                 "complex": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2"}
@@ -1176,6 +1178,7 @@ def main():
 
     steps(args.warmup)
     torch.cuda.synchronize()
+
     graphed = getattr(ev, "_graph_wanted", False)
     evs = None if graphed else [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                                 for _ in range(args.steps)]
@@ -1188,6 +1191,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+
     if graphed and n_local:  # the sweep kernel alone: events on the launch stream of eager evaluations
         from mmre.link import LinkSweep
         sw = LinkSweep(spec)
@@ -1217,6 +1221,12 @@ def main():
         bpt = bytes_per_triple(model, dim)
         triples_launch = n_local * e_local
         tps = triples_launch / (sweep_ms * 1e-3) if sweep_ms > 0 else 0.0
+        # the TransE sweep kernel that counted: the probe's code width (8 / 16) or the f32 fallback
+        l1_bits = fst.get("bits") if fst is not None and fst["kind"] == "l1q" else None
+        if model == "transe" and l1_bits == 16:
+            KERNEL_NAMES["transe"] = "k_sweep_valu<5, false, false, 0>"
+        elif model == "transe" and fst is not None and fst["kind"] == "l1q" and l1_bits is None:
+            KERNEL_NAMES["transe"] = "k_sweep_valu<0, false, false, 0>"
         traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
         if model in ("distmult", "complex") and fst is not None and fst["kind"] == "bf3" and not fst["fallback"]:
             # the split-bf16 filter: three bf16 products of K = dim x planes per triple on the bf16
@@ -1236,7 +1246,7 @@ def main():
             roof = {"bound": "mfma", "achieved": ach, "peak": MFMA_F32_PEAK / 1e12, "unit": "TFLOP/s",
                     "frac": ach * 1e12 / MFMA_F32_PEAK, "flops_per_triple": flops}
         else:
-            ops = valu_ops_per_triple(model, dim)
+            ops = valu_ops_per_triple(model, dim, l1_bits)
             ach = tps * ops / 1e12
             roof = {"bound": "valu", "achieved": ach, "peak": VALU_LANE_OPS / 1e12,
                     "unit": "TOP/s (VALU lane-ops: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz)",
@@ -1247,8 +1257,9 @@ def main():
             "triples_per_launch": triples_launch, "bytes_per_triple": bpt,
             "hbm_algorithmic_x": tps * bpt / (HBM_PEAK_GBS * 1e9),
             "hbm_measured_GBs": (traffic / (sweep_ms * 1e-3) / 1e9) if traffic and sweep_ms else None,
-            "note": "binding roof: VALU for TransE/RotatE (TransE: the integer filter's v_sad_u16, two elements per "
-                    "half-rate instruction = 1 slot per element, MMRE_L1_FILTER=0: sub + add-with-abs; RotatE: sub, sub, mul, "
+            "note": "binding roof: VALU for TransE/RotatE (TransE: the integer filter's v_sad_u8, four elements per "
+                    "half-rate instruction = 1/2 slot per element -- the 16-bit codes' v_sad_u16 when the probe picks them: "
+                    "1 slot --, MMRE_L1_FILTER=0: sub + add-with-abs; RotatE: sub, sub, mul, "
                     "fma, add + v_sqrt_f32 at 4 slots, the fast filter's loop), f32 MFMA for "
                     "DistMult/ComplEx. hbm_algorithmic_x = SURVEY 8(d) algorithmic bytes (one entity row per "
                     "scored triple) / 8 TB/s: > 1 because each entity row is reused across a 128-query LDS tile; "
@@ -1288,9 +1299,11 @@ def main():
             out["l1_filter"] = {"undecided_pairs": fst["undecided"],
                                 "undecided_frac": fst["undecided"] / pairs if pairs else None,
                                 "fallback_to_f32": fst["fallback"],
-                                "note": "pairs the 16-bit code bound left undecided, each rescored with the canonical "
-                                        "f32 chain (mmre_link_l1q_stats, rank 0's last evaluation); fallback_to_f32 = "
-                                        "the quantization pass found M > 128 x mean|x| and the sweep ran the f32 path"}
+                                "code_bits": fst.get("bits"),
+                                "note": "pairs the code bound (8- or 16-bit codes, code_bits: the device-side probe's "
+                                        "choice) left undecided, each rescored with the canonical f32 chain "
+                                        "(mmre_link_l1q_stats, rank 0's last evaluation); fallback_to_f32 = the "
+                                        "quantization pass found M > 128 x mean|x| and the sweep ran the f32 path"}
         elif fst is not None and fst["kind"] == "bf3":
             pairs = int(n_local) * int(e_local)
             out["mfma_filter"] = {"undecided_pairs": fst["undecided"],

@@ -1804,6 +1804,14 @@ __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ 
   if ((threadIdx.x & 63) == 0 && und) atomicAdd(work + 2, und);
 }
 
+// Zeroes n words: the filters' workspace headers at the start of each sweep. A kernel, not
+// hipMemsetAsync: replayed from a captured hipGraph, the memset node of the 4,352-byte L1
+// header left words 2-3 holding stale bytes (the probe's count read garbage and the graph's
+// evaluations switched to the 16-bit codes), while eager runs were right.
+__global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ p, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
+}
+
 // Sum of the undecided-pair slots and the code-width word -> out[0], out[1] (mmre_link_l1q_stats).
 __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
@@ -2549,7 +2557,7 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   const int64_t tw = (n_ent + 31) / 32;
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
-  MMRE_CHECK(hipMemsetAsync(hdr, 0, L1Q_PART, st));
+  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, st, hdr, L1Q_PART / 4);
   hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)n_abs), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
                      kp, hdr);
   if (bits != 16) {
@@ -2648,7 +2656,7 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   const double K = (double)ktot;
   const float cb = (float)(1.02 * (7.0 * K * std::ldexp(1.0, -24) * (1.0 + std::ldexp(1.0, -7)) +
                                    3.02 * std::ldexp(1.0, -16) + std::ldexp(1.0, -29) * std::sqrt(K)));
-  MMRE_CHECK(hipMemsetAsync(hdr, 0, 8, st));
+  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(64), 0, st, hdr, 2);
   const int nkb = ktot / 16;
   hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad * nkb + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad,
                      (int64_t)0, q_pad, nkb, qb, q_pad);
