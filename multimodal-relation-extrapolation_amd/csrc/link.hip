@@ -1721,19 +1721,27 @@ __device__ __forceinline__ bool l1q_fallback(const uint32_t* __restrict__ work, 
 // while the f32 fallback is off and the probe counted more than probe_max undecided pairs; the
 // first block writes L1Q_CODES16 (the other blocks read the word before or after that store
 // and reach the same decision either way).
+// Both planes in one launch: blockIdx.y 0 = the query plane, 1 = the entity slice.
+struct L1QPlane {
+  const float* km;  // k-major float plane, row stride pad
+  int64_t pad, c0, n;  // columns [c0, c0 + n)
+  uint32_t* out;    // code rows, row stride pad
+};
 template <int BITS>
-__global__ __launch_bounds__(256) void k_l1q_quant(const float* __restrict__ km, int64_t pad, int64_t c0, int64_t n,
-                                                   int kp, int kw, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(256) void k_l1q_quant(L1QPlane pq, L1QPlane pe, int kp, int kw,
                                                    uint32_t* __restrict__ work, int n_part, double n_elem,
                                                    float ratio, int mode, uint32_t probe_max) {
+  const float* __restrict__ km = blockIdx.y ? pe.km : pq.km;
+  const int64_t pad = blockIdx.y ? pe.pad : pq.pad, c0 = blockIdx.y ? pe.c0 : pq.c0, n = blockIdx.y ? pe.n : pq.n;
+  uint32_t* __restrict__ out = blockIdx.y ? pe.out : pq.out;
   if (mode == 1) {
     const uint32_t w = __builtin_amdgcn_readfirstlane(work[1]);
     if (w == L1Q_F32) return;
     if (w != L1Q_CODES16 && __builtin_amdgcn_readfirstlane(work[2]) <= probe_max) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) work[1] = L1Q_CODES16;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) work[1] = L1Q_CODES16;
   } else {
     const bool fb = l1q_fallback(work, n_part, n_elem, ratio);
-    if (blockIdx.x == 0 && threadIdx.x == 0) work[1] = fb ? L1Q_F32 : (BITS == 8 ? L1Q_CODES8 : L1Q_CODES16);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) work[1] = fb ? L1Q_F32 : (BITS == 8 ? L1Q_CODES8 : L1Q_CODES16);
     if (fb) return;
   }
   constexpr int PER = 32 / BITS;
@@ -1778,6 +1786,7 @@ __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ 
   const float l1c = __builtin_fmaf((float)kt * 1.03f, l1d, 0x1p-120f);
   uint32_t acc[4] = {0u, 0u, 0u, 0u};
   if (c < n_slice) {  // columns c .. c + 3 lie inside the slice's whole tiles
+#pragma unroll 8
     for (int r = 0; r < kw; ++r) {
       const uint32_t a = uq[(int64_t)r * q_pad + q];
       const uint4 e = *reinterpret_cast<const uint4*>(ue + (int64_t)r * e_pad + c);
@@ -2560,26 +2569,21 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, st, hdr, L1Q_PART / 4);
   hipLaunchKernelGGL(k_l1q_absmax, dim3((unsigned)n_abs), dim3(256), 0, st, d_q_km, q_pad, d_ent_km + e_begin, e_pad, e_cols,
                      kp, hdr);
-  if (bits != 16) {
-    hipLaunchKernelGGL(k_l1q_quant<8>, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k4, vq, hdr,
-                       n_abs, n_elem, ratio, 0, 0u);
-    hipLaunchKernelGGL(k_l1q_quant<8>, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k4, ve, hdr,
-                       n_abs, n_elem, ratio, 0, 0u);
-  }
+  const L1QPlane p8q{d_q_km, q_pad, 0, q_pad, vq}, p8e{d_ent_km, e_pad, e_begin, e_cols, ve};
+  const L1QPlane p16q{d_q_km, q_pad, 0, q_pad, uq}, p16e{d_ent_km, e_pad, e_begin, e_cols, ue};
+  if (bits != 16)
+    hipLaunchKernelGGL(k_l1q_quant<8>, dim3(1024, 2), dim3(256), 0, st, p8q, p8e, kp, k4, hdr, n_abs, n_elem, ratio, 0,
+                       0u);
   if (bits == 0) {
     hipLaunchKernelGGL(k_l1q_probe, dim3(L1Q_PROBE_Q), dim3(256), 0, st, vq, q_pad, n_query, ve + e_begin, e_pad,
                        n_slice, k4, n_planes(MMRE_TRANSE_L1) * kp, d_truth, pred_kind, margin, hdr);
     const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
     const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);
-    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr,
-                       n_abs, n_elem, ratio, 1, probe_max);
-    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr,
-                       n_abs, n_elem, ratio, 1, probe_max);
+    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(1024, 2), dim3(256), 0, st, p16q, p16e, kp, k2, hdr, n_abs, n_elem, ratio,
+                       1, probe_max);
   } else if (bits == 16) {
-    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_q_km, q_pad, (int64_t)0, q_pad, kp, k2, uq, hdr,
-                       n_abs, n_elem, ratio, 0, 0u);
-    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(2048), dim3(256), 0, st, d_ent_km, e_pad, e_begin, e_cols, kp, k2, ue, hdr,
-                       n_abs, n_elem, ratio, 0, 0u);
+    hipLaunchKernelGGL(k_l1q_quant<16>, dim3(1024, 2), dim3(256), 0, st, p16q, p16e, kp, k2, hdr, n_abs, n_elem, ratio,
+                       0, 0u);
   }
   MMRE_CHECK_LAUNCH();
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
