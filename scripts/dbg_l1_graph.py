@@ -34,3 +34,20 @@ for graph in (False, True):
     tk = [ev.launch(), ev.launch()]
     ev.finish(tk[0]); ev.finish(tk[1])
     print(f"graph={graph} pipelined: {hdr(ev)} {ev.filter_stats()}", flush=True)
+    pending = None
+    for i in range(40):
+        t = ev.launch()
+        if pending is not None:
+            ev.finish(pending)
+        pending = t
+    ev.finish(pending)
+    print(f"graph={graph} after 40 pipelined: {hdr(ev)} {ev.filter_stats()}", flush=True)
+    sw = LinkSweep(spec)
+    bufs = sw.alloc_queries(len(ev.q_host[0]))
+    for _ in range(3):
+        sw.run(*ev.q, filt=ev.filt, type_masks=ev.masks_tc, buffers=bufs)
+    torch.cuda.synchronize()
+    print(f"graph={graph} eager twin: {sw.filter_stats(bufs)}", flush=True)
+    del sw, bufs
+    ev.run()
+    print(f"graph={graph} after the twin: {hdr(ev)} {ev.filter_stats()}", flush=True)
