@@ -1770,8 +1770,14 @@ __global__ __launch_bounds__(256) void k_l1q_quant(L1QPlane pq, L1QPlane pe, int
 // query column (evenly spaced over the queries) against L1Q_PROBE_E consecutive entity columns
 // of the slice (the start spread over the slice), scored with the 8-bit codes; the pairs inside
 // their query's undecided band (the epilogue's test in its float form) are counted into hdr[2].
-constexpr int L1Q_PROBE_Q = 64, L1Q_PROBE_E = 1024;
-constexpr double L1Q_PROBE_FRAC = 0.01;  // undecided fraction of the sample above which 16-bit codes
+// 512 queries x 256 entities: the undecided pairs concentrate on a few queries (C2: a sample of
+// 64 queries read 0.19 % where the whole evaluation has 0.38 %), so many queries, short windows.
+// The threshold: where the 8-bit sweep's rescoring stops paying. Spread over every query tile
+// (C2 at N = 1, 0.38 %) the rescoring overlaps the other waves' sums and 8-bit wins (1.32 vs
+// 1.62 ms); concentrated in a rank's share of a few relations it does not: 8-way C2 shares at
+// 0.77 % / 1.18 % took 0.32 / 0.51 ms against 0.26 ms with 16-bit codes (profiles/r4).
+constexpr int L1Q_PROBE_Q = 512, L1Q_PROBE_E = 256;
+constexpr double L1Q_PROBE_FRAC = 0.006;  // undecided fraction of the sample above which 16-bit codes
 __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ uq, int64_t q_pad, int64_t n_query,
                                                    const uint32_t* __restrict__ ue, int64_t e_pad, int64_t n_slice,
                                                    int kw, int kt, const float* __restrict__ thr, int pred_kind,
@@ -1780,7 +1786,7 @@ __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ 
   const PredSel<-1> pred(pred_kind, margin);
   const int64_t q = (int64_t)blockIdx.x * n_query / gridDim.x;
   const int64_t span = n_slice > L1Q_PROBE_E ? n_slice - L1Q_PROBE_E : 0;
-  const int64_t c = (((int64_t)blockIdx.x * span / gridDim.x) & ~(int64_t)3) + 4 * threadIdx.x;
+  const int64_t c = (((int64_t)blockIdx.x * span / gridDim.x) & ~(int64_t)3) + 4 * threadIdx.x;  // 64 threads
   const float l1d = l1q_delta(work, 255.0f);
   const float l1f = (float)(kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
   const float l1c = __builtin_fmaf((float)kt * 1.03f, l1d, 0x1p-120f);
@@ -2575,7 +2581,7 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
     hipLaunchKernelGGL(k_l1q_quant<8>, dim3(1024, 2), dim3(256), 0, st, p8q, p8e, kp, k4, hdr, n_abs, n_elem, ratio, 0,
                        0u);
   if (bits == 0) {
-    hipLaunchKernelGGL(k_l1q_probe, dim3(L1Q_PROBE_Q), dim3(256), 0, st, vq, q_pad, n_query, ve + e_begin, e_pad,
+    hipLaunchKernelGGL(k_l1q_probe, dim3(L1Q_PROBE_Q), dim3(L1Q_PROBE_E / 4), 0, st, vq, q_pad, n_query, ve + e_begin, e_pad,
                        n_slice, k4, n_planes(MMRE_TRANSE_L1) * kp, d_truth, pred_kind, margin, hdr);
     const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
     const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);

@@ -143,8 +143,9 @@ def emulate(a):
             print(f"N=1: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms")
             continue
         worst = max(worst, ms)
+        fst = sw.filter_stats(bufs)
         print(f"rank {k - (1 if one is not None else 0)}: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms, "
-              f"sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms")
+              f"sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms, filter {fst}")
     ratio = f", N=1 / slowest = {one / worst:.2f}x" if one else ""
     print(f"{a.config} world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "
           f"slowest rank {worst:.3f} ms (+ all-gather + metric reduction){ratio}")
