@@ -360,11 +360,35 @@ struct L1Q {
   int kp_f;
   int kt;                  // floats per row (the canonical chain's length, padding rows are 0)
   const uint32_t* gate;    // gated launches: run only if *gate is the sweep's code-width word (L1Q_F32 for the f32 sweep)
+  const float* q_l1c;      // 8-bit codes, tight bound: per query row sum |eps_q| (upper bound); nullptr: uniform bound
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
   return m == 0.0f ? 0.0f : (m < INFINITY ? (2.0f * m) / levels : INFINITY);
 }
+// Integer thresholds of the L1 filter for one query row (prediction = the score): with a = delta
+// S_int, |S - a| <= l1f a + l1c, so S_int < x = (th - l1c) / (delta (1 + l1f)) gives S < th and
+// S_int >= y = (th + l1c) / (delta (1 - l1f)) gives S >= th; x, y shrunk / grown by 2^-18 against
+// the float rounding of their own computation. With the tight 8-bit bound the accumulator also
+// holds the entity's error offset o_e (its code row `words`: S_int + o_e), l1c is the query's own
+// error sum, and o_e >= sum |eps_e| / (delta (1 - l1f)): S_int + o_e < t_sure proves S < th and
+// S_int + o_e >= t_out + 2 o_max proves S >= th (o_max: the largest offset of the slice).
+__device__ __forceinline__ void l1_int_thresholds(float th, float l1c, float l1d, float l1f, uint32_t omax2,
+                                                  uint32_t& t_sure, uint32_t& t_span) {
+  uint32_t ts = 0u, to = 0xFFFFFFFFu;
+  if (l1d < INFINITY) {
+    const float x = (th - l1c) / (l1d * (1.0f + l1f)) * (1.0f - 0x1p-18f);
+    const float y = (th + l1c) / (l1d * (1.0f - l1f)) * (1.0f + 0x1p-18f);
+    ts = x > 0.0f ? (uint32_t)floorf(fminf(x, 0x1p31f)) : 0u;
+    to = y > 0.0f ? (uint32_t)ceilf(fminf(y, 0x1p31f)) : 0u;
+    // y <= 0 or NaN (a padding query row's -inf threshold, a NaN truth): no pair beats it, no
+    // band -- the offsets must not open one (a band there sent padding rows to the rescoring)
+    if (to != 0u) to = to + omax2 < to ? 0xFFFFFFFFu : to + omax2;
+  }
+  t_sure = ts;
+  t_span = to > ts ? to - ts : 0u;
+}
+
 __device__ __forceinline__ float l1_exact_rows(const float* __restrict__ q, const float* __restrict__ e, int kt) {
   const float4* q4 = reinterpret_cast<const float4*>(q);
   const float4* e4 = reinterpret_cast<const float4*>(e);
@@ -827,15 +851,12 @@ __device__ __forceinline__ void sweep_valu_body(
         // S < th and S_int >= y = (th + l1c) / (delta (1 - l1f)) gives S >= th; x, y are shrunk /
         // grown by 2^-18 against the float rounding of their own computation. Once per query
         // row and query tile, not per unit.
-        uint32_t t_sure = 0u, t_out = 0xFFFFFFFFu;
-        if (l1d < INFINITY) {
-          const float x = (th - l1c) / (l1d * (1.0f + l1f)) * (1.0f - 0x1p-18f);
-          const float y = (th + l1c) / (l1d * (1.0f - l1f)) * (1.0f + 0x1p-18f);
-          t_sure = x > 0.0f ? (uint32_t)floorf(fminf(x, 0x1p31f)) : 0u;
-          t_out = y > 0.0f ? (uint32_t)ceilf(fminf(y, 0x1p31f)) : 0u;
-        }
+        uint32_t t_sure, t_span;
+        const bool tight = OP == 6 && l1.q_l1c != nullptr;
+        l1_int_thresholds(th, tight ? (v ? l1.q_l1c[q] : 0.0f) + 0x1p-120f : l1c, l1d, l1f, tight ? 2u * l1.hdr[3] : 0u,
+                          t_sure, t_span);
         sm.s_ts[slot][tid] = t_sure;
-        sm.s_tw[slot][tid] = t_out > t_sure ? t_out - t_sure : 0u;
+        sm.s_tw[slot][tid] = t_span;
       }
       if constexpr (TC) {
         s_rel[slot][tid] = v ? (int32_t)qr[q] : 0;
@@ -904,6 +925,7 @@ __device__ __forceinline__ void sweep_valu_body(
   auto rescore = [&](int2 p) {
     const int64_t q = p.x;
     const int e = p.y;
+    if (q >= n_query) return;  // padding query rows never reach the list (no band); a guard
     const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
     if (pred(sx) < thr[q]) {
       atomicAdd(&counts[q], 1);
@@ -920,7 +942,9 @@ __device__ __forceinline__ void sweep_valu_body(
   uint32_t lo = 0xFFFFFFFFu;  // RotatE: min of the sqrt inputs' bits over this unit (see rot_mag)
   // L1 filter: the code rows actually used in the last stage (the plane is padded to whole
   // stages; 100 of 104 rows at d = 200: the pad rows' zeros are not swept)
-  const int kk_last = L1F ? ((((l1.kt + (OP == 6 ? 3 : 1)) >> (OP == 6 ? 2 : 1)) + 1) & ~1) - (nkc - 1) * KC : KC;
+  // (OP 6: the words of the k values + the entity error-offset row, l1q_quant8)
+  const int kk_last = L1F ? ((((l1.kt + (OP == 6 ? 3 : 1)) >> (OP == 6 ? 2 : 1)) + (OP == 6 ? 2 : 1)) & ~1) - (nkc - 1) * KC
+                          : KC;
   // the L1 filter's code-width word (L1Q_CODES8 / _CODES16 / _F32: which of the gated sweeps
   // counts), in flight with the stage
   const uint32_t fb_flag = L1F ? l1.hdr[1] : 0u;
@@ -1766,6 +1790,83 @@ __global__ __launch_bounds__(256) void k_l1q_quant(L1QPlane pq, L1QPlane pe, int
   }
 }
 
+// The 8-bit codes (mode 0: the fallback test first, then the code-width word = 8-bit), written
+// word row by word row like k_l1q_quant, plus one more row after the k values' words: with
+// TIGHT (prediction = the score, no type masks, kt <= 1984) each column's quantization error
+// sum E = sum_k |x_k - (delta code_k - M)| is reduced in the workgroup (32 columns x 8 row
+// groups); a query row stores its bound 1.01 E + kt 2^-20 M (float rounding of the map and the
+// sum) for the thresholds (q_l1c), an entity column stores o = ceil(bound / (delta (1 - l1f)))
+// as four bytes summing to o in that row, so the sweep's own v_sad_u8 adds o to every pair's sum
+// (the query's row is 0), and hdr[3] gets the slice's largest o. The pair's bound is then the
+// two rows' error sums -- about K delta / 2 -- instead of 1.03 K delta.
+template <bool TIGHT>
+__global__ __launch_bounds__(256) void k_l1q_quant8(L1QPlane pq, L1QPlane pe, int kp, int kw, int kt,
+                                                    uint32_t* __restrict__ work, int n_part, double n_elem,
+                                                    float ratio, float* __restrict__ q_l1c) {
+  const bool fb = l1q_fallback(work, n_part, n_elem, ratio);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) work[1] = fb ? L1Q_F32 : L1Q_CODES8;
+  if (fb) return;
+  const bool ent = blockIdx.y != 0;
+  const float* __restrict__ km = ent ? pe.km : pq.km;
+  const int64_t pad = ent ? pe.pad : pq.pad, c0 = ent ? pe.c0 : pq.c0, n = ent ? pe.n : pq.n;
+  uint32_t* __restrict__ out = ent ? pe.out : pq.out;
+  const float mx = __uint_as_float(*work);
+  const float inv = (mx > 0.0f && mx < INFINITY) ? 255.0f / (2.0f * mx) : 0.0f;
+  const float off = (mx < INFINITY) ? mx : 0.0f;
+  const float delta = (mx > 0.0f && mx < INFINITY) ? (2.0f * mx) / 255.0f : 0.0f;  // l1q_delta's
+  const float l1f = (float)(kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+  const int words = (kt + 3) >> 2;  // row `words`: the error offsets
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  __shared__ float s_err[8][32];
+  for (int64_t cb = (int64_t)blockIdx.x * 32; cb < n; cb += (int64_t)gridDim.x * 32) {  // uniform
+    const bool live = cb + cl < n;
+    const int64_t c = c0 + cb + cl;
+    float err = 0.0f;
+    for (int r = g; r < kw; r += 8) {
+      uint32_t word = 0u;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int k = 4 * r + h;
+        if (live && k < kp) {
+          const float x = km[(int64_t)k * pad + c];
+          float t = (x + off) * inv;
+          t = t == t ? fminf(fmaxf(t, 0.0f), 255.0f) : 0.0f;
+          const float code = rintf(t);
+          word |= (uint32_t)code << (8 * h);
+          if constexpr (TIGHT) err += fabsf(x - (code * delta - off));
+        }
+      }
+      if (live && !(TIGHT && r == words)) out[(int64_t)r * pad + c] = word;
+    }
+    if constexpr (TIGHT) {
+      s_err[g][cl] = err;
+      __syncthreads();
+      if (g == 0 && live) {
+        float e = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e += s_err[i][cl];
+        const float eb = __builtin_fmaf(e, 1.01f, (float)kt * 0x1p-20f * mx);
+        uint32_t wv = 0u;
+        if (!ent) {
+          q_l1c[c] = eb;
+        } else {
+          uint32_t o = delta > 0.0f ? (uint32_t)ceilf(fminf(eb / (delta * (1.0f - l1f)) * (1.0f + 0x1p-17f), 1020.0f))
+                                    : 0u;
+          if (o) atomicMax(work + 3, o);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t b = o < 255u ? o : 255u;
+            wv |= b << (8 * h);
+            o -= b;
+          }
+        }
+        out[(int64_t)words * pad + c] = wv;
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // The code-width probe (runs when the 8-bit codes were made): L1Q_PROBE_Q workgroups, each one
 // query column (evenly spaced over the queries) against L1Q_PROBE_E consecutive entity columns
 // of the slice (the start spread over the slice), scored with the 8-bit codes; the pairs inside
@@ -1781,7 +1882,8 @@ constexpr double L1Q_PROBE_FRAC = 0.006;  // undecided fraction of the sample ab
 __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ uq, int64_t q_pad, int64_t n_query,
                                                    const uint32_t* __restrict__ ue, int64_t e_pad, int64_t n_slice,
                                                    int kw, int kt, const float* __restrict__ thr, int pred_kind,
-                                                   float margin, uint32_t* __restrict__ work) {
+                                                   float margin, uint32_t* __restrict__ work,
+                                                   const float* __restrict__ q_l1c) {
   if (__builtin_amdgcn_readfirstlane(work[1]) != L1Q_CODES8) return;
   const PredSel<-1> pred(pred_kind, margin);
   const int64_t q = (int64_t)blockIdx.x * n_query / gridDim.x;
@@ -1804,6 +1906,12 @@ __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ 
   }
   const float th = thr[q];
   uint32_t und = 0u;
+  if (q_l1c != nullptr) {  // the tight bound (prediction = the score): the sweep's integer test
+    uint32_t t_sure, t_span;
+    l1_int_thresholds(th, q_l1c[q] + 0x1p-120f, l1d, l1f, 2u * work[3], t_sure, t_span);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) und += (uint32_t)((acc[j] - t_sure < t_span) & (c + j < n_slice));
+  } else
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float a = (float)acc[j] * l1d;
@@ -1839,7 +1947,8 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
 }
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
-static int l1q_rows8(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 3) / 4, KC); }
+// (+ 1: the entity error-offset row of the tight bound, k_l1q_quant8)
+static int l1q_rows8(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 3) / 4 + 1, KC); }
 
 // ------------------------------------------------- split-bf16 MFMA filter ---
 // DistMult / ComplEx count-only sweeps through a filter with exact rescoring, as the VALU
@@ -2530,7 +2639,7 @@ extern "C" int mmre_link_sweep(int model, int pred_kind, float margin, const flo
 
 extern "C" int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
   if (dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
-  return L1Q_HDR + 4 * (int64_t)(l1q_rows(dim) + l1q_rows8(dim)) * (e_pad + q_pad);
+  return L1Q_HDR + 4 * (int64_t)(l1q_rows(dim) + l1q_rows8(dim)) * (e_pad + q_pad) + 4 * q_pad;
 }
 
 extern "C" int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream) {
@@ -2559,6 +2668,7 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   uint32_t* ue = uq + (int64_t)k2 * q_pad;
   uint32_t* vq = ue + (int64_t)k2 * e_pad;              // 8-bit planes
   uint32_t* ve = vq + (int64_t)k4 * q_pad;
+  float* q_l1c = (float*)(ve + (int64_t)k4 * e_pad);     // tight bound: per query row error sums
   const int64_t e_cols = round_up(e_end, TE) - e_begin;  // the slice's whole tiles
   // fallback ratio M / mean|x| (MMRE_L1Q_RATIO: experiments; <= 0 forces the fallback)
   static const char* ratio_env = getenv("MMRE_L1Q_RATIO");
@@ -2577,12 +2687,23 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
                      kp, hdr);
   const L1QPlane p8q{d_q_km, q_pad, 0, q_pad, vq}, p8e{d_ent_km, e_pad, e_begin, e_cols, ve};
   const L1QPlane p16q{d_q_km, q_pad, 0, q_pad, uq}, p16e{d_ent_km, e_pad, e_begin, e_cols, ue};
-  if (bits != 16)
-    hipLaunchKernelGGL(k_l1q_quant<8>, dim3(1024, 2), dim3(256), 0, st, p8q, p8e, kp, k4, hdr, n_abs, n_elem, ratio, 0,
-                       0u);
+  // the tight per-pair bound (k_l1q_quant8): prediction = the score, no type masks (their sweep
+  // keeps the uniform bound), and error offsets that fit one code row (kt <= 1984);
+  // MMRE_L1_TIGHT=0 keeps the uniform bound (A/B)
+  const char* tight_env = getenv("MMRE_L1_TIGHT");
+  const int kt = n_planes(MMRE_TRANSE_L1) * kp;
+  const bool tight = pred_kind == 0 && d_type_head == nullptr && kt <= 1984 && !(tight_env && tight_env[0] == '0');
+  if (bits != 16) {
+    if (tight)
+      hipLaunchKernelGGL(k_l1q_quant8<true>, dim3(512, 2), dim3(256), 0, st, p8q, p8e, kp, k4, kt, hdr, n_abs, n_elem,
+                         ratio, q_l1c);
+    else
+      hipLaunchKernelGGL(k_l1q_quant8<false>, dim3(512, 2), dim3(256), 0, st, p8q, p8e, kp, k4, kt, hdr, n_abs, n_elem,
+                         ratio, q_l1c);
+  }
   if (bits == 0) {
     hipLaunchKernelGGL(k_l1q_probe, dim3(L1Q_PROBE_Q), dim3(L1Q_PROBE_E / 4), 0, st, vq, q_pad, n_query, ve + e_begin, e_pad,
-                       n_slice, k4, n_planes(MMRE_TRANSE_L1) * kp, d_truth, pred_kind, margin, hdr);
+                       n_slice, k4, kt, d_truth, pred_kind, margin, hdr, tight ? q_l1c : nullptr);
     const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
     const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);
     hipLaunchKernelGGL(k_l1q_quant<16>, dim3(1024, 2), dim3(256), 0, st, p16q, p16e, kp, k2, hdr, n_abs, n_elem, ratio,
@@ -2593,7 +2714,7 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   }
   MMRE_CHECK_LAUNCH();
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               n_planes(MMRE_TRANSE_L1) * kp, nullptr};
+               kt, nullptr, tight ? q_l1c : nullptr};
   const bool tc = d_type_head != nullptr;
   // the gated sweeps: the one the code-width word names counts, the others' workgroups leave
   if (bits != 16) {
