@@ -1822,7 +1822,8 @@ __global__ __launch_bounds__(256) void k_l1q_quant8(L1QPlane pq, L1QPlane pe, in
     const bool live = cb + cl < n;
     const int64_t c = c0 + cb + cl;
     float err = 0.0f;
-    for (int r = g; r < kw; r += 8) {
+#pragma unroll 4
+    for (int r = g; r < kw; r += 8) {  // 4 word rows' loads in flight per thread
       uint32_t word = 0u;
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
@@ -2695,10 +2696,10 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   const bool tight = pred_kind == 0 && d_type_head == nullptr && kt <= 1984 && !(tight_env && tight_env[0] == '0');
   if (bits != 16) {
     if (tight)
-      hipLaunchKernelGGL(k_l1q_quant8<true>, dim3(512, 2), dim3(256), 0, st, p8q, p8e, kp, k4, kt, hdr, n_abs, n_elem,
+      hipLaunchKernelGGL(k_l1q_quant8<true>, dim3(2048, 2), dim3(256), 0, st, p8q, p8e, kp, k4, kt, hdr, n_abs, n_elem,
                          ratio, q_l1c);
     else
-      hipLaunchKernelGGL(k_l1q_quant8<false>, dim3(512, 2), dim3(256), 0, st, p8q, p8e, kp, k4, kt, hdr, n_abs, n_elem,
+      hipLaunchKernelGGL(k_l1q_quant8<false>, dim3(2048, 2), dim3(256), 0, st, p8q, p8e, kp, k4, kt, hdr, n_abs, n_elem,
                          ratio, q_l1c);
   }
   if (bits == 0) {
