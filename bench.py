@@ -1061,6 +1061,27 @@ def _coll_dev(dist, dev):
     return dev if dist.get_backend() == "nccl" else torch.device("cpu")
 
 
+def _self_launch(n: int) -> int:
+    """`python bench.py --gpus N` (N > 1) without WORLD_SIZE: run this same command as N ranks of
+    one torch.distributed.run job (one process per GPU, rendezvous on 127.0.0.1, a free port) and
+    return its exit code. Called before any GPU call (counting devices does not initialise the
+    GPU on this image); exits non-zero when the node has fewer than N GPUs, unless the gloo
+    rehearsal (MMRE_BENCH_GLOO=1: every rank on cuda:0) was asked for."""
+    import socket
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < n and os.environ.get("MMRE_BENCH_GLOO") != "1":
+        print(f"bench.py: --gpus {n} but this node has {have} GPU(s); not measuring", file=sys.stderr)
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1091,15 +1112,21 @@ def main():
                          "the entity table (every query against 1/N of the entities, one all-reduce)")
     args = ap.parse_args()
 
-    from mmre.link import FilterIndex, ScoreSpec, rotate_phase_denom
-    from mmre.sharding import EntityShardedLinkEvaluation, ShardedLinkEvaluation
-    from mmre.workloads import structured_tables, synthetic_large, train_transe, zs_workload
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around this process: start the N ranks here, as fresh children under
+        # torch.distributed.run, before anything touches the GPU -- never a silent one-GPU run
+        sys.exit(_self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure a different GPU count",
+              file=sys.stderr)
+        sys.exit(2)
+
+    from mmre.link import FilterIndex, ScoreSpec, rotate_phase_denom
+    from mmre.sharding import EntityShardedLinkEvaluation, ShardedLinkEvaluation
+    from mmre.workloads import structured_tables, synthetic_large, train_transe, zs_workload
     # MMRE_BENCH_GLOO=1 rehearses the N > 1 path on a one-GPU box: every rank on cuda:0, gloo
     # collectives through host tensors (the driver's multi-GPU runs use RCCL, one rank per GPU)
     rehearse = world > 1 and os.environ.get("MMRE_BENCH_GLOO") == "1"

@@ -149,7 +149,7 @@ int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d
  * mmre_link_sweep / mmre_link_sweep_range (bit for bit; replaces the same Test.h:65-192 scan),
  * faster. The k-major planes are quantized over the largest |x| of both to 8-bit codes (four k
  * per dword, summed with one v_sad_u8 per four elements) or, when a fixed sample of pairs
- * scored with those codes leaves more than 1 % undecided, to 16-bit codes (v_sad_u16, two
+ * scored with those codes leaves more than 0.6 % undecided, to 16-bit codes (v_sad_u16, two
  * elements per instruction); the choice is made on the device (short launches on the stream,
  * no host round trip). Every pair the quantization error bound leaves on both sides of its
  * query's threshold is rescored with the canonical f32 chain from the row-major copies
@@ -164,7 +164,9 @@ int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
  * codes, 1 = the f32 fallback instead of the codes. The fallback is taken on the device when M
  * (the largest |x|) exceeds 128 x the mean |x| of the two planes -- one outlier value stretching
  * the code range, which would leave most pairs undecided -- or is not finite. Counts are the
- * same either way. */
+ * same either way. d_out[2] = undecided-list entries the rescoring refused because their query
+ * or entity id was out of range (a guard on the list's invariant: 0 unless the build is
+ * defective). d_out holds 3 uint64. */
 int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
 int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
                         int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,

@@ -253,6 +253,21 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
   }
 }
 
+// A value the compiler cannot see through: what is computed from it is computed where it is
+// used, not hoisted out of a loop into a register (or scratch) kept live across the loop.
+__device__ __forceinline__ int vgpr_opaque(int x) {
+  __asm__ volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t sgpr_opaque(uint32_t x) {
+  __asm__ volatile("" : "+s"(x));
+  return x;
+}
+__device__ __forceinline__ int sgpr_opaque(int x) {
+  __asm__ volatile("" : "+s"(x));
+  return x;
+}
+
 // ------------------------------------------------------------ score ops ----
 // OP: 0 TransE L1, 1 TransE L2, 2 RotatE, 3 DistMult, 4 ComplEx, 5 / 6 TransE L1 on 16-bit /
 // 8-bit codes (the integer filter; acc carries a uint32 in float bits). One k step.
@@ -361,6 +376,7 @@ struct L1Q {
   int kt;                  // floats per row (the canonical chain's length, padding rows are 0)
   const uint32_t* gate;    // gated launches: run only if *gate is the sweep's code-width word (L1Q_F32 for the f32 sweep)
   const float* q_l1c;      // 8-bit codes, tight bound: per query row sum |eps_q| (upper bound); nullptr: uniform bound
+  uint32_t* guard;         // hdr[4]: pairs the rescoring refused (query or entity id out of range; must stay 0)
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
@@ -411,6 +427,18 @@ __host__ __device__ inline int op_of_model(int model) {
 
 __device__ __forceinline__ bool type_bit(const uint32_t* __restrict__ mask, int64_t words, int64_t r, int64_t e) {
   return (mask[r * words + (e >> 5)] >> (e & 31)) & 1u;
+}
+// The type bits of a VALU-sweep thread's 8 entity columns for relation r: columns 0-3 are ids
+// e0 .. e0 + 3, columns 4-7 e0 + 64 .. e0 + 67 (e0 a multiple of 4: each group of four lies in
+// one 32-bit word); bit j = column j. Two loads per query row instead of one per pair, and no
+// per-pair branch (the per-pair `better && type_bit(...)` kept ~100 VGPRs of masks and
+// addresses live in the type-constrained sweeps: they spilled). Columns at or past e_end: 0.
+__device__ __forceinline__ uint32_t type_bits8(const uint32_t* __restrict__ mask, int64_t words, int64_t r, int e0,
+                                               int e_end) {
+  const uint32_t* row = mask + r * words;
+  const uint32_t lo = e0 < e_end ? (row[e0 >> 5] >> (e0 & 31)) & 15u : 0u;
+  const uint32_t hi = e0 + 64 < e_end ? (row[(e0 + 64) >> 5] >> (e0 & 31)) & 15u : 0u;
+  return lo | (hi << 4);
 }
 
 // Two scores of the query vector sq against entity rows e1 and e2 at once (two independent
@@ -838,7 +866,12 @@ __device__ __forceinline__ void sweep_valu_body(
     l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
   }
 
+  // load_meta and the count flush run once per query tile; what they compute from tid and the
+  // filter constants is recomputed there from opaque copies (vgpr_opaque / sgpr_opaque), not
+  // hoisted by the compiler into per-lane values kept live across the sweep (that kept ~21 of
+  // them in scratch: a scratch store of ~90 B per lane at every wave's start)
   auto load_meta = [&](int qtile, int slot) {
+    const int tid = vgpr_opaque(threadIdx.x);
     if (tid < TQ) {
       const int64_t q = (int64_t)qtile * TQ + tid;
       const bool v = q < n_query;
@@ -853,7 +886,11 @@ __device__ __forceinline__ void sweep_valu_body(
         // row and query tile, not per unit.
         uint32_t t_sure, t_span;
         const bool tight = OP == 6 && l1.q_l1c != nullptr;
-        l1_int_thresholds(th, tight ? (v ? l1.q_l1c[q] : 0.0f) + 0x1p-120f : l1c, l1d, l1f, tight ? 2u * l1.hdr[3] : 0u,
+        const int ktm = sgpr_opaque(l1.kt);
+        const float md = __uint_as_float(sgpr_opaque(__float_as_uint(l1d)));
+        const float mf = (float)(ktm + 4) * 0x1p-23f * (1.0f + 0x1p-8f);  // = l1f
+        const float mc = __builtin_fmaf((float)ktm * 1.03f, md, 0x1p-120f);  // = l1c
+        l1_int_thresholds(th, tight ? (v ? l1.q_l1c[q] : 0.0f) + 0x1p-120f : mc, md, mf, tight ? 2u * l1.hdr[3] : 0u,
                           t_sure, t_span);
         sm.s_ts[slot][tid] = t_sure;
         sm.s_tw[slot][tid] = t_span;
@@ -925,7 +962,14 @@ __device__ __forceinline__ void sweep_valu_body(
   auto rescore = [&](int2 p) {
     const int64_t q = p.x;
     const int e = p.y;
-    if (q >= n_query) return;  // padding query rows never reach the list (no band); a guard
+    // a guard on the list's invariant: every entry is a (query row, slice column) pair of the
+    // unit just swept, with q < n_query (padding query rows open no band) and 0 <= e < n_ent.
+    // A pair outside is counted in hdr[4] (mmre_link_l1q_stats, asserted 0 by the filter tests)
+    // and never reaches a row gather.
+    if ((uint64_t)q >= (uint64_t)n_query || (uint32_t)e >= (uint32_t)n_ent) {
+      if (l1.guard) atomicAdd(l1.guard, 1u);
+      return;
+    }
     const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
     if (pred(sx) < thr[q]) {
       atomicAdd(&counts[q], 1);
@@ -954,13 +998,14 @@ __device__ __forceinline__ void sweep_valu_body(
   __syncthreads();
   if (L1F && __builtin_amdgcn_readfirstlane(fb_flag) != (OP == 6 ? L1Q_CODES8 : L1Q_CODES16)) return;  // uniform
 
+  constexpr int KKU = 2;  // LDS rows of operands per inner-loop iteration
   int buf = 0;
   for (int unit = u0; unit < u1; ++unit) {
     for (int kc = 0; kc < nkc; ++kc) {
       const bool more = ld_unit < u1;
       if (more) gload();
       const int kk_n = (L1F && kc == nkc - 1) ? kk_last : KC;
-#pragma unroll 2
+#pragma unroll KKU
       for (int kk = 0; kk < kk_n; ++kk) {
         float4 a0 = sq[buf][0][kk][tq], a1 = sq[buf][0][kk][16 + tq];
         float4 x0 = se[buf][0][kk][te], x1 = se[buf][0][kk][16 + te];
@@ -1053,47 +1098,37 @@ __device__ __forceinline__ void sweep_valu_body(
 #pragma unroll
               for (int j = 0; j < 8; ++j) accp[i][j] = f32x2{0.0f, 0.0f};
           }
-          uint32_t unc[2] = {0u, 0u};  // undecided pairs, bit i * 8 + j (rows 0-3 / 4-7)
+          // undecided pairs: pair (i, j) is bit 31 - ((i & 3) * 8 + j) of unc[i >> 2] (rows 0-3 /
+          // 4-7; the whole-tile epilogue shifts the bits in, pair by pair)
+          uint32_t unc[2] = {0u, 0u};
           bool whole = false;
           if constexpr (L1F && PK == 0 && !TC) {
-            // L1 filter, a whole entity tile (every tile but the last, uniform): per pair one
-            // compare + carry-add for the count and one subtract + compare for the undecided
-            // band [t_sure, t_out), its wave-wide ballot OR-ed into one scalar mask. The count
-            // needs no truth test: the truth's S is th itself, which no pair below t_sure
-            // reaches (S_int < t_sure proves S < th). The per-pair bits of the rescoring loop
-            // are built only when a wave holds an undecided pair (~7 % of waves at C2), with
-            // the truth excluded there.
+            // L1 filter, a whole entity tile (every tile but the last, uniform), ONE pass: per
+            // pair d = S_int - t_sure (its borrow, S_int < t_sure, carry-added to the count) and
+            // the undecided band d < t_out - t_sure carry-shifted into the pair's bit: four VALU
+            // per pair (v_sub_co, v_addc, v_cmp, v_addc). The count needs no truth test: the
+            // truth's S is th itself, which no pair below t_sure reaches (S_int < t_sure proves
+            // S < th). The truth's own pair is in the band; the rescoring list skips it. (A first
+            // pass with a wave-wide "any" ballot and the per-pair bits rebuilt when it was set
+            // paid ~420 more VALU per wave and unit: at C2 nearly every wave holds an undecided
+            // pair in every unit -- a quarter of them hold a truth.)
             if (ebase + TE <= n_ent) {
               whole = true;
-              const int32_t ecol = (int32_t)(e_base + ebase) + te * 4;  // entity id of column 0
-              uint64_t any = 0;
 #pragma unroll
               for (int i = 0; i < 8; ++i) {
                 const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
                 const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
                 int c = 0;
+                uint32_t u = unc[i >> 2];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                   const uint32_t si = __float_as_uint(acc[i][j]);
+                  const uint32_t d = si - t_sure;
                   c += si < t_sure;
-                  any |= __ballot(si - t_sure < t_span);
+                  u = u + u + (uint32_t)(d < t_span);
                 }
+                unc[i >> 2] = u;
                 s_cnt[0][i][tid] += c;
-              }
-              if (any) {  // rare: per-pair bits (thresholds re-read: no register held across)
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                  const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
-                  const uint32_t t_sure = *(volatile uint32_t*)&sm.s_ts[slot][ql];
-                  const uint32_t t_span = *(volatile uint32_t*)&sm.s_tw[slot][ql];
-                  const int32_t toff = *(volatile int32_t*)&s_true[slot][ql] - ecol;
-#pragma unroll
-                  for (int j = 0; j < 8; ++j) {
-                    const uint32_t si = __float_as_uint(acc[i][j]);
-                    const bool u = (si - t_sure < t_span) & (toff != ((j < 4) ? j : 60 + j));
-                    unc[i >> 2] |= (uint32_t)u << ((i & 3) * 8 + j);
-                  }
-                }
               }
             }
           }
@@ -1104,6 +1139,9 @@ __device__ __forceinline__ void sweep_valu_body(
             const float th = s_thr[slot][ql];
             const int32_t tr = s_true[slot][ql];
             int c = 0, cc = 0;
+            const uint32_t tb = TC ? type_bits8(s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail, type_words,
+                                                s_rel[slot][ql], (int)(e_base + ebase) + te * 4, (int)(e_base + n_ent))
+                                   : 0u;
             if constexpr (L1F && PK == 0) {
               // prediction = the score: the integer thresholds of load_meta
               const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
@@ -1115,11 +1153,8 @@ __device__ __forceinline__ void sweep_valu_body(
                 const bool sure = si < t_sure;
                 const bool better = sure & valid;
                 c += better;
-                if constexpr (TC) {
-                  const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                  cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
-                }
-                unc[i >> 2] |= (uint32_t)((si - t_sure < t_span) & valid) << ((i & 3) * 8 + j);
+                if constexpr (TC) cc += better & ((tb >> j) & 1u);
+                unc[i >> 2] |= (uint32_t)((si - t_sure < t_span) & valid) << (31 - ((i & 3) * 8 + j));
               }
               s_cnt[0][i][tid] += c;
               if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
@@ -1143,11 +1178,8 @@ __device__ __forceinline__ void sweep_valu_body(
               const bool out = (fin & (fminf(p1, p2) >= th)) | (th != th);
               const bool better = sure & valid;
               c += better;
-              if constexpr (TC) {
-                const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-                cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
-              }
-              unc[i >> 2] |= (uint32_t)(!sure & !out & valid) << ((i & 3) * 8 + j);
+              if constexpr (TC) cc += better & ((tb >> j) & 1u);
+              unc[i >> 2] |= (uint32_t)(!sure & !out & valid) << (31 - ((i & 3) * 8 + j));
             }
             s_cnt[0][i][tid] += c;
             if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
@@ -1157,18 +1189,25 @@ __device__ __forceinline__ void sweep_valu_body(
             const int lane = tid & 63;
             for (;;) {  // uniform: one undecided pair per lane and round into the list
               const bool has = (unc[0] | unc[1]) != 0u;
-              const uint64_t bal = __ballot(has);
-              if (bal == 0) break;
+              if (__ballot(has) == 0) break;
+              bool keep = false;
+              int2 pr = make_int2(0, 0);
               if (has) {
                 const int h = unc[0] ? 0 : 1;
-                const int b = __builtin_ctz(unc[h]);
-                unc[h] &= unc[h] - 1u;
-                const int i = h * 4 + (b >> 3), j = b & 7;
+                const int p = __builtin_clz(unc[h]);  // pair p = (i & 3) * 8 + j sits at bit 31 - p
+                unc[h] &= ~(0x80000000u >> p);
+                const int i = h * 4 + (p >> 3), j = p & 7;
                 const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
                 const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
+                keep = (int)(e + e_base) != s_true[slot][ql];  // the truth's own pair is not rescored
+                pr = make_int2((int)(q0 + ql), e);
+              }
+              const uint64_t bal = __ballot(keep);
+              if (keep) {
+                // list_n < 64 at the top of every round and a round appends <= 64: pos < 128
                 const int pos = list_n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                wl[pos] = make_int2((int)(q0 + ql), e);
+                wl[pos] = pr;
               }
               const int nb = __builtin_popcountll(bal);
               list_n += nb;
@@ -1183,9 +1222,9 @@ __device__ __forceinline__ void sweep_valu_body(
           for (int h = 0; h < 2; ++h) {
             uint32_t m = LIST ? 0u : unc[h];  // (the L1 filter's pairs went to the wave's list)
             while (m) {  // rare: exact rescoring, one pair at a time
-              const int b = __builtin_ctz(m);
-              m &= m - 1u;
-              const int i = h * 4 + (b >> 3), j = b & 7;
+              const int p = __builtin_clz(m);
+              m &= ~(0x80000000u >> p);
+              const int i = h * 4 + (p >> 3), j = p & 7;
               const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
               const int e = (int)ebase + ((j < 4) ? te * 4 + j : 64 + te * 4 + (j - 4));
               float sx;
@@ -1249,6 +1288,9 @@ __device__ __forceinline__ void sweep_valu_body(
           const float th = s_thr[slot][ql];
           const int32_t tr = s_true[slot][ql];
           int c = 0, cc = 0;
+          const uint32_t tb = TC ? type_bits8(s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail, type_words,
+                                              s_rel[slot][ql], (int)(e_base + ebase) + te * 4, (int)(e_base + n_ent))
+                                 : 0u;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             // 32-bit ids (int32 by check_link_args); bitwise &: no per-pair branch
@@ -1256,10 +1298,7 @@ __device__ __forceinline__ void sweep_valu_body(
             const float v = pred(op_final<OP>(acc[i][j]));
             const bool better = (v < th) & (e + e_base != tr) & (e < n_ent);
             c += better;
-            if constexpr (TC) {
-              const uint32_t* m = s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail;
-              cc += better && type_bit(m, type_words, s_rel[slot][ql], e + e_base);
-            }
+            if constexpr (TC) cc += better & ((tb >> j) & 1u);
             if constexpr (STORE) {
               if (q0 + ql < n_query && e < n_ent) scores[(q0 + ql) * n_ent + e] = v;
             }
@@ -1273,6 +1312,8 @@ __device__ __forceinline__ void sweep_valu_body(
         int next_qt = cur_qt, next_et = cur_et;
         if (!last) um.at(unit + 1, next_qt, next_et);
         if (last || next_qt != cur_qt) {  // uniform: flush this query tile's counts
+          const int tid = vgpr_opaque(threadIdx.x);  // (see load_meta)
+          const int tq = tid >> 4, te = tid & 15;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             int c = s_cnt[0][i][tid], cc = TC ? s_cnt[TC ? 1 : 0][i][tid] : 0;
@@ -1936,7 +1977,8 @@ __global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ p, in
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
 }
 
-// Sum of the undecided-pair slots and the code-width word -> out[0], out[1] (mmre_link_l1q_stats).
+// Sum of the undecided-pair slots, the code-width word and the rescoring guard's count -> out[0..2]
+// (mmre_link_l1q_stats).
 __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
   const unsigned long long* sl =
@@ -1945,6 +1987,7 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
   for (int i = 0; i < L1Q_SLOTS; ++i) t += *reinterpret_cast<const uint32_t*>(sl + i * L1Q_SLOT_STRIDE);
   out[0] = t;
   out[1] = work[1];
+  out[2] = work[4];
 }
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
@@ -2355,7 +2398,8 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
   constexpr int fast = (OP == 2) ? 3 : 0;  // RotatE -(m - s), TransE s
   if constexpr (OP == 5 || OP == 6) {  // the integer filter: count-only sweeps
     if (store) return MMRE_ERR_ARG;
-    if (tc) MMRE_LV1(true, false, -1);
+    if (tc && pk == fast) MMRE_LV1(true, false, fast);  // integer thresholds (prediction = the score)
+    else if (tc) MMRE_LV1(true, false, -1);
     else if (pk == fast) MMRE_LV1(false, false, fast);
     else MMRE_LV1(false, false, -1);
   } else {
@@ -2715,7 +2759,7 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   }
   MMRE_CHECK_LAUNCH();
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               kt, nullptr, tight ? q_l1c : nullptr};
+               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4};
   const bool tc = d_type_head != nullptr;
   // the gated sweeps: the one the code-width word names counts, the others' workgroups leave
   if (bits != 16) {

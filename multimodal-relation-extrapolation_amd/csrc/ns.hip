@@ -2224,7 +2224,13 @@ extern "C" int64_t mmre_rows_backward_workspace(int model, int64_t n_rows, int64
   return w.total;
 }
 
-static int gen_nc_rows(int dim) { return dim <= 64 ? 1 : dim <= 128 ? 2 : dim <= 256 ? 4 : dim <= 512 ? 8 : 0; }
+// 64-float chunks per lane of the rows backward's slot / owner kernels. Up to 2,048 floats per
+// row plane (the reference's examples train TransE at dim 1,024 with SigmoidLoss and cross
+// sampling, OpenKE/examples/train_transe_WN18_adv_sigmoidloss.py): the wide instances keep
+// their rows in more registers (they may spill at NC 32; these rows are not a hot shape).
+static int gen_nc_rows(int dim) {
+  return dim <= 64 ? 1 : dim <= 128 ? 2 : dim <= 256 ? 4 : dim <= 512 ? 8 : dim <= 1024 ? 16 : dim <= 2048 ? 32 : 0;
+}
 
 // coefficients in w.coef already (or to be read from d_coef): slots, then the owner pass
 static int rows_backward_impl(const NSArgs& A, const float* d_coef, int64_t n_rows, int64_t n_ent, int64_t n_rel,
@@ -2252,7 +2258,9 @@ static int rows_backward_impl(const NSArgs& A, const float* d_coef, int64_t n_ro
   if (nc == 1) MMRE_ROWS(1);
   else if (nc == 2) MMRE_ROWS(2);
   else if (nc == 4) MMRE_ROWS(4);
-  else MMRE_ROWS(8);
+  else if (nc == 8) MMRE_ROWS(8);
+  else if (nc == 16) MMRE_ROWS(16);
+  else MMRE_ROWS(32);
 #undef MMRE_ROWS
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;

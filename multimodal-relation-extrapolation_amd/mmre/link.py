@@ -315,18 +315,20 @@ class LinkSweep:
         """The integer filter's record of the last run() on `buffers` (mmre_link_l1q_stats):
         dict(undecided=pairs rescored with the canonical chain, fallback=True if the sweep ran
         the f32 path because the codes were too coarse, bits=8 | 16 the code width the sweep
-        used -- None on the fallback), or None if that run did not use the filter (not TransE
+        used -- None on the fallback, guarded=list entries refused by the rescoring's range guard,
+        always 0), or None if that run did not use the filter (not TransE
         L1, score-storing, MMRE_L1_FILTER=0). Synchronises the stream."""
         if not buffers.get("l1q_used"):
             return None
         wk = buffers["l1q_work"]
         out = buffers.get("l1q_stats")
         if out is None:
-            out = buffers["l1q_stats"] = torch.zeros(2, dtype=torch.int64, device=self.device)
+            out = buffers["l1q_stats"] = torch.zeros(3, dtype=torch.int64, device=self.device)
         call("mmre_link_l1q_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
-        u, w = (int(x) for x in out.cpu())
-        # the code-width word: 0 = 8-bit codes, 1 = the f32 fallback, 2 = 16-bit codes
-        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w))
+        u, w, g = (int(x) for x in out.cpu())
+        # the code-width word: 0 = 8-bit codes, 1 = the f32 fallback, 2 = 16-bit codes; guarded =
+        # undecided-list entries the rescoring refused as out of range (0 unless a defect)
+        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g)
 
 
 def _rows_view(c):

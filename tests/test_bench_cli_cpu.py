@@ -1,0 +1,35 @@
+"""bench.py's GPU-count contract: `--gpus N` with N > 1 either
+launches N ranks itself (torch.distributed.run, before any GPU call) or exits non-zero -- it
+never measures one GPU under an N-GPU label. On this CPU-only container there are no GPUs, so
+the self-launch must refuse; a WORLD_SIZE that disagrees with --gpus must refuse too."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MMRE_BENCH_GLOO")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                          env=env, timeout=300, cwd=REPO)
+
+
+def test_gpus_n_without_launcher_refuses_when_the_node_lacks_gpus():
+    import torch
+    if torch.cuda.device_count() >= 2:
+        return  # a GPU node would launch the ranks for real; the contract is checked on CPU hosts
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {})
+    assert r.returncode == 2, (r.returncode, r.stderr[-500:])
+    assert "not measuring" in r.stderr
+    assert r.stdout.strip() == ""   # no JSON line
+
+
+def test_world_size_mismatch_refuses():
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2, (r.returncode, r.stderr[-500:])
+    assert "refusing" in r.stderr
+    assert r.stdout.strip() == ""

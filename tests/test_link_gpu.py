@@ -53,11 +53,17 @@ def _run(spec, qh, qr, qt, qm, index=None, tc=False, scores=True, grouped=True, 
         filt = tuple(torch.from_numpy(a).to(dev) for a in lists)
         if tc:
             masks = tuple(torch.from_numpy(m).to(dev) for m in index.type_masks())
-    res = LinkSweep(spec).run(*(torch.from_numpy(np.asarray(x, np.int64)).to(dev) for x in (qh, qr, qt)),
-                              torch.from_numpy(np.asarray(qm, np.int8)).to(dev), filt=filt, type_masks=masks,
-                              return_scores=scores, q_rows=q_rows)
+    sw = LinkSweep(spec)
+    bufs = sw.alloc_queries(len(qh))
+    res = sw.run(*(torch.from_numpy(np.asarray(x, np.int64)).to(dev) for x in (qh, qr, qt)),
+                 torch.from_numpy(np.asarray(qm, np.int8)).to(dev), filt=filt, type_masks=masks,
+                 return_scores=scores, q_rows=q_rows, buffers=bufs)
     torch.cuda.synchronize()
     out = {k: (v.cpu().numpy() if v is not None else None) for k, v in res.items()}
+    st = sw.l1q_stats(bufs)
+    if st is not None:  # the rescoring's range guard never fires
+        assert st["guarded"] == 0, st
+    out["l1q"] = st
     return out
 
 

@@ -69,6 +69,7 @@ def test_reference_ranks_full_size(config, golden):
         print(f"{config}: L1 filter ({st['bits']}-bit codes) left {st['undecided']} of {2 * n * E} pairs undecided "
               f"({frac:.2e}), all rescored")
         assert st["bits"] == 8, st   # trained tables: the probe keeps the 8-bit codes
+        assert st["guarded"] == 0, st  # no undecided-list entry outside the query / slice range
         assert frac < 1e-2, frac
     # the GPU's own scores of the truth and of every listed near entity (score-storing sweep)
     qm = np.r_[np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)]

@@ -150,7 +150,9 @@ def _c2_eval(w, dev, norm_flag):
             sw.run(*args, filt=filt, buffers=bufs, sweep_events=ev)
             torch.cuda.synchronize()
             ts.append(ev[0].elapsed_time(ev[1]))
-        return bufs["counts"].cpu().numpy().copy(), float(np.median(ts)), sw.l1q_stats(bufs)
+        st = sw.l1q_stats(bufs)
+        assert st is None or st["guarded"] == 0, st
+        return bufs["counts"].cpu().numpy().copy(), float(np.median(ts)), st
     return sw, run
 
 
