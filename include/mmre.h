@@ -166,13 +166,37 @@ int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
  * the code range, which would leave most pairs undecided -- or is not finite. Counts are the
  * same either way. d_out[2] = undecided-list entries the rescoring refused because their query
  * or entity id was out of range (a guard on the list's invariant: 0 unless the build is
- * defective). d_out holds 3 uint64. */
+ * defective), d_out[3] = the largest per-entity error offset of the 8-bit codes' tight bound (in
+ * code steps; 0 with the uniform bound). d_out holds 4 uint64. */
 int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
 int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
                         int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,
                         const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode, int64_t n_query,
                         int64_t q_pad, int dim, const uint32_t* d_type_head, const uint32_t* d_type_tail,
                         int32_t* d_counts, const float* d_truth, void* d_work, int64_t work_bytes, void* stream);
+
+/* The whole count-only TransE L1 link-prediction evaluation of a query set in ONE call (prediction
+ * = the score, filter groups, no type constraints) -- what mmre_link_prepare_entities +
+ * mmre_link_prepare_queries + mmre_link_truth_grouped + mmre_link_sweep_l1q compute, with the same
+ * outputs bit for bit (the entity / query planes and rows, q_true, truth scores, counts), in
+ * seven launches instead of thirteen: query blocks normalise their own anchor and truth rows
+ * from the raw table (no wait on the entity prep), the truth scores ride on the query prep,
+ * list scores share a launch with the quantization, filter counts with the code-width probe.
+ * Replaces Tester.run_link_prediction's loop (Tester.py:70-91: getHeadBatch/getTailBatch
+ * Test.h:36-53, TransE.predict TransE.py:104-110, testHead/testTail Test.h:65-192) for TransE.
+ * d_ent / d_rel: the raw tables (n_ent x dim, n_rel x dim); norm_flag as TransE's. Filter
+ * groups as for mmre_link_truth_grouped (FilterIndex.groups; restricted to [e_begin, e_end)
+ * for an entity slice). d_work: mmre_link_evaluate_l1q_workspace(dim, e_pad, q_pad) bytes,
+ * ZEROED before the first call (it holds grid tickets; every call leaves them zero). */
+int64_t mmre_link_evaluate_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
+int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t n_ent, const float* d_rel, int64_t n_rel,
+                           int dim, const int64_t* d_qh, const int64_t* d_qr, const int64_t* d_qt,
+                           const int8_t* d_qmode, int64_t n_query, const int64_t* d_grp_qoff, const int32_t* d_grp_q,
+                           int64_t n_groups, const int64_t* d_filt_off, const int32_t* d_filt_ids,
+                           const int32_t* d_entry_q, int64_t n_entries, int64_t e_begin, int64_t e_end,
+                           float* d_ent_km, int64_t e_pad, float* d_ent_rows, float* d_q_km, int64_t q_pad,
+                           float* d_q_rows, int32_t* d_q_true, float* d_list_scores, int32_t* d_counts,
+                           float* d_truth, void* d_work, int64_t work_bytes, void* stream);
 
 /* DistMult / ComplEx (MMRE_DISTMULT, MMRE_COMPLEX) count-only sweep through a split-bf16 MFMA
  * filter: same counts as mmre_link_sweep / mmre_link_sweep_range without type constraints (bit

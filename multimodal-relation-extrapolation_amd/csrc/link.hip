@@ -1892,6 +1892,11 @@ __global__ __launch_bounds__(256) void k_l1q_quant8(L1QPlane pq, L1QPlane pe, in
         if (!ent) {
           q_l1c[c] = eb;
         } else {
+          // o <= 1020 (four bytes of 255) without the clamp ever acting: each element's code error
+          // is at most delta / 2 (rounding to nearest; |x| <= M, so no value is clipped) plus the
+          // float rounding of the map, so E <= kt delta / 2 (1 + 2^-20) and o <= 1.01 kt / 2 (1 +
+          // 2^-16) + kt 2^-20 M / delta + 1 <= 0.506 kt + 1 = 1,005 at the host guard kt <= 1,984
+          // (tests/test_sweep_filters_gpu.py::test_l1_tight_offsets_at_kt_1984 reads the largest o)
           uint32_t o = delta > 0.0f ? (uint32_t)ceilf(fminf(eb / (delta * (1.0f - l1f)) * (1.0f + 0x1p-17f), 1020.0f))
                                     : 0u;
           if (o) atomicMax(work + 3, o);
@@ -1977,8 +1982,8 @@ __global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ p, in
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
 }
 
-// Sum of the undecided-pair slots, the code-width word and the rescoring guard's count -> out[0..2]
-// (mmre_link_l1q_stats).
+// Sum of the undecided-pair slots, the code-width word, the rescoring guard's count and the largest
+// error offset of the tight bound -> out[0..3] (mmre_link_l1q_stats).
 __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
   const unsigned long long* sl =
@@ -1988,6 +1993,7 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
   out[0] = t;
   out[1] = work[1];
   out[2] = work[4];
+  out[3] = work[3];
 }
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
@@ -2412,6 +2418,538 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
 #undef MMRE_LV1
   MMRE_CHECK_LAUNCH();
   return finalize ? launch_finalize(st, counts, n_query, tc) : MMRE_OK;
+}
+
+// ------------------------------------------ fused TransE L1 evaluation (round 5) ---
+// mmre_link_evaluate_l1q: the whole count-only TransE L1 evaluation of a query set -- entity
+// prep, query prep, truth scores, filter-list scores and counts, the L1 filter's quantization
+// and code-width probe, the sweep -- in seven launches instead of thirteen, with what is
+// independent fused into the same launch (block ranges of one grid doing different work):
+//   K1 k_eval_prep        entity rows (normalised, k-major + row-major) | query rows, each
+//                         query block normalising its own anchor and truth rows from the raw
+//                         table (no dependency on the entity blocks), the truth scores, and
+//                         per block max |x| / sum |x| of the planes; the last block (ticket)
+//                         reduces them to M, decides codes vs the f32 fallback, zeroes the
+//                         filter header
+//   K2 k_eval_quant_list  filter-list scores | 8-bit codes + the tight bound's error sums +
+//                         16-bit codes, one read of the planes
+//   K3 k_eval_count_probe filter counts per group | the code-width probe (last probe block
+//                         decides 8 vs 16 bits)
+//   K4-K6                 the three gated sweeps (8-bit, 16-bit, f32; the code-width word
+//                         names the one that counts), then k_counts_finalize
+// Values are bit-identical to the separate path (same canonical chains in the same order):
+// tests/test_eval_fused_gpu.py holds counts, truths and planes equal.
+struct EvalL1 {
+  const float* ent;      // raw entity table (n_ent, dim)
+  const float* rel;      // raw relation table (n_rel, dim)
+  int64_t n_ent;
+  int dim, kp, norm, rb;
+  const int64_t* qh;
+  const int64_t* qr;
+  const int64_t* qt;
+  const int8_t* qmode;
+  int64_t n_query;
+  float* ent_km;
+  int64_t e_pad;
+  float* ent_rows;
+  float* q_km;
+  int64_t q_pad;
+  float* q_rows;
+  int32_t* q_true;
+  float* truth;
+  int64_t e_begin, e_cols;  // the swept slice (its columns feed M)
+  int n_eblk, n_qblk;
+  float* pstat;             // per K1 block: max |x|, sum |x| (2 floats)
+  uint32_t* ticket;         // [0] K1's, [1] the probe's
+  uint32_t* hdr;            // the L1 filter header
+  double n_elem;
+  float ratio;
+};
+
+// canonical sum of squares over x[0..dim) (k ascending, LDS reads batched 16 per round) and
+// F.normalize's clamp: the divisor k_prep_rows uses
+__device__ __forceinline__ float canon_norm(const float* x, int dim) {
+  float ss = 0.0f;
+  int k = 0;
+  for (; k + 16 <= dim; k += 16) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = x[k + u];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) ss = ss + v[u] * v[u];
+  }
+  for (; k < dim; ++k) ss = ss + x[k] * x[k];
+  const float nr = sqrtf(ss);
+  return nr < 1e-12f ? 1e-12f : nr;
+}
+
+__device__ __forceinline__ void abs_stat(float v, float& mx, float& sa) {
+  if (!(v - v == 0.0f)) mx = INFINITY;  // inf / NaN: no codes (the f32 sweep counts)
+  else {
+    mx = fmaxf(mx, fabsf(v));
+    sa += fabsf(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
+  extern __shared__ float lds[];
+  __shared__ float s_nrm[64];
+  __shared__ int64_t s_a[32], s_t[32], s_r[32];
+  __shared__ int s_head[32];
+  __shared__ float s_rn[32];
+  __shared__ float s_m[4], s_s[4];
+  __shared__ uint32_t s_last;
+  const int kp = P.kp, kt = kp, ls = kt + 1, rb = P.rb, dim = P.dim;
+  const int tid = threadIdx.x, lane = tid & 31, slot = tid >> 5;
+  float mx = 0.0f, sa = 0.0f;
+  if ((int)blockIdx.x < P.n_eblk) {  // ---- entity rows (k_prep_rows for TransE)
+    const int64_t e0 = (int64_t)blockIdx.x * rb;
+    for (int i = slot; i < rb; i += 8) {
+      const int64_t e = e0 + i;
+      float* x = lds + i * ls;
+#pragma unroll 4
+      for (int k = lane; k < kt; k += 32) x[k] = (e < P.n_ent && k < dim) ? P.ent[e * dim + k] : 0.0f;
+    }
+    __syncthreads();
+    if (P.norm) {
+      if (tid < rb) s_nrm[tid] = canon_norm(lds + tid * ls, dim);
+      __syncthreads();
+      for (int i = slot; i < rb; i += 8) {
+        float* x = lds + i * ls;
+        const float nr = s_nrm[i];
+        for (int k = lane; k < kt; k += 32) x[k] = x[k] / nr;
+      }
+      __syncthreads();
+    }
+    const bool in_slice = e0 >= P.e_begin && e0 < P.e_begin + P.e_cols;
+    for (int i = slot; i < rb; i += 8) {
+      const int64_t e = e0 + i;
+      const float* x = lds + i * ls;
+      if (e < P.n_ent) {
+#pragma unroll 4
+        for (int k = lane; k < kt; k += 32) P.ent_rows[e * kt + k] = x[k];
+      }
+      if (in_slice && e < P.e_pad)
+        for (int k = lane; k < kt; k += 32) abs_stat(x[k], mx, sa);
+    }
+    write_k_major(lds, ls, rb, kt, P.ent_km, P.e_pad, e0);
+  } else {  // ---- query rows: q = h + r (tail) / -(r - t) (head), and the truth scores
+    const int64_t q0 = (int64_t)(blockIdx.x - P.n_eblk) * rb;
+    float* y0 = lds + rb * ls;  // the truth rows
+    if (tid < rb) {
+      const int64_t q = q0 + tid;
+      int64_t a = -1, tr = -1, r = 0;
+      int head = 0;
+      if (q < P.n_query) {
+        head = P.qmode[q] == MMRE_HEAD_BATCH;
+        a = head ? P.qt[q] : P.qh[q];
+        tr = head ? P.qh[q] : P.qt[q];
+        r = P.qr[q];
+        P.q_true[q] = (int32_t)tr;
+      }
+      s_a[tid] = a;
+      s_t[tid] = tr;
+      s_r[tid] = r;
+      s_head[tid] = head;
+      if (P.norm) {  // the relation row's norm, k_prep_queries' canonical order
+        const float* rp = P.rel + r * dim;
+        float ss = 0.0f;
+        int k = 0;
+        if ((dim & 3) == 0) {
+          for (; k + 64 <= dim; k += 64) {
+            float4 v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = reinterpret_cast<const float4*>(rp + k)[u];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              ss = ss + v[u].x * v[u].x;
+              ss = ss + v[u].y * v[u].y;
+              ss = ss + v[u].z * v[u].z;
+              ss = ss + v[u].w * v[u].w;
+            }
+          }
+        }
+        for (; k + 16 <= dim; k += 16) {
+          float v[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) v[u] = rp[k + u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) ss = ss + v[u] * v[u];
+        }
+        for (; k < dim; ++k) ss = ss + rp[k] * rp[k];
+        const float nr = sqrtf(ss);
+        s_rn[tid] = nr < 1e-12f ? 1e-12f : nr;
+      }
+    }
+    __syncthreads();
+    for (int i = slot; i < rb; i += 8) {
+      const int64_t a = s_a[i], tr = s_t[i];
+      float* x = lds + i * ls;
+      float* y = y0 + i * ls;
+#pragma unroll 4
+      for (int k = lane; k < kt; k += 32) {
+        x[k] = (a >= 0 && k < dim) ? P.ent[a * dim + k] : 0.0f;
+        y[k] = (tr >= 0 && k < dim) ? P.ent[tr * dim + k] : 0.0f;
+      }
+    }
+    __syncthreads();
+    if (P.norm) {  // the anchor and truth rows normalised exactly as k_prep_rows does
+      if (tid < 2 * rb) s_nrm[tid] = canon_norm(lds + tid * ls, dim);  // rows 0..rb-1: x, rb..2rb-1: y
+      __syncthreads();
+      for (int i = slot; i < 2 * rb; i += 8) {
+        float* x = lds + i * ls;
+        const float nr = s_nrm[i];
+        for (int k = lane; k < kt; k += 32) x[k] = x[k] / nr;
+      }
+      __syncthreads();
+    }
+    for (int i = slot; i < rb; i += 8) {
+      float* x = lds + i * ls;
+      const bool valid = s_a[i] >= 0;
+      const int64_t r = s_r[i];
+      const bool head = s_head[i];
+      for (int k = lane; k < kp; k += 32) {
+        if (!valid || k >= dim) {
+          x[k] = 0.0f;
+          continue;
+        }
+        // head_batch: score = h + (r - t) -> q = -(r - t); tail_batch: (h + r) - t -> q = h + r
+        const float b = P.norm ? P.rel[r * dim + k] / s_rn[i] : P.rel[r * dim + k];
+        x[k] = head ? -(b - x[k]) : (x[k] + b);
+      }
+    }
+    __syncthreads();
+    if (tid < rb && q0 + tid < P.n_query) {  // the truth's score: the canonical chain, k ascending
+      const float* x = lds + tid * ls;
+      const float* y = y0 + tid * ls;
+      float acc = 0.0f;
+      int k = 0;
+      for (; k + 8 <= kp; k += 8) {
+        float a[8], b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          a[u] = x[k + u];
+          b[u] = y[k + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + fabsf(a[u] - b[u]);
+      }
+      for (; k < kp; ++k) acc = acc + fabsf(x[k] - y[k]);
+      P.truth[q0 + tid] = acc;  // prediction = the score (TransE.py:104-110)
+    }
+    write_k_major(lds, ls, rb, kt, P.q_km, P.q_pad, q0);
+    for (int i = slot; i < rb; i += 8) {
+      const int64_t q = q0 + i;
+      const float* x = lds + i * ls;
+      if (q < P.n_query) {
+#pragma unroll 4
+        for (int k = lane; k < kt; k += 32) P.q_rows[q * kt + k] = x[k];
+      }
+      if (q < P.q_pad)
+        for (int k = lane; k < kt; k += 32) abs_stat(x[k], mx, sa);
+    }
+  }
+  // ---- the block's |x| statistics, then the last block's reduction (ticket)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o));
+    sa += __shfl_xor(sa, o);
+  }
+  if ((tid & 63) == 0) {
+    s_m[tid >> 6] = mx;
+    s_s[tid >> 6] = sa;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    P.pstat[2 * blockIdx.x] = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    P.pstat[2 * blockIdx.x + 1] = (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]);
+    __threadfence();  // release the partial before the ticket
+    s_last = atomicAdd(&P.ticket[0], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // acquire every block's partial
+  const int nb = (int)gridDim.x;
+  float m = 0.0f, s = 0.0f;
+  for (int b = tid; b < nb; b += 256) {  // fixed order per thread, fixed tree below: deterministic
+    m = fmaxf(m, __hip_atomic_load(&P.pstat[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    s += __hip_atomic_load(&P.pstat[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    m = fmaxf(m, __shfl_xor(m, o));
+    s += __shfl_xor(s, o);
+  }
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    s_m[tid >> 6] = m;
+    s_s[tid >> 6] = s;
+  }
+  __syncthreads();
+  // zero the rest of the header (probe count, largest offset, guard, undecided slots)
+  for (int i = 2 + tid; i < L1Q_PART / 4; i += 256) P.hdr[i] = 0u;
+  if (tid == 0) {
+    const float M = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    const float sum = (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]);
+    // the fallback test of l1q_fallback: M non-finite, or M > ratio x mean |x|
+    const bool fb = !(M < INFINITY) || (double)M > (double)P.ratio * ((double)sum / P.n_elem);
+    P.hdr[0] = __float_as_uint(M < INFINITY ? M : INFINITY);
+    P.hdr[1] = fb ? L1Q_F32 : L1Q_CODES8;
+    P.ticket[0] = 0u;
+    P.ticket[1] = 0u;
+  }
+}
+
+// The filter-list score of one entry (k_filter_scores' list task, TransE L1, prediction = the
+// score): the canonical chain over kp floats, 64 floats of each row in flight per round.
+__device__ __forceinline__ float l1_row_score64(const float* __restrict__ qv, const float* __restrict__ ev, int kp) {
+  float acc = 0.0f;
+  int k0 = 0;
+  for (; k0 + 64 <= kp; k0 += 64) {
+    float4 a[16], x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      a[i] = *reinterpret_cast<const float4*>(qv + k0 + 4 * i);
+      x[i] = *reinterpret_cast<const float4*>(ev + k0 + 4 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      acc = acc + fabsf(a[i].x - x[i].x);
+      acc = acc + fabsf(a[i].y - x[i].y);
+      acc = acc + fabsf(a[i].z - x[i].z);
+      acc = acc + fabsf(a[i].w - x[i].w);
+    }
+  }
+  for (; k0 < kp; k0 += 8) {  // kp % 8 == 0
+    float4 a[2], x[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      a[i] = *reinterpret_cast<const float4*>(qv + k0 + 4 * i);
+      x[i] = *reinterpret_cast<const float4*>(ev + k0 + 4 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      acc = acc + fabsf(a[i].x - x[i].x);
+      acc = acc + fabsf(a[i].y - x[i].y);
+      acc = acc + fabsf(a[i].z - x[i].z);
+      acc = acc + fabsf(a[i].w - x[i].w);
+    }
+  }
+  return acc;
+}
+
+struct EvalQuant {  // K2's quantization operands (k_l1q_quant8<TIGHT> + the 16-bit words)
+  L1QPlane pq, pe;  // 8-bit planes
+  uint32_t* out16q;
+  uint32_t* out16e;
+  int kw, k2, kt, n_blk;  // 8-bit word rows, 16-bit word rows, floats per row, blocks per plane
+  int tight;
+  float* q_l1c;
+};
+
+__global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, const int32_t* __restrict__ ids,
+                                                         const int32_t* __restrict__ entry_q, int64_t n_entries,
+                                                         float* __restrict__ list_v, int n_lblk) {
+  if ((int)blockIdx.x < n_lblk) {  // ---- filter-list scores (k_filter_scores' list tasks)
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n_entries) return;
+    const int64_t j = ids[p], vq = entry_q[p];
+    if (j < 0 || j >= P.n_ent || vq < 0 || vq >= P.n_query) {
+      list_v[p] = __builtin_nanf("");  // never < a threshold: an invalid id is not counted
+      return;
+    }
+    list_v[p] = l1_row_score64(P.q_rows + vq * P.kp, P.ent_rows + j * P.kp, P.kp);
+    return;
+  }
+  // ---- the codes: 8-bit words (+ the tight bound's error row) and 16-bit words in one pass
+  const uint32_t* work = P.hdr;
+  if (__builtin_amdgcn_readfirstlane(work[1]) == L1Q_F32) return;  // K1 chose the f32 sweep
+  const int b = (int)blockIdx.x - n_lblk;
+  const bool ent = b >= Q.n_blk;
+  const int bx = ent ? b - Q.n_blk : b;
+  const L1QPlane& pl = ent ? Q.pe : Q.pq;
+  const float* __restrict__ km = pl.km;
+  const int64_t pad = pl.pad, c0 = pl.c0, n = pl.n;
+  uint32_t* __restrict__ out = pl.out;
+  uint32_t* __restrict__ out16 = ent ? Q.out16e : Q.out16q;
+  const int kp = P.kp, kw = Q.kw, k2 = Q.k2, kt = Q.kt;
+  const float mx = __uint_as_float(work[0]);
+  const float inv = (mx > 0.0f && mx < INFINITY) ? 255.0f / (2.0f * mx) : 0.0f;
+  const float inv16 = (mx > 0.0f && mx < INFINITY) ? 65535.0f / (2.0f * mx) : 0.0f;
+  const float off = (mx < INFINITY) ? mx : 0.0f;
+  const float delta = (mx > 0.0f && mx < INFINITY) ? (2.0f * mx) / 255.0f : 0.0f;
+  const float l1f = (float)(kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+  const int words = (kt + 3) >> 2;
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  __shared__ float s_err[8][32];
+  for (int64_t cb = (int64_t)bx * 32; cb < n; cb += (int64_t)Q.n_blk * 32) {  // uniform
+    const bool live = cb + cl < n;
+    const int64_t c = c0 + cb + cl;
+    float err = 0.0f;
+#pragma unroll 2
+    for (int r = g; r < kw; r += 8) {
+      uint32_t word = 0u, w16a = 0u, w16b = 0u;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int k = 4 * r + h;
+        if (live && k < kp) {
+          const float x = km[(int64_t)k * pad + c];
+          float t = (x + off) * inv;
+          t = t == t ? fminf(fmaxf(t, 0.0f), 255.0f) : 0.0f;
+          const float code = rintf(t);
+          word |= (uint32_t)code << (8 * h);
+          if (Q.tight) err += fabsf(x - (code * delta - off));
+          float t16 = (x + off) * inv16;
+          t16 = t16 == t16 ? fminf(fmaxf(t16, 0.0f), 65535.0f) : 0.0f;
+          const uint32_t c16 = (uint32_t)rintf(t16);
+          if (h < 2) w16a |= c16 << (16 * h);
+          else w16b |= c16 << (16 * (h - 2));
+        }
+      }
+      if (live) {
+        if (!(Q.tight && r == words)) out[(int64_t)r * pad + c] = word;
+        if (2 * r < k2) out16[(int64_t)(2 * r) * pad + c] = w16a;
+        if (2 * r + 1 < k2) out16[(int64_t)(2 * r + 1) * pad + c] = w16b;
+      }
+    }
+    if (Q.tight) {
+      s_err[g][cl] = err;
+      __syncthreads();
+      if (g == 0 && live) {
+        float e = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) e += s_err[i][cl];
+        const float eb = __builtin_fmaf(e, 1.01f, (float)kt * 0x1p-20f * mx);
+        uint32_t wv = 0u;
+        if (!ent) {
+          Q.q_l1c[c] = eb;
+        } else {
+          // (<= 1,005 at kt <= 1,984 without the clamp acting: see k_l1q_quant8)
+          uint32_t o = delta > 0.0f ? (uint32_t)ceilf(fminf(eb / (delta * (1.0f - l1f)) * (1.0f + 0x1p-17f), 1020.0f))
+                                    : 0u;
+          if (o) atomicMax(P.hdr + 3, o);
+#pragma unroll
+          for (int h = 0; h < 4; ++h) {
+            const uint32_t bb = o < 255u ? o : 255u;
+            wv |= bb << (8 * h);
+            o -= bb;
+          }
+        }
+        out[(int64_t)words * pad + c] = wv;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// K3: filter counts (one 64-thread block per filter group, k_filter_count without type masks)
+// | the code-width probe (k_l1q_probe's sample), whose last block (ticket) turns the code-width
+// word to the 16-bit codes when the sample's undecided fraction is over L1Q_PROBE_FRAC.
+// force_bits 8 / 16 (MMRE_L1_BITS): no probe; 16 sets the word (unless the f32 fallback).
+__global__ __launch_bounds__(64) void k_eval_count_probe(
+    const int64_t* __restrict__ grp_qoff, const int32_t* __restrict__ grp_q, int64_t n_groups, int n_cblk,
+    const int64_t* __restrict__ off, const int32_t* __restrict__ ids, const float* __restrict__ list_v,
+    const int32_t* __restrict__ qtrue, const float* __restrict__ thr, int64_t n_query, int64_t n_ent,
+    int32_t* __restrict__ counts, const uint32_t* __restrict__ uq, int64_t q_pad, const uint32_t* __restrict__ ue,
+    int64_t e_pad, int64_t n_slice, int kw, int kt, const float* __restrict__ q_l1c, uint32_t* __restrict__ hdr,
+    uint32_t* __restrict__ ticket, uint32_t probe_max, int force_bits) {
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < n_cblk) {
+    __shared__ __attribute__((aligned(16))) int32_t s_id[64];
+    __shared__ __attribute__((aligned(16))) float s_v[64];
+    for (int64_t g = blockIdx.x; g < n_groups; g += n_cblk) {
+      const int64_t qa = grp_qoff[g], qb = grp_qoff[g + 1];
+      const int64_t la = off[g], lb = off[g + 1];
+      for (int64_t qc = qa; qc < qb; qc += 64) {
+        const int64_t qi = qc + tid;
+        const bool active = qi < qb;
+        const int64_t q = active ? grp_q[qi] : 0;
+        const int32_t tr = active ? qtrue[q] : -1;
+        const float th = active ? thr[q] : 0.0f;
+        int c = 0;
+        for (int64_t lc = la; lc < lb; lc += 64) {
+          const int nl = (int)((lb - lc) < 64 ? (lb - lc) : 64);
+          __syncthreads();  // s_* reuse
+          {
+            int32_t id = -1;
+            float v = 0.0f;
+            if (tid < nl) {
+              const int64_t j = ids[lc + tid];
+              if (j >= 0 && j < n_ent) {
+                id = (int32_t)j;
+                v = list_v[lc + tid];
+              }
+            }
+            s_id[tid] = id;  // entries nl..63 stay invalid: the loop below reads whole quads
+            s_v[tid] = v;
+          }
+          __syncthreads();
+          if (active) {
+            for (int i = 0; i < nl; i += 4) {  // branch-free, 4 entries per LDS read
+              const int4 e = *reinterpret_cast<const int4*>(&s_id[i]);
+              const float4 v = *reinterpret_cast<const float4*>(&s_v[i]);
+              c += ((e.x >= 0) & (e.x != tr) & (v.x < th)) + ((e.y >= 0) & (e.y != tr) & (v.y < th)) +
+                   ((e.z >= 0) & (e.z != tr) & (v.z < th)) + ((e.w >= 0) & (e.w != tr) & (v.w < th));
+            }
+          }
+        }
+        if (active) {
+          counts[0 * n_query + q] = 0;
+          counts[1 * n_query + q] = -c;
+          counts[2 * n_query + q] = 0;
+          counts[3 * n_query + q] = 0;
+        }
+      }
+    }
+    return;
+  }
+  // ---- the probe
+  const uint32_t w = __builtin_amdgcn_readfirstlane(hdr[1]);
+  if (force_bits != 0) {
+    if (force_bits == 16 && w != L1Q_F32 && blockIdx.x == (unsigned)n_cblk && tid == 0) hdr[1] = L1Q_CODES16;
+    return;
+  }
+  if (w != L1Q_CODES8) return;  // the f32 fallback: no codes to probe
+  const int pb = (int)blockIdx.x - n_cblk, n_pb = (int)gridDim.x - n_cblk;
+  const int64_t q = (int64_t)pb * n_query / n_pb;
+  const int64_t span = n_slice > L1Q_PROBE_E ? n_slice - L1Q_PROBE_E : 0;
+  const int64_t c = (((int64_t)pb * span / n_pb) & ~(int64_t)3) + 4 * tid;
+  const float l1d = l1q_delta(hdr, 255.0f);
+  const float l1f = (float)(kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+  const float l1c = __builtin_fmaf((float)kt * 1.03f, l1d, 0x1p-120f);
+  uint32_t acc[4] = {0u, 0u, 0u, 0u};
+  if (c < n_slice) {
+#pragma unroll 8
+    for (int r = 0; r < kw; ++r) {
+      const uint32_t a = uq[(int64_t)r * q_pad + q];
+      const uint4 e = *reinterpret_cast<const uint4*>(ue + (int64_t)r * e_pad + c);
+      acc[0] = __builtin_amdgcn_sad_u8(a, e.x, acc[0]);
+      acc[1] = __builtin_amdgcn_sad_u8(a, e.y, acc[1]);
+      acc[2] = __builtin_amdgcn_sad_u8(a, e.z, acc[2]);
+      acc[3] = __builtin_amdgcn_sad_u8(a, e.w, acc[3]);
+    }
+  }
+  uint32_t t_sure, t_span;
+  l1_int_thresholds(thr[q], (q_l1c ? q_l1c[q] : l1c) + (q_l1c ? 0x1p-120f : 0.0f), l1d, l1f, q_l1c ? 2u * hdr[3] : 0u,
+                    t_sure, t_span);
+  uint32_t und = 0u;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) und += (uint32_t)((acc[j] - t_sure < t_span) & (c + j < n_slice));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) und += __shfl_xor(und, o);
+  __shared__ uint32_t s_last;
+  if (tid == 0) {
+    if (und) atomicAdd(hdr + 2, und);
+    __threadfence();
+    s_last = atomicAdd(&ticket[1], 1u) == (uint32_t)n_pb - 1;
+  }
+  __syncthreads();
+  if (s_last && tid == 0) {
+    __threadfence();
+    const uint32_t total = __hip_atomic_load(hdr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (total > probe_max) hdr[1] = L1Q_CODES16;
+    ticket[1] = 0u;
+  }
 }
 
 }  // namespace mmre
@@ -2881,4 +3419,138 @@ extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, con
                                      void* stream) {
   return sweep_impl(model, pred_kind, margin, d_ent_km, n_ent, e_pad, e_begin, e_end, d_q_km, d_q_true, d_qr, d_qmode,
                     n_query, q_pad, dim, d_type_head, d_type_tail, d_counts, d_truth, nullptr, (hipStream_t)stream);
+}
+
+// ---------------------------------------- fused TransE L1 evaluation (round 5) ---
+static int eval_rb(int kp) { return stage_rows(2 * kp + 1); }  // K1's query blocks stage two row sets
+static int64_t eval_extra_bytes(int dim, int64_t e_pad, int64_t q_pad) {
+  const int rb = eval_rb(plane_rows(MMRE_TRANSE_L1, dim));
+  const int64_t nblk = (e_pad + rb - 1) / rb + (q_pad + rb - 1) / rb;
+  return 256 + 8 * nblk;  // tickets, then K1's per-block statistics
+}
+
+extern "C" int64_t mmre_link_evaluate_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
+  const int64_t base = mmre_link_l1q_workspace(dim, e_pad, q_pad);
+  return base > 0 ? base + eval_extra_bytes(dim, e_pad, q_pad) : 0;
+}
+
+extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t n_ent, const float* d_rel,
+                                      int64_t n_rel, int dim, const int64_t* d_qh, const int64_t* d_qr,
+                                      const int64_t* d_qt, const int8_t* d_qmode, int64_t n_query,
+                                      const int64_t* d_grp_qoff, const int32_t* d_grp_q, int64_t n_groups,
+                                      const int64_t* d_filt_off, const int32_t* d_filt_ids, const int32_t* d_entry_q,
+                                      int64_t n_entries, int64_t e_begin, int64_t e_end, float* d_ent_km,
+                                      int64_t e_pad, float* d_ent_rows, float* d_q_km, int64_t q_pad, float* d_q_rows,
+                                      int32_t* d_q_true, float* d_list_scores, int32_t* d_counts, float* d_truth,
+                                      void* d_work, int64_t work_bytes, void* stream) {
+  if (!d_ent || !d_rel || !d_qh || !d_qr || !d_qt || !d_qmode || !d_ent_km || !d_ent_rows || !d_q_km || !d_q_rows ||
+      !d_q_true || !d_counts || !d_truth || !d_grp_qoff || !d_grp_q || !d_filt_off)
+    return MMRE_ERR_ARG;
+  if (n_ent <= 0 || n_rel <= 0 || dim <= 0 || n_query <= 0 || n_groups <= 0 || n_groups > n_query || n_entries < 0)
+    return MMRE_ERR_ARG;
+  if (e_pad < n_ent || e_pad % TE || q_pad < n_query || q_pad % TQ) return MMRE_ERR_ARG;
+  if (e_begin < 0 || e_begin % TE || e_end <= e_begin || e_end > n_ent) return MMRE_ERR_ARG;
+  if (n_entries > 0 && (!d_filt_ids || !d_entry_q || !d_list_scores)) return MMRE_ERR_WORKSPACE;
+  if (n_ent > (int64_t)INT32_MAX - 256 || n_query >= (int64_t)INT32_MAX) return MMRE_ERR_SHAPE;
+  if (!d_work || work_bytes < mmre_link_evaluate_l1q_workspace(dim, e_pad, q_pad)) return MMRE_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int kp = plane_rows(MMRE_TRANSE_L1, dim), kt = kp, k2 = l1q_rows(dim), k4 = l1q_rows8(dim);
+  const int rb = eval_rb(kp);
+  const size_t lds1 = sizeof(float) * 2 * (size_t)rb * (kt + 1);
+  if (lds1 > 64 * 1024) return MMRE_ERR_SHAPE;
+  char* w = (char*)d_work;
+  uint32_t* hdr = (uint32_t*)w;
+  uint32_t* uq = (uint32_t*)(w + L1Q_HDR);
+  uint32_t* ue = uq + (int64_t)k2 * q_pad;
+  uint32_t* vq = ue + (int64_t)k2 * e_pad;
+  uint32_t* ve = vq + (int64_t)k4 * q_pad;
+  float* q_l1c = (float*)(ve + (int64_t)k4 * e_pad);
+  char* extra = w + mmre_link_l1q_workspace(dim, e_pad, q_pad);
+  uint32_t* ticket = (uint32_t*)extra;  // zero before the first call (the caller zeroes the workspace once)
+  float* pstat = (float*)(extra + 256);
+  const int64_t e_cols = round_up(e_end, TE) - e_begin;
+  const int64_t n_slice = e_end - e_begin;
+  const int n_et = (int)((n_slice + TE - 1) / TE);
+  static const char* ratio_env = getenv("MMRE_L1Q_RATIO");
+  static const char* tight_env = getenv("MMRE_L1_TIGHT");
+  const char* bits_env = getenv("MMRE_L1_BITS");
+  const int bits = bits_env ? atoi(bits_env) : 0;
+  const bool tight = kt <= 1984 && !(tight_env && tight_env[0] == '0');
+  EvalL1 P{};
+  P.ent = d_ent;
+  P.rel = d_rel;
+  P.n_ent = n_ent;
+  P.dim = dim;
+  P.kp = kp;
+  P.norm = norm_flag ? 1 : 0;
+  P.rb = rb;
+  P.qh = d_qh;
+  P.qr = d_qr;
+  P.qt = d_qt;
+  P.qmode = d_qmode;
+  P.n_query = n_query;
+  P.ent_km = d_ent_km;
+  P.e_pad = e_pad;
+  P.ent_rows = d_ent_rows;
+  P.q_km = d_q_km;
+  P.q_pad = q_pad;
+  P.q_rows = d_q_rows;
+  P.q_true = d_q_true;
+  P.truth = d_truth;
+  P.e_begin = e_begin;
+  P.e_cols = e_cols;
+  P.n_eblk = (int)((e_pad + rb - 1) / rb);
+  P.n_qblk = (int)((q_pad + rb - 1) / rb);
+  P.pstat = pstat;
+  P.ticket = ticket;
+  P.hdr = hdr;
+  P.n_elem = (double)kp * (double)(q_pad + e_cols);
+  P.ratio = ratio_env ? (float)atof(ratio_env) : 128.0f;
+  // K1: prep + truths + |x| statistics (the last block decides codes vs f32 and resets the header)
+  hipLaunchKernelGGL(k_eval_prep, dim3((unsigned)(P.n_eblk + P.n_qblk)), dim3(256), lds1, st, P);
+  MMRE_CHECK_LAUNCH();
+  // K2: list scores | codes (8-bit words + error row, 16-bit words)
+  EvalQuant Q{};
+  Q.pq = L1QPlane{d_q_km, q_pad, 0, q_pad, vq};
+  Q.pe = L1QPlane{d_ent_km, e_pad, e_begin, e_cols, ve};
+  Q.out16q = uq;
+  Q.out16e = ue;
+  Q.kw = k4;
+  Q.k2 = k2;
+  Q.kt = kt;
+  Q.n_blk = 512;
+  Q.tight = tight ? 1 : 0;
+  Q.q_l1c = q_l1c;
+  const int n_lblk = (int)((n_entries + 255) / 256);
+  hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), 0, st, P, Q, d_filt_ids,
+                     d_entry_q, n_entries, d_list_scores, n_lblk);
+  MMRE_CHECK_LAUNCH();
+  // K3: filter counts | the code-width probe
+  const int n_cblk = (int)std::min<int64_t>(n_groups, 65536);
+  const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
+  const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);
+  hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_cblk + L1Q_PROBE_Q)), dim3(64), 0, st, d_grp_qoff, d_grp_q,
+                     n_groups, n_cblk, d_filt_off, d_filt_ids, d_list_scores, d_q_true, d_truth, n_query, n_ent,
+                     d_counts, vq, q_pad, ve + e_begin, e_pad, n_slice, k4, kt, tight ? q_l1c : nullptr, hdr,
+                     ticket, probe_max, bits == 8 || bits == 16 ? bits : 0);
+  MMRE_CHECK_LAUNCH();
+  // the sweeps: the one the code-width word names counts, the others' workgroups leave
+  const int64_t tw = (n_ent + 31) / 32;
+  const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
+               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4};
+  int rc = launch_valu<6>(false, false, st, (const float*)(ve + e_begin), e_pad, n_slice, n_et, (int)e_begin,
+                          (const float*)vq, q_pad, n_query, k4, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr,
+                          nullptr, tw, d_counts, nullptr, l1, false);
+  if (rc) return rc;
+  L1Q l16 = l1;
+  l16.gate = hdr + 1;
+  rc = launch_valu<5>(false, false, st, (const float*)(ue + e_begin), e_pad, n_slice, n_et, (int)e_begin,
+                      (const float*)uq, q_pad, n_query, k2, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr, nullptr,
+                      tw, d_counts, nullptr, l16, false);
+  if (rc) return rc;
+  L1Q gate{};
+  gate.gate = hdr + 1;
+  return launch_valu<0>(false, false, st, d_ent_km + e_begin, e_pad, n_slice, n_et, (int)e_begin, d_q_km, q_pad,
+                        n_query, kp, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr, nullptr, tw, d_counts,
+                        nullptr, gate, true);
 }

@@ -178,6 +178,9 @@ class LinkSweep:
         # DistMult / ComplEx count-only sweeps without type constraints through the split-bf16
         # MFMA filter (mmre_link_sweep_bf3); MMRE_MFMA_FILTER=0 keeps the f32 MFMA sweep
         self.mfma_filter = os.environ.get("MMRE_MFMA_FILTER", "1") != "0"
+        # count-only TransE L1 runs with filter groups as ONE call (mmre_link_evaluate_l1q, seven
+        # launches instead of thirteen); MMRE_FUSED_EVAL=0 keeps the separate entry points
+        self.fused_eval = os.environ.get("MMRE_FUSED_EVAL", "1") != "0"
 
     def prepare_entities(self):
         s = self.spec
@@ -207,6 +210,8 @@ class LinkSweep:
         Returns dict(counts=(4, Q) int32 [raw, filt, raw_tc, filt_tc], truth=(Q,), scores=(Q, E)|None)."""
         s = self.spec
         n = int(qh.shape[0])
+        if n > 0 and self._fusable(filt, type_masks, return_scores, prepare, sweep_events, q_rows):
+            return self._run_fused(qh, qr, qt, qmode, filt, buffers, entity_range)
         if n == 0:  # e.g. a rank that owns no test relation (world > #relations): nothing to sweep
             if sweep_events is not None:  # keep the caller's timing events valid (an empty interval)
                 sweep_events[0].record()
@@ -287,6 +292,41 @@ class LinkSweep:
         b["bf3_used"] = bf3
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
 
+    def _fusable(self, filt, type_masks, return_scores, prepare, sweep_events, q_rows):
+        """The fused TransE L1 evaluation (mmre_link_evaluate_l1q) covers count-only runs with
+        filter groups, no type masks, prediction = the score, the entity table prepared in the
+        same call; sweep_events (the sweep kernel alone) keep the separate launches.
+        MMRE_FUSED_EVAL=0 keeps the separate path (A/B)."""
+        return (self.model_id == MODEL_IDS["transe"] and self.l1_filter and self.fused_eval and not return_scores
+                and prepare and sweep_events is None and q_rows and type_masks is None and filt is not None
+                and len(filt) == 5 and int(self.spec.pred_kind) == 0)
+
+    def _run_fused(self, qh, qr, qt, qmode, filt, buffers, entity_range):
+        s = self.spec
+        n = int(qh.shape[0])
+        b = buffers if buffers is not None else self.alloc_queries(n)
+        gqo, gq, off, ids, entry_q = filt
+        n_entries = int(ids.shape[0])
+        lv = b.get("list_scores")
+        if lv is None or lv.shape[0] < n_entries:
+            lv = b["list_scores"] = torch.empty(max(n_entries, 1), dtype=torch.float32, device=self.device)
+        need = int(_lib.lib().mmre_link_evaluate_l1q_workspace(s.dim, self.e_pad, b["q_pad"]))
+        wk = b.get("l1q_work")
+        if wk is None or wk.numel() < need or not b.get("l1q_work_zeroed"):
+            # zeroed once: the call's grid tickets start at 0 and are left at 0
+            wk = b["l1q_work"] = torch.zeros(need, dtype=torch.uint8, device=self.device)
+            b["l1q_work_zeroed"] = True
+        e0, e1 = (0, self.n_ent) if entity_range is None else (int(entity_range[0]), int(entity_range[1]))
+        call("mmre_link_evaluate_l1q", int(bool(s.norm_flag)), ptr(self._ent), self.n_ent, ptr(self._rel), self.n_rel,
+             s.dim, ptr(qh), ptr(qr), ptr(qt), ptr(qmode), n, ptr(gqo), ptr(gq), int(gqo.shape[0]) - 1, ptr(off),
+             ptr(ids), ptr(entry_q), n_entries, e0, e1, ptr(self.ent_km), self.e_pad, ptr(self.ent_rows),
+             ptr(b["q_km"]), b["q_pad"], ptr(b["q_rows"]), ptr(b["q_true"]), ptr(lv), ptr(b["counts"]),
+             ptr(b["truth"]), ptr(wk), int(wk.numel()), stream_ptr(self.device))
+        self.prepared = True
+        b["l1q_used"] = True
+        b["bf3_used"] = False
+        return dict(counts=b["counts"], truth=b["truth"], scores=None)
+
     def bf3_stats(self, buffers):
         """The split-bf16 MFMA filter's record of the last run() on `buffers` (mmre_link_bf3_stats):
         dict(undecided=pairs rescored with the canonical chain, fallback=True if the pair list
@@ -323,12 +363,12 @@ class LinkSweep:
         wk = buffers["l1q_work"]
         out = buffers.get("l1q_stats")
         if out is None:
-            out = buffers["l1q_stats"] = torch.zeros(3, dtype=torch.int64, device=self.device)
+            out = buffers["l1q_stats"] = torch.zeros(4, dtype=torch.int64, device=self.device)
         call("mmre_link_l1q_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
-        u, w, g = (int(x) for x in out.cpu())
+        u, w, g, o = (int(x) for x in out.cpu())
         # the code-width word: 0 = 8-bit codes, 1 = the f32 fallback, 2 = 16-bit codes; guarded =
         # undecided-list entries the rescoring refused as out of range (0 unless a defect)
-        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g)
+        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g, max_offset=o)
 
 
 def _rows_view(c):
