@@ -2258,7 +2258,12 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
 #pragma unroll
                 for (int bj = 0; bj < 2; ++bj) {
                   if (!und[bj]) continue;
-                  const uint32_t i = atomicAdd(&hdr[0], 1u);
+                  // the counter stops near cap once the list is full (a non-finite table can make
+                  // every pair undecided: 1.6e10 at C5 would wrap a 32-bit counter), so the stats
+                  // read a saturated count with the overflow flag, not a wrapped one
+                  uint32_t i = 0xFFFFFFFFu;
+                  if (__hip_atomic_load(&hdr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)cap)
+                    i = atomicAdd(&hdr[0], 1u);
                   if (i < (uint64_t)cap) pairs[i] = make_int2((int)q, (int)((bj ? e1 : e0) + e_base));
                   else hdr[1] = 1u;
                 }

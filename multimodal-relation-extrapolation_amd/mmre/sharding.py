@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 
-def lpt_partition(rel_of_query: np.ndarray, world: int, split: bool = True):
+def lpt_partition(rel_of_query: np.ndarray, world: int, split: bool = True, weights=None):
     """Assign the queries to `world` ranks by relation, heaviest relation first onto the
     least-loaded rank (LPT). With split (SURVEY.md §8(e)'s fallback) no rank takes more than
     the share ceil(Q / world): a relation that does not fit the least-loaded rank fills it with
@@ -22,11 +22,17 @@ def lpt_partition(rel_of_query: np.ndarray, world: int, split: bool = True):
     cuts in all, and every rank's queries stay relation-major (Test.h's order). DB15K-ZS's
     largest relation holds 18 % of the queries, which caps whole-relation LPT at 5.4x on 8
     ranks. Deterministic (every rank computes the same partition). Returns one boolean mask
-    over the queries per rank."""
+    over the queries per rank.
+
+    weights (per query, > 0): pack by cost instead of by count (cost_weights: a query whose
+    pairs the L1 filter leaves undecided costs more than its sweep), same rules with the
+    share = total weight / world."""
     rel_of_query = np.asarray(rel_of_query)
     Q = len(rel_of_query)
     if Q == 0:
         return [np.zeros(0, bool) for _ in range(world)]
+    if weights is not None:
+        return _lpt_weighted(rel_of_query, world, split, np.asarray(weights, np.float64))
     share = -(-Q // world)
     order_q = np.argsort(rel_of_query, kind="stable")
     rels, starts, counts = np.unique(rel_of_query[order_q], return_index=True, return_counts=True)
@@ -43,6 +49,44 @@ def lpt_partition(rel_of_query: np.ndarray, world: int, split: bool = True):
             lo += take
             left -= take
     return [own == k for k in range(world)]
+
+
+def _lpt_weighted(rel_of_query, world, split, w):
+    Q = len(rel_of_query)
+    if w.shape != (Q,) or not np.all(w > 0):
+        raise ValueError("lpt_partition: weights must be positive, one per query")
+    share = float(w.sum()) / world
+    order_q = np.argsort(rel_of_query, kind="stable")
+    rels, starts, counts = np.unique(rel_of_query[order_q], return_index=True, return_counts=True)
+    wq = w[order_q]
+    cw = np.concatenate([[0.0], np.cumsum(wq)])                  # prefix weights in relation-major order
+    rel_w = cw[starts + counts] - cw[starts]
+    order = np.lexsort((rels, -rel_w))                            # heaviest first, ties by relation id
+    load = np.zeros(world, np.float64)
+    own = np.zeros(Q, np.int64)
+    for i in order:
+        lo, hi = int(starts[i]), int(starts[i] + counts[i])
+        while lo < hi:
+            k = int(np.argmin(load))
+            room = share - load[k]
+            rest = cw[hi] - cw[lo]
+            if not split or rest <= room * (1 + 1e-9) or room <= 0:
+                take = hi - lo
+            else:  # the longest run of the relation's queries that fits the room (at least one)
+                take = max(int(np.searchsorted(cw, cw[lo] + room, side="right")) - 1 - lo, 1)
+            own[order_q[lo:lo + take]] = k
+            load[k] += cw[lo + take] - cw[lo]
+            lo += take
+    return [own == k for k in range(world)]
+
+
+def cost_weights(undecided_per_query, n_ent: int, pair_cost: float = 140.0):
+    """Per-query sweep cost for lpt_partition(weights=): the query's n_ent swept pairs plus
+    pair_cost x its pairs the L1 filter left undecided (each gathered and rescored with the
+    canonical chain: ~140 swept pairs' worth on MI355X), from one calibration
+    evaluation (mmre_link_evaluate_l1q's per-query counters)."""
+    u = np.asarray(undecided_per_query, np.float64)
+    return float(n_ent) + pair_cost * u
 
 
 class ShardPlan:

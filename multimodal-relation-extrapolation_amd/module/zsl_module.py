@@ -7,8 +7,9 @@ ZSLmodule.eval (:635-745).
   names (state_dict-compatible) and `forward(query, support, query_meta, support_meta) ->
   (query_g, matching_scores)`. In eval mode forward runs on the GPU (csrc/extractor.hip):
   per-row neighbour / entity encoders folded through reshape_layer, then the SupportEncoder
-  on MFMA. Training mode (dropout; pretrain_Extractor / the GAN loop) is not part of this build
-  and raises.
+  on MFMA. In training mode (the three nn.Dropout(0.2)) it runs the pretraining step's
+  launch chain (mmre.extractor_train: dropped neighbour sums gathered on the GPU, the linears
+  on the split-K GEMM, counter-hash dropout masks).
 * `ZSLGraph` builds symbol2id / symbol2vec / connections / e1_degrees exactly as the
   reference does, with numpy instead of per-element Python loops.
 * `ZSLEvaluator.eval(relation_vecs, test_candidates)` is ZSLmodule.eval's ranking for every
@@ -21,9 +22,10 @@ ZSLmodule.eval (:635-745).
   adversarial loop on mmre.gan.ZSLGANStep, hipGraph-replayed D / G steps, then save + eval),
   `eval(generate_model, mode, meta, load_pretrain)` -> (hits10, hits5, mrr) with every
   relation's generate() in one batched call and every candidate ranked in one launch
-  sequence, `save` / `load` / `save_pretrain` / `load_pretrain`. The Extractor's own
-  pretraining (`pretrain_Extractor`, :289-348: Extractor training with dropout) is outside
-  this path; the Extractor keeps its current (or load_pretrain'ed) weights.
+  sequence, `save` / `load` / `save_pretrain` / `load_pretrain`, and the Extractor's own
+  pretraining (`pretrain_Extractor`, :289-348: margin loss over dropped-out Extractor vectors,
+  torch Adam) through mmre.extractor_train.PretrainStep, captured once per batch shape into a
+  hipGraph.
 """
 import json
 import os
@@ -65,8 +67,8 @@ class Extractor(nn.Module):
 
     def _require_eval(self):
         if self.training:
-            raise MMREError("Extractor runs in eval mode on this path (pretrain_Extractor / GAN training, "
-                            "zsl_module.py:289-600, are outside it): call .eval()")
+            raise MMREError("Extractor.encode_pairs is the eval-mode encoder (training mode goes through "
+                            "forward(), mmre.extractor_train): call .eval()")
 
     def encode_pairs(self, pairs, meta, targets_=None, normalize=False, want_g=True):
         """query_g (and optionally scores vs targets_) of (B, 2) symbol pairs with their meta."""

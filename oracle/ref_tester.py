@@ -267,9 +267,11 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
 
     keys = (("l_rank", "l_filter_rank"), ("r_rank", "r_filter_rank"))
     t_keep = 0.0
+    t_idx = np.zeros(n, np.float64)  # per test triple (both sweeps), the fixture bookkeeping excluded
     t0 = time.perf_counter()
     with stdout_to_stderr():
         for idx in range(n):
+            ti = time.perf_counter()
             lib.getHeadBatch(ph.ctypes.data, pt.ctypes.data, pr.ctypes.data)
             s = np.ascontiguousarray(predict(torch.from_numpy(ph), torch.from_numpy(pt[:1]),
                                              torch.from_numpy(pr[:1]), "head_batch"), np.float32)
@@ -286,6 +288,7 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             counts[1, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[1], before)]
             q[idx, 0] = ph[0]
             k0 = time.perf_counter()
+            t_idx[idx] = k0 - ti
             keep(0, idx, head_s, int(q[idx, 0]))   # the head sweep's truth is the tail batch's anchor
             keep(1, idx, s, int(q[idx, 2]))
             t_keep += time.perf_counter() - k0
@@ -295,7 +298,7 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
                             lib.getTestLinkHit3(0), lib.getTestLinkHit1(0)], np.float32)
     if not all(math.isfinite(float(m)) for m in metrics):
         raise RuntimeError("Base.so returned non-finite metrics")
-    out = dict(counts=counts, q=q, metrics=metrics, elapsed=np.float64(elapsed),
+    out = dict(counts=counts, q=q, metrics=metrics, elapsed=np.float64(elapsed), t_idx=t_idx,
                threads=np.int64(torch.get_num_threads()), n_ent=np.int64(E), tie_rel=np.float64(tie_rel),
                truth_scores=truth_s, score_absmax=smax)
     if scores is not None:

@@ -353,3 +353,29 @@ def test_bench_quotes_pmc_traffic_only_for_this_build(tmp_path, monkeypatch):
     tot, src, per = bench.pmc_step_traffic("ns", ["k_ns_prepass(", "k_ns_transe_fused<4, false>"])
     assert tot == (3.0 + 5.0) * 1024.0 and len(per) == 2
     assert bench.pmc_step_traffic("ns", ["k_ns_row_owner"])[0] is None
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_lpt_partition_weighted(world):
+    """Cost-aware packing: with per-query weights the ranks' weight loads
+    are balanced to within one query piece, pieces stay contiguous runs of a relation, and
+    uniform weights reproduce the count-based partition's balance."""
+    from mmre.data import load_zs_test
+    from mmre.sharding import cost_weights, lpt_partition
+    z = load_zs_test("FB15K-237-ZS")
+    qr = np.concatenate([z["r"], z["r"]])
+    rng = np.random.default_rng(world)
+    und = np.where(rng.random(len(qr)) < 0.05, rng.integers(100, 3000, len(qr)), rng.integers(0, 40, len(qr)))
+    und[qr == np.bincount(qr).argmax()] *= 10       # one relation's queries are costly
+    w = cost_weights(und, 14208)
+    masks = lpt_partition(qr, world, weights=w)
+    assert np.array_equal(np.sum(masks, 0), np.ones(len(qr)))
+    loads = np.array([w[m].sum() for m in masks])
+    assert loads.max() <= w.sum() / world + w.max() + 1e-6
+    for m in masks:
+        for r in np.unique(qr[m]):
+            idx = np.nonzero(qr == r)[0]
+            mine = np.nonzero(m[idx])[0]
+            assert 1 + int(np.sum(np.diff(mine) > 1)) <= world + 1
+    u = lpt_partition(qr, world, weights=np.ones(len(qr)))
+    assert len(qr) / max(m.sum() for m in u) >= 0.93 * world

@@ -10,8 +10,9 @@ agreement is not vacuous:
     C2  FB15K-237-ZS TransE d=200 norm_flag   every test triple: 35,192 sweeps x 14,208
         (the HEADLINE config, on the bench's TRAINED tables: 300 steps of this build's
         deterministic HIP trainer, retrained here and checked by sha256; production path =
-        the 16-bit-code integer filter, mmre_link_sweep_l1q, whose undecided-pair count is
-        asserted too)
+        the L1 integer filter (mmre_link_evaluate_l1q / mmre_link_sweep_l1q), whose code width
+        the device-side probe picks -- 8-bit codes on these trained tables, asserted -- and
+        whose undecided-pair count is asserted too)
     C3  DB15K-ZS ComplEx d=200 (MFMA sweep)    every test triple: 11,306 sweeps x 12,741
     C4  FB15K-237-ZS RotatE d=512 (VALU sweep) 1,000 seeded triples: 2,000 sweeps x 14,208
     C5  synthetic DistMult d=256 (MFMA sweep)  every test triple:  8,192 sweeps x 1,000,000
