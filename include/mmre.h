@@ -167,7 +167,9 @@ int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
  * same either way. d_out[2] = undecided-list entries the rescoring refused because their query
  * or entity id was out of range (a guard on the list's invariant: 0 unless the build is
  * defective), d_out[3] = the largest per-entity error offset of the 8-bit codes' tight bound (in
- * code steps; 0 with the uniform bound). d_out holds 4 uint64. */
+ * code steps; 0 with the uniform bound), d_out[4] = pairs of the 8-bit band that the second
+ * rescoring level (16-bit row codes, mmre_link_evaluate_l1q) left to the f32 chain. d_out holds
+ * 5 uint64. */
 int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
 int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
                         int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,
@@ -187,7 +189,9 @@ int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, cons
  * d_ent / d_rel: the raw tables (n_ent x dim, n_rel x dim); norm_flag as TransE's. Filter
  * groups as for mmre_link_truth_grouped (FilterIndex.groups; restricted to [e_begin, e_end)
  * for an entity slice). d_work: mmre_link_evaluate_l1q_workspace(dim, e_pad, q_pad) bytes,
- * ZEROED before the first call (it holds grid tickets; every call leaves them zero). */
+ * ZEROED before the first call (it holds grid tickets; every call leaves them zero).
+ * d_undecided_q (NULL or n_query uint32): per query, the pairs the filter left undecided and
+ * rescored with the canonical chain (the relation-sharded partition's cost calibration). */
 int64_t mmre_link_evaluate_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
 int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t n_ent, const float* d_rel, int64_t n_rel,
                            int dim, const int64_t* d_qh, const int64_t* d_qr, const int64_t* d_qt,
@@ -196,7 +200,8 @@ int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t n_ent, con
                            const int32_t* d_entry_q, int64_t n_entries, int64_t e_begin, int64_t e_end,
                            float* d_ent_km, int64_t e_pad, float* d_ent_rows, float* d_q_km, int64_t q_pad,
                            float* d_q_rows, int32_t* d_q_true, float* d_list_scores, int32_t* d_counts,
-                           float* d_truth, void* d_work, int64_t work_bytes, void* stream);
+                           float* d_truth, uint32_t* d_undecided_q, void* d_work, int64_t work_bytes,
+                           void* stream);
 
 /* DistMult / ComplEx (MMRE_DISTMULT, MMRE_COMPLEX) count-only sweep through a split-bf16 MFMA
  * filter: same counts as mmre_link_sweep / mmre_link_sweep_range without type constraints (bit

@@ -377,6 +377,10 @@ struct L1Q {
   const uint32_t* gate;    // gated launches: run only if *gate is the sweep's code-width word (L1Q_F32 for the f32 sweep)
   const float* q_l1c;      // 8-bit codes, tight bound: per query row sum |eps_q| (upper bound); nullptr: uniform bound
   uint32_t* guard;         // hdr[4]: pairs the rescoring refused (query or entity id out of range; must stay 0)
+  uint32_t* und_q;         // optional per-query count of rescored pairs (cost calibration of the sharding)
+  const uint32_t* q16r;    // 8-bit sweeps, prediction = the score: row-major 16-bit code rows (k2w words
+  const uint32_t* e16r;    // per row; whole table for the entities) -- the rescoring's second level; nullptr: none
+  int k2w;
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
@@ -970,8 +974,41 @@ __device__ __forceinline__ void sweep_valu_body(
       if (l1.guard) atomicAdd(l1.guard, 1u);
       return;
     }
+    if (l1.und_q) atomicAdd(&l1.und_q[q], 1u);
+    const float th = thr[q];
+    if constexpr (OP == 6 && PK == 0) {
+      // second level: the pair's 16-bit codes (row-major copies: 2 x k2w words, one v_sad_u16 per
+      // two elements) decide ~99 % of the 8-bit band's pairs under the 16-bit codes' uniform bound
+      // (the 16-bit sweep's test, load_meta's l1_int_thresholds at delta16 = 2M / 65535); only
+      // what stays undecided there takes the f32 chain (half the bytes of the f32 rows, a quarter
+      // of the VALU: the 8-bit band's rescoring was what a rank's share of a few dense relations
+      // paid for)
+      if (l1.q16r != nullptr) {
+        const uint4* a = reinterpret_cast<const uint4*>(l1.q16r + q * (int64_t)l1.k2w);
+        const uint4* b = reinterpret_cast<const uint4*>(l1.e16r + (int64_t)(e + e_base) * l1.k2w);
+        uint32_t s16 = 0u;
+#pragma unroll 5
+        for (int i = 0; i < l1.k2w / 4; ++i) {
+          const uint4 x = a[i], y = b[i];
+          s16 = __builtin_amdgcn_sad_u16(x.x, y.x, s16);
+          s16 = __builtin_amdgcn_sad_u16(x.y, y.y, s16);
+          s16 = __builtin_amdgcn_sad_u16(x.z, y.z, s16);
+          s16 = __builtin_amdgcn_sad_u16(x.w, y.w, s16);
+        }
+        const float d16 = l1q_delta(l1.hdr, 65535.0f);
+        const float f16 = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
+        uint32_t t_sure, t_span;
+        l1_int_thresholds(th, __builtin_fmaf((float)l1.kt * 1.03f, d16, 0x1p-120f), d16, f16, 0u, t_sure, t_span);
+        if (s16 < t_sure) {  // S < th for sure
+          atomicAdd(&counts[q], 1);
+          return;
+        }
+        if (s16 - t_sure >= t_span) return;  // S >= th for sure
+        atomicAdd(l1.guard + 1, 1u);  // hdr[5]: pairs left to the f32 chain (the second level's record)
+      }
+    }
     const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
-    if (pred(sx) < thr[q]) {
+    if (pred(sx) < th) {
       atomicAdd(&counts[q], 1);
       if constexpr (TC) {
         const uint32_t* tm = qmode[q] == MMRE_HEAD_BATCH ? type_head : type_tail;
@@ -1926,6 +1963,9 @@ __global__ __launch_bounds__(256) void k_l1q_quant8(L1QPlane pq, L1QPlane pe, in
 // 0.77 % / 1.18 % took 0.32 / 0.51 ms against 0.26 ms with 16-bit codes (profiles/r4).
 constexpr int L1Q_PROBE_Q = 512, L1Q_PROBE_E = 256;
 constexpr double L1Q_PROBE_FRAC = 0.006;  // undecided fraction of the sample above which 16-bit codes
+// the same with the second rescoring level (16-bit row codes before the f32 chain: an undecided
+// pair costs ~3x less, so the 8-bit codes pay up to a wider band)
+constexpr double L1Q_PROBE_FRAC_L2 = 0.02;
 __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ uq, int64_t q_pad, int64_t n_query,
                                                    const uint32_t* __restrict__ ue, int64_t e_pad, int64_t n_slice,
                                                    int kw, int kt, const float* __restrict__ thr, int pred_kind,
@@ -1982,8 +2022,9 @@ __global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ p, in
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
 }
 
-// Sum of the undecided-pair slots, the code-width word, the rescoring guard's count and the largest
-// error offset of the tight bound -> out[0..3] (mmre_link_l1q_stats).
+// Sum of the undecided-pair slots, the code-width word, the rescoring guard's count, the largest
+// error offset of the tight bound and the pairs the second level left to the f32 chain -> out[0..4]
+// (mmre_link_l1q_stats).
 __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
   const unsigned long long* sl =
@@ -1994,6 +2035,7 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
   out[1] = work[1];
   out[2] = work[4];
   out[3] = work[3];
+  out[4] = work[5];
 }
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
@@ -2464,6 +2506,7 @@ struct EvalL1 {
   float* truth;
   int64_t e_begin, e_cols;  // the swept slice (its columns feed M)
   int n_eblk, n_qblk;
+  uint32_t* und_q;          // optional per-query rescored-pair counters (zeroed here)
   float* pstat;             // per K1 block: max |x|, sum |x| (2 floats)
   uint32_t* ticket;         // [0] K1's, [1] the probe's
   uint32_t* hdr;            // the L1 filter header
@@ -2551,6 +2594,7 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
         tr = head ? P.qh[q] : P.qt[q];
         r = P.qr[q];
         P.q_true[q] = (int32_t)tr;
+        if (P.und_q) P.und_q[q] = 0u;
       }
       s_a[tid] = a;
       s_t[tid] = tr;
@@ -2665,15 +2709,22 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     s_s[tid >> 6] = sa;
   }
   __syncthreads();
+  // The hand-off of the partials to the last block (MI355X_MICROARCH.md, hand-off table row 1):
+  // write-through (sc1) stores of the two floats, the storing wave's vmcnt(0) wait, then ONE
+  // agent-scope atomic add per block to the unsharded ticket; the block whose add returns
+  // gridDim - 1 is last, and reads every partial with sc1 loads after a barrier. No
+  // __threadfence(): its L2 write-back (buffer_wbl2) in each of ~3,000 blocks, each with freshly
+  // dirtied rows, serialised K1 to 163 us (measured) against ~45 us without.
   if (tid == 0) {
-    P.pstat[2 * blockIdx.x] = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
-    P.pstat[2 * blockIdx.x + 1] = (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]);
-    __threadfence();  // release the partial before the ticket
-    s_last = atomicAdd(&P.ticket[0], 1u) == gridDim.x - 1;
+    __hip_atomic_store(&P.pstat[2 * blockIdx.x], fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3])),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&P.pstat[2 * blockIdx.x + 1], (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(&P.ticket[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();  // acquire every block's partial
   const int nb = (int)gridDim.x;
   float m = 0.0f, s = 0.0f;
   for (int b = tid; b < nb; b += 256) {  // fixed order per thread, fixed tree below: deterministic
@@ -2747,6 +2798,8 @@ struct EvalQuant {  // K2's quantization operands (k_l1q_quant8<TIGHT> + the 16-
   L1QPlane pq, pe;  // 8-bit planes
   uint32_t* out16q;
   uint32_t* out16e;
+  uint32_t* rows16q;  // row-major 16-bit code rows (k2 words per row; nullptr: not made)
+  uint32_t* rows16e;
   int kw, k2, kt, n_blk;  // 8-bit word rows, 16-bit word rows, floats per row, blocks per plane
   int tight;
   float* q_l1c;
@@ -2777,6 +2830,8 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
   const int64_t pad = pl.pad, c0 = pl.c0, n = pl.n;
   uint32_t* __restrict__ out = pl.out;
   uint32_t* __restrict__ out16 = ent ? Q.out16e : Q.out16q;
+  uint32_t* __restrict__ rows16 = ent ? Q.rows16e : Q.rows16q;
+  extern __shared__ uint32_t s16[];  // [32][k2 + 1]: the 16-bit words staged for the row-major copy
   const int kp = P.kp, kw = Q.kw, k2 = Q.k2, kt = Q.kt;
   const float mx = __uint_as_float(work[0]);
   const float inv = (mx > 0.0f && mx < INFINITY) ? 255.0f / (2.0f * mx) : 0.0f;
@@ -2816,6 +2871,18 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
         if (2 * r < k2) out16[(int64_t)(2 * r) * pad + c] = w16a;
         if (2 * r + 1 < k2) out16[(int64_t)(2 * r + 1) * pad + c] = w16b;
       }
+      if (rows16 != nullptr) {
+        if (2 * r < k2) s16[cl * (k2 + 1) + 2 * r] = w16a;
+        if (2 * r + 1 < k2) s16[cl * (k2 + 1) + 2 * r + 1] = w16b;
+      }
+    }
+    if (rows16 != nullptr) {  // the 32 columns' rows, written whole (consecutive threads: consecutive words)
+      __syncthreads();
+      for (int i = threadIdx.x; i < 32 * k2; i += 256) {
+        const int col = i / k2, wd = i - col * k2;
+        if (cb + col < n) rows16[(c0 + cb + col) * (int64_t)k2 + wd] = s16[col * (k2 + 1) + wd];
+      }
+      __syncthreads();
     }
     if (Q.tight) {
       s_err[g][cl] = err;
@@ -2943,14 +3010,13 @@ __global__ __launch_bounds__(64) void k_eval_count_probe(
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) und += __shfl_xor(und, o);
   __shared__ uint32_t s_last;
-  if (tid == 0) {
-    if (und) atomicAdd(hdr + 2, und);
-    __threadfence();
-    s_last = atomicAdd(&ticket[1], 1u) == (uint32_t)n_pb - 1;
+  if (tid == 0) {  // the counts reach the last probe block as in K1's hand-off (no __threadfence)
+    if (und) __hip_atomic_fetch_add(hdr + 2, und, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_last = __hip_atomic_fetch_add(&ticket[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)n_pb - 1;
   }
   __syncthreads();
   if (s_last && tid == 0) {
-    __threadfence();
     const uint32_t total = __hip_atomic_load(hdr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (total > probe_max) hdr[1] = L1Q_CODES16;
     ticket[1] = 0u;
@@ -3428,10 +3494,17 @@ extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, con
 
 // ---------------------------------------- fused TransE L1 evaluation (round 5) ---
 static int eval_rb(int kp) { return stage_rows(2 * kp + 1); }  // K1's query blocks stage two row sets
-static int64_t eval_extra_bytes(int dim, int64_t e_pad, int64_t q_pad) {
+// the 16-bit codes' row-major copies (the 8-bit sweep's second rescoring level) when their
+// staging fits K2's LDS (k2 <= 256 words: dim <= 504)
+static bool eval_rows16(int dim) { return l1q_rows(dim) <= 256; }
+static int64_t eval_stat_bytes(int dim, int64_t e_pad, int64_t q_pad) {
   const int rb = eval_rb(plane_rows(MMRE_TRANSE_L1, dim));
   const int64_t nblk = (e_pad + rb - 1) / rb + (q_pad + rb - 1) / rb;
-  return 256 + 8 * nblk;  // tickets, then K1's per-block statistics
+  return round_up(256 + 8 * nblk, 256);  // tickets, then K1's per-block statistics
+}
+static int64_t eval_extra_bytes(int dim, int64_t e_pad, int64_t q_pad) {
+  const int64_t rows16 = eval_rows16(dim) ? 4 * (int64_t)l1q_rows(dim) * (q_pad + e_pad) : 0;
+  return eval_stat_bytes(dim, e_pad, q_pad) + rows16;
 }
 
 extern "C" int64_t mmre_link_evaluate_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
@@ -3447,7 +3520,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
                                       int64_t n_entries, int64_t e_begin, int64_t e_end, float* d_ent_km,
                                       int64_t e_pad, float* d_ent_rows, float* d_q_km, int64_t q_pad, float* d_q_rows,
                                       int32_t* d_q_true, float* d_list_scores, int32_t* d_counts, float* d_truth,
-                                      void* d_work, int64_t work_bytes, void* stream) {
+                                      uint32_t* d_undecided_q, void* d_work, int64_t work_bytes, void* stream) {
   if (!d_ent || !d_rel || !d_qh || !d_qr || !d_qt || !d_qmode || !d_ent_km || !d_ent_rows || !d_q_km || !d_q_rows ||
       !d_q_true || !d_counts || !d_truth || !d_grp_qoff || !d_grp_q || !d_filt_off)
     return MMRE_ERR_ARG;
@@ -3473,6 +3546,10 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   char* extra = w + mmre_link_l1q_workspace(dim, e_pad, q_pad);
   uint32_t* ticket = (uint32_t*)extra;  // zero before the first call (the caller zeroes the workspace once)
   float* pstat = (float*)(extra + 256);
+  static const char* lvl2_env = getenv("MMRE_L1_RESCORE16");  /* A/B: 0 = the f32 chain for every pair */
+  const bool rows16 = eval_rows16(dim) && !(lvl2_env && lvl2_env[0] == '0');
+  uint32_t* q16r = rows16 ? (uint32_t*)(extra + eval_stat_bytes(dim, e_pad, q_pad)) : nullptr;
+  uint32_t* e16r = rows16 ? q16r + (int64_t)k2 * q_pad : nullptr;
   const int64_t e_cols = round_up(e_end, TE) - e_begin;
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
@@ -3506,6 +3583,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   P.e_cols = e_cols;
   P.n_eblk = (int)((e_pad + rb - 1) / rb);
   P.n_qblk = (int)((q_pad + rb - 1) / rb);
+  P.und_q = d_undecided_q;
   P.pstat = pstat;
   P.ticket = ticket;
   P.hdr = hdr;
@@ -3520,6 +3598,8 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   Q.pe = L1QPlane{d_ent_km, e_pad, e_begin, e_cols, ve};
   Q.out16q = uq;
   Q.out16e = ue;
+  Q.rows16q = q16r;
+  Q.rows16e = e16r;
   Q.kw = k4;
   Q.k2 = k2;
   Q.kt = kt;
@@ -3527,13 +3607,16 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   Q.tight = tight ? 1 : 0;
   Q.q_l1c = q_l1c;
   const int n_lblk = (int)((n_entries + 255) / 256);
-  hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), 0, st, P, Q, d_filt_ids,
+  const size_t lds2 = rows16 ? sizeof(uint32_t) * 32 * (size_t)(k2 + 1) : 0;
+  hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), lds2, st, P, Q, d_filt_ids,
                      d_entry_q, n_entries, d_list_scores, n_lblk);
   MMRE_CHECK_LAUNCH();
   // K3: filter counts | the code-width probe
   const int n_cblk = (int)std::min<int64_t>(n_groups, 65536);
   const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
-  const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);
+  static const char* pf_env = getenv("MMRE_L1_PROBE_FRAC");  /* experiments: the 16-bit switch point */
+  const double pfrac = pf_env ? atof(pf_env) : (rows16 ? L1Q_PROBE_FRAC_L2 : L1Q_PROBE_FRAC);
+  const uint32_t probe_max = (uint32_t)std::min(pfrac * (double)sample, 4.0e9);
   hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_cblk + L1Q_PROBE_Q)), dim3(64), 0, st, d_grp_qoff, d_grp_q,
                      n_groups, n_cblk, d_filt_off, d_filt_ids, d_list_scores, d_q_true, d_truth, n_query, n_ent,
                      d_counts, vq, q_pad, ve + e_begin, e_pad, n_slice, k4, kt, tight ? q_l1c : nullptr, hdr,
@@ -3542,7 +3625,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   // the sweeps: the one the code-width word names counts, the others' workgroups leave
   const int64_t tw = (n_ent + 31) / 32;
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4};
+               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4, d_undecided_q, q16r, e16r, k2};
   int rc = launch_valu<6>(false, false, st, (const float*)(ve + e_begin), e_pad, n_slice, n_et, (int)e_begin,
                           (const float*)vq, q_pad, n_query, k4, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr,
                           nullptr, tw, d_counts, nullptr, l1, false);

@@ -36,7 +36,7 @@ SIGNATURES = {
                                   I64, P]),
     "mmre_link_evaluate_l1q_workspace": (I64, [I32, I64, I64]),
     "mmre_link_evaluate_l1q": (I32, [I32, P, I64, P, I64, I32, P, P, P, P, I64, P, P, I64, P, P, P, I64, I64, I64, P,
-                                     I64, P, P, I64, P, P, P, P, P, P, I64, P]),
+                                     I64, P, P, I64, P, P, P, P, P, P, P, I64, P]),
     "mmre_link_bf3_workspace": (I64, [I32, I32, I64, I64]),
     "mmre_link_bf3_stats": (I32, [P, I64, P, P]),
     "mmre_link_sweep_bf3": (I32, [I32, I32, F32, P, P, I64, I64, I64, I64, P, P, P, P, P, I64, I64, I32, P, P, P,

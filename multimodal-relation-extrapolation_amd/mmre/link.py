@@ -181,6 +181,7 @@ class LinkSweep:
         # count-only TransE L1 runs with filter groups as ONE call (mmre_link_evaluate_l1q, seven
         # launches instead of thirteen); MMRE_FUSED_EVAL=0 keeps the separate entry points
         self.fused_eval = os.environ.get("MMRE_FUSED_EVAL", "1") != "0"
+        self._last_l2 = False   # the last run used the fused path (its second rescoring level reports `exact`)
 
     def prepare_entities(self):
         s = self.spec
@@ -198,7 +199,7 @@ class LinkSweep:
                     truth=torch.empty(n_query, dtype=torch.float32, device=dev), q_pad=q_pad)
 
     def run(self, qh, qr, qt, qmode, filt=None, type_masks=None, return_scores=False, buffers=None,
-            prepare=True, sweep_events=None, q_rows=True, entity_range=None):
+            prepare=True, sweep_events=None, q_rows=True, entity_range=None, undecided_q=None):
         """qh/qr/qt int64 and qmode int8 device tensors. filt: per-query CSR (off int64, ids int32)
         or filter groups (grp_qoff, grp_q, off, ids, entry_q), see FilterIndex.groups.
         sweep_events: optional (start, end) torch.cuda.Event pair recorded around the sweep kernel alone
@@ -207,11 +208,15 @@ class LinkSweep:
         entity_range (e0, e1), e0 a multiple of 128: sweep only those entities (filt restricted
         to them: FilterIndex.groups(..., entity_range)); summing counts over a partition of the
         table gives the whole-table counts (mmre_link_sweep_range).
+        undecided_q: optional (Q,) int32 device tensor receiving, per query, the pairs the L1
+        filter rescored (fused TransE L1 runs only; the sharding's cost calibration).
         Returns dict(counts=(4, Q) int32 [raw, filt, raw_tc, filt_tc], truth=(Q,), scores=(Q, E)|None)."""
         s = self.spec
         n = int(qh.shape[0])
         if n > 0 and self._fusable(filt, type_masks, return_scores, prepare, sweep_events, q_rows):
-            return self._run_fused(qh, qr, qt, qmode, filt, buffers, entity_range)
+            return self._run_fused(qh, qr, qt, qmode, filt, buffers, entity_range, undecided_q)
+        if undecided_q is not None:
+            raise ValueError("undecided_q: only the fused TransE L1 evaluation counts undecided pairs per query")
         if n == 0:  # e.g. a rank that owns no test relation (world > #relations): nothing to sweep
             if sweep_events is not None:  # keep the caller's timing events valid (an empty interval)
                 sweep_events[0].record()
@@ -290,6 +295,7 @@ class LinkSweep:
             sweep_events[1].record()
         b["l1q_used"] = l1q
         b["bf3_used"] = bf3
+        self._last_l2 = False
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
 
     def _fusable(self, filt, type_masks, return_scores, prepare, sweep_events, q_rows):
@@ -301,7 +307,7 @@ class LinkSweep:
                 and prepare and sweep_events is None and q_rows and type_masks is None and filt is not None
                 and len(filt) == 5 and int(self.spec.pred_kind) == 0)
 
-    def _run_fused(self, qh, qr, qt, qmode, filt, buffers, entity_range):
+    def _run_fused(self, qh, qr, qt, qmode, filt, buffers, entity_range, undecided_q=None):
         s = self.spec
         n = int(qh.shape[0])
         b = buffers if buffers is not None else self.alloc_queries(n)
@@ -321,10 +327,11 @@ class LinkSweep:
              s.dim, ptr(qh), ptr(qr), ptr(qt), ptr(qmode), n, ptr(gqo), ptr(gq), int(gqo.shape[0]) - 1, ptr(off),
              ptr(ids), ptr(entry_q), n_entries, e0, e1, ptr(self.ent_km), self.e_pad, ptr(self.ent_rows),
              ptr(b["q_km"]), b["q_pad"], ptr(b["q_rows"]), ptr(b["q_true"]), ptr(lv), ptr(b["counts"]),
-             ptr(b["truth"]), ptr(wk), int(wk.numel()), stream_ptr(self.device))
+             ptr(b["truth"]), ptr(undecided_q), ptr(wk), int(wk.numel()), stream_ptr(self.device))
         self.prepared = True
         b["l1q_used"] = True
         b["bf3_used"] = False
+        self._last_l2 = True
         return dict(counts=b["counts"], truth=b["truth"], scores=None)
 
     def bf3_stats(self, buffers):
@@ -363,12 +370,13 @@ class LinkSweep:
         wk = buffers["l1q_work"]
         out = buffers.get("l1q_stats")
         if out is None:
-            out = buffers["l1q_stats"] = torch.zeros(4, dtype=torch.int64, device=self.device)
+            out = buffers["l1q_stats"] = torch.zeros(5, dtype=torch.int64, device=self.device)
         call("mmre_link_l1q_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
-        u, w, g, o = (int(x) for x in out.cpu())
+        u, w, g, o, x = (int(v) for v in out.cpu())
         # the code-width word: 0 = 8-bit codes, 1 = the f32 fallback, 2 = 16-bit codes; guarded =
         # undecided-list entries the rescoring refused as out of range (0 unless a defect)
-        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g, max_offset=o)
+        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g, max_offset=o,
+                    exact=x if self._last_l2 else None)
 
 
 def _rows_view(c):

@@ -80,6 +80,32 @@ def _lpt_weighted(rel_of_query, world, split, w):
     return [own == k for k in range(world)]
 
 
+def calibrate_weights(spec, qh, qr, qt, qm, index, device, group=None):
+    """Per-query costs for the relation-sharded partition, from ONE evaluation of every query
+    before any timing: the pairs the TransE L1 filter leaves undecided concentrate on some
+    relations' queries (an 8-way share of C2 put 1.2 % of its pairs in the 8-bit band where the
+    whole evaluation has 0.2 %), and each costs ~140 swept pairs. Rank 0's counts are broadcast
+    so every rank packs the same partition. None (count-based packing) for other models."""
+    import torch.distributed as dist
+    from .link import LinkSweep
+    if spec is None or index is None or spec.model != "transe":
+        return None
+    sw = LinkSweep(spec)
+    if not sw._fusable((0,) * 5, None, False, True, None, True):
+        return None
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    filt = tuple(to(a) for a in index.groups(qh, qr, qt, qm))
+    und = torch.zeros(len(qh), dtype=torch.int32, device=device)
+    sw.run(to(qh), to(qr), to(qt), to(qm), filt=filt, undecided_q=und)
+    w = torch.from_numpy(cost_weights(und.cpu().numpy(), sw.n_ent))
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        t = w.to(device) if dist.get_backend(group) == "nccl" else w
+        dist.broadcast(t, dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        w = t.cpu()
+    del sw
+    return w.numpy()
+
+
 def cost_weights(undecided_per_query, n_ent: int, pair_cost: float = 140.0):
     """Per-query sweep cost for lpt_partition(weights=): the query's n_ent swept pairs plus
     pair_cost x its pairs the L1 filter left undecided (each gathered and rescored with the
@@ -100,12 +126,14 @@ class ShardPlan:
         self.sizes = [int(m.sum()) for m in masks]
         self.pad = max(max(self.sizes), 1)
         self.ids = [np.nonzero(m)[0] for m in masks]
-        cols, dst = [], []
+        # one gather from the all-gathered (world, 4, pad) block into (4, n_total) global order:
+        # global column q of count row c <- flat index (rank(q) * 4 + c) * pad + local(q)
+        src = np.empty((4, self.n_total), np.int64)
         for k in range(self.world):
-            cols.append(k * self.pad + np.arange(self.sizes[k]))
-            dst.append(self.ids[k])
-        self.cols = torch.from_numpy(np.concatenate(cols).astype(np.int64)).to(device)
-        self.dst = torch.from_numpy(np.concatenate(dst).astype(np.int64)).to(device)
+            for c in range(4):
+                src[c, self.ids[k]] = (k * 4 + c) * self.pad + np.arange(self.sizes[k])
+        self.src = torch.from_numpy(src).to(device)
+        self.buf = None   # persistent exchange buffers (allocated on first use)
         self.device = device
 
 
@@ -114,19 +142,19 @@ def gather_counts(local_counts: torch.Tensor, plan: ShardPlan, group=None):
     collective of world x 4 x pad int32 (about 282 KB in total at FB15K-237-ZS), no index
     exchange (every rank knows the partition)."""
     import torch.distributed as dist
-    buf = torch.zeros((4, plan.pad), dtype=torch.int32, device=plan.device)
+    if plan.buf is None:
+        # persistent: the padding columns are never read (plan.src skips them), so no zeroing
+        plan.buf = torch.empty((4, plan.pad), dtype=torch.int32, device=plan.device)
+        plan.out = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32, device=plan.device)
+    buf, out = plan.buf, plan.out
     buf[:, :local_counts.shape[1]] = local_counts
-    out = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32, device=plan.device)
     if buf.is_cuda and dist.get_backend(group) == "gloo":  # gloo (tests): the exchange goes through host memory
         host = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32)
         dist.all_gather_into_tensor(host, buf.cpu(), group=group)
         out.copy_(host)
     else:
         dist.all_gather_into_tensor(out, buf, group=group)  # rank-major concatenation along dim 0
-    out = out.view(plan.world, 4, plan.pad)
-    full = torch.empty((4, plan.n_total), dtype=torch.int32, device=plan.device)
-    full[:, plan.dst] = out.permute(1, 0, 2).reshape(4, -1)[:, plan.cols]
-    return full
+    return torch.take(out, plan.src)   # (4, n_total) in global query order, one gather
 
 
 class ShardedLinkEvaluation:
@@ -147,7 +175,7 @@ class ShardedLinkEvaluation:
     bracket the whole replay, not the sweep kernel alone."""
 
     def __init__(self, spec, test_h, test_r, test_t, index=None, type_constrain=False, group=None,
-                 device=None, local_runner=None, graph=False):
+                 device=None, local_runner=None, graph=False, cost=None):
         import torch.distributed as dist
         from .link import HEAD, TAIL
         self.group = group
@@ -157,11 +185,14 @@ class ShardedLinkEvaluation:
         self.n = len(th)
         qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
         qm = np.concatenate([np.full(self.n, HEAD, np.int8), np.full(self.n, TAIL, np.int8)])
-        self.masks = lpt_partition(qr, self.world)
-        mine = self.masks[self.rank]
         dev = torch.device(device) if device is not None else (spec.ent.device if spec is not None else
                                                                torch.device("cpu"))
         self.device = dev
+        self.weights = None
+        if cost == "undecided" and self.world > 1 and local_runner is None and not type_constrain:
+            self.weights = calibrate_weights(spec, qh, qr, qt, qm, index, dev, group)
+        self.masks = lpt_partition(qr, self.world, weights=self.weights)
+        mine = self.masks[self.rank]
         to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         self.q = [to(qh[mine]), to(qr[mine]), to(qt[mine]), to(qm[mine])]
         self.q_host = (qh[mine], qr[mine], qt[mine], qm[mine])

@@ -34,6 +34,8 @@ def main():
                     "against 1/W of the entity tiles) instead of query-sharded")
     ap.add_argument("--graph", action="store_true", help="--emulate-world: replay each rank's local evaluation "
                     "from a hipGraph")
+    ap.add_argument("--pack", default="cost", choices=["cost", "count"],
+                    help="--emulate-world: LPT by calibrated per-query cost (bench default) or by query count")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="--emulate-world: workload (c2: the bench's trained TransE tables; c3-c5: the "
                          "structured tables of the reference fixtures)")
@@ -100,7 +102,12 @@ def emulate(a):
     qh, qr, qt = np.concatenate([th, th]), np.concatenate([tr, tr]), np.concatenate([tt, tt])
     qm = np.concatenate([np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)])
     from mmre.sharding import entity_slices
-    masks = lpt_partition(qr, a.emulate_world)
+    weights = None
+    if a.pack == "cost" and not a.entity:  # the bench's packing: one calibration evaluation's per-query costs
+        from mmre.sharding import calibrate_weights
+        weights = calibrate_weights(spec, qh, qr, qt, qm, index, dev)
+    masks = lpt_partition(qr, a.emulate_world, weights=weights)
+    print(f"packing: {'cost-weighted (calibrated undecided pairs)' if weights is not None else 'query count'}")
     slices = entity_slices(w["n_ent"], a.emulate_world)
     if a.entity:
         masks = [np.ones(2 * n, bool)] * a.emulate_world

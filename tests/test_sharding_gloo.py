@@ -111,7 +111,7 @@ def _spec(w, model, dim, dev):
                      phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
 
 
-def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_triples=None):
+def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_triples=None, cost=None):
     """Each rank: the HIP sweep on cuda:0 through ShardedLinkEvaluation.launch/finish (counts
     exchanged over gloo through host memory); rank 0 also runs the single-process evaluation
     and the out-of-order ticket sequence."""
@@ -125,14 +125,17 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_tr
     E = w["n_ent"]
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
     spec = _spec(w, model, dim, dev)
-    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev, graph=graph)
+    ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev, graph=graph,
+                               cost=cost)
+    assert (ev.weights is not None) == (cost == "undecided" and model == "transe" and world > 1)
     a = ev.launch()
     b = ev.launch()
     mb, cb = ev.finish(b)        # out of order: b first, then a third launch while a is pending
     c = ev.launch()
     ma, ca = ev.finish(a)
     mc, cc = ev.finish(c)
-    out = dict(counts_a=ca, counts_b=cb, counts_c=cc, n_local=np.array(int(ev.masks[rank].sum())))
+    out = dict(counts_a=ca, counts_b=cb, counts_c=cc, n_local=np.array(int(ev.masks[rank].sum())),
+               masks=np.stack(ev.masks))
     if rank == 0:
         m1, (h1, t1) = evaluate_link_prediction(spec, w["test_h"], w["test_r"], w["test_t"], index=index)
         out["single"] = np.concatenate([h1, t1], 1)
@@ -142,29 +145,36 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dataset,model,dim,world,graph,keep", [("FB15K-237-ZS", "transe", 200, 2, False, None),
-                                                                 ("FB15K-237-ZS", "transe", 200, 2, True, None),
-                                                                 ("DB15K-ZS", "complex", 200, 3, True, None),
-                                                                 ("FB15K-237-ZS", "rotate", 512, 8, True, None),
-                                                                 ("FB15K-237-ZS", "transe", 200, 8, True, 3)])
-def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph, keep):
+@pytest.mark.parametrize("dataset,model,dim,world,graph,keep,cost", [
+    ("FB15K-237-ZS", "transe", 200, 2, False, None, None),
+    ("FB15K-237-ZS", "transe", 200, 2, True, None, None),
+    ("DB15K-ZS", "complex", 200, 3, True, None, None),
+    ("FB15K-237-ZS", "rotate", 512, 8, True, None, None),
+    ("FB15K-237-ZS", "transe", 200, 8, True, 3, None),
+    ("FB15K-237-ZS", "transe", 200, 2, True, None, "undecided"),
+    ("FB15K-237-ZS", "transe", 200, 8, True, None, "undecided")])
+def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph, keep, cost):
     """The multi-rank path with the real HIP sweep at full size (C2; C3 with its largest
     relation split across ranks; C4 RotatE d 512 at world 8, the driver's node size, every
     rank on the one GPU of the box), eager and with each rank's local evaluation replayed from
     a hipGraph: every rank's gathered counts -- for three overlapping evaluations finished out
     of order -- and rank 0's metrics are bit-equal to one process. keep=3: three test triples
-    (6 sweeps) over 8 ranks, so two ranks own an empty shard and still join the all-gather."""
+    (6 sweeps) over 8 ranks, so two ranks own an empty shard and still join the all-gather.
+    cost="undecided": the partition packed by calibrated per-query cost (rank 0's calibration
+    broadcast: every rank holds the same masks)."""
     port = _free_port()
     res = str(tmp_path / "hip")
-    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph, keep), nprocs=world, join=True)
+    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph, keep, cost), nprocs=world, join=True)
     outs = [dict(np.load(f"{res}_{k}.npz")) for k in range(world)]
     single = outs[0]["single"]
     assert bool(outs[0]["metrics_equal"])
     for o in outs:
         for key in ("counts_a", "counts_b", "counts_c"):
             assert np.array_equal(o[key], single), key
+        assert np.array_equal(o["masks"], outs[0]["masks"])   # every rank packed the same partition
     assert sum(int(o["n_local"]) for o in outs) == single.shape[1]
-    assert max(int(o["n_local"]) for o in outs) <= -(-single.shape[1] // world)
+    if cost is None:
+        assert max(int(o["n_local"]) for o in outs) <= -(-single.shape[1] // world)
 
 
 def _entity_worker(rank, world, port, res_path, dataset, model, dim):
