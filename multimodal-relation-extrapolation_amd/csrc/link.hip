@@ -268,6 +268,83 @@ __device__ __forceinline__ int sgpr_opaque(int x) {
   return x;
 }
 
+// v_writelane_b32 with an immediate lane select (the lane must be a compile-time constant after
+// unrolling: the switch folds away). Writes the wave-uniform s into lane `lane` of v.
+template <int L>
+__device__ __forceinline__ int writelane_c(int v, int s) {
+  __asm__ volatile("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "n"(L));
+  return v;
+}
+__device__ __forceinline__ int writelane_imm(int v, int s, int lane) {
+  switch (lane) {
+    case 0: return writelane_c<0>(v, s);
+    case 1: return writelane_c<1>(v, s);
+    case 2: return writelane_c<2>(v, s);
+    case 3: return writelane_c<3>(v, s);
+    case 4: return writelane_c<4>(v, s);
+    case 5: return writelane_c<5>(v, s);
+    case 6: return writelane_c<6>(v, s);
+    case 7: return writelane_c<7>(v, s);
+    case 8: return writelane_c<8>(v, s);
+    case 9: return writelane_c<9>(v, s);
+    case 10: return writelane_c<10>(v, s);
+    case 11: return writelane_c<11>(v, s);
+    case 12: return writelane_c<12>(v, s);
+    case 13: return writelane_c<13>(v, s);
+    case 14: return writelane_c<14>(v, s);
+    case 15: return writelane_c<15>(v, s);
+    case 16: return writelane_c<16>(v, s);
+    case 17: return writelane_c<17>(v, s);
+    case 18: return writelane_c<18>(v, s);
+    case 19: return writelane_c<19>(v, s);
+    case 20: return writelane_c<20>(v, s);
+    case 21: return writelane_c<21>(v, s);
+    case 22: return writelane_c<22>(v, s);
+    case 23: return writelane_c<23>(v, s);
+    case 24: return writelane_c<24>(v, s);
+    case 25: return writelane_c<25>(v, s);
+    case 26: return writelane_c<26>(v, s);
+    case 27: return writelane_c<27>(v, s);
+    case 28: return writelane_c<28>(v, s);
+    case 29: return writelane_c<29>(v, s);
+    case 30: return writelane_c<30>(v, s);
+    case 31: return writelane_c<31>(v, s);
+    case 32: return writelane_c<32>(v, s);
+    case 33: return writelane_c<33>(v, s);
+    case 34: return writelane_c<34>(v, s);
+    case 35: return writelane_c<35>(v, s);
+    case 36: return writelane_c<36>(v, s);
+    case 37: return writelane_c<37>(v, s);
+    case 38: return writelane_c<38>(v, s);
+    case 39: return writelane_c<39>(v, s);
+    case 40: return writelane_c<40>(v, s);
+    case 41: return writelane_c<41>(v, s);
+    case 42: return writelane_c<42>(v, s);
+    case 43: return writelane_c<43>(v, s);
+    case 44: return writelane_c<44>(v, s);
+    case 45: return writelane_c<45>(v, s);
+    case 46: return writelane_c<46>(v, s);
+    case 47: return writelane_c<47>(v, s);
+    case 48: return writelane_c<48>(v, s);
+    case 49: return writelane_c<49>(v, s);
+    case 50: return writelane_c<50>(v, s);
+    case 51: return writelane_c<51>(v, s);
+    case 52: return writelane_c<52>(v, s);
+    case 53: return writelane_c<53>(v, s);
+    case 54: return writelane_c<54>(v, s);
+    case 55: return writelane_c<55>(v, s);
+    case 56: return writelane_c<56>(v, s);
+    case 57: return writelane_c<57>(v, s);
+    case 58: return writelane_c<58>(v, s);
+    case 59: return writelane_c<59>(v, s);
+    case 60: return writelane_c<60>(v, s);
+    case 61: return writelane_c<61>(v, s);
+    case 62: return writelane_c<62>(v, s);
+    case 63: return writelane_c<63>(v, s);
+    default: return v;
+  }
+}
+
 // ------------------------------------------------------------ score ops ----
 // OP: 0 TransE L1, 1 TransE L2, 2 RotatE, 3 DistMult, 4 ComplEx, 5 / 6 TransE L1 on 16-bit /
 // 8-bit codes (the integer filter; acc carries a uint32 in float bits). One k step.
@@ -797,6 +874,40 @@ struct UnitMap {
       qt = j / r;
       et = el0 + j % r;
     }
+  }
+};
+
+// Work units for a persistent grid whose P workgroups per XCD group run in lock-step windows
+// (k_sweep_bf3, round 5): the group owns the contiguous entity tiles [e_lo, e_hi); a window is
+// QB query tiles x EB entity tiles (QB x EB <= P), member m of the group always takes window
+// position (m / EB, m % EB); windows advance along the entity tiles first, then to the next QB
+// query tiles. The P concurrent units of a group therefore share QB query tiles (resident in the
+// XCD's L2 for the whole entity pass) and EB entity tiles (each fetched once per window from
+// HBM / MALL), instead of ~P different tiles of each operand (the contiguous ranges of UnitMap:
+// at C5 every unit re-streamed both 128-KB operand tiles, 120 GB per launch). A member's unit i:
+// query-block i / n_e, entity-block i % n_e (n_e = its entity windows): consecutive units of a
+// workgroup keep their query tile, so counts flush once per query block.
+struct BlockMap {
+  int count, qin, ein, QB, EB, e_lo, n_e;
+  __device__ __forceinline__ BlockMap(int grp, int n_groups, int member, int P, int n_qt, int n_et, int qb, int eb) {
+    e_lo = (int)((int64_t)n_et * grp / n_groups);
+    const int e_hi = (int)((int64_t)n_et * (grp + 1) / n_groups);
+    const int m_e = e_hi - e_lo;
+    QB = qb;
+    EB = eb;
+    qin = member / EB;
+    ein = member - qin * EB;
+    count = 0;
+    n_e = 0;
+    if (qin >= QB || m_e <= 0) return;
+    n_e = ein < m_e ? (m_e - ein + EB - 1) / EB : 0;                  // entity windows holding its column
+    const int n_q = qin < n_qt ? (n_qt - qin + QB - 1) / QB : 0;     // query windows holding its row
+    count = n_q * n_e;
+  }
+  __device__ __forceinline__ void at(int i, int& qt, int& et) const {
+    const int a = i / n_e, b = i - a * n_e;
+    qt = a * QB + qin;
+    et = e_lo + b * EB + ein;
   }
 };
 
@@ -2154,7 +2265,8 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
     const uint4* __restrict__ ent_b, int64_t e_pad, int64_t n_ent, const uint4* __restrict__ q_b, int64_t q_pad,
     int64_t n_query, int nkb, int n_et, int e_base, int n_groups, int pred_kind, float margin,
     const float* __restrict__ thr, const float* __restrict__ qn, const float* __restrict__ en, float cb,
-    int32_t* __restrict__ counts, uint32_t* __restrict__ hdr, int2* __restrict__ pairs, int64_t cap, int emajor) {
+    int32_t* __restrict__ counts, uint32_t* __restrict__ hdr, int2* __restrict__ pairs, int64_t cap, int emajor,
+    int blk_qb, int blk_eb) {
   __shared__ uint4 sq[2][TQ * 4];
   __shared__ uint4 se[2][TE * 4];
   __shared__ __attribute__((aligned(16))) float s_th[2][TQ];
@@ -2166,10 +2278,18 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
   const int lrow = lane >> 5, lcol = lane & 31;
   const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
   const int per_grp = gridDim.x / n_groups;
+  // blk_qb > 0: the lock-step window order (BlockMap, one unit range per member); else the
+  // contiguous ranges of UnitMap
+  const bool blocked = blk_qb > 0;
   const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et, emajor != 0);
-  const int u0 = (int)((int64_t)gmem * um.count / per_grp);
-  const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
+  const BlockMap bm(grp, n_groups, gmem, per_grp, (int)(q_pad / TQ), n_et, blocked ? blk_qb : 1, blocked ? blk_eb : 1);
+  const int u0 = blocked ? 0 : (int)((int64_t)gmem * um.count / per_grp);
+  const int u1 = blocked ? bm.count : (int)((int64_t)(gmem + 1) * um.count / per_grp);
   if (u0 >= u1) return;  // uniform over the workgroup
+  auto unit_at = [&](int i, int& qt, int& et) {
+    if (blocked) bm.at(i, qt, et);
+    else um.at(i, qt, et);
+  };
 
   int tpar = 0;
   int cntv = 0;  // lane L: the count of wave row L (tile row wq * 64 + L) in the current query tile
@@ -2192,7 +2312,7 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
 
   uint4 rq0, rq1, re0, re1;
   int ld_unit = u0, ld_kb = 0, ld_qt, ld_et;
-  um.at(u0, ld_qt, ld_et);
+  unit_at(u0, ld_qt, ld_et);
   auto gload = [&]() {
     const uint4* qp = q_b + ((int64_t)ld_kb * q_pad + (int64_t)ld_qt * TQ) * 4;
     const uint4* ep = ent_b + ((int64_t)ld_kb * e_pad + (int64_t)ld_et * TE) * 4;
@@ -2202,7 +2322,7 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
     re1 = ep[tid + NT];
     if (++ld_kb == nkb) {
       ld_kb = 0;
-      if (++ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
+      if (++ld_unit < u1) unit_at(ld_unit, ld_qt, ld_et);
     }
   };
   auto swrite = [&](int buf) {
@@ -2222,7 +2342,7 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
 
   int cur_qt, cur_et;
-  um.at(u0, cur_qt, cur_et);
+  unit_at(u0, cur_qt, cur_et);
   load_rows(cur_qt);
   gload();
   swrite(0);
@@ -2257,6 +2377,11 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
         const int64_t e0 = ebase + lcol, e1 = ebase + 32 + lcol;
         const bool ev0 = e0 < n_ent, ev1 = e1 < n_ent;
         const float ne0 = ev0 ? en[e0] : 0.0f, ne1 = ev1 ? en[e1] : 0.0f;
+        // this unit's per-row counts, assembled lane by lane: row L0's count into lane L0 by
+        // v_writelane (the popcounts are wave-uniform), one add into cntv at the end -- a
+        // `lane == L0 ? c : ...` select per row made the compiler keep 32 lane-compare masks
+        // live across the sweep (SGPR spills into VGPR lanes)
+        int ctmp = 0;
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -2293,9 +2418,12 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
             const int L0 = bi * 32 + (r & 3) + 8 * (r >> 2);
             const int c_lo = __popcll(m0 & 0xffffffffull) + __popcll(m1 & 0xffffffffull);
             const int c_hi = __popcll(m0 >> 32) + __popcll(m1 >> 32);
-            cntv += lane == L0 ? c_lo : (lane == L0 + 4 ? c_hi : 0);
+            ctmp = writelane_imm(ctmp, c_lo, L0);
+            ctmp = writelane_imm(ctmp, c_hi, L0 + 4);
             if (__builtin_expect(und[0] | und[1], 0)) {  // rare: list the pair(s) for exact rescoring
-              const int64_t q = q0 + row_of(bi, r);
+              // (the row from an opaque lane id: recomputed here, not 32 row indices kept live)
+              const int ol = vgpr_opaque(lane);
+              const int64_t q = q0 + wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ol >> 5);
               if (q < n_query) {
 #pragma unroll
                 for (int bj = 0; bj < 2; ++bj) {
@@ -2313,6 +2441,7 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
             }
           }
         }
+        cntv += ctmp;
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -2321,7 +2450,7 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
             for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.0f;
         const bool last = unit + 1 >= u1;
         int next_qt = cur_qt, next_et = cur_et;
-        if (!last) um.at(unit + 1, next_qt, next_et);
+        if (!last) unit_at(unit + 1, next_qt, next_et);
         if (last || next_qt != cur_qt) {  // uniform: leave this query tile
           flush_rows(cur_qt);
           if (!last) load_rows(next_qt);
@@ -2507,8 +2636,7 @@ struct EvalL1 {
   int64_t e_begin, e_cols;  // the swept slice (its columns feed M)
   int n_eblk, n_qblk;
   uint32_t* und_q;          // optional per-query rescored-pair counters (zeroed here)
-  float* pstat;             // per K1 block: max |x|, sum |x| (2 floats)
-  uint32_t* ticket;         // [0] K1's, [1] the probe's
+  uint32_t* ticket;         // [0] K1's ticket, [1] the probe's, [2] max |x| bits, [4..5] sum |x| (uint64, 2^-16)
   uint32_t* hdr;            // the L1 filter header
   double n_elem;
   float ratio;
@@ -2709,48 +2837,38 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     s_s[tid >> 6] = sa;
   }
   __syncthreads();
-  // The hand-off of the partials to the last block (MI355X_MICROARCH.md, hand-off table row 1):
-  // write-through (sc1) stores of the two floats, the storing wave's vmcnt(0) wait, then ONE
-  // agent-scope atomic add per block to the unsharded ticket; the block whose add returns
-  // gridDim - 1 is last, and reads every partial with sc1 loads after a barrier. No
-  // __threadfence(): its L2 write-back (buffer_wbl2) in each of ~3,000 blocks, each with freshly
-  // dirtied rows, serialised K1 to 163 us (measured) against ~45 us without.
+  // The hand-off to the last block (MI355X_MICROARCH.md, hand-off table row 1): each block folds
+  // its max |x| (atomicMax of the float bits: non-negative floats order as their bits) and its
+  // sum |x| (fixed point, 2^-16, into a 64-bit integer: integer adds commute, so the total is
+  // the same whatever the order) into accumulator words with agent-scope atomics, waits for them
+  // (vmcnt(0)), then adds ONE to the ticket; the block whose add returns gridDim - 1 is last and
+  // reads the two words with sc1 loads after a barrier. Round 5 history: a __threadfence() per
+  // block (L2 write-back of every block's freshly written rows) took K1 to 163 us; per-block
+  // partials read back by the last block cost a ~30 us serial tail of dependent sc1 loads.
   if (tid == 0) {
-    __hip_atomic_store(&P.pstat[2 * blockIdx.x], fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3])),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&P.pstat[2 * blockIdx.x + 1], (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    const float bm = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    const float bs = fminf((s_s[0] + s_s[1]) + (s_s[2] + s_s[3]), 0x1p31f);  // (clamped: only the fallback test reads it)
+    __hip_atomic_fetch_max(&P.ticket[2], __float_as_uint(bm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(P.ticket + 4),
+                           (unsigned long long)(bs * 65536.0f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     s_last = __hip_atomic_fetch_add(&P.ticket[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   }
   __syncthreads();
   if (!s_last) return;
-  const int nb = (int)gridDim.x;
-  float m = 0.0f, s = 0.0f;
-  for (int b = tid; b < nb; b += 256) {  // fixed order per thread, fixed tree below: deterministic
-    m = fmaxf(m, __hip_atomic_load(&P.pstat[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    s += __hip_atomic_load(&P.pstat[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    m = fmaxf(m, __shfl_xor(m, o));
-    s += __shfl_xor(s, o);
-  }
-  __syncthreads();
-  if ((tid & 63) == 0) {
-    s_m[tid >> 6] = m;
-    s_s[tid >> 6] = s;
-  }
-  __syncthreads();
   // zero the rest of the header (probe count, largest offset, guard, undecided slots)
   for (int i = 2 + tid; i < L1Q_PART / 4; i += 256) P.hdr[i] = 0u;
   if (tid == 0) {
-    const float M = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
-    const float sum = (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]);
+    const float M = __uint_as_float(__hip_atomic_load(&P.ticket[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const double sum = (double)__hip_atomic_load(reinterpret_cast<unsigned long long*>(P.ticket + 4),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / 65536.0;
     // the fallback test of l1q_fallback: M non-finite, or M > ratio x mean |x|
-    const bool fb = !(M < INFINITY) || (double)M > (double)P.ratio * ((double)sum / P.n_elem);
+    const bool fb = !(M < INFINITY) || (double)M > (double)P.ratio * (sum / P.n_elem);
     P.hdr[0] = __float_as_uint(M < INFINITY ? M : INFINITY);
     P.hdr[1] = fb ? L1Q_F32 : L1Q_CODES8;
+    P.ticket[2] = 0u;  // the accumulators start at 0 for the next call
+    P.ticket[4] = 0u;
+    P.ticket[5] = 0u;
     P.ticket[0] = 0u;
     P.ticket[1] = 0u;
   }
@@ -3396,6 +3514,24 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
                         d_counts, nullptr, gate, true);
 }
 
+// The lock-step window QB x EB for P workgroups per XCD group (BlockMap): about 8 query tiles
+// (MMRE_BF3_QB) by P / QB entity tiles, evened out so the last window along each axis is not
+// mostly empty (C5: P 96, 64 query tiles, 976 entity tiles per group -> 8 x 12; C3: 89 x 12-13
+// -> 7 x 13).
+static void bf3_window(int P, int n_qt, int m_e, int& qb, int& eb) {
+  static const char* qb_env = getenv("MMRE_BF3_QB");
+  int q = qb_env ? atoi(qb_env) : 8;
+  q = std::max(1, std::min(q, std::min(P, n_qt)));
+  int e = std::max(1, std::min(P / q, m_e));
+  const int ne = (m_e + e - 1) / e;      // windows along the entity tiles, then even them out
+  e = (m_e + ne - 1) / ne;
+  q = std::max(1, std::min(P / e, n_qt));
+  const int nq = (n_qt + q - 1) / q;
+  q = (n_qt + nq - 1) / nq;
+  qb = q;
+  eb = e;
+}
+
 extern "C" int64_t mmre_link_bf3_workspace(int model, int dim, int64_t e_pad, int64_t q_pad) {
   if (!mfma_model(model) || dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
   const int64_t ktot = (int64_t)n_planes(model) * plane_rows(model, dim);
@@ -3455,16 +3591,23 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
   static const char* order_env = getenv("MMRE_MFMA_EMAJOR");
   const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
+  static const char* blk_env = getenv("MMRE_BF3_BLOCKED"); /* A/B: 0 = the contiguous unit ranges */
+  const bool blocked = !(blk_env && blk_env[0] == '0');
 #define MMRE_BF3(PKV)                                                                                           \
   do {                                                                                                          \
     const int res = resident_groups((const void*)k_sweep_bf3<PKV>, NT);                                        \
     const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                        \
     int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;              \
+    int bq = 0, be = 0;                                                                                        \
+    if (blocked && n_et >= 8 && res % 8 == 0) { /* the lock-step windows: one resident wave of workgroups */  \
+      g = res;                                                                                                  \
+      bf3_window(res / 8, (int)(q_pad / TQ), n_et / 8, bq, be);                                                \
+    }                                                                                                           \
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                           \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                          \
     hipLaunchKernelGGL((k_sweep_bf3<PKV>), dim3((unsigned)g), dim3(NT), 0, st, eb, e_pad, n_slice, qb, q_pad,   \
                        n_query, ktot / 16, n_et, (int)e_begin, ng, pred_kind, margin, d_truth, qn, en, cb,     \
-                       d_counts, hdr, pairs, cap, emajor);                                                     \
+                       d_counts, hdr, pairs, cap, emajor, bq, be);                                             \
     MMRE_CHECK_LAUNCH();                                                                                       \
     hipLaunchKernelGGL((k_bf3_fallback_zero), dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, hdr,  \
                        d_counts, n_query);                                                                     \
@@ -3497,11 +3640,7 @@ static int eval_rb(int kp) { return stage_rows(2 * kp + 1); }  // K1's query blo
 // the 16-bit codes' row-major copies (the 8-bit sweep's second rescoring level) when their
 // staging fits K2's LDS (k2 <= 256 words: dim <= 504)
 static bool eval_rows16(int dim) { return l1q_rows(dim) <= 256; }
-static int64_t eval_stat_bytes(int dim, int64_t e_pad, int64_t q_pad) {
-  const int rb = eval_rb(plane_rows(MMRE_TRANSE_L1, dim));
-  const int64_t nblk = (e_pad + rb - 1) / rb + (q_pad + rb - 1) / rb;
-  return round_up(256 + 8 * nblk, 256);  // tickets, then K1's per-block statistics
-}
+static int64_t eval_stat_bytes(int, int64_t, int64_t) { return 256; }  // tickets and K1's accumulators
 static int64_t eval_extra_bytes(int dim, int64_t e_pad, int64_t q_pad) {
   const int64_t rows16 = eval_rows16(dim) ? 4 * (int64_t)l1q_rows(dim) * (q_pad + e_pad) : 0;
   return eval_stat_bytes(dim, e_pad, q_pad) + rows16;
@@ -3545,7 +3684,6 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   float* q_l1c = (float*)(ve + (int64_t)k4 * e_pad);
   char* extra = w + mmre_link_l1q_workspace(dim, e_pad, q_pad);
   uint32_t* ticket = (uint32_t*)extra;  // zero before the first call (the caller zeroes the workspace once)
-  float* pstat = (float*)(extra + 256);
   static const char* lvl2_env = getenv("MMRE_L1_RESCORE16");  /* A/B: 0 = the f32 chain for every pair */
   const bool rows16 = eval_rows16(dim) && !(lvl2_env && lvl2_env[0] == '0');
   uint32_t* q16r = rows16 ? (uint32_t*)(extra + eval_stat_bytes(dim, e_pad, q_pad)) : nullptr;
@@ -3584,7 +3722,6 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   P.n_eblk = (int)((e_pad + rb - 1) / rb);
   P.n_qblk = (int)((q_pad + rb - 1) / rb);
   P.und_q = d_undecided_q;
-  P.pstat = pstat;
   P.ticket = ticket;
   P.hdr = hdr;
   P.n_elem = (double)kp * (double)(q_pad + e_cols);
