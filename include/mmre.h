@@ -167,9 +167,7 @@ int64_t mmre_link_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad);
  * same either way. d_out[2] = undecided-list entries the rescoring refused because their query
  * or entity id was out of range (a guard on the list's invariant: 0 unless the build is
  * defective), d_out[3] = the largest per-entity error offset of the 8-bit codes' tight bound (in
- * code steps; 0 with the uniform bound), d_out[4] = pairs of the 8-bit band that the second
- * rescoring level (16-bit row codes, mmre_link_evaluate_l1q) left to the f32 chain. d_out holds
- * 5 uint64. */
+ * code steps; 0 with the uniform bound). d_out holds 4 uint64. */
 int mmre_link_l1q_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream);
 int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_ent_km, const float* d_ent_rows, int64_t n_ent,
                         int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km, const float* d_q_rows,

@@ -455,9 +455,6 @@ struct L1Q {
   const float* q_l1c;      // 8-bit codes, tight bound: per query row sum |eps_q| (upper bound); nullptr: uniform bound
   uint32_t* guard;         // hdr[4]: pairs the rescoring refused (query or entity id out of range; must stay 0)
   uint32_t* und_q;         // optional per-query count of rescored pairs (cost calibration of the sharding)
-  const uint32_t* q16r;    // 8-bit sweeps, prediction = the score: row-major 16-bit code rows (k2w words
-  const uint32_t* e16r;    // per row; whole table for the entities) -- the rescoring's second level; nullptr: none
-  int k2w;
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
@@ -1087,37 +1084,6 @@ __device__ __forceinline__ void sweep_valu_body(
     }
     if (l1.und_q) atomicAdd(&l1.und_q[q], 1u);
     const float th = thr[q];
-    if constexpr (OP == 6 && PK == 0) {
-      // second level: the pair's 16-bit codes (row-major copies: 2 x k2w words, one v_sad_u16 per
-      // two elements) decide ~99 % of the 8-bit band's pairs under the 16-bit codes' uniform bound
-      // (the 16-bit sweep's test, load_meta's l1_int_thresholds at delta16 = 2M / 65535); only
-      // what stays undecided there takes the f32 chain (half the bytes of the f32 rows, a quarter
-      // of the VALU: the 8-bit band's rescoring was what a rank's share of a few dense relations
-      // paid for)
-      if (l1.q16r != nullptr) {
-        const uint4* a = reinterpret_cast<const uint4*>(l1.q16r + q * (int64_t)l1.k2w);
-        const uint4* b = reinterpret_cast<const uint4*>(l1.e16r + (int64_t)(e + e_base) * l1.k2w);
-        uint32_t s16 = 0u;
-#pragma unroll 5
-        for (int i = 0; i < l1.k2w / 4; ++i) {
-          const uint4 x = a[i], y = b[i];
-          s16 = __builtin_amdgcn_sad_u16(x.x, y.x, s16);
-          s16 = __builtin_amdgcn_sad_u16(x.y, y.y, s16);
-          s16 = __builtin_amdgcn_sad_u16(x.z, y.z, s16);
-          s16 = __builtin_amdgcn_sad_u16(x.w, y.w, s16);
-        }
-        const float d16 = l1q_delta(l1.hdr, 65535.0f);
-        const float f16 = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
-        uint32_t t_sure, t_span;
-        l1_int_thresholds(th, __builtin_fmaf((float)l1.kt * 1.03f, d16, 0x1p-120f), d16, f16, 0u, t_sure, t_span);
-        if (s16 < t_sure) {  // S < th for sure
-          atomicAdd(&counts[q], 1);
-          return;
-        }
-        if (s16 - t_sure >= t_span) return;  // S >= th for sure
-        atomicAdd(l1.guard + 1, 1u);  // hdr[5]: pairs left to the f32 chain (the second level's record)
-      }
-    }
     const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
     if (pred(sx) < th) {
       atomicAdd(&counts[q], 1);
@@ -2074,9 +2040,7 @@ __global__ __launch_bounds__(256) void k_l1q_quant8(L1QPlane pq, L1QPlane pe, in
 // 0.77 % / 1.18 % took 0.32 / 0.51 ms against 0.26 ms with 16-bit codes (profiles/r4).
 constexpr int L1Q_PROBE_Q = 512, L1Q_PROBE_E = 256;
 constexpr double L1Q_PROBE_FRAC = 0.006;  // undecided fraction of the sample above which 16-bit codes
-// the same with the second rescoring level (16-bit row codes before the f32 chain: an undecided
-// pair costs ~3x less, so the 8-bit codes pay up to a wider band)
-constexpr double L1Q_PROBE_FRAC_L2 = 0.02;
+
 __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ uq, int64_t q_pad, int64_t n_query,
                                                    const uint32_t* __restrict__ ue, int64_t e_pad, int64_t n_slice,
                                                    int kw, int kt, const float* __restrict__ thr, int pred_kind,
@@ -2133,9 +2097,8 @@ __global__ __launch_bounds__(256) void k_zero_words(uint32_t* __restrict__ p, in
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = 0u;
 }
 
-// Sum of the undecided-pair slots, the code-width word, the rescoring guard's count, the largest
-// error offset of the tight bound and the pairs the second level left to the f32 chain -> out[0..4]
-// (mmre_link_l1q_stats).
+// Sum of the undecided-pair slots, the code-width word, the rescoring guard's count and the largest
+// error offset of the tight bound -> out[0..3] (mmre_link_l1q_stats).
 __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long long* __restrict__ out) {
   if (threadIdx.x != 0) return;
   const unsigned long long* sl =
@@ -2146,7 +2109,6 @@ __global__ void k_l1q_stats(const uint32_t* __restrict__ work, unsigned long lon
   out[1] = work[1];
   out[2] = work[4];
   out[3] = work[3];
-  out[4] = work[5];
 }
 
 static int l1q_rows(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1, dim) + 1) / 2, KC); }
@@ -2603,23 +2565,29 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
 // independent fused into the same launch (block ranges of one grid doing different work):
 //   K1 k_eval_prep        entity rows (normalised, k-major + row-major) | query rows, each
 //                         query block normalising its own anchor and truth rows from the raw
-//                         table (no dependency on the entity blocks), the truth scores, and
-//                         per block max |x| / sum |x| of the planes; the last block (ticket)
-//                         reduces them to M, decides codes vs the f32 fallback, zeroes the
-//                         filter header
+//                         table (no dependency on the entity blocks), the truth scores; per
+//                         block max |x| / sum |x| of the planes (plain stores); block 0 zeroes
+//                         the filter header
 //   K2 k_eval_quant_list  filter-list scores | 8-bit codes + the tight bound's error sums +
-//                         16-bit codes, one read of the planes
-//   K3 k_eval_count_probe filter counts per group | the code-width probe (last probe block
-//                         decides 8 vs 16 bits)
+//                         16-bit codes, one read of the planes; every quantization block reduces
+//                         K1's per-block statistics itself (same order: the same M everywhere),
+//                         the first writes M and the codes / f32 word
+//   K3 k_eval_count_probe filter counts, a wave per group | the code-width probe, a wave per
+//                         sampled query (the last of its 128 blocks decides 8 vs 16 bits)
 //   K4-K6                 the three gated sweeps (8-bit, 16-bit, f32; the code-width word
 //                         names the one that counts), then k_counts_finalize
+// No cross-workgroup hand-off inside K1 / K2: grid-wide results pass at kernel boundaries.
+// Measured on the way (MI355X, C2, per evaluation): a __threadfence() per K1 block (L2
+// write-back of each block's freshly written rows) 163 us for K1; per-block partials read back by
+// a ticket's last block ~30 us of serial sc1 loads; three same-address atomics per block
+// (max, sum, ticket: ~3,100 blocks) 128 us -- same-address atomics serialise at ~13 ns each.
 // Values are bit-identical to the separate path (same canonical chains in the same order):
 // tests/test_eval_fused_gpu.py holds counts, truths and planes equal.
 struct EvalL1 {
   const float* ent;      // raw entity table (n_ent, dim)
   const float* rel;      // raw relation table (n_rel, dim)
   int64_t n_ent;
-  int dim, kp, norm, rb;
+  int dim, kp, norm, rb, rbq;  // rows per entity block, queries per query block (two row sets)
   const int64_t* qh;
   const int64_t* qr;
   const int64_t* qt;
@@ -2636,7 +2604,8 @@ struct EvalL1 {
   int64_t e_begin, e_cols;  // the swept slice (its columns feed M)
   int n_eblk, n_qblk;
   uint32_t* und_q;          // optional per-query rescored-pair counters (zeroed here)
-  uint32_t* ticket;         // [0] K1's ticket, [1] the probe's, [2] max |x| bits, [4..5] sum |x| (uint64, 2^-16)
+  float* pstat;             // per K1 block: max |x|, sum |x|
+  uint32_t* ticket;         // [1]: the probe's ticket
   uint32_t* hdr;            // the L1 filter header
   double n_elem;
   float ratio;
@@ -2674,8 +2643,7 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
   __shared__ int s_head[32];
   __shared__ float s_rn[32];
   __shared__ float s_m[4], s_s[4];
-  __shared__ uint32_t s_last;
-  const int kp = P.kp, kt = kp, ls = kt + 1, rb = P.rb, dim = P.dim;
+  const int kp = P.kp, kt = kp, ls = kt + 1, rb = P.rb, rbq = P.rbq, dim = P.dim;
   const int tid = threadIdx.x, lane = tid & 31, slot = tid >> 5;
   float mx = 0.0f, sa = 0.0f;
   if ((int)blockIdx.x < P.n_eblk) {  // ---- entity rows (k_prep_rows for TransE)
@@ -2710,9 +2678,9 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     }
     write_k_major(lds, ls, rb, kt, P.ent_km, P.e_pad, e0);
   } else {  // ---- query rows: q = h + r (tail) / -(r - t) (head), and the truth scores
-    const int64_t q0 = (int64_t)(blockIdx.x - P.n_eblk) * rb;
-    float* y0 = lds + rb * ls;  // the truth rows
-    if (tid < rb) {
+    const int64_t q0 = (int64_t)(blockIdx.x - P.n_eblk) * rbq;
+    float* y0 = lds + rbq * ls;  // the truth rows
+    if (tid < rbq) {
       const int64_t q = q0 + tid;
       int64_t a = -1, tr = -1, r = 0;
       int head = 0;
@@ -2759,7 +2727,7 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
       }
     }
     __syncthreads();
-    for (int i = slot; i < rb; i += 8) {
+    for (int i = slot; i < rbq; i += 8) {
       const int64_t a = s_a[i], tr = s_t[i];
       float* x = lds + i * ls;
       float* y = y0 + i * ls;
@@ -2771,16 +2739,16 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     }
     __syncthreads();
     if (P.norm) {  // the anchor and truth rows normalised exactly as k_prep_rows does
-      if (tid < 2 * rb) s_nrm[tid] = canon_norm(lds + tid * ls, dim);  // rows 0..rb-1: x, rb..2rb-1: y
+      if (tid < 2 * rbq) s_nrm[tid] = canon_norm(lds + tid * ls, dim);  // rows 0..rbq-1: x, rbq..2rbq-1: y
       __syncthreads();
-      for (int i = slot; i < 2 * rb; i += 8) {
+      for (int i = slot; i < 2 * rbq; i += 8) {
         float* x = lds + i * ls;
         const float nr = s_nrm[i];
         for (int k = lane; k < kt; k += 32) x[k] = x[k] / nr;
       }
       __syncthreads();
     }
-    for (int i = slot; i < rb; i += 8) {
+    for (int i = slot; i < rbq; i += 8) {
       float* x = lds + i * ls;
       const bool valid = s_a[i] >= 0;
       const int64_t r = s_r[i];
@@ -2796,7 +2764,7 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
       }
     }
     __syncthreads();
-    if (tid < rb && q0 + tid < P.n_query) {  // the truth's score: the canonical chain, k ascending
+    if (tid < rbq && q0 + tid < P.n_query) {  // the truth's score: the canonical chain, k ascending
       const float* x = lds + tid * ls;
       const float* y = y0 + tid * ls;
       float acc = 0.0f;
@@ -2814,8 +2782,8 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
       for (; k < kp; ++k) acc = acc + fabsf(x[k] - y[k]);
       P.truth[q0 + tid] = acc;  // prediction = the score (TransE.py:104-110)
     }
-    write_k_major(lds, ls, rb, kt, P.q_km, P.q_pad, q0);
-    for (int i = slot; i < rb; i += 8) {
+    write_k_major(lds, ls, rbq, kt, P.q_km, P.q_pad, q0);
+    for (int i = slot; i < rbq; i += 8) {
       const int64_t q = q0 + i;
       const float* x = lds + i * ls;
       if (q < P.n_query) {
@@ -2826,7 +2794,8 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
         for (int k = lane; k < kt; k += 32) abs_stat(x[k], mx, sa);
     }
   }
-  // ---- the block's |x| statistics, then the last block's reduction (ticket)
+  // ---- the block's |x| statistics (K2 reduces them); block 0 zeroes the filter header's
+  // counters (probe count, largest offset, guard, undecided slots) for K2 / K3 / the sweeps
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     mx = fmaxf(mx, __shfl_xor(mx, o));
@@ -2837,41 +2806,12 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     s_s[tid >> 6] = sa;
   }
   __syncthreads();
-  // The hand-off to the last block (MI355X_MICROARCH.md, hand-off table row 1): each block folds
-  // its max |x| (atomicMax of the float bits: non-negative floats order as their bits) and its
-  // sum |x| (fixed point, 2^-16, into a 64-bit integer: integer adds commute, so the total is
-  // the same whatever the order) into accumulator words with agent-scope atomics, waits for them
-  // (vmcnt(0)), then adds ONE to the ticket; the block whose add returns gridDim - 1 is last and
-  // reads the two words with sc1 loads after a barrier. Round 5 history: a __threadfence() per
-  // block (L2 write-back of every block's freshly written rows) took K1 to 163 us; per-block
-  // partials read back by the last block cost a ~30 us serial tail of dependent sc1 loads.
   if (tid == 0) {
-    const float bm = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
-    const float bs = fminf((s_s[0] + s_s[1]) + (s_s[2] + s_s[3]), 0x1p31f);  // (clamped: only the fallback test reads it)
-    __hip_atomic_fetch_max(&P.ticket[2], __float_as_uint(bm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(P.ticket + 4),
-                           (unsigned long long)(bs * 65536.0f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add(&P.ticket[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    P.pstat[2 * blockIdx.x] = fmaxf(fmaxf(s_m[0], s_m[1]), fmaxf(s_m[2], s_m[3]));
+    P.pstat[2 * blockIdx.x + 1] = (s_s[0] + s_s[1]) + (s_s[2] + s_s[3]);
   }
-  __syncthreads();
-  if (!s_last) return;
-  // zero the rest of the header (probe count, largest offset, guard, undecided slots)
-  for (int i = 2 + tid; i < L1Q_PART / 4; i += 256) P.hdr[i] = 0u;
-  if (tid == 0) {
-    const float M = __uint_as_float(__hip_atomic_load(&P.ticket[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const double sum = (double)__hip_atomic_load(reinterpret_cast<unsigned long long*>(P.ticket + 4),
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) / 65536.0;
-    // the fallback test of l1q_fallback: M non-finite, or M > ratio x mean |x|
-    const bool fb = !(M < INFINITY) || (double)M > (double)P.ratio * (sum / P.n_elem);
-    P.hdr[0] = __float_as_uint(M < INFINITY ? M : INFINITY);
-    P.hdr[1] = fb ? L1Q_F32 : L1Q_CODES8;
-    P.ticket[2] = 0u;  // the accumulators start at 0 for the next call
-    P.ticket[4] = 0u;
-    P.ticket[5] = 0u;
-    P.ticket[0] = 0u;
-    P.ticket[1] = 0u;
-  }
+  if (blockIdx.x == 0)
+    for (int i = 2 + tid; i < L1Q_PART / 4; i += 256) P.hdr[i] = 0u;
 }
 
 // The filter-list score of one entry (k_filter_scores' list task, TransE L1, prediction = the
@@ -2916,8 +2856,6 @@ struct EvalQuant {  // K2's quantization operands (k_l1q_quant8<TIGHT> + the 16-
   L1QPlane pq, pe;  // 8-bit planes
   uint32_t* out16q;
   uint32_t* out16e;
-  uint32_t* rows16q;  // row-major 16-bit code rows (k2 words per row; nullptr: not made)
-  uint32_t* rows16e;
   int kw, k2, kt, n_blk;  // 8-bit word rows, 16-bit word rows, floats per row, blocks per plane
   int tight;
   float* q_l1c;
@@ -2937,9 +2875,40 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
     list_v[p] = l1_row_score64(P.q_rows + vq * P.kp, P.ent_rows + j * P.kp, P.kp);
     return;
   }
+  // ---- M and the codes / f32 decision from K1's per-block statistics: every quantization block
+  // reduces them in the same order (the same M and decision everywhere, deterministic); the
+  // first one publishes them in the header for K3 and the sweeps (the l1q_fallback test:
+  // M non-finite, or M > ratio x mean |x|)
+  __shared__ float s_rm[4], s_rs[4];
+  {
+    const int nst = P.n_eblk + P.n_qblk;
+    float m = 0.0f, sm = 0.0f;
+#pragma unroll 8
+    for (int i = threadIdx.x; i < nst; i += 256) {
+      const float2 v = reinterpret_cast<const float2*>(P.pstat)[i];
+      m = fmaxf(m, v.x);
+      sm += v.y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      m = fmaxf(m, __shfl_xor(m, o));
+      sm += __shfl_xor(sm, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      s_rm[threadIdx.x >> 6] = m;
+      s_rs[threadIdx.x >> 6] = sm;
+    }
+    __syncthreads();
+  }
+  const float mx = fmaxf(fmaxf(s_rm[0], s_rm[1]), fmaxf(s_rm[2], s_rm[3]));
+  const float msum = (s_rs[0] + s_rs[1]) + (s_rs[2] + s_rs[3]);
+  const bool fb = !(mx < INFINITY) || (double)mx > (double)P.ratio * ((double)msum / P.n_elem);
+  if ((int)blockIdx.x == n_lblk && threadIdx.x == 0) {
+    P.hdr[0] = __float_as_uint(mx < INFINITY ? mx : INFINITY);
+    P.hdr[1] = fb ? L1Q_F32 : L1Q_CODES8;
+  }
+  if (fb) return;  // the f32 sweep counts: no codes
   // ---- the codes: 8-bit words (+ the tight bound's error row) and 16-bit words in one pass
-  const uint32_t* work = P.hdr;
-  if (__builtin_amdgcn_readfirstlane(work[1]) == L1Q_F32) return;  // K1 chose the f32 sweep
   const int b = (int)blockIdx.x - n_lblk;
   const bool ent = b >= Q.n_blk;
   const int bx = ent ? b - Q.n_blk : b;
@@ -2948,10 +2917,7 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
   const int64_t pad = pl.pad, c0 = pl.c0, n = pl.n;
   uint32_t* __restrict__ out = pl.out;
   uint32_t* __restrict__ out16 = ent ? Q.out16e : Q.out16q;
-  uint32_t* __restrict__ rows16 = ent ? Q.rows16e : Q.rows16q;
-  extern __shared__ uint32_t s16[];  // [32][k2 + 1]: the 16-bit words staged for the row-major copy
   const int kp = P.kp, kw = Q.kw, k2 = Q.k2, kt = Q.kt;
-  const float mx = __uint_as_float(work[0]);
   const float inv = (mx > 0.0f && mx < INFINITY) ? 255.0f / (2.0f * mx) : 0.0f;
   const float inv16 = (mx > 0.0f && mx < INFINITY) ? 65535.0f / (2.0f * mx) : 0.0f;
   const float off = (mx < INFINITY) ? mx : 0.0f;
@@ -2989,18 +2955,6 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
         if (2 * r < k2) out16[(int64_t)(2 * r) * pad + c] = w16a;
         if (2 * r + 1 < k2) out16[(int64_t)(2 * r + 1) * pad + c] = w16b;
       }
-      if (rows16 != nullptr) {
-        if (2 * r < k2) s16[cl * (k2 + 1) + 2 * r] = w16a;
-        if (2 * r + 1 < k2) s16[cl * (k2 + 1) + 2 * r + 1] = w16b;
-      }
-    }
-    if (rows16 != nullptr) {  // the 32 columns' rows, written whole (consecutive threads: consecutive words)
-      __syncthreads();
-      for (int i = threadIdx.x; i < 32 * k2; i += 256) {
-        const int col = i / k2, wd = i - col * k2;
-        if (cb + col < n) rows16[(c0 + cb + col) * (int64_t)k2 + wd] = s16[col * (k2 + 1) + wd];
-      }
-      __syncthreads();
     }
     if (Q.tight) {
       s_err[g][cl] = err;
@@ -3032,26 +2986,28 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
   }
 }
 
-// K3: filter counts (one 64-thread block per filter group, k_filter_count without type masks)
-// | the code-width probe (k_l1q_probe's sample), whose last block (ticket) turns the code-width
-// word to the 16-bit codes when the sample's undecided fraction is over L1Q_PROBE_FRAC.
-// force_bits 8 / 16 (MMRE_L1_BITS): no probe; 16 sets the word (unless the f32 fallback).
-__global__ __launch_bounds__(64) void k_eval_count_probe(
+// K3: filter counts (k_filter_count without type masks, one WAVE per filter group, four per
+// block) | the code-width probe (k_l1q_probe's sample, one wave per sampled query: 128 blocks, so
+// the probe's count and ticket take 128 same-address atomics each, not 512), whose last block
+// turns the code-width word to the 16-bit codes when the sample's undecided fraction is over
+// the threshold. force_bits 8 / 16 (MMRE_L1_BITS): no probe; 16 sets the word (unless f32).
+__global__ __launch_bounds__(256) void k_eval_count_probe(
     const int64_t* __restrict__ grp_qoff, const int32_t* __restrict__ grp_q, int64_t n_groups, int n_cblk,
     const int64_t* __restrict__ off, const int32_t* __restrict__ ids, const float* __restrict__ list_v,
     const int32_t* __restrict__ qtrue, const float* __restrict__ thr, int64_t n_query, int64_t n_ent,
     int32_t* __restrict__ counts, const uint32_t* __restrict__ uq, int64_t q_pad, const uint32_t* __restrict__ ue,
     int64_t e_pad, int64_t n_slice, int kw, int kt, const float* __restrict__ q_l1c, uint32_t* __restrict__ hdr,
     uint32_t* __restrict__ ticket, uint32_t probe_max, int force_bits) {
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if ((int)blockIdx.x < n_cblk) {
-    __shared__ __attribute__((aligned(16))) int32_t s_id[64];
-    __shared__ __attribute__((aligned(16))) float s_v[64];
-    for (int64_t g = blockIdx.x; g < n_groups; g += n_cblk) {
+    // the wave's own LDS slices: written and read by the same wave (wave barriers, no block sync)
+    __shared__ __attribute__((aligned(16))) int32_t s_id[4][64];
+    __shared__ __attribute__((aligned(16))) float s_v[4][64];
+    for (int64_t g = (int64_t)blockIdx.x * 4 + wv; g < n_groups; g += (int64_t)n_cblk * 4) {
       const int64_t qa = grp_qoff[g], qb = grp_qoff[g + 1];
       const int64_t la = off[g], lb = off[g + 1];
       for (int64_t qc = qa; qc < qb; qc += 64) {
-        const int64_t qi = qc + tid;
+        const int64_t qi = qc + lane;
         const bool active = qi < qb;
         const int64_t q = active ? grp_q[qi] : 0;
         const int32_t tr = active ? qtrue[q] : -1;
@@ -3059,27 +3015,27 @@ __global__ __launch_bounds__(64) void k_eval_count_probe(
         int c = 0;
         for (int64_t lc = la; lc < lb; lc += 64) {
           const int nl = (int)((lb - lc) < 64 ? (lb - lc) : 64);
-          __syncthreads();  // s_* reuse
-          {
-            int32_t id = -1;
-            float v = 0.0f;
-            if (tid < nl) {
-              const int64_t j = ids[lc + tid];
-              if (j >= 0 && j < n_ent) {
-                id = (int32_t)j;
-                v = list_v[lc + tid];
-              }
+          int32_t id = -1;
+          float v = 0.0f;
+          if (lane < nl) {
+            const int64_t j = ids[lc + lane];
+            if (j >= 0 && j < n_ent) {
+              id = (int32_t)j;
+              v = list_v[lc + lane];
             }
-            s_id[tid] = id;  // entries nl..63 stay invalid: the loop below reads whole quads
-            s_v[tid] = v;
           }
-          __syncthreads();
+          __builtin_amdgcn_wave_barrier();  // the previous round's reads are done
+          s_id[wv][lane] = id;  // entries nl..63 stay invalid: the loop below reads whole quads
+          s_v[wv][lane] = v;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           if (active) {
             for (int i = 0; i < nl; i += 4) {  // branch-free, 4 entries per LDS read
-              const int4 e = *reinterpret_cast<const int4*>(&s_id[i]);
-              const float4 v = *reinterpret_cast<const float4*>(&s_v[i]);
-              c += ((e.x >= 0) & (e.x != tr) & (v.x < th)) + ((e.y >= 0) & (e.y != tr) & (v.y < th)) +
-                   ((e.z >= 0) & (e.z != tr) & (v.z < th)) + ((e.w >= 0) & (e.w != tr) & (v.w < th));
+              const int4 e = *reinterpret_cast<const int4*>(&s_id[wv][i]);
+              const float4 vv = *reinterpret_cast<const float4*>(&s_v[wv][i]);
+              c += ((e.x >= 0) & (e.x != tr) & (vv.x < th)) + ((e.y >= 0) & (e.y != tr) & (vv.y < th)) +
+                   ((e.z >= 0) & (e.z != tr) & (vv.z < th)) + ((e.w >= 0) & (e.w != tr) & (vv.w < th));
             }
           }
         }
@@ -3100,10 +3056,10 @@ __global__ __launch_bounds__(64) void k_eval_count_probe(
     return;
   }
   if (w != L1Q_CODES8) return;  // the f32 fallback: no codes to probe
-  const int pb = (int)blockIdx.x - n_cblk, n_pb = (int)gridDim.x - n_cblk;
+  const int pb = ((int)blockIdx.x - n_cblk) * 4 + wv, n_pb = ((int)gridDim.x - n_cblk) * 4;
   const int64_t q = (int64_t)pb * n_query / n_pb;
   const int64_t span = n_slice > L1Q_PROBE_E ? n_slice - L1Q_PROBE_E : 0;
-  const int64_t c = (((int64_t)pb * span / n_pb) & ~(int64_t)3) + 4 * tid;
+  const int64_t c = (((int64_t)pb * span / n_pb) & ~(int64_t)3) + 4 * lane;
   const float l1d = l1q_delta(hdr, 255.0f);
   const float l1f = (float)(kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
   const float l1c = __builtin_fmaf((float)kt * 1.03f, l1d, 0x1p-120f);
@@ -3127,11 +3083,16 @@ __global__ __launch_bounds__(64) void k_eval_count_probe(
   for (int j = 0; j < 4; ++j) und += (uint32_t)((acc[j] - t_sure < t_span) & (c + j < n_slice));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) und += __shfl_xor(und, o);
+  __shared__ uint32_t s_und[4];
   __shared__ uint32_t s_last;
-  if (tid == 0) {  // the counts reach the last probe block as in K1's hand-off (no __threadfence)
-    if (und) __hip_atomic_fetch_add(hdr + 2, und, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) s_und[wv] = und;
+  __syncthreads();
+  if (tid == 0) {  // the block's count, then the ticket (the hand-off of K1's table row 1: atomics, vmcnt(0))
+    const uint32_t bu = (s_und[0] + s_und[1]) + (s_und[2] + s_und[3]);
+    if (bu) __hip_atomic_fetch_add(hdr + 2, bu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_last = __hip_atomic_fetch_add(&ticket[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)n_pb - 1;
+    s_last = __hip_atomic_fetch_add(&ticket[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (uint32_t)(gridDim.x - n_cblk) - 1;
   }
   __syncthreads();
   if (s_last && tid == 0) {
@@ -3636,14 +3597,16 @@ extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, con
 }
 
 // ---------------------------------------- fused TransE L1 evaluation (round 5) ---
-static int eval_rb(int kp) { return stage_rows(2 * kp + 1); }  // K1's query blocks stage two row sets
-// the 16-bit codes' row-major copies (the 8-bit sweep's second rescoring level) when their
-// staging fits K2's LDS (k2 <= 256 words: dim <= 504)
-static bool eval_rows16(int dim) { return l1q_rows(dim) <= 256; }
-static int64_t eval_stat_bytes(int, int64_t, int64_t) { return 256; }  // tickets and K1's accumulators
+// K1's blocks: rb entity rows, or rb / 2 queries with their truth rows (two row sets): the
+// same LDS, 16 rows of kt + 1 floats at C2 (12.9 KB)
+static int eval_rb(int kp) { return stage_rows(kp); }
+static int eval_rbq(int kp) { return std::max(1, eval_rb(kp) / 2); }
+static int64_t eval_blocks(int dim, int64_t e_pad, int64_t q_pad) {
+  const int kp = plane_rows(MMRE_TRANSE_L1, dim);
+  return (e_pad + eval_rb(kp) - 1) / eval_rb(kp) + (q_pad + eval_rbq(kp) - 1) / eval_rbq(kp);
+}
 static int64_t eval_extra_bytes(int dim, int64_t e_pad, int64_t q_pad) {
-  const int64_t rows16 = eval_rows16(dim) ? 4 * (int64_t)l1q_rows(dim) * (q_pad + e_pad) : 0;
-  return eval_stat_bytes(dim, e_pad, q_pad) + rows16;
+  return 256 + round_up(8 * eval_blocks(dim, e_pad, q_pad), 256);  // tickets, K1's per-block statistics
 }
 
 extern "C" int64_t mmre_link_evaluate_l1q_workspace(int dim, int64_t e_pad, int64_t q_pad) {
@@ -3672,8 +3635,8 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   if (!d_work || work_bytes < mmre_link_evaluate_l1q_workspace(dim, e_pad, q_pad)) return MMRE_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const int kp = plane_rows(MMRE_TRANSE_L1, dim), kt = kp, k2 = l1q_rows(dim), k4 = l1q_rows8(dim);
-  const int rb = eval_rb(kp);
-  const size_t lds1 = sizeof(float) * 2 * (size_t)rb * (kt + 1);
+  const int rb = eval_rb(kp), rbq = eval_rbq(kp);
+  const size_t lds1 = sizeof(float) * (size_t)std::max(rb, 2 * rbq) * (kt + 1);
   if (lds1 > 64 * 1024) return MMRE_ERR_SHAPE;
   char* w = (char*)d_work;
   uint32_t* hdr = (uint32_t*)w;
@@ -3684,10 +3647,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   float* q_l1c = (float*)(ve + (int64_t)k4 * e_pad);
   char* extra = w + mmre_link_l1q_workspace(dim, e_pad, q_pad);
   uint32_t* ticket = (uint32_t*)extra;  // zero before the first call (the caller zeroes the workspace once)
-  static const char* lvl2_env = getenv("MMRE_L1_RESCORE16");  /* A/B: 0 = the f32 chain for every pair */
-  const bool rows16 = eval_rows16(dim) && !(lvl2_env && lvl2_env[0] == '0');
-  uint32_t* q16r = rows16 ? (uint32_t*)(extra + eval_stat_bytes(dim, e_pad, q_pad)) : nullptr;
-  uint32_t* e16r = rows16 ? q16r + (int64_t)k2 * q_pad : nullptr;
+  float* pstat = (float*)(extra + 256);
   const int64_t e_cols = round_up(e_end, TE) - e_begin;
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
@@ -3704,6 +3664,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   P.kp = kp;
   P.norm = norm_flag ? 1 : 0;
   P.rb = rb;
+  P.rbq = rbq;
   P.qh = d_qh;
   P.qr = d_qr;
   P.qt = d_qt;
@@ -3720,7 +3681,8 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   P.e_begin = e_begin;
   P.e_cols = e_cols;
   P.n_eblk = (int)((e_pad + rb - 1) / rb);
-  P.n_qblk = (int)((q_pad + rb - 1) / rb);
+  P.n_qblk = (int)((q_pad + rbq - 1) / rbq);
+  P.pstat = pstat;
   P.und_q = d_undecided_q;
   P.ticket = ticket;
   P.hdr = hdr;
@@ -3735,8 +3697,6 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   Q.pe = L1QPlane{d_ent_km, e_pad, e_begin, e_cols, ve};
   Q.out16q = uq;
   Q.out16e = ue;
-  Q.rows16q = q16r;
-  Q.rows16e = e16r;
   Q.kw = k4;
   Q.k2 = k2;
   Q.kt = kt;
@@ -3744,17 +3704,16 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   Q.tight = tight ? 1 : 0;
   Q.q_l1c = q_l1c;
   const int n_lblk = (int)((n_entries + 255) / 256);
-  const size_t lds2 = rows16 ? sizeof(uint32_t) * 32 * (size_t)(k2 + 1) : 0;
-  hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), lds2, st, P, Q, d_filt_ids,
+  hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), 0, st, P, Q, d_filt_ids,
                      d_entry_q, n_entries, d_list_scores, n_lblk);
   MMRE_CHECK_LAUNCH();
   // K3: filter counts | the code-width probe
-  const int n_cblk = (int)std::min<int64_t>(n_groups, 65536);
+  const int n_cblk = (int)std::min<int64_t>((n_groups + 3) / 4, 65536);  // four groups (waves) per block
   const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
   static const char* pf_env = getenv("MMRE_L1_PROBE_FRAC");  /* experiments: the 16-bit switch point */
-  const double pfrac = pf_env ? atof(pf_env) : (rows16 ? L1Q_PROBE_FRAC_L2 : L1Q_PROBE_FRAC);
+  const double pfrac = pf_env ? atof(pf_env) : L1Q_PROBE_FRAC;
   const uint32_t probe_max = (uint32_t)std::min(pfrac * (double)sample, 4.0e9);
-  hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_cblk + L1Q_PROBE_Q)), dim3(64), 0, st, d_grp_qoff, d_grp_q,
+  hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_cblk + L1Q_PROBE_Q / 4)), dim3(256), 0, st, d_grp_qoff, d_grp_q,
                      n_groups, n_cblk, d_filt_off, d_filt_ids, d_list_scores, d_q_true, d_truth, n_query, n_ent,
                      d_counts, vq, q_pad, ve + e_begin, e_pad, n_slice, k4, kt, tight ? q_l1c : nullptr, hdr,
                      ticket, probe_max, bits == 8 || bits == 16 ? bits : 0);
@@ -3762,7 +3721,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   // the sweeps: the one the code-width word names counts, the others' workgroups leave
   const int64_t tw = (n_ent + 31) / 32;
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4, d_undecided_q, q16r, e16r, k2};
+               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4, d_undecided_q};
   int rc = launch_valu<6>(false, false, st, (const float*)(ve + e_begin), e_pad, n_slice, n_et, (int)e_begin,
                           (const float*)vq, q_pad, n_query, k4, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr,
                           nullptr, tw, d_counts, nullptr, l1, false);

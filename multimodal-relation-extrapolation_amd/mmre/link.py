@@ -181,7 +181,6 @@ class LinkSweep:
         # count-only TransE L1 runs with filter groups as ONE call (mmre_link_evaluate_l1q, seven
         # launches instead of thirteen); MMRE_FUSED_EVAL=0 keeps the separate entry points
         self.fused_eval = os.environ.get("MMRE_FUSED_EVAL", "1") != "0"
-        self._last_l2 = False   # the last run used the fused path (its second rescoring level reports `exact`)
 
     def prepare_entities(self):
         s = self.spec
@@ -295,7 +294,6 @@ class LinkSweep:
             sweep_events[1].record()
         b["l1q_used"] = l1q
         b["bf3_used"] = bf3
-        self._last_l2 = False
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
 
     def _fusable(self, filt, type_masks, return_scores, prepare, sweep_events, q_rows):
@@ -331,7 +329,6 @@ class LinkSweep:
         self.prepared = True
         b["l1q_used"] = True
         b["bf3_used"] = False
-        self._last_l2 = True
         return dict(counts=b["counts"], truth=b["truth"], scores=None)
 
     def bf3_stats(self, buffers):
@@ -370,13 +367,12 @@ class LinkSweep:
         wk = buffers["l1q_work"]
         out = buffers.get("l1q_stats")
         if out is None:
-            out = buffers["l1q_stats"] = torch.zeros(5, dtype=torch.int64, device=self.device)
+            out = buffers["l1q_stats"] = torch.zeros(4, dtype=torch.int64, device=self.device)
         call("mmre_link_l1q_stats", ptr(wk), int(wk.numel()), ptr(out), stream_ptr(self.device))
-        u, w, g, o, x = (int(v) for v in out.cpu())
+        u, w, g, o = (int(v) for v in out.cpu())
         # the code-width word: 0 = 8-bit codes, 1 = the f32 fallback, 2 = 16-bit codes; guarded =
         # undecided-list entries the rescoring refused as out of range (0 unless a defect)
-        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g, max_offset=o,
-                    exact=x if self._last_l2 else None)
+        return dict(undecided=u, fallback=w == 1, bits={0: 8, 2: 16}.get(w), guarded=g, max_offset=o)
 
 
 def _rows_view(c):

@@ -81,6 +81,12 @@ def main():
           f"host metrics {met:.3f} ms | empty sync {empty:.4f} ms")
 
 
+# The RCCL all-gather of the count lists (world x 4 x pad int32, ~0.56 MB in all at C2) over
+# xGMI at 8 ranks, which a one-GPU box cannot run: a latency-bound ring of 7 steps of ~70 KB; an
+# estimate, stated as one wherever it is used.
+EST_ALLGATHER_MS = 0.030
+
+
 def emulate(a):
     """Per-rank cost of a W-way relation-sharded C2 step on this one GPU: each rank's LPT share
     swept and reduced alone (the all-gather is not included)."""
@@ -112,7 +118,7 @@ def emulate(a):
     if a.entity:
         masks = [np.ones(2 * n, bool)] * a.emulate_world
     to = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(dev)
-    worst = 0.0
+    worst = worst_x = 0.0
     if a.emulate_world > 1:  # N = 1 under the same harness, for the ratio
         masks = [np.ones(2 * n, bool)] + list(masks)
         slices = [(0, w["n_ent"])] + list(slices)
@@ -144,7 +150,41 @@ def emulate(a):
                 torch.cuda.current_stream().synchronize()
             for _ in range(3):
                 step()
-        ms = timeit(step, a.reps)
+        ms_sync = timeit(step, a.reps)
+        # pipelined as bench.py runs it: evaluation i + 1 enqueued before i's counts are waited
+        # for (D2H into alternating pinned buffers), one synchronisation at the end
+        hosts = [torch.empty_like(host) for _ in range(2)]
+
+        def piped(reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for i in range(reps):
+                if a.graph:
+                    g.replay()
+                    c = gc
+                else:
+                    c = sw.run(*q, filt=filt, buffers=bufs, entity_range=er)["counts"]
+                hosts[i & 1].copy_(c, non_blocking=True)
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t) / reps * 1e3
+        piped(3)
+        ms = piped(max(a.reps, 50))
+        # the count exchange's own kernels (copy into the all-gather buffer + the one gather into
+        # global order; mmre.sharding.gather_counts) on this GPU; the RCCL all-gather itself cannot
+        # run on one GPU: EST_ALLGATHER_MS stands in for it (see the summary line)
+        xch = 0.0
+        if a.emulate_world > 1 and not a.entity and k > 0:
+            from mmre.sharding import ShardPlan
+            plan = ShardPlan(list(masks[1:]), dev)
+            buf = torch.empty((4, plan.pad), dtype=torch.int32, device=dev)
+            out = torch.zeros((plan.world * 4, plan.pad), dtype=torch.int32, device=dev)
+            local = bufs["counts"]
+
+            def exchange():
+                buf[:, :local.shape[1]] = local
+                return torch.take(out, plan.src)
+            exchange()
+            xch = timeit(exchange, 50)
         # the sweep kernel alone: events on the launch stream around it, eager twins of the
         # evaluation (the separate launches; the sweep kernel is the same one)
         sw2 = LinkSweep(spec)
@@ -157,15 +197,23 @@ def emulate(a):
         sweep = float(np.median(ts))
         if a.emulate_world > 1 and k == 0:
             one = ms
-            print(f"N=1: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms")
+            print(f"N=1: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms pipelined ({ms_sync:.3f} ms with a sync "
+                  f"per evaluation)")
             continue
         worst = max(worst, ms)
+        worst_x = max(worst_x, xch)
         fst = sw.filter_stats(bufs)
-        print(f"rank {k - (1 if one is not None else 0)}: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms, "
-              f"sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms, filter {fst}")
-    ratio = f", N=1 / slowest = {one / worst:.2f}x" if one else ""
-    print(f"{a.config} world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "
-          f"slowest rank {worst:.3f} ms (+ all-gather + metric reduction){ratio}")
+        print(f"rank {k - (1 if one is not None else 0)}: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms pipelined "
+              f"({ms_sync:.3f} synced), sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms, exchange kernels "
+              f"{xch:.3f} ms, filter {fst}")
+    if one is not None:
+        est = 0.0 if a.entity else EST_ALLGATHER_MS
+        tot = worst + worst_x + est
+        print(f"{a.config} world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "
+              f"slowest rank {worst:.3f} ms + exchange kernels {worst_x:.3f} ms + RCCL all-gather estimate "
+              f"{est:.3f} ms = {tot:.3f} ms per evaluation; N=1 {one:.3f} ms: {one / worst:.2f}x before the "
+              f"exchange, {one / tot:.2f}x with it (the host metric reduction overlaps the next evaluation, "
+              f"as at N=1)")
 
 
 if __name__ == "__main__":

@@ -104,8 +104,8 @@ def test_fused_huge_values_take_the_f32_fallback(monkeypatch):
 
 def test_fused_c2_slices_graph_and_repeats(monkeypatch):
     """C2 (FB15K-237-ZS TransE d=200, xavier tables: the probe picks the 16-bit codes; and
-    the same tables scaled into a tight band: 8-bit): fused == separate, entity slices sum to
-    the whole table, graph replays and repeated calls give the same counts."""
+    the 8-bit codes forced): fused == separate, entity slices sum to the whole table, graph
+    replays and repeated calls give the same counts."""
     from mmre.link import FilterIndex, HEAD, TAIL, ScoreSpec
     from mmre.workloads import zs_workload
     w = zs_workload("FB15K-237-ZS", "transe", 200)
@@ -117,15 +117,13 @@ def test_fused_c2_slices_graph_and_repeats(monkeypatch):
     fused = _eval(spec, qh, qr, qt, qm, index, True, monkeypatch, reps=3, graph=True)
     sep = _eval(spec, qh, qr, qt, qm, index, False, monkeypatch)
     _same(fused, sep)
-    # forced 8-bit codes on these tables put ~30 % of the pairs in the band: the second rescoring
-    # level (16-bit row codes) decides nearly all of them, the f32 chain the rest
+    # forced 8-bit codes on these tables put ~16 % of the pairs in the band (all rescored)
     monkeypatch.setenv("MMRE_L1_BITS", "8")
     f8 = _eval(spec, qh, qr, qt, qm, index, True, monkeypatch)
     s8 = _eval(spec, qh, qr, qt, qm, index, False, monkeypatch)
     monkeypatch.delenv("MMRE_L1_BITS")
     _same(f8, s8)
     assert np.array_equal(f8["counts"], fused["counts"])
-    assert f8["st"]["exact"] is not None and f8["st"]["exact"] < 0.05 * f8["st"]["undecided"], f8["st"]
     print(f"C2 forced 8-bit: {f8['st']}")
     total = np.zeros_like(fused["counts"])
     for e0, e1 in ((0, 4096), (4096, 9984), (9984, E)):
