@@ -1117,6 +1117,9 @@ def main():
                     help="C3/C4/C5: OpenKE-initialised tables (truths rank ~E/2) instead of structured ones")
     ap.add_argument("--eager", action="store_true",
                     help="link configs: launch each rank's local evaluation eagerly (default: one hipGraph replay)")
+    ap.add_argument("--pack", default="cost", choices=["cost", "count"],
+                    help="N > 1 relation-sharded: LPT by per-query cost (one calibration evaluation counts the pairs "
+                         "the L1 filter leaves undecided; TransE) or by query count")
     ap.add_argument("--shard", default="relation", choices=["relation", "entity"],
                     help="N > 1 link configs: split the queries (relation-sharded, one all-gather; default) or "
                          "the entity table (every query against 1/N of the entities, one all-reduce)")
@@ -1196,7 +1199,7 @@ def main():
         # the rank's local evaluation (entity / query prep, truth and filter kernels, sweep)
         # replayed from one hipGraph; kernel_ms comes from an eager twin after the timed region
         ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev,
-                                   graph=not args.eager)
+                                   graph=not args.eager, cost="undecided" if args.pack == "cost" else None)
         n_local = int(ev.masks[rank].sum())
         e_local = E
 
@@ -1323,8 +1326,9 @@ def main():
                "config": {"workload": cfg["workload"], "n_entities": E, "dim": dim, "n_sweeps": 2 * n,
                           "parallelism": (f"entity-sharded x{world} (1/N of the entity tiles per rank), {coll} all-reduce "
                                           f"of the count table" if args.shard == "entity" else
-                                          f"query-sharded x{world} (relation-major LPT with relation splits), {coll} "
-                                          f"all-gather of rank counts"),
+                                          f"query-sharded x{world} (relation-major LPT with relation splits"
+                                          f"{', packed by calibrated per-query cost' if getattr(ev, 'weights', None) is not None else ''}"
+                                          f"), {coll} all-gather of rank counts"),
                           "launch": "hipGraph replay of each rank's local evaluation" if graphed else "eager"},
                "roofline": roof,
                "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],

@@ -455,6 +455,9 @@ struct L1Q {
   const float* q_l1c;      // 8-bit codes, tight bound: per query row sum |eps_q| (upper bound); nullptr: uniform bound
   uint32_t* guard;         // hdr[4]: pairs the rescoring refused (query or entity id out of range; must stay 0)
   uint32_t* und_q;         // optional per-query count of rescored pairs (cost calibration of the sharding)
+  int32_t* fin_counts;     // gated f32 launch of the fused evaluation: the finalize (filtered += raw) rides
+  int64_t fin_n;           // on it -- every workgroup's slice when the gate is shut, the last workgroup's
+  uint32_t* fin_ticket;    // pass after the sweep when it is open (fin_counts nullptr: a separate launch)
 };
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
@@ -948,6 +951,7 @@ __device__ __forceinline__ void sweep_valu_body(
   static_assert(NPL == ((OP == 2) ? 2 : 1), "planes");
   // filters: RotatE's raw-sqrt sum (rot_bound / rot_exact), TransE L1's 16-bit codes (L1Q)
   constexpr bool L1F = OP == 5 || OP == 6;  // TransE L1's integer filter (16- / 8-bit codes)
+  constexpr bool w8 = OP == 6;
   constexpr bool FAST = (OP == 2 || L1F) && !STORE;
   auto& sq = sm.sq;
   auto& se = sm.se;
@@ -973,7 +977,7 @@ __device__ __forceinline__ void sweep_valu_body(
   // L1 filter constants (uniform): code step, bound slope and offset
   float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
   if constexpr (L1F) {
-    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr, OP == 6 ? 255.0f : 65535.0f))));
+    l1d = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(l1q_delta(l1.hdr, w8 ? 255.0f : 65535.0f))));
     l1f = (float)(l1.kt + 4) * 0x1p-23f * (1.0f + 0x1p-8f);
     l1c = __builtin_fmaf((float)l1.kt * 1.03f, l1d, 0x1p-120f);
   }
@@ -997,7 +1001,7 @@ __device__ __forceinline__ void sweep_valu_body(
         // grown by 2^-18 against the float rounding of their own computation. Once per query
         // row and query tile, not per unit.
         uint32_t t_sure, t_span;
-        const bool tight = OP == 6 && l1.q_l1c != nullptr;
+        const bool tight = w8 && l1.q_l1c != nullptr;
         const int ktm = sgpr_opaque(l1.kt);
         const float md = __uint_as_float(sgpr_opaque(__float_as_uint(l1d)));
         const float mf = (float)(ktm + 4) * 0x1p-23f * (1.0f + 0x1p-8f);  // = l1f
@@ -1101,7 +1105,7 @@ __device__ __forceinline__ void sweep_valu_body(
   // L1 filter: the code rows actually used in the last stage (the plane is padded to whole
   // stages; 100 of 104 rows at d = 200: the pad rows' zeros are not swept)
   // (OP 6: the words of the k values + the entity error-offset row, l1q_quant8)
-  const int kk_last = L1F ? ((((l1.kt + (OP == 6 ? 3 : 1)) >> (OP == 6 ? 2 : 1)) + (OP == 6 ? 2 : 1)) & ~1) - (nkc - 1) * KC
+  const int kk_last = L1F ? ((((l1.kt + (w8 ? 3 : 1)) >> (w8 ? 2 : 1)) + (w8 ? 2 : 1)) & ~1) - (nkc - 1) * KC
                           : KC;
   // the L1 filter's code-width word (L1Q_CODES8 / _CODES16 / _F32: which of the gated sweeps
   // counts), in flight with the stage
@@ -1110,7 +1114,7 @@ __device__ __forceinline__ void sweep_valu_body(
   gload();
   swrite(0);
   __syncthreads();
-  if (L1F && __builtin_amdgcn_readfirstlane(fb_flag) != (OP == 6 ? L1Q_CODES8 : L1Q_CODES16)) return;  // uniform
+  if (L1F && __builtin_amdgcn_readfirstlane(fb_flag) != (w8 ? L1Q_CODES8 : L1Q_CODES16)) return;  // uniform
 
   constexpr int KKU = 2;  // LDS rows of operands per inner-loop iteration
   int buf = 0;
@@ -1496,11 +1500,39 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
   // filter's grew the kernel by half and its register spills (18 -> 23)
   if (l1.gate != nullptr) {
     const uint32_t want = OP == 6 ? L1Q_CODES8 : OP == 5 ? L1Q_CODES16 : L1Q_F32;
-    if (__builtin_amdgcn_readfirstlane(*l1.gate) != want) return;
+    if (__builtin_amdgcn_readfirstlane(*l1.gate) != want) {
+      if (l1.fin_counts != nullptr) {  // shut (the codes counted): this workgroup's slice of the finalize
+        for (int64_t q = (int64_t)blockIdx.x * NT + threadIdx.x; q < l1.fin_n; q += (int64_t)gridDim.x * NT) {
+          l1.fin_counts[l1.fin_n + q] += l1.fin_counts[q];
+          if constexpr (TC) l1.fin_counts[3 * l1.fin_n + q] += l1.fin_counts[2 * l1.fin_n + q];
+        }
+      }
+      return;
+    }
   }
   sweep_valu_body<OP, TC, STORE, PK, NPL>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
                                           n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head, type_tail,
                                           type_words, counts, scores, l1);
+  if (l1.gate != nullptr && l1.fin_counts != nullptr) {
+    // open (the rare f32 fallback): the finalize after every workgroup's counts, by the last
+    // workgroup (each wave's count atomics drained, then ONE ticket add per workgroup)
+    __shared__ uint32_t s_last;
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+      s_last = __hip_atomic_fetch_add(l1.fin_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (s_last) {
+      for (int64_t q = threadIdx.x; q < l1.fin_n; q += NT) {
+        atomicAdd(&l1.fin_counts[l1.fin_n + q],
+                  __hip_atomic_load(&l1.fin_counts[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if constexpr (TC)
+          atomicAdd(&l1.fin_counts[3 * l1.fin_n + q],
+                    __hip_atomic_load(&l1.fin_counts[2 * l1.fin_n + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      if (threadIdx.x == 0) *l1.fin_ticket = 0u;
+    }
+  }
 }
 
 // filtered columns += raw columns (after the sweep): counts[1] = counts[0] + (minus the listed
@@ -2143,7 +2175,7 @@ static int l1q_rows8(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1,
 // the counts are the exact sweep's bit for bit. ~2e-4 of the C3 pairs and 2e-5 of C5's land
 // in the list. A list that overflows its capacity sets a flag on the device: the raw counts
 // are reset and the exact f32 sweep runs instead (gated launches, no host round trip).
-// Workspace: header (BF3_HDR bytes: word 0 appended pairs, word 1 overflow flag) | pair list
+// Workspace: header (BF3_HDR bytes: word 1 overflow flag, words 2-3 the appended pairs (uint64)) | pair list
 // (bf3_cap int2) | |q| (q_pad floats) | |e| (e_pad floats) | split query planes (K/16 blocks
 // x q_pad rows x 64 B: hi[16] | lo[16]) | split entity planes (K/16 x e_pad x 64 B).
 constexpr int BF3_HDR = 256;
@@ -2390,13 +2422,12 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
 #pragma unroll
                 for (int bj = 0; bj < 2; ++bj) {
                   if (!und[bj]) continue;
-                  // the counter stops near cap once the list is full (a non-finite table can make
-                  // every pair undecided: 1.6e10 at C5 would wrap a 32-bit counter), so the stats
-                  // read a saturated count with the overflow flag, not a wrapped one
-                  uint32_t i = 0xFFFFFFFFu;
-                  if (__hip_atomic_load(&hdr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)cap)
-                    i = atomicAdd(&hdr[0], 1u);
-                  if (i < (uint64_t)cap) pairs[i] = make_int2((int)q, (int)((bj ? e1 : e0) + e_base));
+                  // a 64-bit counter (header words 2-3): a non-finite table can make every pair
+                  // undecided (1.6e10 at C5), which would wrap a 32-bit one. (A check-then-add
+                  // -- an sc1 load of the counter before each add -- made C3 3x slower: the loads
+                  // queue behind every workgroup's atomics on that one address.)
+                  const unsigned long long i = atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 2), 1ull);
+                  if (i < (unsigned long long)cap) pairs[i] = make_int2((int)q, (int)((bj ? e1 : e0) + e_base));
                   else hdr[1] = 1u;
                 }
               }
@@ -2447,7 +2478,8 @@ __global__ __launch_bounds__(256) void k_bf3_rescore(const uint32_t* __restrict_
                                                      int32_t* __restrict__ counts) {
   if (hdr[1] != 0u) return;  // overflow: the exact sweep counted everything
   const PredSel<PK> pred(pred_kind, margin);
-  const int64_t n = (int64_t)hdr[0] < cap ? (int64_t)hdr[0] : cap;
+  const unsigned long long listed = *reinterpret_cast<const unsigned long long*>(hdr + 2);
+  const int64_t n = listed < (unsigned long long)cap ? (int64_t)listed : cap;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int2 p = pairs[i];
     const float4* a = reinterpret_cast<const float4*>(q_rows + (int64_t)p.x * ktot);
@@ -2467,7 +2499,7 @@ __global__ __launch_bounds__(256) void k_bf3_rescore(const uint32_t* __restrict_
 
 __global__ void k_bf3_stats(const uint32_t* __restrict__ hdr, unsigned long long* __restrict__ out) {
   if (threadIdx.x == 0) {
-    out[0] = hdr[0];
+    out[0] = *reinterpret_cast<const unsigned long long*>(hdr + 2);
     out[1] = hdr[1];
   }
 }
@@ -3538,7 +3570,7 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   const double K = (double)ktot;
   const float cb = (float)(1.02 * (7.0 * K * std::ldexp(1.0, -24) * (1.0 + std::ldexp(1.0, -7)) +
                                    3.02 * std::ldexp(1.0, -16) + std::ldexp(1.0, -29) * std::sqrt(K)));
-  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(64), 0, st, hdr, 2);
+  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(64), 0, st, hdr, 4);
   const int nkb = ktot / 16;
   hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad * nkb + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad,
                      (int64_t)0, q_pad, nkb, qb, q_pad);
@@ -3722,6 +3754,9 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   const int64_t tw = (n_ent + 31) / 32;
   const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
                kt, nullptr, tight ? q_l1c : nullptr, hdr + 4, d_undecided_q};
+  // the 8-bit sweep (it leaves unless the word names the 8-bit codes) and the gated 16-bit one
+  // (one launch for both widths was tried: with both SAD loops in one kernel the allocator
+  // spilled 58-81 VGPRs)
   int rc = launch_valu<6>(false, false, st, (const float*)(ve + e_begin), e_pad, n_slice, n_et, (int)e_begin,
                           (const float*)vq, q_pad, n_query, k4, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr,
                           nullptr, tw, d_counts, nullptr, l1, false);
@@ -3732,9 +3767,13 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
                       (const float*)uq, q_pad, n_query, k2, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr, nullptr,
                       tw, d_counts, nullptr, l16, false);
   if (rc) return rc;
+  // the f32 fallback, gated on the word; it also carries the finalize (filtered += raw)
   L1Q gate{};
   gate.gate = hdr + 1;
+  gate.fin_counts = d_counts;
+  gate.fin_n = n_query;
+  gate.fin_ticket = hdr + 6;
   return launch_valu<0>(false, false, st, d_ent_km + e_begin, e_pad, n_slice, n_et, (int)e_begin, d_q_km, q_pad,
                         n_query, kp, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr, nullptr, tw, d_counts,
-                        nullptr, gate, true);
+                        nullptr, gate, false);
 }
