@@ -2607,7 +2607,9 @@ static int launch_valu(bool tc, bool store, hipStream_t st, const float* ent_km,
 //   K3 k_eval_count_probe filter counts, a wave per group | the code-width probe, a wave per
 //                         sampled query (the last of its 128 blocks decides 8 vs 16 bits)
 //   K4-K6                 the three gated sweeps (8-bit, 16-bit, f32; the code-width word
-//                         names the one that counts), then k_counts_finalize
+//                         names the one that counts); the f32 launch also carries the
+//                         finalize (filtered += raw): each workgroup's slice when its gate is
+//                         shut, the last workgroup's pass (ticket) when it is open
 // No cross-workgroup hand-off inside K1 / K2: grid-wide results pass at kernel boundaries.
 // Measured on the way (MI355X, C2, per evaluation): a __threadfence() per K1 block (L2
 // write-back of each block's freshly written rows) 163 us for K1; per-block partials read back by

@@ -10,6 +10,8 @@ the reference's sequential order, so rank 0's metrics are bit-equal to the singl
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -115,17 +117,37 @@ def cost_weights(undecided_per_query, n_ent: int, pair_cost: float = 140.0):
     return float(n_ent) + pair_cost * u
 
 
+def rank_order(mask, weights=None, tile: int = 128):
+    """The query ids of one rank's share in sweep order. Without per-query costs: ascending
+    (relation-major, Test.h order). With them (the calibration's undecided-pair counts): the
+    heavy queries SPREAD over the sweep's query tiles -- ids sorted by cost, heaviest first, and
+    dealt round-robin to the ceil(n / tile) tiles -- so every 128-query tile carries a like
+    share of the pairs the L1 filter leaves undecided. The Test.h order puts a heavy relation's
+    queries in the same few tiles, whose units then rescore for longest and trail the sweep;
+    sorting heaviest-first made that worse (C2 8-way, slowest rank 0.277 -> 0.332 ms). Counts
+    are per query, so the order changes no result. MMRE_RANK_ORDER=id|heavy|spread (A/B)."""
+    ids = np.nonzero(mask)[0]
+    mode = os.environ.get("MMRE_RANK_ORDER", "spread")
+    if weights is None or mode == "id" or len(ids) == 0:
+        return ids
+    ids = ids[np.argsort(-np.asarray(weights, np.float64)[ids], kind="stable")]
+    if mode == "heavy":
+        return ids
+    n_t = -(-len(ids) // tile)
+    return np.concatenate([ids[t::n_t] for t in range(n_t)])
+
+
 class ShardPlan:
     """Everything each rank precomputes once from the (deterministic, identical on every rank)
-    lpt_partition masks: its own query ids, the padded width, and the device index maps that
-    put all-gathered columns back into global query order."""
+    lpt_partition masks: its own query ids (in rank_order), the padded width, and the device
+    index maps that put all-gathered columns back into global query order."""
 
-    def __init__(self, masks, device):
+    def __init__(self, masks, device, weights=None):
         self.world = len(masks)
         self.n_total = len(masks[0])
         self.sizes = [int(m.sum()) for m in masks]
         self.pad = max(max(self.sizes), 1)
-        self.ids = [np.nonzero(m)[0] for m in masks]
+        self.ids = [rank_order(m, weights) for m in masks]
         # one gather from the all-gathered (world, 4, pad) block into (4, n_total) global order:
         # global column q of count row c <- flat index (rank(q) * 4 + c) * pad + local(q)
         src = np.empty((4, self.n_total), np.int64)
@@ -189,10 +211,11 @@ class ShardedLinkEvaluation:
                                                                torch.device("cpu"))
         self.device = dev
         self.weights = None
-        if cost == "undecided" and self.world > 1 and local_runner is None and not type_constrain:
+        if cost == "undecided" and local_runner is None and not type_constrain:
             self.weights = calibrate_weights(spec, qh, qr, qt, qm, index, dev, group)
         self.masks = lpt_partition(qr, self.world, weights=self.weights)
-        mine = self.masks[self.rank]
+        mine = rank_order(self.masks[self.rank], self.weights)   # this rank's query ids, sweep order
+        self.order = mine
         to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
         self.q = [to(qh[mine]), to(qr[mine]), to(qt[mine]), to(qm[mine])]
         self.q_host = (qh[mine], qr[mine], qt[mine], qm[mine])
@@ -206,12 +229,18 @@ class ShardedLinkEvaluation:
                     raise ValueError("type_constrain=True needs the FilterIndex's type constraints "
                                      "(type_constrain.txt, Reader.h:266-317)")
                 self.masks_tc = tuple(to(m) for m in tm)
-        self.plan = ShardPlan(self.masks, dev) if self.world > 1 else None
+        self.plan = ShardPlan(self.masks, dev, self.weights) if self.world > 1 else None
+        # one GPU with a cost order: the local columns go back to query order by one gather
+        self._unperm = None
+        if self.world == 1 and not np.array_equal(mine, np.arange(len(qh))):
+            inv = np.empty(len(mine), np.int64)
+            inv[mine] = np.arange(len(mine))
+            self._unperm = to(inv)
         self._default_runner = local_runner is None
         if local_runner is None:
             from .link import LinkSweep
             sw = LinkSweep(spec)
-            bufs = sw.alloc_queries(int(mine.sum()))
+            bufs = sw.alloc_queries(len(mine))
 
             def local_runner(qh_, qr_, qt_, qm_, filt, masks_tc, events=None):
                 return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs,
@@ -242,7 +271,9 @@ class ShardedLinkEvaluation:
     def counts(self, events=None):
         """(4, 2n) int32 counts in global query order (head block, then tail block)."""
         local = self._local(events)
-        return gather_counts(local, self.plan, self.group) if self.world > 1 else local
+        if self.world > 1:
+            return gather_counts(local, self.plan, self.group)
+        return local if self._unperm is None else local.index_select(1, self._unperm)
 
     def launch(self, events=None):
         """Enqueue one evaluation -- sweep, (world > 1) all-gather, and the D2H of the count

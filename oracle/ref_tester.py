@@ -316,6 +316,95 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
     return out
 
 
+def run_parallel(w: dict, th, tr, tt, procs: int, timeout_s: float | None = None, **meta_extra):
+    """The Tester loop over the sample (th, tr, tt) -- kept in Test.h order -- cut into `procs`
+    contiguous chunks, each a child process with its own Base.so on one torch thread (torch's
+    intra-op threads do not speed the reference's predict up: 1.4 s per C4 triple on 1 thread,
+    1.7 s on 8). Each chunk's train2id is the filter set minus its own test triples, so every
+    child filters with the whole filter set, exactly as one run over the sample would.
+
+    Merged result = run_tester's, over the whole sample: counts / q / truth_scores /
+    score_absmax / near lists in the one-run order ([head sweeps | tail sweeps] for the CSR
+    lists), elapsed = the slowest chunk's Tester loop (the chunks run side by side; startup
+    and the near-list bookkeeping excluded), threads = the processes used. Base.so's metrics
+    are per chunk; the sample's are the Test.h:232-327 reduction of the merged counts
+    restated by the oracle (oracle.link_metrics), which must reproduce every chunk's Base.so
+    metrics bit for bit first (kept as chunk_metrics)."""
+    import shutil
+    import subprocess
+    import tempfile
+    sys.path.insert(0, HERE)
+    import oracle as orc
+    th, tr, tt = (np.asarray(x, np.int64) for x in (th, tr, tt))
+    n = len(th)
+    procs = max(1, min(int(procs), n))
+    bounds = np.linspace(0, n, procs + 1).round().astype(np.int64)
+    tmps, kids = [], []
+    try:
+        for c in range(procs):
+            a, b = int(bounds[c]), int(bounds[c + 1])
+            tmp = tempfile.mkdtemp(prefix=f"mmre_refpar{c}_")
+            tmps.append(tmp)
+            prepare_workdir(tmp, w, th[a:b], tr[a:b], tt[a:b], threads=1, **meta_extra)
+        env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+        for tmp in tmps:
+            kids.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), tmp], stdout=subprocess.DEVNULL,
+                                         stderr=subprocess.DEVNULL, env=env))
+        t0 = time.time()
+        for k in kids:
+            left = None if timeout_s is None else max(1.0, timeout_s - (time.time() - t0))
+            if k.wait(timeout=left) != 0:
+                raise RuntimeError(f"ref_tester chunk failed rc={k.returncode}")
+        parts = []
+        for tmp in tmps:
+            with np.load(os.path.join(tmp, "result.npz"), allow_pickle=False) as z:
+                parts.append({k: z[k] for k in z.files})
+    finally:
+        for k in kids:
+            if k.poll() is None:
+                k.kill()
+                k.wait()
+        for tmp in tmps:
+            shutil.rmtree(tmp, ignore_errors=True)
+
+    def tc4(c):  # (2, m, 2) [raw, filt] -> the oracle's (m, 4) per side
+        z = np.zeros((c.shape[1], 4), np.int64)
+        return [np.concatenate([c[s], z[:, :2]], 1) for s in (0, 1)]
+
+    for c, p in enumerate(parts):
+        m = orc.link_metrics(*tc4(p["counts"]))["filter"]
+        mine = np.array([m[k] for k in orc.METRIC_NAMES], np.float32)
+        if not np.array_equal(mine.view(np.uint32), p["metrics"].astype(np.float32).view(np.uint32)):
+            raise RuntimeError(f"chunk {c}: the oracle's metric reduction {mine} differs from Base.so's {p['metrics']}")
+    cat1 = lambda k: np.concatenate([p[k] for p in parts], axis=1)
+    counts = cat1("counts")
+    m = orc.link_metrics(*tc4(counts))["filter"]
+    out = dict(counts=counts, q=np.concatenate([p["q"] for p in parts]),
+               metrics=np.array([m[k] for k in orc.METRIC_NAMES], np.float32),
+               chunk_metrics=np.stack([p["metrics"] for p in parts]), chunk_n=np.diff(bounds),
+               elapsed=np.float64(max(float(p["elapsed"]) for p in parts)),
+               elapsed_chunks=np.array([float(p["elapsed"]) for p in parts]),
+               t_idx=np.concatenate([p["t_idx"] for p in parts]), threads=np.int64(procs),
+               n_ent=parts[0]["n_ent"], tie_rel=parts[0]["tie_rel"], truth_scores=cat1("truth_scores"),
+               score_absmax=cat1("score_absmax"), near_ties=cat1("near_ties"))
+    if "scores" in parts[0]:
+        out["scores"] = cat1("scores")
+    if "near_off" in parts[0]:
+        ids, sc, cnt = [], [], []
+        for side in (0, 1):
+            for p in parts:
+                nc, off = p["counts"].shape[1], p["near_off"]
+                for i in range(side * nc, (side + 1) * nc):
+                    ids.append(p["near_ids"][off[i]:off[i + 1]])
+                    sc.append(p["near_scores"][off[i]:off[i + 1]])
+                    cnt.append(off[i + 1] - off[i])
+        out["near_off"] = np.r_[0, np.cumsum(cnt)].astype(np.int64)
+        out["near_ids"] = np.concatenate(ids).astype(np.int32) if ids else np.zeros(0, np.int32)
+        out["near_scores"] = np.concatenate(sc).astype(np.float32) if sc else np.zeros(0, np.float32)
+        out["near_rel"] = parts[0]["near_rel"]
+    return out
+
+
 if __name__ == "__main__":
     r = run_tester(sys.argv[1])
     print(f"ref_tester: {r['counts'].shape[1]} test triples x 2 sweeps in {float(r['elapsed']):.2f} s "

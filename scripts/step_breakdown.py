@@ -36,6 +36,8 @@ def main():
                     "from a hipGraph")
     ap.add_argument("--pack", default="cost", choices=["cost", "count"],
                     help="--emulate-world: LPT by calibrated per-query cost (bench default) or by query count")
+    ap.add_argument("--no-order", action="store_true",
+                    help="--emulate-world: keep each rank's queries ascending (default: heaviest calibrated cost first)")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="--emulate-world: workload (c2: the bench's trained TransE tables; c3-c5: the "
                          "structured tables of the reference fixtures)")
@@ -123,13 +125,15 @@ def emulate(a):
         masks = [np.ones(2 * n, bool)] + list(masks)
         slices = [(0, w["n_ent"])] + list(slices)
     one = None
+    from mmre.sharding import rank_order
     for k, m in enumerate(masks):
         er = slices[k] if a.entity else None
+        m = rank_order(m, None if a.no_order else weights)  # the rank's queries in the bench's sweep order
         q = [to(x[m]) for x in (qh, qr, qt, qm)]
         filt = tuple(to(x) for x in index.groups(qh[m], qr[m], qt[m], qm[m], entity_range=er))
         sw = LinkSweep(spec)
-        bufs = sw.alloc_queries(int(m.sum()))
-        host = torch.empty((4, int(m.sum())), dtype=torch.int32, pin_memory=True)
+        bufs = sw.alloc_queries(len(m))
+        host = torch.empty((4, len(m)), dtype=torch.int32, pin_memory=True)
         ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
 
         def step():
@@ -175,7 +179,7 @@ def emulate(a):
         xch = 0.0
         if a.emulate_world > 1 and not a.entity and k > 0:
             from mmre.sharding import ShardPlan
-            plan = ShardPlan(list(masks[1:]), dev)
+            plan = ShardPlan(list(masks[1:]), dev, None if a.no_order else weights)
             buf = torch.empty((4, plan.pad), dtype=torch.int32, device=dev)
             out = torch.zeros((plan.world * 4, plan.pad), dtype=torch.int32, device=dev)
             local = bufs["counts"]
@@ -188,7 +192,7 @@ def emulate(a):
         # the sweep kernel alone: events on the launch stream around it, eager twins of the
         # evaluation (the separate launches; the sweep kernel is the same one)
         sw2 = LinkSweep(spec)
-        b2 = sw2.alloc_queries(int(m.sum()))
+        b2 = sw2.alloc_queries(len(m))
         ts = []
         for _ in range(5):
             sw2.run(*q, filt=filt, buffers=b2, sweep_events=ev, entity_range=er)
@@ -197,13 +201,13 @@ def emulate(a):
         sweep = float(np.median(ts))
         if a.emulate_world > 1 and k == 0:
             one = ms
-            print(f"N=1: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms pipelined ({ms_sync:.3f} ms with a sync "
+            print(f"N=1: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined ({ms_sync:.3f} ms with a sync "
                   f"per evaluation)")
             continue
         worst = max(worst, ms)
         worst_x = max(worst_x, xch)
         fst = sw.filter_stats(bufs)
-        print(f"rank {k - (1 if one is not None else 0)}: {int(m.sum())} sweeps, local evaluation {ms:.3f} ms pipelined "
+        print(f"rank {k - (1 if one is not None else 0)}: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined "
               f"({ms_sync:.3f} synced), sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms, exchange kernels "
               f"{xch:.3f} ms, filter {fst}")
     if one is not None:

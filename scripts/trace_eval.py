@@ -4,7 +4,7 @@ nothing else in the process, for per-kernel A/B traces of the fused / separate p
     rocprofv3 --kernel-trace --stats -d <dir> -o run -- python scripts/trace_eval.py [N] [world W] [rank K]
 
 With `world W rank K` the evaluation is rank K's share of the W-way relation-sharded C2
-(cost-packed, as bench.py packs it)."""
+(cost-packed and in the sweep order bench.py uses: mmre.sharding.rank_order)."""
 import os
 import sys
 
@@ -14,7 +14,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from mmre.link import HEAD, TAIL, FilterIndex, LinkSweep  # noqa: E402
-from mmre.sharding import calibrate_weights, lpt_partition  # noqa: E402
+from mmre.sharding import calibrate_weights, lpt_partition, rank_order  # noqa: E402
 from mmre.workloads import train_transe, workload_spec, zs_workload  # noqa: E402
 
 n_rep = int(sys.argv[1]) if len(sys.argv) > 1 else 50
@@ -29,16 +29,15 @@ index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], w["n_ent"], w["
 n = len(w["test_h"])
 qh, qr, qt = (np.r_[w[k], w[k]] for k in ("test_h", "test_r", "test_t"))
 qm = np.r_[np.full(n, HEAD, np.int8), np.full(n, TAIL, np.int8)]
-m = np.ones(2 * n, bool)
-if world > 1:
-    m = lpt_partition(qr, world, weights=calibrate_weights(spec, qh, qr, qt, qm, index, dev))[rank]
+wts = calibrate_weights(spec, qh, qr, qt, qm, index, dev)   # the bench's packing and sweep order
+m = rank_order(lpt_partition(qr, world, weights=wts)[rank], wts)
 to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 q = [to(x[m]) for x in (qh, qr, qt, qm)]
 filt = tuple(to(a) for a in index.groups(qh[m], qr[m], qt[m], qm[m]))
 sw = LinkSweep(spec)
-bufs = sw.alloc_queries(int(m.sum()))
+bufs = sw.alloc_queries(len(m))
 torch.cuda.synchronize()
 for _ in range(n_rep):
     sw.run(*q, filt=filt, buffers=bufs)
 torch.cuda.synchronize()
-print(f"{n_rep} evaluations of {int(m.sum())} sweeps: {sw.filter_stats(bufs)}", flush=True)
+print(f"{n_rep} evaluations of {len(m)} sweeps: {sw.filter_stats(bufs)}", flush=True)

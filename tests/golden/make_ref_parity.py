@@ -14,11 +14,12 @@ and a seeded test sample:
         (norm_flag; the bench's TRAINED tables: 300 steps of this build's HIP trainer, written by
         scripts/dump_trained_tables.py on a GPU box, sha256 checked here and in the GPU test)
     C3  DB15K-ZS ComplEx d=200      all 5,653 test triples  -> 11,306 sweeps x 12,741 entities
-    C4  FB15K-237-ZS RotatE d=512   1,000 test triples      ->  2,000 sweeps x 14,208 entities
+    C4  FB15K-237-ZS RotatE d=512   all 17,596 test triples -> 35,192 sweeps x 14,208 entities
     C5  synthetic DistMult d=256    all 4,096 test triples  ->  8,192 sweeps x 1,000,000 entities
 
 The REFERENCE's CPU path ranks the sample: the OpenKE Tester loop (Tester.py:70-91) over the
-reference's own Base.so (getHeadBatch / testHead / getTailBatch / testTail /
+reference's own Base.so (the sample cut into contiguous chunks, one child process each:
+ref_tester.run_parallel) (getHeadBatch / testHead / getTailBatch / testTail /
 test_link_prediction, Test.h:36-327) with the reference models' predict op sequences on torch
 CPU (oracle/ref_tester.py, pinned bit-for-bit against the reference's own predictions by
 tests/test_oracle_golden.py). Stored per fixture:
@@ -30,20 +31,20 @@ tests/test_oracle_golden.py). Stored per fixture:
     score_absmax (2, n)    max |predict| over the sweep
     near_off/ids/scores    per sweep (head sweeps then tail sweeps), every other entity whose
                            reference score lies within near_rel x max|predict| of the truth's
-    metrics                Base.so's filtered MRR, MR, hit@10, hit@3, hit@1 (getTestLink*)
+    metrics                filtered MRR, MR, hit@10, hit@3, hit@1 of the whole sample: the Test.h
+                           reduction of the merged counts (oracle.link_metrics), which reproduces
+                           every chunk's Base.so getTestLink* bit for bit (chunk_metrics, chunk_n)
 
 tests/test_ref_parity_gpu.py holds the HIP sweep to these exactly (see there).
 
-Usage:  python tests/golden/make_ref_parity.py [c2 c3 c4 c5]   (C4 takes ~15 min on 8 cores)
+Usage:  python tests/golden/make_ref_parity.py [c2 c3 c4 c5]   (C4: ~1.4 s per test triple per
+        process, ~55 min on 8 processes; MMRE_REF_PROCS sets the process count)
         (c2 reads gpurun_out/trained_c2.npz)
 """
 from __future__ import annotations
 
 import os
-import shutil
-import subprocess
 import sys
-import tempfile
 import time
 
 import numpy as np
@@ -57,7 +58,7 @@ for p in (os.path.join(REPO, "multimodal-relation-extrapolation_amd"), os.path.j
 NEAR_REL = 1e-5
 
 
-def make(config: str, threads: int = 8, tables_path: str | None = None):
+def make(config: str, procs: int = 8, tables_path: str | None = None):
     import ref_tester
     from mmre.workloads import TRAINED_TABLES, ref_parity_workload, tables_sha256
     t0 = time.time()
@@ -69,19 +70,9 @@ def make(config: str, threads: int = 8, tables_path: str | None = None):
         with np.load(tables_path, allow_pickle=False) as z:
             assert str(z["sha256"]) == sha, "trained tables' sha256 differs from the one the GPU run recorded"
     print(f"{config}: workload + structured tables in {time.time() - t0:.1f} s, sha256 {sha[:16]}", flush=True)
-    tmp = tempfile.mkdtemp(prefix=f"mmre_refpar_{config}_")
-    try:
-        ref_tester.prepare_workdir(tmp, w, w["test_h"], w["test_r"], w["test_t"], threads=threads, summary=True,
-                                   near_rel=NEAR_REL)
-        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "ref_tester.py"), tmp], cwd=REPO,
-                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"ref_tester failed rc={r.returncode}")
-        print(r.stdout.strip(), flush=True)
-        with np.load(os.path.join(tmp, "result.npz"), allow_pickle=False) as z:
-            res = {k: z[k] for k in z.files}
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+    res = ref_tester.run_parallel(w, w["test_h"], w["test_r"], w["test_t"], procs, summary=True, near_rel=NEAR_REL)
+    print(f"{config}: {len(res['q'])} test triples on {procs} processes, slowest chunk {float(res['elapsed']):.1f} s",
+          flush=True)
     q = res["q"]
     assert np.array_equal(q[:, 0], w["test_h"]) and np.array_equal(q[:, 1], w["test_r"]) \
         and np.array_equal(q[:, 2], w["test_t"]), "Base.so's testList order differs from the workload's"
@@ -89,8 +80,8 @@ def make(config: str, threads: int = 8, tables_path: str | None = None):
                q=q.astype(np.int32), counts=res["counts"].astype(np.int32),
                truth_scores=res["truth_scores"], score_absmax=res["score_absmax"],
                near_rel=np.float64(NEAR_REL), near_off=res["near_off"], near_ids=res["near_ids"],
-               near_scores=res["near_scores"], metrics=res["metrics"], ref_elapsed_s=res["elapsed"],
-               ref_threads=res["threads"], n_ent=res["n_ent"])
+               near_scores=res["near_scores"], metrics=res["metrics"], chunk_metrics=res["chunk_metrics"],
+               chunk_n=res["chunk_n"], ref_elapsed_s=res["elapsed"], ref_threads=res["threads"], n_ent=res["n_ent"])
     path = os.path.join(HERE, f"ref_parity_{config}.npz")
     np.savez_compressed(path, **out)
     c = res["counts"][:, :, 1]
@@ -101,4 +92,4 @@ def make(config: str, threads: int = 8, tables_path: str | None = None):
 
 if __name__ == "__main__":
     for cfg in (sys.argv[1:] or ["c3", "c4", "c5"]):
-        make(cfg)
+        make(cfg, procs=int(os.environ.get("MMRE_REF_PROCS", "8")))

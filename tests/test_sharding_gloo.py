@@ -127,7 +127,7 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_tr
     spec = _spec(w, model, dim, dev)
     ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev, graph=graph,
                                cost=cost)
-    assert (ev.weights is not None) == (cost == "undecided" and model == "transe" and world > 1)
+    assert (ev.weights is not None) == (cost == "undecided" and model == "transe")
     a = ev.launch()
     b = ev.launch()
     mb, cb = ev.finish(b)        # out of order: b first, then a third launch while a is pending
@@ -151,6 +151,7 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_tr
     ("DB15K-ZS", "complex", 200, 3, True, None, None),
     ("FB15K-237-ZS", "rotate", 512, 8, True, None, None),
     ("FB15K-237-ZS", "transe", 200, 8, True, 3, None),
+    ("FB15K-237-ZS", "transe", 200, 1, True, None, "undecided"),
     ("FB15K-237-ZS", "transe", 200, 2, True, None, "undecided"),
     ("FB15K-237-ZS", "transe", 200, 8, True, None, "undecided")])
 def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph, keep, cost):
@@ -161,7 +162,8 @@ def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, wor
     of order -- and rank 0's metrics are bit-equal to one process. keep=3: three test triples
     (6 sweeps) over 8 ranks, so two ranks own an empty shard and still join the all-gather.
     cost="undecided": the partition packed by calibrated per-query cost (rank 0's calibration
-    broadcast: every rank holds the same masks)."""
+    broadcast: every rank holds the same masks) and each rank's queries swept heaviest first
+    (world 1: the whole set reordered, the counts put back in query order by one gather)."""
     port = _free_port()
     res = str(tmp_path / "hip")
     mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph, keep, cost), nprocs=world, join=True)
