@@ -1124,6 +1124,10 @@ def main():
                     help="C3/C4/C5: OpenKE-initialised tables (truths rank ~E/2) instead of structured ones")
     ap.add_argument("--eager", action="store_true",
                     help="link configs: launch each rank's local evaluation eagerly (default: one hipGraph replay)")
+    ap.add_argument("--eval-streams", type=int, default=2, choices=[1, 2],
+                    help="link configs: evaluation slots on separate HIP streams (2: evaluation i + 1's prep / "
+                         "quantization / filter kernels run beside evaluation i's sweep; every evaluation does all "
+                         "of its work)")
     ap.add_argument("--pack", default="cost", choices=["cost", "count"],
                     help="N > 1 relation-sharded: LPT by per-query cost (one calibration evaluation counts the pairs "
                          "the L1 filter leaves undecided; TransE) or by query count")
@@ -1206,7 +1210,8 @@ def main():
         # the rank's local evaluation (entity / query prep, truth and filter kernels, sweep)
         # replayed from one hipGraph; kernel_ms comes from an eager twin after the timed region
         ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev,
-                                   graph=not args.eager, cost="undecided" if args.pack == "cost" else None)
+                                   graph=not args.eager, cost="undecided" if args.pack == "cost" else None,
+                                   streams=args.eval_streams)
         n_local = int(ev.masks[rank].sum())
         e_local = E
 
@@ -1336,7 +1341,9 @@ def main():
                                           f"query-sharded x{world} (relation-major LPT with relation splits"
                                           f"{', packed by calibrated per-query cost' if getattr(ev, 'weights', None) is not None else ''}"
                                           f"), {coll} all-gather of rank counts"),
-                          "launch": "hipGraph replay of each rank's local evaluation" if graphed else "eager"},
+                          "launch": ("hipGraph replay of each rank's local evaluation" if graphed else "eager") +
+                                    (", two evaluation slots on two HIP streams (consecutive evaluations overlap)"
+                                     if getattr(ev, "_streams", None) else "")},
                "roofline": roof,
                "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
                            "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],

@@ -2670,12 +2670,11 @@ __device__ __forceinline__ void abs_stat(float v, float& mx, float& sa) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
+__global__ __launch_bounds__(256, 7) void k_eval_prep(EvalL1 P) {
   extern __shared__ float lds[];
   __shared__ float s_nrm[64];
   __shared__ int64_t s_a[32], s_t[32], s_r[32];
   __shared__ int s_head[32];
-  __shared__ float s_rn[32];
   __shared__ float s_m[4], s_s[4];
   const int kp = P.kp, kt = kp, ls = kt + 1, rb = P.rb, rbq = P.rbq, dim = P.dim;
   const int tid = threadIdx.x, lane = tid & 31, slot = tid >> 5;
@@ -2712,8 +2711,13 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     }
     write_k_major(lds, ls, rb, kt, P.ent_km, P.e_pad, e0);
   } else {  // ---- query rows: q = h + r (tail) / -(r - t) (head), and the truth scores
+    // Two dependent global rounds: the ids, then the anchor, truth and relation rows of every
+    // query at once (into LDS); the norms and the combine work from LDS. (Reading the relation
+    // row for its norm and again for the combine, each in its own dependent rounds, made a
+    // block's latency ~27 us: K1 31.7 us for an 8-way share of C2.)
     const int64_t q0 = (int64_t)(blockIdx.x - P.n_eblk) * rbq;
-    float* y0 = lds + rbq * ls;  // the truth rows
+    float* y0 = lds + rbq * ls;      // the truth rows
+    float* z0 = lds + 2 * rbq * ls;  // the relation rows
     if (tid < rbq) {
       const int64_t q = q0 + tid;
       int64_t a = -1, tr = -1, r = 0;
@@ -2730,50 +2734,24 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
       s_t[tid] = tr;
       s_r[tid] = r;
       s_head[tid] = head;
-      if (P.norm) {  // the relation row's norm, k_prep_queries' canonical order
-        const float* rp = P.rel + r * dim;
-        float ss = 0.0f;
-        int k = 0;
-        if ((dim & 3) == 0) {
-          for (; k + 64 <= dim; k += 64) {
-            float4 v[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = reinterpret_cast<const float4*>(rp + k)[u];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              ss = ss + v[u].x * v[u].x;
-              ss = ss + v[u].y * v[u].y;
-              ss = ss + v[u].z * v[u].z;
-              ss = ss + v[u].w * v[u].w;
-            }
-          }
-        }
-        for (; k + 16 <= dim; k += 16) {
-          float v[16];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) v[u] = rp[k + u];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) ss = ss + v[u] * v[u];
-        }
-        for (; k < dim; ++k) ss = ss + rp[k] * rp[k];
-        const float nr = sqrtf(ss);
-        s_rn[tid] = nr < 1e-12f ? 1e-12f : nr;
-      }
     }
     __syncthreads();
     for (int i = slot; i < rbq; i += 8) {
-      const int64_t a = s_a[i], tr = s_t[i];
+      const int64_t a = s_a[i], tr = s_t[i], r = s_r[i];
       float* x = lds + i * ls;
       float* y = y0 + i * ls;
-#pragma unroll 4
+      float* z = z0 + i * ls;
+#pragma unroll 8
       for (int k = lane; k < kt; k += 32) {
         x[k] = (a >= 0 && k < dim) ? P.ent[a * dim + k] : 0.0f;
         y[k] = (tr >= 0 && k < dim) ? P.ent[tr * dim + k] : 0.0f;
+        z[k] = (a >= 0 && k < dim) ? P.rel[r * dim + k] : 0.0f;
       }
     }
     __syncthreads();
-    if (P.norm) {  // the anchor and truth rows normalised exactly as k_prep_rows does
-      if (tid < 2 * rbq) s_nrm[tid] = canon_norm(lds + tid * ls, dim);  // rows 0..rbq-1: x, rbq..2rbq-1: y
+    if (P.norm) {  // anchor, truth (k_prep_rows' canonical order) and relation rows
+      // (k_prep_queries' order: the same k-ascending sum of squares and clamp)
+      if (tid < 3 * rbq) s_nrm[tid] = canon_norm(lds + tid * ls, dim);  // x | y | z rows
       __syncthreads();
       for (int i = slot; i < 2 * rbq; i += 8) {
         float* x = lds + i * ls;
@@ -2784,16 +2762,17 @@ __global__ __launch_bounds__(256) void k_eval_prep(EvalL1 P) {
     }
     for (int i = slot; i < rbq; i += 8) {
       float* x = lds + i * ls;
+      const float* z = z0 + i * ls;
       const bool valid = s_a[i] >= 0;
-      const int64_t r = s_r[i];
       const bool head = s_head[i];
+      const float rn = P.norm ? s_nrm[2 * rbq + i] : 1.0f;
       for (int k = lane; k < kp; k += 32) {
         if (!valid || k >= dim) {
           x[k] = 0.0f;
           continue;
         }
         // head_batch: score = h + (r - t) -> q = -(r - t); tail_batch: (h + r) - t -> q = h + r
-        const float b = P.norm ? P.rel[r * dim + k] / s_rn[i] : P.rel[r * dim + k];
+        const float b = P.norm ? z[k] / rn : z[k];
         x[k] = head ? -(b - x[k]) : (x[k] + b);
       }
     }
@@ -2895,7 +2874,7 @@ struct EvalQuant {  // K2's quantization operands (k_l1q_quant8<TIGHT> + the 16-
   float* q_l1c;
 };
 
-__global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, const int32_t* __restrict__ ids,
+__global__ __launch_bounds__(256, 4) void k_eval_quant_list(EvalL1 P, EvalQuant Q, const int32_t* __restrict__ ids,
                                                          const int32_t* __restrict__ entry_q, int64_t n_entries,
                                                          float* __restrict__ list_v, int n_lblk) {
   if ((int)blockIdx.x < n_lblk) {  // ---- filter-list scores (k_filter_scores' list tasks)
@@ -2964,35 +2943,50 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
     const bool live = cb + cl < n;
     const int64_t c = c0 + cb + cl;
     float err = 0.0f;
-#pragma unroll 2
-    for (int r = g; r < kw; r += 8) {
-      uint32_t word = 0u, w16a = 0u, w16b = 0u;
+    // four word rows of a thread in flight together (kw <= 64 word rows -- d <= 256 -- is two
+    // load rounds instead of four; eight took 167 VGPRs), then coded in the same order as before
+    for (int r0 = g; r0 < kw; r0 += 32) {
+      float xv[4][4];
 #pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        const int k = 4 * r + h;
-        if (live && k < kp) {
-          const float x = km[(int64_t)k * pad + c];
-          float t = (x + off) * inv;
-          t = t == t ? fminf(fmaxf(t, 0.0f), 255.0f) : 0.0f;
-          const float code = rintf(t);
-          word |= (uint32_t)code << (8 * h);
-          if (Q.tight) err += fabsf(x - (code * delta - off));
-          float t16 = (x + off) * inv16;
-          t16 = t16 == t16 ? fminf(fmaxf(t16, 0.0f), 65535.0f) : 0.0f;
-          const uint32_t c16 = (uint32_t)rintf(t16);
-          if (h < 2) w16a |= c16 << (16 * h);
-          else w16b |= c16 << (16 * (h - 2));
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int k = 4 * (r0 + 8 * j) + h;
+          xv[j][h] = (live && r0 + 8 * j < kw && k < kp) ? km[(int64_t)k * pad + c] : 0.0f;
         }
-      }
-      if (live) {
-        if (!(Q.tight && r == words)) out[(int64_t)r * pad + c] = word;
-        if (2 * r < k2) out16[(int64_t)(2 * r) * pad + c] = w16a;
-        if (2 * r + 1 < k2) out16[(int64_t)(2 * r + 1) * pad + c] = w16b;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = r0 + 8 * j;
+        if (r >= kw) break;
+        uint32_t word = 0u, w16a = 0u, w16b = 0u;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const int k = 4 * r + h;
+          if (live && k < kp) {
+            const float x = xv[j][h];
+            float t = (x + off) * inv;
+            t = t == t ? fminf(fmaxf(t, 0.0f), 255.0f) : 0.0f;
+            const float code = rintf(t);
+            word |= (uint32_t)code << (8 * h);
+            if (Q.tight) err += fabsf(x - (code * delta - off));
+            float t16 = (x + off) * inv16;
+            t16 = t16 == t16 ? fminf(fmaxf(t16, 0.0f), 65535.0f) : 0.0f;
+            const uint32_t c16 = (uint32_t)rintf(t16);
+            if (h < 2) w16a |= c16 << (16 * h);
+            else w16b |= c16 << (16 * (h - 2));
+          }
+        }
+        if (live) {
+          if (!(Q.tight && r == words)) out[(int64_t)r * pad + c] = word;
+          if (2 * r < k2) out16[(int64_t)(2 * r) * pad + c] = w16a;
+          if (2 * r + 1 < k2) out16[(int64_t)(2 * r + 1) * pad + c] = w16b;
+        }
       }
     }
     if (Q.tight) {
       s_err[g][cl] = err;
       __syncthreads();
+      uint32_t o_max = 0u;  // this chunk's largest entity offset (wave 0), one atomic per chunk
       if (g == 0 && live) {
         float e = 0.0f;
 #pragma unroll
@@ -3005,7 +2999,7 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
           // (<= 1,005 at kt <= 1,984 without the clamp acting: see k_l1q_quant8)
           uint32_t o = delta > 0.0f ? (uint32_t)ceilf(fminf(eb / (delta * (1.0f - l1f)) * (1.0f + 0x1p-17f), 1020.0f))
                                     : 0u;
-          if (o) atomicMax(P.hdr + 3, o);
+          o_max = o;
 #pragma unroll
           for (int h = 0; h < 4; ++h) {
             const uint32_t bb = o < 255u ? o : 255u;
@@ -3014,6 +3008,11 @@ __global__ __launch_bounds__(256) void k_eval_quant_list(EvalL1 P, EvalQuant Q, 
           }
         }
         out[(int64_t)words * pad + c] = wv;
+      }
+      if (ent && threadIdx.x < 64) {  // uniform per wave: 32 lanes' offsets -> one atomicMax
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) o_max = max(o_max, (uint32_t)__shfl_xor((int)o_max, sh));
+        if (threadIdx.x == 0 && o_max) atomicMax(P.hdr + 3, o_max);
       }
       __syncthreads();
     }
@@ -3670,7 +3669,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   hipStream_t st = (hipStream_t)stream;
   const int kp = plane_rows(MMRE_TRANSE_L1, dim), kt = kp, k2 = l1q_rows(dim), k4 = l1q_rows8(dim);
   const int rb = eval_rb(kp), rbq = eval_rbq(kp);
-  const size_t lds1 = sizeof(float) * (size_t)std::max(rb, 2 * rbq) * (kt + 1);
+  const size_t lds1 = sizeof(float) * (size_t)std::max(rb, 3 * rbq) * (kt + 1);
   if (lds1 > 64 * 1024) return MMRE_ERR_SHAPE;
   char* w = (char*)d_work;
   uint32_t* hdr = (uint32_t*)w;
@@ -3734,10 +3733,13 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   Q.kw = k4;
   Q.k2 = k2;
   Q.kt = kt;
-  Q.n_blk = 512;
+  const int n_lblk = (int)((n_entries + 255) / 256);
+  // quantization blocks per plane: the list blocks and both planes' blocks resident at once (one
+  // round: 2 x 512 + the list blocks took two at an 8-way share of C2, 23 us)
+  Q.n_blk = (int)std::min<int64_t>(512, std::max<int64_t>(64, (resident_groups((const void*)k_eval_quant_list, 256) -
+                                                              n_lblk) / 2));
   Q.tight = tight ? 1 : 0;
   Q.q_l1c = q_l1c;
-  const int n_lblk = (int)((n_entries + 255) / 256);
   hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), 0, st, P, Q, d_filt_ids,
                      d_entry_q, n_entries, d_list_scores, n_lblk);
   MMRE_CHECK_LAUNCH();

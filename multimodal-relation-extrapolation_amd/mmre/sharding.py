@@ -155,20 +155,21 @@ class ShardPlan:
             for c in range(4):
                 src[c, self.ids[k]] = (k * 4 + c) * self.pad + np.arange(self.sizes[k])
         self.src = torch.from_numpy(src).to(device)
-        self.buf = None   # persistent exchange buffers (allocated on first use)
+        self.bufs = {}    # persistent exchange buffers per evaluation slot (allocated on first use)
         self.device = device
 
 
-def gather_counts(local_counts: torch.Tensor, plan: ShardPlan, group=None):
+def gather_counts(local_counts: torch.Tensor, plan: ShardPlan, group=None, slot: int = 0):
     """All-gather per-rank (4, n_local) int32 count lists into global query order: ONE
     collective of world x 4 x pad int32 (about 282 KB in total at FB15K-237-ZS), no index
-    exchange (every rank knows the partition)."""
+    exchange (every rank knows the partition). `slot`: the evaluation slot whose exchange
+    buffers to use (evaluations in flight on different streams must not share them)."""
     import torch.distributed as dist
-    if plan.buf is None:
+    if slot not in plan.bufs:
         # persistent: the padding columns are never read (plan.src skips them), so no zeroing
-        plan.buf = torch.empty((4, plan.pad), dtype=torch.int32, device=plan.device)
-        plan.out = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32, device=plan.device)
-    buf, out = plan.buf, plan.out
+        plan.bufs[slot] = (torch.empty((4, plan.pad), dtype=torch.int32, device=plan.device),
+                           torch.empty((plan.world * 4, plan.pad), dtype=torch.int32, device=plan.device))
+    buf, out = plan.bufs[slot]
     buf[:, :local_counts.shape[1]] = local_counts
     if buf.is_cuda and dist.get_backend(group) == "gloo":  # gloo (tests): the exchange goes through host memory
         host = torch.empty((plan.world * 4, plan.pad), dtype=torch.int32)
@@ -194,10 +195,16 @@ class ShardedLinkEvaluation:
     query prep, truth/filter kernels, sweep -- is captured once into a hipGraph and replayed,
     so its ~6 launches cost one; what a rank pays whatever its share shrinks.
     The all-gather and the D2H stay outside the graph. Timing events passed to counts() then
-    bracket the whole replay, not the sweep kernel alone."""
+    bracket the whole replay, not the sweep kernel alone.
+
+    streams=2 (default runner on a GPU): two evaluation slots, each with its own LinkSweep
+    buffers, hipGraph, exchange buffers and HIP stream; launch() alternates them, so evaluation
+    i + 1's short latency-bound kernels (prep, quantization, filter counts) run beside the tail
+    of evaluation i's sweep instead of after it. Every evaluation still does all of its work
+    from the raw tables; only independent evaluations overlap."""
 
     def __init__(self, spec, test_h, test_r, test_t, index=None, type_constrain=False, group=None,
-                 device=None, local_runner=None, graph=False, cost=None):
+                 device=None, local_runner=None, graph=False, cost=None, streams=1):
         import torch.distributed as dist
         from .link import HEAD, TAIL
         self.group = group
@@ -237,42 +244,57 @@ class ShardedLinkEvaluation:
             inv[mine] = np.arange(len(mine))
             self._unperm = to(inv)
         self._default_runner = local_runner is None
+        n_slots = 2 if (streams > 1 and local_runner is None and dev.type == "cuda") else 1
+        self._runners = [local_runner] * n_slots
         if local_runner is None:
             from .link import LinkSweep
-            sw = LinkSweep(spec)
-            bufs = sw.alloc_queries(len(mine))
+            self._sweeps = []
+            for j in range(n_slots):
+                sw = LinkSweep(spec)
+                bufs = sw.alloc_queries(len(mine))
 
-            def local_runner(qh_, qr_, qt_, qm_, filt, masks_tc, events=None):
-                return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs,
-                              sweep_events=events)["counts"]
-            self.sweep, self.sweep_buffers = sw, bufs
-        self.local_runner = local_runner
+                def run_slot(qh_, qr_, qt_, qm_, filt, masks_tc, events=None, sw=sw, bufs=bufs):
+                    return sw.run(qh_, qr_, qt_, qm_, filt=filt, type_masks=masks_tc, buffers=bufs,
+                                  sweep_events=events)["counts"]
+                self._runners[j] = run_slot
+                self._sweeps.append((sw, bufs))
+            self.sweep, self.sweep_buffers = self._sweeps[0]
+        self.local_runner = self._runners[0]
+        self._streams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if n_slots > 1 else None
         self._graph_wanted = bool(graph) and dev.type == "cuda" and self._default_runner
-        self._graph = None
+        self._graphs = [None] * n_slots
+        self._graph_outs = [None] * n_slots
 
-    def _local(self, events=None):
+    def _local(self, events=None, slot=0):
+        run = self._runners[slot]
         if not self._graph_wanted:
-            return self.local_runner(*self.q, self.filt, self.masks_tc, events)
-        if self._graph is None:
+            return run(*self.q, self.filt, self.masks_tc, events)
+        if self._graphs[slot] is None:
             # one eager run allocates every lazily sized buffer, then capture on a side stream
-            self.local_runner(*self.q, self.filt, self.masks_tc, None)
+            run(*self.q, self.filt, self.masks_tc, None)
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._graph_out = self.local_runner(*self.q, self.filt, self.masks_tc, None)
-            self._graph = g
+                self._graph_outs[slot] = run(*self.q, self.filt, self.masks_tc, None)
+            self._graphs[slot] = g
         if events is not None:
             events[0].record()
-        self._graph.replay()
+        self._graphs[slot].replay()
         if events is not None:
             events[1].record()
-        return self._graph_out
+        return self._graph_outs[slot]
 
     def counts(self, events=None):
-        """(4, 2n) int32 counts in global query order (head block, then tail block)."""
-        local = self._local(events)
+        """(4, 2n) int32 counts in global query order (head block, then tail block), on the
+        current stream (which first waits for slot 0's stream, whose buffers it reuses)."""
+        if self._streams is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._streams[0])
+        return self._counts(events, 0)
+
+    def _counts(self, events=None, slot=0):
+        local = self._local(events, slot)
         if self.world > 1:
-            return gather_counts(local, self.plan, self.group)
+            return gather_counts(local, self.plan, self.group, slot)
         return local if self._unperm is None else local.index_select(1, self._unperm)
 
     def launch(self, events=None):
@@ -284,9 +306,25 @@ class ShardedLinkEvaluation:
         free = getattr(self, "_free", None)
         if free is not None and not free:
             raise RuntimeError("ShardedLinkEvaluation: finish() a ticket before launching a third")
+        if self._streams is not None:
+            # the evaluation slot = the free pinned buffer; its stream first waits for whatever
+            # the caller's stream has enqueued (the inputs)
+            if free is None:
+                self._free = free = [0, 1]
+            slot = free[0]
+            st = self._streams[slot]
+            st.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(st):
+                ticket = self._stage(self._counts(events, slot), st)
+            return ticket
         c = self.counts(events)
         if not c.is_cuda:
             return [c.numpy(), None, None]
+        return self._stage(c, torch.cuda.current_stream(c.device))
+
+    def _stage(self, c, stream):
+        """D2H of the count table into a free pinned buffer on `stream`; the ticket."""
+        free = getattr(self, "_free", None)
         hosts = getattr(self, "_hosts", None)
         if hosts is None or hosts[0].shape != c.shape:
             if free is not None and len(free) != 2:
@@ -297,7 +335,7 @@ class ShardedLinkEvaluation:
         h = hosts[slot]
         h.copy_(c, non_blocking=True)
         done = torch.cuda.Event()
-        done.record(torch.cuda.current_stream(c.device))
+        done.record(stream)
         return [h, done, slot]
 
     def finish(self, ticket, copy_counts=True):
@@ -400,7 +438,7 @@ class EntityShardedLinkEvaluation(ShardedLinkEvaluation):
         self.plan = None
         self._default_runner = False
         self._graph_wanted = False
-        self._graph = None
+        self._streams = None
         sw = LinkSweep(spec)
         bufs = sw.alloc_queries(2 * self.n)
         e0, e1 = self.entity_range

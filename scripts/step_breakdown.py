@@ -36,6 +36,8 @@ def main():
                     "from a hipGraph")
     ap.add_argument("--pack", default="cost", choices=["cost", "count"],
                     help="--emulate-world: LPT by calibrated per-query cost (bench default) or by query count")
+    ap.add_argument("--streams", type=int, default=2, choices=[1, 2],
+                    help="--emulate-world --graph: evaluation slots on separate streams (bench.py --eval-streams)")
     ap.add_argument("--no-order", action="store_true",
                     help="--emulate-world: keep each rank's queries ascending (default: heaviest calibrated cost first)")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
@@ -155,24 +157,57 @@ def emulate(a):
             for _ in range(3):
                 step()
         ms_sync = timeit(step, a.reps)
-        # pipelined as bench.py runs it: evaluation i + 1 enqueued before i's counts are waited
-        # for (D2H into alternating pinned buffers), one synchronisation at the end
+        # the bench's loop (bench.py steps(), ShardedLinkEvaluation.launch / finish): evaluation
+        # i is enqueued (graph replay + D2H of its counts into one of two pinned buffers), then
+        # the host waits for evaluation i - 1 and runs the Test.h metric reduction of the WHOLE
+        # count table (every rank reduces the gathered 4 x 2n table; here a full-size stand-in),
+        # so evaluation i runs while the host reduces i - 1. With two streams (streams=2) the
+        # evaluations alternate between two buffer sets / graphs / streams.
         hosts = [torch.empty_like(host) for _ in range(2)]
-
-        def piped(reps):
+        full = np.zeros((4, 2 * n), np.int32)
+        slots = [(sw, bufs, g if a.graph else None, gc if a.graph else None)]
+        if a.graph and a.streams == 2:
+            sw_b = LinkSweep(spec)
+            bufs_b = sw_b.alloc_queries(len(m))
+            sw_b.run(*q, filt=filt, buffers=bufs_b, entity_range=er)
             torch.cuda.synchronize()
+            g_b = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_b):
+                gc_b = sw_b.run(*q, filt=filt, buffers=bufs_b, entity_range=er)["counts"]
+            slots.append((sw_b, bufs_b, g_b, gc_b))
+        ss = [torch.cuda.Stream() for _ in slots] if len(slots) > 1 else [torch.cuda.current_stream()]
+
+        def looped(reps, n_slots):
+            torch.cuda.synchronize()
+            done = [torch.cuda.Event(), torch.cuda.Event()]
             t = time.perf_counter()
+            pend = None
             for i in range(reps):
-                if a.graph:
-                    g.replay()
-                    c = gc
-                else:
-                    c = sw.run(*q, filt=filt, buffers=bufs, entity_range=er)["counts"]
-                hosts[i & 1].copy_(c, non_blocking=True)
+                j = i % n_slots
+                s_w, b_w, g_w, c_w = slots[j]
+                with torch.cuda.stream(ss[j]):
+                    if g_w is not None:
+                        g_w.replay()
+                        c = c_w
+                    else:
+                        c = s_w.run(*q, filt=filt, buffers=b_w, entity_range=er)["counts"]
+                    hosts[i & 1].copy_(c, non_blocking=True)
+                    done[i & 1].record(ss[j])
+                if pend is not None:
+                    done[pend].synchronize()
+                    link_metrics(full[:, :n], full[:, n:])
+                pend = i & 1
+            done[pend].synchronize()
+            link_metrics(full[:, :n], full[:, n:])
             torch.cuda.synchronize()
             return (time.perf_counter() - t) / reps * 1e3
-        piped(3)
-        ms = piped(max(a.reps, 50))
+        looped(3, 1)
+        ms1 = looped(max(a.reps, 50), 1)
+        ms = ms1
+        if len(slots) > 1:
+            looped(3, 2)
+            ms = looped(max(a.reps, 50), 2)
+            assert np.array_equal(slots[0][3].cpu().numpy(), slots[1][3].cpu().numpy())
         # the count exchange's own kernels (copy into the all-gather buffer + the one gather into
         # global order; mmre.sharding.gather_counts) on this GPU; the RCCL all-gather itself cannot
         # run on one GPU: EST_ALLGATHER_MS stands in for it (see the summary line)
@@ -201,13 +236,14 @@ def emulate(a):
         sweep = float(np.median(ts))
         if a.emulate_world > 1 and k == 0:
             one = ms
-            print(f"N=1: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined ({ms_sync:.3f} ms with a sync "
-                  f"per evaluation)")
+            print(f"N=1: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined{' on 2 streams' if ms != ms1 else ''} "
+                  f"(one stream {ms1:.3f}; {ms_sync:.3f} ms with a sync per evaluation)")
             continue
         worst = max(worst, ms)
         worst_x = max(worst_x, xch)
         fst = sw.filter_stats(bufs)
         print(f"rank {k - (1 if one is not None else 0)}: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined "
+              f"(one stream {ms1:.3f}) "
               f"({ms_sync:.3f} synced), sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms, exchange kernels "
               f"{xch:.3f} ms, filter {fst}")
     if one is not None:

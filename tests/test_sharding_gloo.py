@@ -111,7 +111,7 @@ def _spec(w, model, dim, dev):
                      phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
 
 
-def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_triples=None, cost=None):
+def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_triples=None, cost=None, streams=1):
     """Each rank: the HIP sweep on cuda:0 through ShardedLinkEvaluation.launch/finish (counts
     exchanged over gloo through host memory); rank 0 also runs the single-process evaluation
     and the out-of-order ticket sequence."""
@@ -126,7 +126,8 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_tr
     index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
     spec = _spec(w, model, dim, dev)
     ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev, graph=graph,
-                               cost=cost)
+                               cost=cost, streams=streams)
+    assert (ev._streams is not None) == (streams == 2)
     assert (ev.weights is not None) == (cost == "undecided" and model == "transe")
     a = ev.launch()
     b = ev.launch()
@@ -145,16 +146,16 @@ def _gpu_worker(rank, world, port, res_path, dataset, model, dim, graph, keep_tr
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dataset,model,dim,world,graph,keep,cost", [
-    ("FB15K-237-ZS", "transe", 200, 2, False, None, None),
-    ("FB15K-237-ZS", "transe", 200, 2, True, None, None),
-    ("DB15K-ZS", "complex", 200, 3, True, None, None),
-    ("FB15K-237-ZS", "rotate", 512, 8, True, None, None),
-    ("FB15K-237-ZS", "transe", 200, 8, True, 3, None),
-    ("FB15K-237-ZS", "transe", 200, 1, True, None, "undecided"),
-    ("FB15K-237-ZS", "transe", 200, 2, True, None, "undecided"),
-    ("FB15K-237-ZS", "transe", 200, 8, True, None, "undecided")])
-def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph, keep, cost):
+@pytest.mark.parametrize("dataset,model,dim,world,graph,keep,cost,streams", [
+    ("FB15K-237-ZS", "transe", 200, 2, False, None, None, 1),
+    ("FB15K-237-ZS", "transe", 200, 2, True, None, None, 1),
+    ("DB15K-ZS", "complex", 200, 3, True, None, None, 2),
+    ("FB15K-237-ZS", "rotate", 512, 8, True, None, None, 1),
+    ("FB15K-237-ZS", "transe", 200, 8, True, 3, None, 2),
+    ("FB15K-237-ZS", "transe", 200, 1, True, None, "undecided", 2),
+    ("FB15K-237-ZS", "transe", 200, 2, True, None, "undecided", 1),
+    ("FB15K-237-ZS", "transe", 200, 8, True, None, "undecided", 2)])
+def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, world, graph, keep, cost, streams):
     """The multi-rank path with the real HIP sweep at full size (C2; C3 with its largest
     relation split across ranks; C4 RotatE d 512 at world 8, the driver's node size, every
     rank on the one GPU of the box), eager and with each rank's local evaluation replayed from
@@ -163,10 +164,13 @@ def test_sharded_hip_sweep_equals_single_rank(tmp_path, dataset, model, dim, wor
     (6 sweeps) over 8 ranks, so two ranks own an empty shard and still join the all-gather.
     cost="undecided": the partition packed by calibrated per-query cost (rank 0's calibration
     broadcast: every rank holds the same masks) and each rank's queries swept heaviest first
-    (world 1: the whole set reordered, the counts put back in query order by one gather)."""
+    (world 1: the whole set reordered, the counts put back in query order by one gather).
+    streams=2: two evaluation slots on two HIP streams, so the three overlapping evaluations
+    run on alternating buffers / graphs / exchange buffers."""
     port = _free_port()
     res = str(tmp_path / "hip")
-    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph, keep, cost), nprocs=world, join=True)
+    mp.spawn(_gpu_worker, args=(world, port, res, dataset, model, dim, graph, keep, cost, streams), nprocs=world,
+             join=True)
     outs = [dict(np.load(f"{res}_{k}.npz")) for k in range(world)]
     single = outs[0]["single"]
     assert bool(outs[0]["metrics_equal"])
