@@ -512,7 +512,7 @@ def bench_ns(args, world, rank, dev, dist):
         graphs = []
         fork = torch.cuda.Stream(dev)
         cur = torch.cuda.current_stream(dev)
-        for par in ((0,) if (not args.ns_prefetch) else (0, 1)):
+        for par in ((0,) if (not args.ns_prefetch and tstep is None) else (0, 1)):
             opt.zero_grad(set_to_none=True)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -533,8 +533,8 @@ def bench_ns(args, world, rank, dev, dist):
                     if not (not args.ns_prefetch):
                         torch.cuda.current_stream(dev).wait_stream(fork)
             graphs.append(g)
-            if tstep is not None:
-                break
+            if tstep is not None and (not tstep.pipeline or len(graphs) == 2):
+                break  # the pipelined one-call step: one graph per parity, replayed alternately
         graph = graphs[0]
         if not (not args.ns_prefetch):
             smp.sample(B, k, out=bufs[0])  # the first batch; every replay then prefetches the next
@@ -553,6 +553,19 @@ def bench_ns(args, world, rank, dev, dist):
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    pipe_ms = None
+    if graph is not None and tstep is not None and tstep.pipeline:
+        # the pipelined step's two launches (fused loss kernel; row owner with SGD, the loss, the
+        # next batch's sampler and the updated rows' pre-pass): events around replays of its graphs
+        pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for i, (a_, b_) in enumerate(pev):
+            a_.record()
+            graphs[(args.steps + i) % 2].replay()
+            b_.record()
+        torch.cuda.synchronize()
+        pipe_ms = float(np.mean([a_.elapsed_time(b_) for a_, b_ in pev]))
+    if tstep is not None and graph is not None:
+        tstep.invalidate()  # the replays advanced the device state past the step object's record
     if graph is not None:  # the fused call and the step's parts timed on eager steps after the timed region
         loss = g_loss.detach().clone()
         del g_loss, g_b, graph, graphs  # drop the captured autograd graphs before eager backward passes
@@ -619,8 +632,10 @@ def bench_ns(args, world, rank, dev, dist):
             fwd_bytes = n_rows * (2 * eb + rb) + n_rows * 3 * 8
             grad_bytes = E * eb + R * rb
             slot_bytes = 2 * (B * (3 + 3 * k)) * 2 * 4 * (256 if d > 128 else 128)
-        ach = (fwd_bytes + grad_bytes) / (fused_ms * 1e-3) / 1e9
-        step_kernels = (["k_ns_prepass(", "k_ns_transe_fused<4, false, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
+        kern_ms = pipe_ms if pipe_ms is not None else fused_ms
+        ach = (fwd_bytes + grad_bytes) / (kern_ms * 1e-3) / 1e9
+        step_kernels = (["k_ns_transe_fused<4, false, false>", "k_ns_row_owner<4, false>"] if pipe_ms is not None else
+                        ["k_ns_prepass(", "k_ns_transe_fused<4, false, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
                         if model == "transe" else
                         ["k_ns_gen_forward<4, ", "k_ns_reduce(", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"])
         pmc_cfg = "ns" if model == "transe" else f"ns_{model}"  # profiles/pmc_<pmc_cfg>.json
@@ -636,7 +651,10 @@ def bench_ns(args, world, rank, dev, dist):
                           f"{model} d=200 training step at the C2 training shape (margin loss)", "model": model,
                           "batch": B, "neg_ent": k, "rows_per_step": n_rows,
                           "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}",
-                          "step": ("mmre_ns_step_openke (sampler + pre-pass, fused loss, row owner + SGD + loss "
+                          "step": ("mmre_ns_step_openke_pipe (fused loss kernel; row owner + SGD + loss reduction "
+                                   "+ the next batch's sampler + the updated rows' pre-pass: 2 launches)"
+                                   if tstep is not None and tstep.pipeline else
+                                   "mmre_ns_step_openke (sampler + pre-pass, fused loss, row owner + SGD + loss "
                                    "reduction: 3 launches)" if tstep is not None else
                                    "sampler.sample + fused_ns_loss + backward + SGD.step (drop-in path)"),
                           "launch": ("eager" if not graph else "hipGraph replay of the whole step" +
@@ -647,21 +665,27 @@ def bench_ns(args, world, rank, dev, dist):
                                             "2 x FETCH_SIZE + WRITE_SIZE)",
                             "traffic_source": tsrc, "traffic_per_kernel": tper,
                             "traffic_x_algorithmic": (traffic / (fwd_bytes + grad_bytes)) if traffic else None,
-                            "kernel": ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false, false> + "
-                                       "k_ns_reduce (the loss) + k_ns_row_owner<4, false>" if model == "transe" else
-                                       "mmre_ns_forward_backward = k_ns_forward + k_ns_reduce + k_ns_gen_slots + "
-                                       "k_ns_gen_owner") + ": events around hipGraph replays of the one-shot C-ABI call",
-                            "kernel_ms": fused_ms, "eager_fused_forward_ms": fused_fwd_ms,
+                            "kernel": ("mmre_ns_step_openke_pipe = k_ns_transe_fused<4, false, false> + "
+                                       "k_ns_row_owner<4, false> (+ the loss reduction, the next batch's sampler "
+                                       "workgroups and the updated rows' pre-pass in its grid): events around "
+                                       "hipGraph replays of the step (one graph per parity)" if pipe_ms is not None else
+                                       ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false, false> + "
+                                        "k_ns_reduce (the loss) + k_ns_row_owner<4, false>" if model == "transe" else
+                                        "mmre_ns_forward_backward = k_ns_forward + k_ns_reduce + k_ns_gen_slots + "
+                                        "k_ns_gen_owner") + ": events around hipGraph replays of the one-shot C-ABI call"),
+                            "kernel_ms": kern_ms, "forward_backward_ms": fused_ms, "eager_fused_forward_ms": fused_fwd_ms,
                             "eager_fused_grad_ms": fused_grad_ms,
                             "algorithmic_bytes": fwd_bytes + grad_bytes, "slot_bytes": slot_bytes,
-                            "implementation_frac": (fwd_bytes + grad_bytes + slot_bytes) / (fused_ms * 1e-3)
+                            "implementation_frac": (fwd_bytes + grad_bytes + slot_bytes) / (kern_ms * 1e-3)
                                                    / (HBM_PEAK_GBS * 1e9),
                             "step_forward_ms": fwd_ms, "step_backward_ms": bwd_ms,
                             "note": "no float atomics: the gradient contributions are bucketed by table row and "
                                     "one wave per table row summing them in batch order (bit-reproducible); the "
-                                    "TransE step is three launches (mmre_ns_step_openke): the sampler's workgroups beside the "
-                                    "pre-pass, the fused loss kernel, the row-owner pass with the SGD step and the loss "
-                                    "reduction folded in -- bit-identical to the drop-in path's five (--ns-autograd)"},
+                                    "TransE step is two launches (mmre_ns_step_openke_pipe): the fused loss kernel, the "
+                                    "row-owner pass with the SGD step, the loss reduction, the NEXT batch's sampler and "
+                                    "the pre-pass of the rows it updates folded in (a prefetching loader; the first step "
+                                    "adds the sampler + pre-pass launch) -- bit-identical to mmre_ns_step_openke's three "
+                                    "and the drop-in path's five (--ns-autograd)"},
                "last_loss": float(loss.detach())}
         if world == 1 and not args.no_cpu_baseline and model == "transe":
             out["cpu_baseline"] = ref_trainer_leg(w, B, k, margin)

@@ -430,6 +430,31 @@ int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_total, const 
                         float loss_margin, float adv_temperature, float regul_rate, float* d_score, float* d_loss,
                         float* d_grad_ent, float* d_grad_rel, float* d_work, float lr, void* stream);
 
+/* The same step, pipelined across calls (a prefetching data loader; Trainer.py:43-54 over the
+ * loader's batches): the row owner of this step also samples the NEXT batch into d_next_* (the
+ * sampler's seeds advance by that batch) and writes the norms / normalised copies of the rows it
+ * updates -- the pre-pass the next step needs (a row without gradient keeps its parameters, so
+ * its entries stay current) -- and zeroes the other parity's slot counts. prepared: bit 0 =
+ * d_batch_* already holds this step's batch (the previous call's d_next_*), bit 1 = the pre-pass
+ * and the slot counts of `parity` are current (the previous call was this one's other parity,
+ * d_ent / d_rel / d_work unchanged since). prepared = 3 skips the first launch; otherwise it
+ * samples d_batch_* (bit 0 clear) and runs the pre-pass, as mmre_ns_step_openke (whose d_work
+ * layout this shares). d_next_h == NULL: no next batch (the next call: prepared bit 0 clear).
+ * Batches, losses, gradients, parameters and seeds are bit-identical to consecutive
+ * mmre_ns_step_openke calls. */
+int mmre_ns_step_openke_pipe(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                             const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                             const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                             const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                             const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode,
+                             const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
+                             int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, int model, int norm_flag,
+                             float* d_ent, float* d_rel, int64_t n_ent, int64_t n_rel, int dim, int64_t batch,
+                             int64_t neg, float loss_margin, float adv_temperature, float regul_rate, float* d_score,
+                             float* d_loss, float* d_grad_ent, float* d_grad_rel, float* d_work, float lr,
+                             void* stream, int64_t prepared, int64_t parity, int64_t* d_next_h, int64_t* d_next_t,
+                             int64_t* d_next_r, float* d_next_y);
+
 /* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
  * batch = n_rows, neg = 0, d_loss = NULL. Its backward (OpenKE Model.forward under any loss,
  * Model.py / SoftplusLoss.py:7-31 / SigmoidLoss.py:7-30; the repo's scoring_fn / _calc,

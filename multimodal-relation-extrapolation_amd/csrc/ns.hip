@@ -469,6 +469,28 @@ struct NSSlots {        // the row-owner gradient's workspace
   uint32_t sentinel;    // n_ent + n_rel: no slot
 };
 
+// The pipelined TransE training step (mmre_ns_step_openke_pipe): what the row owner of step i
+// also does for step i + 1, so that step i + 1 is two launches (fused loss kernel, row owner)
+// instead of three:
+//  * the next batch's sampler workgroups (sa; blocks [block0, block0 + n_blocks) of the grid)
+//    -- the sampler reads only the train index and its seeds, so it runs beside the gradient;
+//  * the pre-pass of every row this step changes: a row's wave that wrote fma(-lr, g, v) also
+//    writes its norm and (norm_flag) its normalised copy, the values k_ns_prepass computes from
+//    the updated table (same arithmetic: sum of squares over c, wave_sum, sqrtf, x / max(n, eps)).
+//    A row without slots keeps its parameters, so its norm and normalised copy stay current;
+//  * the next step's slot counts (the other parity's array, + its overflow count) zeroed.
+// Every step still samples one batch, scores it and updates the rows it touches; only the
+// launch that sampled and re-normalised the (unchanged) rest of the table is gone.
+struct NSNext {
+  OpenKESamplerArgs sa;         // the next batch (n_blocks == 0: none)
+  int64_t block0, n_blocks;     // its sampler workgroups in the row owner's grid
+  int32_t* counts;              // the next step's slot counts [E + R] + overflow count (nullptr: none)
+  float* nrm_e;                 // norms of the updated rows (nullptr: no pre-pass)
+  float* nrm_r;
+  float* ent_n;                 // norm_flag: the updated rows normalised (else nullptr)
+  float* rel_n;
+};
+
 // slot id and its row's occurrences in the batch (the regularization weight) as one bucket entry:
 // ordering entries orders the slot ids
 __device__ __forceinline__ int64_t slot_entry(int64_t slot, float mult) {
@@ -1266,7 +1288,8 @@ __device__ __forceinline__ void transe_owner_row(Ord& ord, bool active, int64_t 
                                                  float nv, int64_t n_ent, int d, int norm_flag, float reg,
                                                  const float* __restrict__ shared, const float* __restrict__ rec,
                                                  int64_t K, const float* __restrict__ grad_loss, float* gent,
-                                                 float* grel, float sgd_lr, float* pent, float* prel) {
+                                                 float* grel, float sgd_lr, float* pent, float* prel,
+                                                 const NSNext& nx) {
   const int lane = threadIdx.x & 63;
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
@@ -1344,6 +1367,17 @@ __device__ __forceinline__ void transe_owner_row(Ord& ord, bool active, int64_t 
 #pragma unroll
     for (int c = 0; c < NC; ++c) p.v[c] = __builtin_fmaf(-sgd_lr, dy.v[c], v.v[c]);
     vstore_row(is_ent ? pent : prel, id, p, d, lane);
+    if (nx.nrm_e) {  // the next step's pre-pass of this row (ns_prepass_block's arithmetic)
+      const float nr = sqrtf(wave_sum(vsq(p)));
+      if (lane == 0) (is_ent ? nx.nrm_e : nx.nrm_r)[id] = nr;
+      if (nx.ent_n) {
+        const float cn = fmaxf(nr, 1e-12f);
+        Vec<NC> o;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) o.v[c] = p.v[c] / cn;
+        vstore_row(is_ent ? nx.ent_n : nx.rel_n, id, o, d, lane);
+      }
+    }
   }
 }
 
@@ -1368,7 +1402,7 @@ __device__ __forceinline__ HubOrder hub_order(int64_t (*s_hub)[NS_HUB], int32_t*
 template <int NC, bool L2>
 __global__ __launch_bounds__(256, NC > 4 ? 5 : 7) void k_ns_row_owner(const float* ent, const float* rel,
                                                       int64_t n_ent, int64_t n_rel, int d, int norm_flag, float reg,
-                                                      const float* __restrict__ nrm_e, const float* __restrict__ nrm_r,
+                                                      const float* nrm_e, const float* nrm_r,
                                                       const float* __restrict__ shared, const float* __restrict__ rec,
                                                       const int32_t* __restrict__ counts,
                                                       const int64_t* __restrict__ bucket, const int64_t* __restrict__ ovf,
@@ -1377,12 +1411,16 @@ __global__ __launch_bounds__(256, NC > 4 ? 5 : 7) void k_ns_row_owner(const floa
                                                       float* __restrict__ grel, float sgd_lr, float* pent,
                                                       float* prel, NSArgs RA, const float* __restrict__ part,
                                                       float* __restrict__ loss, int64_t reduce_block,
-                                                      int64_t row_block0, int n_hub_wg, int64_t n_slots) {
+                                                      int64_t row_block0, int n_hub_wg, int64_t n_slots, NSNext nx) {
   __shared__ int64_t s_hub[4][NS_HUB];
   __shared__ uint16_t s_bits[256];
   __shared__ int32_t s_hc[2];
   if ((int64_t)blockIdx.x == reduce_block) {  // the training step's loss (mmre_ns_step_openke): one extra workgroup
     ns_reduce_block(RA, part, loss);
+    return;
+  }
+  if ((int64_t)blockIdx.x >= nx.block0 && (int64_t)blockIdx.x < nx.block0 + nx.n_blocks) {  // the next batch
+    sampler_openke_block(nx.sa, (int64_t)blockIdx.x - nx.block0, nx.n_blocks);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -1396,12 +1434,16 @@ __global__ __launch_bounds__(256, NC > 4 ? 5 : 7) void k_ns_row_owner(const floa
                    const float nv = (is_ent ? nrm_e : nrm_r)[id];
                    HubOrder ord = hub_order(s_hub, s_hc, bucket, ovf, ovf_n[0], n, row, n_slots);
                    transe_owner_row<NC, L2>(ord, threadIdx.x < 64, row, n, v, nv, n_ent, d, norm_flag, reg, shared,
-                                            rec, K, grad_loss, gent, grel, sgd_lr, pent, prel);
+                                            rec, K, grad_loss, gent, grel, sgd_lr, pent, prel, nx);
                  });
     return;
   }
   const int64_t row = ((int64_t)blockIdx.x - row_block0) * 4 + (threadIdx.x >> 6);
   if (row >= n_ent + n_rel) return;  // wave-uniform
+  if (nx.counts && (threadIdx.x & 63) == 0) {  // the next step's slot counts (the other array)
+    nx.counts[row] = 0;
+    if (row == 0) nx.counts[n_ent + n_rel] = 0;  // its overflow count
+  }
   const bool is_ent = row < n_ent;
   const int64_t id = is_ent ? row : row - n_ent;
   // the count, the bucket's first entries, the row itself and its norm: one round trip, all in
@@ -1426,7 +1468,7 @@ __global__ __launch_bounds__(256, NC > 4 ? 5 : 7) void k_ns_row_owner(const floa
   SlotOrder ord{ovf, n > NS_BUCKET ? ovf_n[0] : 0, n, lane, row, s_hub[threadIdx.x >> 6], pre, 0, 0};
   ord.init();
   transe_owner_row<NC, L2>(ord, true, row, n, v, nv, n_ent, d, norm_flag, reg, shared, rec, K, grad_loss, gent, grel,
-                           sgd_lr, pent, prel);
+                           sgd_lr, pent, prel, nx);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2350,14 +2392,15 @@ static void fused_ws(int model, int norm_flag, int64_t B, int64_t K, int64_t E, 
   w.shared = o;  o = al64(o + (te ? 3 * B * d : 0));
   const int64_t rw = ns_rec_words(8, false, d);
   w.rec = o;     o = al64(o + (te ? K * B * (d > rw ? d : rw) : w.slots * (model == MMRE_DISTMULT ? 1 : 2) * d));
-  w.counts = o;  o = al64(o + E + R + 1);   // + the overflow count
+  w.counts = o;  o = al64(o + 2 * (E + R + 1));   // + the overflow count; two arrays (the pipelined
+                                                  // step's parities: mmre_ns_step_openke_pipe)
   w.bucket = o;  o = al64(o + 2 * (E + R) * NS_BUCKET);   // int64 entries
   w.ovf = o;     o = al64(o + 4 * w.slots);                // int64 (row, entry) pairs
   w.total = o;
 }
 
-static NSSlots ws_slots(float* d_work, const FusedWs& w, int64_t E, int64_t R) {
-  int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts);
+static NSSlots ws_slots(float* d_work, const FusedWs& w, int64_t E, int64_t R, int parity = 0) {
+  int32_t* counts = reinterpret_cast<int32_t*>(d_work + w.counts) + (parity ? E + R + 1 : 0);
   return NSSlots{d_work + w.shared, d_work + w.rec, counts, reinterpret_cast<int64_t*>(d_work + w.bucket),
                  reinterpret_cast<int64_t*>(d_work + w.ovf), counts + E + R, w.sentinel};
 }
@@ -2461,7 +2504,8 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
                            const int64_t* d_r, int64_t batch, int64_t neg, float loss_margin, float adv_temperature,
                            float regul_rate, const float* d_score, const float* d_grad_loss, float* d_grad_ent,
                            float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im, float* d_work, float lr,
-                           float* pe, float* pei, float* pr, float* pri, void* stream, float* d_loss_out = nullptr) {
+                           float* pe, float* pei, float* pr, float* pri, void* stream, float* d_loss_out = nullptr,
+                           int parity = 0, const NSNext* nxp = nullptr) {
   NSArgs A;
   int rc = ns_args(A, model, norm_flag, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim,
                    phase_denom, d_h, d_t, d_r, batch, neg, loss_margin, adv_temperature, regul_rate);
@@ -2473,7 +2517,7 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
   hipStream_t st = (hipStream_t)stream;
   FusedWs w;
   fused_ws(model, norm_flag, batch, neg, n_ent, n_rel, dim, w);
-  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
+  NSSlots S = ws_slots(d_work, w, n_ent, n_rel, parity);
   const double N = (double)batch * (1.0 + (double)neg);
   const dim3 ogrid((unsigned)((n_ent + n_rel + 3) / 4)), blk(256);
   if (!fused_fast(A)) {
@@ -2513,14 +2557,20 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
   // the training step (d_loss_out): one more workgroup reduces the forward's loss partials
   // the hub workgroups first (their count scan starts with the kernel), then (the training
   // step) the loss reduction's workgroup, then one workgroup per 4 table rows
+  // (the pipelined step: then the next batch's sampler workgroups, NSNext)
+  NSNext nx{};
+  if (nxp) nx = *nxp;
+  constexpr bool kSamplerFirst = true;  // the next batch's workgroups before the row workgroups (dispatched early)
   const int64_t reduce_block = d_loss_out ? (int64_t)NS_HUB_WG : -1;
-  const int64_t row_block0 = (int64_t)NS_HUB_WG + (d_loss_out ? 1 : 0);
-  const dim3 ogrid2((unsigned)(row_block0 + ogrid.x));
+  const int64_t head = (int64_t)NS_HUB_WG + (d_loss_out ? 1 : 0);
+  nx.block0 = kSamplerFirst ? head : head + ogrid.x;
+  const int64_t row_block0 = kSamplerFirst ? head + nx.n_blocks : head;
+  const dim3 ogrid2((unsigned)(head + nx.n_blocks + ogrid.x));
 #define MMRE_NS_OWNER(NC_, L2_)                                                                                     \
   hipLaunchKernelGGL((k_ns_row_owner<NC_, L2_>), ogrid2, blk, 0, st, d_ent, d_rel, n_ent, n_rel, dim, norm_flag, reg, \
                      d_work + w.nrm_e, d_work + w.nrm_r, S.shared, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n,         \
                      neg, d_grad_loss, d_grad_ent, d_grad_rel, lr, pe, pr, A, d_work + w.part, d_loss_out,           \
-                     reduce_block, row_block0, NS_HUB_WG, w.slots)
+                     reduce_block, row_block0, NS_HUB_WG, w.slots, nx)
   const int nc = transe_fast_nc(A);
   const bool l2 = model == MMRE_TRANSE_L2;
   if (nc == 1) { if (l2) MMRE_NS_OWNER(1, true); else MMRE_NS_OWNER(1, false); }
@@ -2585,17 +2635,22 @@ extern "C" int mmre_ns_forward_backward(int model, int norm_flag, float model_ma
 // values as mmre_sampler_openke_step + mmre_ns_fused_forward + mmre_ns_fused_grad_sgd (upstream
 // gradient 1), bit for bit: the same device functions in the same order, only regrouped into
 // fewer launches (tests/test_ns_full_gpu.py holds them equal over several steps).
-extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
-                                   const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
-                                   const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
-                                   const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
-                                   const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode,
-                                   const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
-                                   int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, int model, int norm_flag,
-                                   float* d_ent, float* d_rel, int64_t n_ent, int64_t n_rel, int dim, int64_t batch,
-                                   int64_t neg, float loss_margin, float adv_temperature, float regul_rate,
-                                   float* d_score, float* d_loss, float* d_grad_ent, float* d_grad_rel,
-                                   float* d_work, float lr, void* stream) {
+// The pipelined variant (mmre_ns_step_openke_pipe, `prepared` / `parity` / the next batch):
+// launch 1 unless `prepared` is 3 (bit 0: the batch is drawn, bit 1: the pre-pass is current);
+// the row owner also samples the next batch into the d_next_* buffers and does its pre-pass
+// (NSNext), so the next call with prepared = 3 and the other parity is two launches.
+static int step_openke_impl(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                            const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                            const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                            const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                            const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode,
+                            const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
+                            int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, int model, int norm_flag,
+                            float* d_ent, float* d_rel, int64_t n_ent, int64_t n_rel, int dim, int64_t batch,
+                            int64_t neg, float loss_margin, float adv_temperature, float regul_rate, float* d_score,
+                            float* d_loss, float* d_grad_ent, float* d_grad_rel, float* d_work, float lr,
+                            void* stream, int64_t prepared, int64_t parity, int64_t* d_next_h, int64_t* d_next_t,
+                            int64_t* d_next_r, float* d_next_y) {
   if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
       !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y || !d_ticket)
     return MMRE_ERR_ARG;
@@ -2605,6 +2660,9 @@ extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_to
   if (n_blocks < 0 || (n_blocks > 0 && !d_blocks)) return MMRE_ERR_ARG;
   if (!d_score || !d_loss || !d_grad_ent || !d_grad_rel || !d_work || n_rel <= 0 || !(lr != 0.0f))
     return MMRE_ERR_ARG;
+  const bool pipe = d_next_h != nullptr;
+  if (pipe && (!d_next_t || !d_next_r || !d_next_y || d_next_h == d_batch_h)) return MMRE_ERR_ARG;
+  if (parity < 0 || parity > 1 || prepared < 0 || prepared > 3) return MMRE_ERR_ARG;
   NSArgs A;
   int rc = ns_args(A, model, norm_flag, 0.0f, 0, d_ent, nullptr, d_rel, nullptr, dim, 0.0f, d_batch_h, d_batch_t,
                    d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate);
@@ -2613,21 +2671,23 @@ extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_to
   hipStream_t st = (hipStream_t)stream;
   FusedWs w;
   fused_ws(model, norm_flag, batch, neg, n_ent, n_rel, dim, w);
-  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
+  NSSlots S = ws_slots(d_work, w, n_ent, n_rel, (int)parity);
   float* nrm_e = d_work + w.nrm_e;
   float* nrm_r = d_work + w.nrm_r;
   float* ent_n = norm_flag ? d_work + w.ent_n : nullptr;
   float* rel_n = norm_flag ? d_work + w.rel_n : nullptr;
-  // 1. sampler workgroups + pre-pass workgroups
   const int64_t rows = batch * (1 + neg);
   const int64_t n_sampler = (rows + 255) / 256;
   const OpenKESamplerArgs sa{d_train_list, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head, d_lef_tail,
                              d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, train_total, n_ent, n_rel,
                              d_seeds, work_threads, batch, neg, 0, mode, d_blocks, n_blocks, d_batch_h, d_batch_t,
                              d_batch_r, d_batch_y, d_ticket, mmre_sampler_draws_per_positive(neg, 0, mode), nullptr};
-  hipLaunchKernelGGL(k_ns_step_prep, dim3((unsigned)(n_sampler + (n_ent + n_rel + 3) / 4)), dim3(256), 0, st, sa,
-                     n_sampler, d_ent, n_ent, d_rel, n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, S.counts, S.ovf_n);
-  MMRE_CHECK_LAUNCH();
+  if (prepared != 3) {  // 1. sampler workgroups (unless the batch is drawn) + pre-pass workgroups
+    const int64_t ns1 = (prepared & 1) ? 0 : n_sampler;
+    hipLaunchKernelGGL(k_ns_step_prep, dim3((unsigned)(ns1 + (n_ent + n_rel + 3) / 4)), dim3(256), 0, st, sa, ns1,
+                       d_ent, n_ent, d_rel, n_rel, dim, nrm_e, nrm_r, ent_n, rel_n, S.counts, S.ovf_n);
+    MMRE_CHECK_LAUNCH();
+  }
   // 2. the fused loss kernel (scores, loss partials, slots)
   const float* ent_u = norm_flag ? ent_n : d_ent;
   const float* rel_u = norm_flag ? rel_n : d_rel;
@@ -2650,9 +2710,47 @@ extern "C" int mmre_ns_step_openke(const int64_t* d_train_list, int64_t train_to
   else { if (l2) MMRE_NS_FUSED(8, true); else MMRE_NS_FUSED(8, false); }
 #undef MMRE_NS_FUSED
   MMRE_CHECK_LAUNCH();
-  // 3. gradient + SGD, and the loss
+  // 3. gradient + SGD, and the loss (+ the pipelined step's next batch and pre-pass)
+  NSNext nx{};
+  if (pipe) {
+    nx.sa = sa;
+    nx.sa.bh = d_next_h;
+    nx.sa.bt = d_next_t;
+    nx.sa.br = d_next_r;
+    nx.sa.by = d_next_y;
+    nx.n_blocks = n_sampler;
+    nx.counts = ws_slots(d_work, w, n_ent, n_rel, (int)(1 - parity)).counts;
+    nx.nrm_e = nrm_e;
+    nx.nrm_r = nrm_r;
+    nx.ent_n = ent_n;
+    nx.rel_n = rel_n;
+  }
   return fused_grad_impl(model, norm_flag, 0.0f, 0, d_ent, nullptr, d_rel, nullptr, n_ent, n_rel, dim, 0.0f,
                          d_batch_h, d_batch_t, d_batch_r, batch, neg, loss_margin, adv_temperature, regul_rate, d_score,
                          nullptr, d_grad_ent, nullptr, d_grad_rel, nullptr, d_work, lr, d_ent, nullptr, d_rel, nullptr,
-                         stream, d_loss);
+                         stream, d_loss, (int)parity, pipe ? &nx : nullptr);
+}
+
+#define MMRE_STEP_OPENKE_PARAMS                                                                                      \
+  const int64_t *d_train_list, int64_t train_total, const int64_t *d_head_hrt, const int64_t *d_tail_hrt,             \
+      const int64_t *d_rel_hrt, const int64_t *d_lef_head, const int64_t *d_rig_head, const int64_t *d_lef_tail,      \
+      const int64_t *d_rig_tail, const int64_t *d_lef_rel, const int64_t *d_rig_rel, const float *d_left_mean,       \
+      const float *d_right_mean, uint64_t *d_seeds, int64_t work_threads, int64_t mode, const int32_t *d_blocks,     \
+      int64_t n_blocks, int64_t *d_batch_h, int64_t *d_batch_t, int64_t *d_batch_r, float *d_batch_y,               \
+      int32_t *d_ticket, int model, int norm_flag, float *d_ent, float *d_rel, int64_t n_ent, int64_t n_rel, int dim, \
+      int64_t batch, int64_t neg, float loss_margin, float adv_temperature, float regul_rate, float *d_score,         \
+      float *d_loss, float *d_grad_ent, float *d_grad_rel, float *d_work, float lr, void *stream
+#define MMRE_STEP_OPENKE_ARGS                                                                                        \
+  d_train_list, train_total, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head, d_lef_tail, d_rig_tail,     \
+      d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, d_seeds, work_threads, mode, d_blocks, n_blocks, d_batch_h,  \
+      d_batch_t, d_batch_r, d_batch_y, d_ticket, model, norm_flag, d_ent, d_rel, n_ent, n_rel, dim, batch, neg,      \
+      loss_margin, adv_temperature, regul_rate, d_score, d_loss, d_grad_ent, d_grad_rel, d_work, lr, stream
+
+extern "C" int mmre_ns_step_openke(MMRE_STEP_OPENKE_PARAMS) {
+  return step_openke_impl(MMRE_STEP_OPENKE_ARGS, 0, 0, nullptr, nullptr, nullptr, nullptr);
+}
+
+extern "C" int mmre_ns_step_openke_pipe(MMRE_STEP_OPENKE_PARAMS, int64_t prepared, int64_t parity, int64_t* d_next_h,
+                                        int64_t* d_next_t, int64_t* d_next_r, float* d_next_y) {
+  return step_openke_impl(MMRE_STEP_OPENKE_ARGS, prepared, parity, d_next_h, d_next_t, d_next_r, d_next_y);
 }

@@ -204,13 +204,25 @@ def score_rows(spec: NSSpec, ent, rel, h, t, r, ent_im=None, rel_im=None):
 class OpenKETrainStep:
     """One OpenKE training step for TransE -- Trainer.train_one_step (Trainer.py:43-54) over the
     loader's Base.cpp sampling, strategy/NegativeSampling + MarginLoss, optim.SGD -- as ONE C-ABI
-    call (mmre_ns_step_openke, three launches): the values of sampler.sample(B, neg, 0, mode) +
-    fused_ns_loss(...).backward() + SGD.step(), bit for bit (tests/test_ns_full_gpu.py). The
-    parameters are updated in place; ent.grad / rel.grad hold the step's gradient tables, `batch`
-    the sampled batch, `score` the row scores. Calling it returns the loss tensor (device)."""
+    call: the values of sampler.sample(B, neg, 0, mode) + fused_ns_loss(...).backward() +
+    SGD.step(), bit for bit (tests/test_ns_full_gpu.py). The parameters are updated in place;
+    ent.grad / rel.grad hold the step's gradient tables, `batch` the batch the step trained on,
+    `score` the row scores. Calling it returns the loss tensor (device).
+
+    pipeline=True (default; mmre_ns_step_openke_pipe): like a prefetching data loader, each step
+    also draws the NEXT batch (in its gradient launch, beside the row owner) and writes the
+    norms of the rows it updates, so the next step is two launches (the fused loss kernel, the
+    row owner) instead of three. Batches, losses, gradients and parameters are the unpipelined
+    sequence's; the sampler is one batch ahead between calls (as with any prefetching loader,
+    another consumer drawing from the same sampler between steps sees batch i + 2, and the
+    prefetched batch is then discarded). The prefetch is used only while it is current: ent /
+    rel modified in place since the previous call (torch's version counters) re-run the
+    pre-pass; the sampler drawn from or reseeded elsewhere re-draws the batch.
+    pipeline=False: mmre_ns_step_openke (three launches every step)."""
 
     def __init__(self, sampler, spec: NSSpec, ent, rel, batch: int, neg: int, loss_margin: float, lr: float,
-                 adv_temperature: float | None = None, regul_rate: float = 0.0, mode: int = 0):
+                 adv_temperature: float | None = None, regul_rate: float = 0.0, mode: int = 0,
+                 pipeline: bool = True):
         if spec.model not in ("transe", "transe_l2") or spec.use_model_margin:
             raise ValueError("OpenKETrainStep: TransE without a model margin (the fused path)")
         require_cuda(ent, rel)
@@ -219,24 +231,54 @@ class OpenKETrainStep:
         self.B, self.K, self.mode = int(batch), int(neg), int(mode)
         self.margin, self.lr = float(loss_margin), float(lr)
         self.adv, self.regul = float(adv_temperature or 0.0), float(regul_rate)
+        self.pipeline = bool(pipeline)
         E, R = int(ent.shape[0]), int(rel.shape[0])
         n = self.B * (1 + self.K)
         self.work = torch.empty(int(lib().mmre_ns_fused_workspace(spec.model_id, int(spec.norm_flag), self.B, self.K, E,
                                                                   R, spec.dim)), dtype=torch.float32, device=dev)
         self.score = torch.empty(n, dtype=torch.float32, device=dev)
         self.loss = torch.empty(1, dtype=torch.float32, device=dev)
-        self.batch = dict(batch_h=torch.empty(n, dtype=torch.int64, device=dev),
+        mk = lambda: dict(batch_h=torch.empty(n, dtype=torch.int64, device=dev),
                           batch_t=torch.empty(n, dtype=torch.int64, device=dev),
                           batch_r=torch.empty(n, dtype=torch.int64, device=dev),
                           batch_y=torch.empty(n, dtype=torch.float32, device=dev))
+        self._bufs = [mk(), mk()] if self.pipeline else [mk()]
+        self.batch = self._bufs[0]
+        self._parity = 0
+        self._ready = None  # (sampler draws, (ent, rel) versions) right after a call that prefetched
         self.ge, self.gr = torch.empty_like(ent), torch.empty_like(rel)  # the step's gradient tables
+
+    def invalidate(self):
+        """Forget the prefetch -- after replaying captured graphs of this step, whose launches this
+        object's host state does not follow: the next call draws a batch and runs the pre-pass."""
+        self._ready = None
+
+    def _state(self):
+        return (self.sampler.draws, (self.ent._version, self.rel._version))
 
     def __call__(self):
         s = self.spec
         E, R = int(self.ent.shape[0]), int(self.rel.shape[0])
-        call("mmre_ns_step_openke", *self.sampler.step_args(self.B, self.K, self.mode, self.batch), s.model_id,
-             int(s.norm_flag), ptr(self.ent), ptr(self.rel), E, R, s.dim, self.B, self.K, self.margin, self.adv,
-             self.regul, ptr(self.score), ptr(self.loss), ptr(self.ge), ptr(self.gr), ptr(self.work),
-             self.lr, stream_ptr(self.ent.device))
+        tail = (s.model_id, int(s.norm_flag), ptr(self.ent), ptr(self.rel), E, R, s.dim, self.B, self.K, self.margin,
+                self.adv, self.regul, ptr(self.score), ptr(self.loss), ptr(self.ge), ptr(self.gr), ptr(self.work),
+                self.lr, stream_ptr(self.ent.device))
+        if not self.pipeline:
+            call("mmre_ns_step_openke", *self.sampler.step_args(self.B, self.K, self.mode, self.batch), *tail)
+        else:
+            p = self._parity
+            cur, nxt = self._bufs[p], self._bufs[1 - p]
+            st = self._state()
+            # bit 0: the current batch was drawn by the previous call's gradient launch (else this
+            # call's first launch draws it); bit 1: the pre-pass that launch made is current
+            prepared = 0
+            if self._ready is not None:
+                prepared = (1 if self._ready[0] == st[0] else 0) | (2 if self._ready[1] == st[1] else 0)
+            args = self.sampler.step_args(self.B, self.K, self.mode, cur, advance=not prepared & 1)
+            call("mmre_ns_step_openke_pipe", *args, *tail, prepared, p, ptr(nxt["batch_h"]), ptr(nxt["batch_t"]),
+                 ptr(nxt["batch_r"]), ptr(nxt["batch_y"]))
+            self.sampler.advance(self.B, self.K, self.mode)
+            self.batch = cur
+            self._parity = 1 - p
+            self._ready = self._state()
         self.ent.grad, self.rel.grad = self.ge, self.gr  # as backward() leaves them
         return self.loss[0]

@@ -70,6 +70,10 @@ class OpenKESampler:
     def seeds(self, value):
         self._seeds = np.asarray(value, np.uint64).copy()
         self._seeds_dev.copy_(torch.from_numpy(self._seeds.view(np.int64)))
+        self.draws = getattr(self, "draws", 0) + 1
+
+    # draws: bumped by every batch drawn and every seed reset -- a prefetching consumer
+    # (mmre.ns.OpenKETrainStep) checks that nobody else drew from this sampler since its prefetch
 
     def sample(self, batch_size: int, neg_ent: int = 1, neg_rel: int = 0, mode: int = 0, out=None, p: bool = False):
         """Base.cpp:161-197 sampling(batch, neg_ent, neg_rel, mode, filter_flag, p); p=True draws the
@@ -102,12 +106,20 @@ class OpenKESampler:
         # ... and the host mirror
         call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, B,
              int(neg_ent), int(neg_rel), int(mode))
+        self.draws += 1
         return out
 
 
-    def step_args(self, batch_size: int, neg_ent: int, mode: int, out):
+    def advance(self, batch_size: int, neg_ent: int, mode: int):
+        """Advance the host mirror by one batch a kernel drew (the device seeds advance there)."""
+        call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, int(batch_size),
+             int(neg_ent), 0, int(mode))
+        self.draws += 1
+
+    def step_args(self, batch_size: int, neg_ent: int, mode: int, out, advance: bool = True):
         """The sampler half of mmre_ns_step_openke's arguments (the step's launch samples the batch
-        into `out` and advances the device seeds); the host mirror advances here, as sample() does."""
+        into `out` and advances the device seeds); the host mirror advances here, as sample() does
+        (advance=False: the arguments only -- the batch was drawn by an earlier launch)."""
         d = self._d
         args = (ptr(d["train_list"]), self.train_total, ptr(d["head_hrt"]), ptr(d["tail_hrt"]), ptr(d["rel_hrt"]),
                 ptr(d["lef_head"]), ptr(d["rig_head"]), ptr(d["lef_tail"]), ptr(d["rig_tail"]), ptr(d["lef_rel"]),
@@ -115,8 +127,8 @@ class OpenKESampler:
                 ptr(d["right_mean"]) if self.bern else None, ptr(self._seeds_dev), self.work_threads, int(mode),
                 ptr(self._blocks), self._n_blocks, ptr(out["batch_h"]), ptr(out["batch_t"]), ptr(out["batch_r"]),
                 ptr(out["batch_y"]), ptr(self._ticket))
-        call("mmre_sampler_advance", self._seeds.ctypes.data_as(ctypes.c_void_p), self.work_threads, int(batch_size),
-             int(neg_ent), 0, int(mode))
+        if advance:
+            self.advance(batch_size, neg_ent, mode)
         return args
 
 

@@ -163,7 +163,9 @@ def emulate(a):
         # count table (every rank reduces the gathered 4 x 2n table; here a full-size stand-in),
         # so evaluation i runs while the host reduces i - 1. With two streams (streams=2) the
         # evaluations alternate between two buffer sets / graphs / streams.
-        hosts = [torch.empty_like(host) for _ in range(2)]
+        # pinned, like the bench's (ShardedLinkEvaluation._stage): empty_like(host) is pageable memory,
+        # whose D2H copy blocks the host and serialised the loop (0.357 vs 0.257 ms for the 8-way rank 3)
+        hosts = [torch.empty(host.shape, dtype=host.dtype, pin_memory=True) for _ in range(2)]
         full = np.zeros((4, 2 * n), np.int32)
         slots = [(sw, bufs, g if a.graph else None, gc if a.graph else None)]
         if a.graph and a.streams == 2:

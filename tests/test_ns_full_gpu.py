@@ -315,12 +315,15 @@ def test_hub_rows_ordered_deterministically(c2_training, model, n_pos):
         assert np.linalg.norm(gg - gw) <= 1e-4 * np.linalg.norm(gw), (n, np.linalg.norm(gg - gw), np.linalg.norm(gw))
 
 
-@pytest.mark.parametrize("regul,adv", [(0.0, None), (0.5, None), (0.0, 1.0)])
-def test_train_step_equals_the_autograd_path(c2_training, regul, adv):
+@pytest.mark.parametrize("regul,adv,pipeline", [(0.0, None, False), (0.5, None, False), (0.0, 1.0, False),
+                                                 (0.0, None, True), (0.5, None, True), (0.0, 1.0, True)])
+def test_train_step_equals_the_autograd_path(c2_training, regul, adv, pipeline):
     """mmre_ns_step_openke (mmre.ns.OpenKETrainStep: sampler + pre-pass in one launch, the fused
-    loss kernel, the row owner with SGD and the loss reduction) against the drop-in path
-    (OpenKESampler.sample + fused_ns_loss + backward + mmre.optim.SGD.step) over four steps at the
-    C2 training shape: batches, losses, scores, gradients, parameters and LCG states bit-identical."""
+    loss kernel, the row owner with SGD and the loss reduction) and its pipelined form
+    (mmre_ns_step_openke_pipe: the row owner also draws the next batch and writes the norms of
+    the rows it updates; two launches a step) against the drop-in path (OpenKESampler.sample +
+    fused_ns_loss + backward + mmre.optim.SGD.step) over four steps at the C2 training shape:
+    batches, losses, scores, gradients, parameters and LCG states bit-identical."""
     from mmre.ns import NSSpec, OpenKETrainStep, fused_ns_loss
     from mmre.optim import SGD
     from mmre.sampler import OpenKESampler
@@ -334,7 +337,8 @@ def test_train_step_equals_the_autograd_path(c2_training, regul, adv):
     sa = OpenKESampler(idx, DEV, bern=True)
     sb = OpenKESampler(idx, DEV, bern=True)
     opt = SGD([ea, ra], lr=lr)
-    step = OpenKETrainStep(sb, spec, eb, rb, B, k, margin, lr, adv_temperature=adv, regul_rate=regul)
+    step = OpenKETrainStep(sb, spec, eb, rb, B, k, margin, lr, adv_temperature=adv, regul_rate=regul,
+                           pipeline=pipeline)
     for i in range(4):
         ba = sa.sample(B, k)
         opt.zero_grad(set_to_none=True)
@@ -350,5 +354,69 @@ def test_train_step_equals_the_autograd_path(c2_training, regul, adv):
         assert torch.equal(sc_a, step.score), i
         assert torch.equal(ea.grad, eb.grad) and torch.equal(ra.grad, rb.grad), i
         assert torch.equal(ea.detach(), eb.detach()) and torch.equal(ra.detach(), rb.detach()), i
+    if pipeline:  # the prefetch drew batch 5 already, into the other buffer
+        b5 = sa.sample(B, k)
+        assert step.batch is step._bufs[1]  # four steps: the last trained on parity 1's buffer
+        torch.cuda.synchronize()
+        for key in ("batch_h", "batch_t", "batch_r", "batch_y"):
+            assert torch.equal(b5[key], step._bufs[0][key]), key
     assert np.array_equal(sa.seeds, sb.seeds)
     assert torch.equal(sa._seeds_dev, sb._seeds_dev)
+
+
+def test_pipelined_train_step_falls_back_when_its_prefetch_is_stale(c2_training):
+    """OpenKETrainStep(pipeline=True) uses the previous call's prefetched batch and pre-pass only
+    while they are current: parameters changed in place between steps re-run the pre-pass (the
+    prefetched batch is kept), a batch drawn from the sampler elsewhere (or a reseed) discards
+    the prefetch and draws again; over a sequence with both, every step equals the unpipelined
+    step on the same sampler history, and a pipelined two-graph replay equals eager steps."""
+    from mmre.ns import NSSpec, OpenKETrainStep
+    from mmre.sampler import OpenKESampler
+    w, idx = c2_training
+    B, k, margin, lr = 2721, 25, 5.0, 1.0
+    spec = NSSpec("transe", 200, norm_flag=True)
+    tabs = [w[x].to(DEV).clone().requires_grad_(True) for x in ("ent", "rel", "ent", "rel")]
+    ea, ra, eb, rb = tabs
+    sa, sb = OpenKESampler(idx, DEV, bern=True), OpenKESampler(idx, DEV, bern=True)
+    plain = OpenKETrainStep(sa, spec, ea, ra, B, k, margin, lr, pipeline=False)
+    pipe = OpenKETrainStep(sb, spec, eb, rb, B, k, margin, lr, pipeline=True)
+
+    def both(tag):
+        la, lb = plain(), pipe()
+        torch.cuda.synchronize()
+        for key in ("batch_h", "batch_t", "batch_r", "batch_y"):
+            assert torch.equal(plain.batch[key], pipe.batch[key]), (tag, key)
+        assert torch.equal(la.reshape(1), lb.reshape(1)), tag
+        assert torch.equal(ea.grad, eb.grad) and torch.equal(ra.grad, rb.grad), tag
+        assert torch.equal(ea.detach(), eb.detach()) and torch.equal(ra.detach(), rb.detach()), tag
+
+    both("first")
+    both("prefetched")
+    with torch.no_grad():  # in-place parameter edits: the pre-pass runs again, the batch is kept
+        for t in (ea, eb):
+            t[:7].mul_(0.5)
+    both("params edited")
+    both("prefetched again")
+    # another consumer draws from the samplers: the pipelined step's prefetched batch is stale
+    # (it drew batch i + 1 before the other consumer drew) and is discarded -- both steps then
+    # train on the next batch each sampler yields from its current state
+    sb.seeds = sa.seeds  # the pipelined step's sampler reset to the plain one's state
+    both("reseeded")
+    # pipelined replays of two captured graphs (one per parity) equal eager pipelined steps
+    both("before capture")
+    graphs = []
+    for _ in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            pipe()
+        graphs.append(g)
+    # the captures advanced the pipelined object's host state by two steps: replay both graphs
+    # and run the plain step twice
+    for g in graphs:
+        g.replay()
+        plain()
+    torch.cuda.synchronize()
+    assert torch.equal(ea.detach(), eb.detach()) and torch.equal(ra.detach(), rb.detach())
+    assert torch.equal(plain.loss, pipe.loss)
+    sa.sample(B, k)  # the pipelined sampler is one batch ahead (its prefetch)
+    assert torch.equal(sa._seeds_dev, sb._seeds_dev) and np.array_equal(sa.seeds, sb.seeds)
