@@ -458,7 +458,20 @@ struct L1Q {
   int32_t* fin_counts;     // gated f32 launch of the fused evaluation: the finalize (filtered += raw) rides
   int64_t fin_n;           // on it -- every workgroup's slice when the gate is shut, the last workgroup's
   uint32_t* fin_ticket;    // pass after the sweep when it is open (fin_counts nullptr: a separate launch)
+  uint32_t* wq;            // dynamic unit scheduling: one zeroed work counter per XCD group (nullptr: static ranges)
 };
+// The sweeps' dynamic-scheduling work counters (L1Q::wq): one per XCD group, each on a 128-B
+// line of its own -- the second half of an undecided-pair counter slot (L1Q_SLOT_STRIDE bytes
+// apart from byte 256; the slot's counter uses its first 8 bytes) -- zeroed with the header
+// before every evaluation (k_zero_words / k_eval_prep). (Eight counters on one line serialised
+// every claim of the grid on that line: C2 sweep 1.03 -> 2.33 ms.) MMRE_SWEEP_DYN=0: the
+// static contiguous unit ranges (A/B).
+constexpr int L1Q_WQ_STRIDE = L1Q_SLOT_STRIDE * 2;  // uint32 words between two groups' counters
+inline uint32_t* l1q_work_counters(const uint32_t* hdr) {
+  static_assert(L1Q_SLOTS >= 8 && L1Q_SLOT_STRIDE * 8 >= 256, "a 128-B half slot per XCD group");
+  static const char* env = getenv("MMRE_SWEEP_DYN");
+  return (env && env[0] == '0') ? nullptr : const_cast<uint32_t*>(hdr) + (256 + 128) / 4;
+}
 __device__ __forceinline__ float l1q_delta(const uint32_t* absmax, float levels) {
   const float m = __uint_as_float(*absmax);
   return m == 0.0f ? 0.0f : (m < INFINITY ? (2.0f * m) / levels : INFINITY);
@@ -934,13 +947,14 @@ struct ValuSmem {
   uint32_t s_unc[NT / 64];           // undecided pairs per wave (the L1 filter's counter)
   uint32_t s_ts[2][TQ];              // L1 filter, prediction = score: per query row, the integer
   uint32_t s_tw[2][TQ];              // thresholds t_sure and t_out - t_sure (load_meta)
+  int s_unit;                        // dynamic scheduling: the unit after the one being swept
   int2 s_pairs[LIST ? NT / 64 : 1][LIST ? 128 : 1];  // L1 filter: each wave's undecided (query, entity) pairs
 };
 
 // The sweep body. Counts go to the raw columns only (counts[0][q], counts[2][q]); the filtered
 // columns (initialised to minus the listed entities that beat the truth by the truth pass)
 // receive them in k_counts_finalize, one coalesced pass after the sweep (half the atomics).
-template <int OP, bool TC, bool STORE, int PK, int NPL>
+template <int OP, bool TC, bool STORE, int PK, int NPL, bool DYN>
 __device__ __forceinline__ void sweep_valu_body(
     ValuSmem<NPL, TC, (OP == 5 || OP == 6) && !TC>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
     const float* __restrict__ q_km, int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups,
@@ -965,14 +979,24 @@ __device__ __forceinline__ void sweep_valu_body(
   const int tq = tid >> 4, te = tid & 15;
   const PredSel<PK> pred(pred_kind, margin);
   // XCD-aware split (UnitMap): the group's units split evenly over its workgroups, each a
-  // contiguous range
+  // contiguous range -- or, with l1.wq (dynamic scheduling, a persistent grid), member m takes
+  // unit m of its group first and every further unit from the group's work counter. The loader
+  // runs one stage ahead of the compute and enters unit U at the top of compute stage nkc - 2 of
+  // the unit before; one stage later thread 0 claims U's successor and publishes it in LDS (its
+  // wave waits for the reply there; the other waves of the CU run on), and the loader reads it
+  // when it leaves U, >= 1 barrier later. (Holding the reply in a register across the stage
+  // instead made it loop-carried: 160 B of scratch per lane.) Units of uneven cost (the
+  // rescoring of undecided pairs) balance themselves instead of leaving a tail of workgroups.
   const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
   const int per_grp = gridDim.x / n_groups;
   const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et);
-  const int u0 = (int)((int64_t)gmem * um.count / per_grp);
-  const int u1 = (int)((int64_t)(gmem + 1) * um.count / per_grp);
-  if (u0 >= u1) return;  // uniform over the workgroup
   const int nkc = kp / KC;
+  // (compiled per mode: a runtime choice between the two kept values of both live across the
+  // loop -- 168 B of scratch per lane; the host passes l1.wq only with nkc >= 2)
+  constexpr bool dyn = DYN;
+  const int u0 = dyn ? gmem : (int)((int64_t)gmem * um.count / per_grp);
+  const int u1 = dyn ? um.count : (int)((int64_t)(gmem + 1) * um.count / per_grp);
+  if (u0 >= u1) return;  // uniform over the workgroup
 
   // L1 filter constants (uniform): code step, bound slope and offset
   float l1d = 0.0f, l1f = 0.0f, l1c = 0.0f;
@@ -1036,7 +1060,12 @@ __device__ __forceinline__ void sweep_valu_body(
     }
     if (++ld_kc == nkc) {
       ld_kc = 0;
-      if (++ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
+      if (dyn) {
+        ld_unit = sm.s_unit;  // published >= 1 barrier ago (see above)
+        if (ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
+      } else if (++ld_unit < u1) {
+        um.at(ld_unit, ld_qt, ld_et);
+      }
     }
   };
   auto swrite = [&](int buf) {
@@ -1115,10 +1144,16 @@ __device__ __forceinline__ void sweep_valu_body(
   swrite(0);
   __syncthreads();
   if (L1F && __builtin_amdgcn_readfirstlane(fb_flag) != (w8 ? L1Q_CODES8 : L1Q_CODES16)) return;  // uniform
+  if (dyn) {  // u0's successor (after the gate: a shut launch claims none); the loader reads it at
+              // compute stage nkc - 2 of u0, which may be stage 0: a barrier of its own
+    if (tid == 0) sm.s_unit = per_grp + (int)atomicAdd(&l1.wq[grp * L1Q_WQ_STRIDE], 1u);
+    __syncthreads();
+  }
 
   constexpr int KKU = 2;  // LDS rows of operands per inner-loop iteration
   int buf = 0;
-  for (int unit = u0; unit < u1; ++unit) {
+  for (int unit = u0; unit < u1;) {
+    int unit_next = unit + 1;
     for (int kc = 0; kc < nkc; ++kc) {
       const bool more = ld_unit < u1;
       if (more) gload();
@@ -1426,9 +1461,10 @@ __device__ __forceinline__ void sweep_valu_body(
           if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
         }
         }  // !FAST
-        const bool last = unit + 1 >= u1;
+        if (dyn) unit_next = ld_unit;  // the loader entered it at the top of the stage before
+        const bool last = unit_next >= u1;
         int next_qt = cur_qt, next_et = cur_et;
-        if (!last) um.at(unit + 1, next_qt, next_et);
+        if (!last) um.at(unit_next, next_qt, next_et);
         if (last || next_qt != cur_qt) {  // uniform: flush this query tile's counts
           const int tid = vgpr_opaque(threadIdx.x);  // (see load_meta)
           const int tq = tid >> 4, te = tid & 15;
@@ -1456,6 +1492,10 @@ __device__ __forceinline__ void sweep_valu_body(
             load_meta(next_qt, slot);
           }
         }
+        // the successor of the unit the loader entered one stage ago (whose id every thread read
+        // then, before that stage's barrier), for the loader's exit from it >= 1 barrier later;
+        // claimed here, after the accumulators were reset, where it costs no registers
+        if (dyn && !last && threadIdx.x == 0) sm.s_unit = per_grp + (int)atomicAdd(&l1.wq[grp * L1Q_WQ_STRIDE], 1u);
         cur_qt = next_qt;
         cur_et = next_et;
       }
@@ -1463,6 +1503,7 @@ __device__ __forceinline__ void sweep_valu_body(
       __syncthreads();
       buf ^= 1;
     }
+    unit = unit_next;
   }
   if constexpr (L1F) {  // the filter's undecided pairs: one atomic per workgroup, 16 slots
     if constexpr (LIST) {
@@ -1482,7 +1523,7 @@ __device__ __forceinline__ void sweep_valu_body(
   }
 }
 
-template <int OP, bool TC, bool STORE, int PK>
+template <int OP, bool TC, bool STORE, int PK, bool DYN = false>
 __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
     int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups, int pred_kind, float margin,
@@ -1510,7 +1551,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
       return;
     }
   }
-  sweep_valu_body<OP, TC, STORE, PK, NPL>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
+  sweep_valu_body<OP, TC, STORE, PK, NPL, DYN>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
                                           n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head, type_tail,
                                           type_words, counts, scores, l1);
   if (l1.gate != nullptr && l1.fin_counts != nullptr) {
@@ -2544,6 +2585,12 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
     const int div = fbdiv ? atoi(fbdiv) : 4;
     g /= div > 1 ? div : 1;
   }
+  // Dynamic scheduling (l1.wq, the TransE L1 filter sweeps): one persistent workgroup per
+  // resident slot, units from the XCD groups' work counters -- the shut gated launch too (its
+  // workgroups only read the gate).
+  constexpr bool DYN_OK = OP == 5 || OP == 6;
+  const bool dyn = DYN_OK && l1.wq != nullptr && kp / KC >= 2;
+  if (dyn) g = resident_groups((const void*)k_sweep_valu<OP, TCV, STV, PK, DYN_OK>, NT);
   // Small sweeps (a rank's share under relation sharding): no more workgroups than the
   // busiest XCD group has units, so every workgroup gets at most one unit and no empty
   // workgroups are dispatched (C2 at 8-way: 4,380 sweeps 0.52 -> 0.47 ms; 4-way 0.89 -> 0.85).
@@ -2558,8 +2605,13 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   if (gmode && gmode[0] == 't') g = 8 * (int)(q_pad / TQ);
   else if (gmode && gmode[0] >= '1' && gmode[0] <= '9') g = atoi(gmode);
   const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;
-  hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad, n_ent, q_km,
-                     q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1);
+  if (dyn)
+    hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK, DYN_OK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad,
+                       n_ent, q_km, q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts,
+                       scores, l1);
+  else
+    hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad, n_ent, q_km,
+                       q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1);
 }
 
 template <int OP>
@@ -3479,8 +3531,9 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
                        0, 0u);
   }
   MMRE_CHECK_LAUNCH();
-  const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4};
+  L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
+         kt, nullptr, tight ? q_l1c : nullptr, hdr + 4};
+  l1.wq = l1q_work_counters(hdr);
   const bool tc = d_type_head != nullptr;
   // the gated sweeps: the one the code-width word names counts, the others' workgroups leave
   if (bits != 16) {
@@ -3585,8 +3638,11 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
   static const char* order_env = getenv("MMRE_MFMA_EMAJOR");
   const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
-  static const char* blk_env = getenv("MMRE_BF3_BLOCKED"); /* A/B: 0 = the contiguous unit ranges */
-  const bool blocked = !(blk_env && blk_env[0] == '0');
+  // the lock-step windows pay where the planes overflow the caches (C5, 1 GB: 16.45 -> 16.24 ms);
+  // on planes that stay L2 / MALL resident the contiguous ranges are faster (C3, 20 MB: 0.75 vs
+  // 0.85 ms, profiles/r5) -- the emajor threshold; MMRE_BF3_BLOCKED=0 / 1 forces either (A/B)
+  static const char* blk_env = getenv("MMRE_BF3_BLOCKED");
+  const bool blocked = blk_env ? blk_env[0] != '0' : emajor != 0;
 #define MMRE_BF3(PKV)                                                                                           \
   do {                                                                                                          \
     const int res = resident_groups((const void*)k_sweep_bf3<PKV>, NT);                                        \
@@ -3756,8 +3812,9 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   MMRE_CHECK_LAUNCH();
   // the sweeps: the one the code-width word names counts, the others' workgroups leave
   const int64_t tw = (n_ent + 31) / 32;
-  const L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
-               kt, nullptr, tight ? q_l1c : nullptr, hdr + 4, d_undecided_q};
+  L1Q l1{d_q_rows, d_ent_rows, hdr, (unsigned long long*)((char*)d_work + 256), d_q_km, d_ent_km + e_begin, kp,
+         kt, nullptr, tight ? q_l1c : nullptr, hdr + 4, d_undecided_q};
+  l1.wq = l1q_work_counters(hdr);
   // the 8-bit sweep (it leaves unless the word names the 8-bit codes) and the gated 16-bit one
   // (one launch for both widths was tried: with both SAD loops in one kernel the allocator
   // spilled 58-81 VGPRs)
