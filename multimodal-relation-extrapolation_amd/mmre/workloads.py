@@ -189,7 +189,7 @@ REF_PARITY = {
     # the tables the bench line is quoted on
     "c2": (("FB15K-237-ZS", "transe", 200), None, 0),
     "c3": (("DB15K-ZS", "complex", 200), None, 11),
-    "c4": (("FB15K-237-ZS", "rotate", 512), 1000, 12),
+    "c4": (("FB15K-237-ZS", "rotate", 512), None, 12),
     "c5": (("synthetic-1M", "distmult", 256), None, 13),
 }
 

@@ -37,8 +37,9 @@ tests/test_oracle_golden.py). Stored per fixture:
 
 tests/test_ref_parity_gpu.py holds the HIP sweep to these exactly (see there).
 
-Usage:  python tests/golden/make_ref_parity.py [c2 c3 c4 c5]   (C4: ~1.4 s per test triple per
-        process, ~55 min on 8 processes; MMRE_REF_PROCS sets the process count)
+Usage:  python tests/golden/make_ref_parity.py [c2 c3 c4 c5]   (C4: 1.4-3.9 s per test triple per
+        process: 9,918 s for all 17,596 on 7 processes of an 8-CPU container; MMRE_REF_PROCS sets
+        the process count)
         (c2 reads gpurun_out/trained_c2.npz)
 """
 from __future__ import annotations

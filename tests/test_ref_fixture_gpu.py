@@ -14,7 +14,8 @@ agreement is not vacuous:
         the device-side probe picks -- 8-bit codes on these trained tables, asserted -- and
         whose undecided-pair count is asserted too)
     C3  DB15K-ZS ComplEx d=200 (MFMA sweep)    every test triple: 11,306 sweeps x 12,741
-    C4  FB15K-237-ZS RotatE d=512 (VALU sweep) 1,000 seeded triples: 2,000 sweeps x 14,208
+    C4  FB15K-237-ZS RotatE d=512 (VALU sweep) every test triple: 35,192 sweeps x 14,208
+        (round 5; the reference's Tester loop took 9,918 s on 7 processes for it)
     C5  synthetic DistMult d=256 (MFMA sweep)  every test triple:  8,192 sweeps x 1,000,000
 (C3-C5 on STRUCTURED tables, mmre.workloads.structured_tables.)
 
