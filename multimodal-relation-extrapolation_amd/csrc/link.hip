@@ -954,7 +954,7 @@ struct ValuSmem {
 // The sweep body. Counts go to the raw columns only (counts[0][q], counts[2][q]); the filtered
 // columns (initialised to minus the listed entities that beat the truth by the truth pass)
 // receive them in k_counts_finalize, one coalesced pass after the sweep (half the atomics).
-template <int OP, bool TC, bool STORE, int PK, int NPL, bool DYN>
+template <int OP, bool TC, bool STORE, int PK, int NPL, int DYNC>
 __device__ __forceinline__ void sweep_valu_body(
     ValuSmem<NPL, TC, (OP == 5 || OP == 6) && !TC>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
     const float* __restrict__ q_km, int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups,
@@ -991,10 +991,18 @@ __device__ __forceinline__ void sweep_valu_body(
   const int per_grp = gridDim.x / n_groups;
   const UnitMap um(grp, n_groups, (int)(q_pad / TQ), n_et);
   const int nkc = kp / KC;
-  // (compiled per mode: a runtime choice between the two kept values of both live across the
-  // loop -- 168 B of scratch per lane; the host passes l1.wq only with nkc >= 2)
-  constexpr bool dyn = DYN;
-  const int u0 = dyn ? gmem : (int)((int64_t)gmem * um.count / per_grp);
+  // (compiled per mode and chunk: a runtime choice between the modes, or a runtime chunk size,
+  // kept values of both live across the loop -- 160-168 B of scratch per lane; the host passes
+  // l1.wq only with nkc >= 2)
+  constexpr bool dyn = DYNC > 0;
+  // dynamic scheduling claims chunks of consecutive units (the units of a group are query-tile
+  // major: a chunk mostly keeps its query tile, so its counts flush and its query metadata loads
+  // once, not at every unit): 4 when a workgroup sweeps many units, 1 for a rank's small share
+  // (launch_valu_one; C2 N = 1, per evaluation: chunks of 1 / 2 / 4 / 8 / 16 units 1.053 / 1.007 /
+  // 0.975 / 0.997 / 1.017 ms; 8-way shares: 1 or 2 best)
+  constexpr int ch_log2 = DYNC >= 4 ? 2 : DYNC >= 2 ? 1 : 0;
+  constexpr int ch_mask = (1 << ch_log2) - 1;
+  const int u0 = dyn ? gmem << ch_log2 : (int)((int64_t)gmem * um.count / per_grp);
   const int u1 = dyn ? um.count : (int)((int64_t)(gmem + 1) * um.count / per_grp);
   if (u0 >= u1) return;  // uniform over the workgroup
 
@@ -1061,7 +1069,8 @@ __device__ __forceinline__ void sweep_valu_body(
     if (++ld_kc == nkc) {
       ld_kc = 0;
       if (dyn) {
-        ld_unit = sm.s_unit;  // published >= 1 barrier ago (see above)
+        // the next unit of the chunk, or the first of the claimed chunk (published >= 1 barrier ago)
+        ld_unit = ((ld_unit + 1) & ch_mask) != 0 ? ld_unit + 1 : sm.s_unit;
         if (ld_unit < u1) um.at(ld_unit, ld_qt, ld_et);
       } else if (++ld_unit < u1) {
         um.at(ld_unit, ld_qt, ld_et);
@@ -1144,8 +1153,8 @@ __device__ __forceinline__ void sweep_valu_body(
   swrite(0);
   __syncthreads();
   if (L1F && __builtin_amdgcn_readfirstlane(fb_flag) != (w8 ? L1Q_CODES8 : L1Q_CODES16)) return;  // uniform
-  if (dyn) {  // u0's successor (after the gate: a shut launch claims none); the loader reads it at
-              // compute stage nkc - 2 of u0, which may be stage 0: a barrier of its own
+  if (dyn && ch_mask == 0) {  // u0's successor (after the gate: a shut launch claims none); the
+                              // loader reads it at compute stage nkc - 2 of u0, which may be stage 0
     if (tid == 0) sm.s_unit = per_grp + (int)atomicAdd(&l1.wq[grp * L1Q_WQ_STRIDE], 1u);
     __syncthreads();
   }
@@ -1492,10 +1501,11 @@ __device__ __forceinline__ void sweep_valu_body(
             load_meta(next_qt, slot);
           }
         }
-        // the successor of the unit the loader entered one stage ago (whose id every thread read
-        // then, before that stage's barrier), for the loader's exit from it >= 1 barrier later;
-        // claimed here, after the accumulators were reset, where it costs no registers
-        if (dyn && !last && threadIdx.x == 0) sm.s_unit = per_grp + (int)atomicAdd(&l1.wq[grp * L1Q_WQ_STRIDE], 1u);
+        // the loader entered the last unit of its chunk one stage ago: the next chunk, claimed for
+        // the loader's exit from it >= 1 barrier later (the previous claim was read long before);
+        // here, after the accumulators were reset, where the claim costs no registers
+        if (dyn && !last && ((unit_next + 1) & ch_mask) == 0 && threadIdx.x == 0)
+          sm.s_unit = (per_grp + (int)atomicAdd(&l1.wq[grp * L1Q_WQ_STRIDE], 1u)) << ch_log2;
         cur_qt = next_qt;
         cur_et = next_et;
       }
@@ -1523,7 +1533,7 @@ __device__ __forceinline__ void sweep_valu_body(
   }
 }
 
-template <int OP, bool TC, bool STORE, int PK, bool DYN = false>
+template <int OP, bool TC, bool STORE, int PK, int DYNC = 0>
 __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent, const float* __restrict__ q_km,
     int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups, int pred_kind, float margin,
@@ -1551,7 +1561,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
       return;
     }
   }
-  sweep_valu_body<OP, TC, STORE, PK, NPL, DYN>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
+  sweep_valu_body<OP, TC, STORE, PK, NPL, DYNC>(sm, ent_km, e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base,
                                           n_groups, pred_kind, margin, thr, qtrue, qr, qmode, type_head, type_tail,
                                           type_words, counts, scores, l1);
   if (l1.gate != nullptr && l1.fin_counts != nullptr) {
@@ -2590,7 +2600,13 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   // workgroups only read the gate).
   constexpr bool DYN_OK = OP == 5 || OP == 6;
   const bool dyn = DYN_OK && l1.wq != nullptr && kp / KC >= 2;
-  if (dyn) g = resident_groups((const void*)k_sweep_valu<OP, TCV, STV, PK, DYN_OK>, NT);
+  int chunk = 0;  // dynamic scheduling: units per claim (0: static ranges)
+  if (dyn) {
+    g = resident_groups((const void*)k_sweep_valu<OP, TCV, STV, PK, DYN_OK ? 4 : 0>, NT);
+    const int64_t per_wg = (q_pad / TQ) * n_et / (g > 0 ? g : 1);
+    static const char* ch_env = getenv("MMRE_SWEEP_CHUNK");  /* A/B: 1 or 4 units per claim */
+    chunk = ch_env ? (atoi(ch_env) >= 4 ? 4 : 1) : (per_wg >= 16 ? 4 : 1);
+  }
   // Small sweeps (a rank's share under relation sharding): no more workgroups than the
   // busiest XCD group has units, so every workgroup gets at most one unit and no empty
   // workgroups are dispatched (C2 at 8-way: 4,380 sweeps 0.52 -> 0.47 ms; 4-way 0.89 -> 0.85).
@@ -2605,10 +2621,14 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
   if (gmode && gmode[0] == 't') g = 8 * (int)(q_pad / TQ);
   else if (gmode && gmode[0] >= '1' && gmode[0] <= '9') g = atoi(gmode);
   const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;
-  if (dyn)
-    hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK, DYN_OK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad,
-                       n_ent, q_km, q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts,
-                       scores, l1);
+  if (chunk == 4)
+    hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK, DYN_OK ? 4 : 0>), dim3((unsigned)g), dim3(NT), 0, st, ent_km,
+                       e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw,
+                       counts, scores, l1);
+  else if (chunk == 1)
+    hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK, DYN_OK ? 1 : 0>), dim3((unsigned)g), dim3(NT), 0, st, ent_km,
+                       e_pad, n_ent, q_km, q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw,
+                       counts, scores, l1);
   else
     hipLaunchKernelGGL((k_sweep_valu<OP, TCV, STV, PK>), dim3((unsigned)g), dim3(NT), 0, st, ent_km, e_pad, n_ent, q_km,
                        q_pad, n_query, kp, n_et, e_base, ng, pk, m, thr, qtrue, qr, qmode, th, tt, tw, counts, scores, l1);
