@@ -2422,10 +2422,16 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
         const int64_t e0 = ebase + lcol, e1 = ebase + 32 + lcol;
         const bool ev0 = e0 < n_ent, ev1 = e1 < n_ent;
         const float ne0 = ev0 ? en[e0] : 0.0f, ne1 = ev1 ? en[e1] : 0.0f;
+        const uint64_t evm[2] = {__ballot(ev0), __ballot(ev1)};
         // this unit's per-row counts, assembled lane by lane: row L0's count into lane L0 by
         // v_writelane (the popcounts are wave-uniform), one add into cntv at the end -- a
         // `lane == L0 ? c : ...` select per row made the compiler keep 32 lane-compare masks
         // live across the sweep (SGPR spills into VGPR lanes)
+        // Per pair: the bound (one multiply), S' - B and S' + B, and three compares whose results
+        // are the wave's masks (v_cmp into an SGPR pair: "beats at both ends", "beats at neither",
+        // non-finite S'); what is counted and what is listed is 64-bit mask logic on the scalar
+        // unit, per row and column block (round 4's per-lane booleans: ~21 VALU instructions per
+        // pair at C5 -- as many issue cycles as the three MFMAs)
         int ctmp = 0;
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
@@ -2436,43 +2442,42 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
             const float tv[4] = {t4.x, t4.y, t4.z, t4.w}, qb[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
           for (int r = r4; r < r4 + 4; ++r) {
-            bool better[2], und[2];
+            const uint64_t mnan = __ballot(tv[r - r4] != tv[r - r4]);  // a NaN threshold: nothing beats it
+            uint64_t msure[2], mund[2];
 #pragma unroll
             for (int bj = 0; bj < 2; ++bj) {
               const float s = acc[bi][bj][r];
               const float bnd = qb[r - r4] * (bj ? ne1 : ne0);
-              const bool fin = fabsf(s) < INFINITY;  // false for inf and NaN
-              bool sure, out;
+              uint64_t hi, lo;
               if constexpr (PK == 2) {
                 // predict = -s: better iff S > -th. Rounding is monotone, so fl(s - B) > -th
                 // implies s - B > -th (every S of the bracket beats the truth) and
                 // fl(s + B) < -th implies s + B < -th (none does); a NaN S' or bound decides nothing
                 const float nt = -tv[r - r4];
-                sure = fin & (s - bnd > nt);
-                out = (fin & (s + bnd < nt)) | (nt != nt);  // a NaN threshold: nothing beats it
+                hi = __ballot(s - bnd > nt);
+                lo = __ballot(s + bnd < nt);
               } else {
                 const float p1 = pred(s - bnd), p2 = pred(s + bnd);
-                sure = fin & (fmaxf(p1, p2) < tv[r - r4]);
-                out = (fin & (fminf(p1, p2) >= tv[r - r4])) | (tv[r - r4] != tv[r - r4]);
+                hi = __ballot(fmaxf(p1, p2) < tv[r - r4]);
+                lo = __ballot(fminf(p1, p2) >= tv[r - r4]);
               }
-              const bool ev = bj ? ev1 : ev0;
-              better[bj] = sure & ev;
-              und[bj] = !sure & !out & ev;
+              const uint64_t nf = __ballot(!__builtin_isfinite(s));  // inf and NaN: undecided
+              msure[bj] = hi & ~nf & evm[bj];
+              mund[bj] = evm[bj] & ~(msure[bj] | (lo & ~nf) | mnan);
             }
-            const uint64_t m0 = __ballot(better[0]), m1 = __ballot(better[1]);
             const int L0 = bi * 32 + (r & 3) + 8 * (r >> 2);
-            const int c_lo = __popcll(m0 & 0xffffffffull) + __popcll(m1 & 0xffffffffull);
-            const int c_hi = __popcll(m0 >> 32) + __popcll(m1 >> 32);
+            const int c_lo = __popcll(msure[0] & 0xffffffffull) + __popcll(msure[1] & 0xffffffffull);
+            const int c_hi = __popcll(msure[0] >> 32) + __popcll(msure[1] >> 32);
             ctmp = writelane_imm(ctmp, c_lo, L0);
             ctmp = writelane_imm(ctmp, c_hi, L0 + 4);
-            if (__builtin_expect(und[0] | und[1], 0)) {  // rare: list the pair(s) for exact rescoring
+            if (__builtin_expect((mund[0] | mund[1]) != 0ull, 0)) {  // rare (uniform): list the pair(s) for exact rescoring
               // (the row from an opaque lane id: recomputed here, not 32 row indices kept live)
               const int ol = vgpr_opaque(lane);
               const int64_t q = q0 + wq * 64 + bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (ol >> 5);
               if (q < n_query) {
 #pragma unroll
                 for (int bj = 0; bj < 2; ++bj) {
-                  if (!und[bj]) continue;
+                  if (!((mund[bj] >> ol) & 1ull)) continue;
                   // a 64-bit counter (header words 2-3): a non-finite table can make every pair
                   // undecided (1.6e10 at C5), which would wrap a 32-bit one. (A check-then-add
                   // -- an sc1 load of the counter before each add -- made C3 3x slower: the loads
