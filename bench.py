@@ -88,8 +88,10 @@ def valu_ops_per_triple(model, dim, l1_bits=16):
     return {"transe": 2 * dim, "transe_l2": 3 * dim, "rotate": 9 * dim}.get(model)
 
 
-KERNEL_NAMES = {"transe": "k_sweep_valu<6, false, false, 0>" if os.environ.get("MMRE_L1_FILTER", "1") != "0"
-                else "k_sweep_valu<0, false, false, 0>", "rotate": "k_sweep_valu<2, false, false, 3>",
+# (the VALU sweeps' names without their last template argument: DYNC, the dynamic scheduling's
+#  units per claim -- 4, 1, or 0 for the static ranges -- depends on the sweep's size)
+KERNEL_NAMES = {"transe": "k_sweep_valu<6, false, false, 0," if os.environ.get("MMRE_L1_FILTER", "1") != "0"
+                else "k_sweep_valu<0, false, false, 0,", "rotate": "k_sweep_valu<2, false, false, 3,",
                 "distmult": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2",
                 "complex": "k_sweep_bf3<2>" if MFMA_FILTER else "k_sweep_mfma<false, false, 2"}
 
@@ -460,12 +462,14 @@ def bench_ns(args, world, rank, dev, dist):
                  batch_y=torch.empty(n_rows, dtype=torch.float32, device=dev)) for _ in range(2)]
 
     tstep = None
-    if model == "transe" and not args.ns_autograd:
-        # the whole step as ONE C-ABI call (mmre_ns_step_openke: sampler + pre-pass in one launch,
-        # the fused loss kernel, the row owner with SGD and the loss reduction), bit-identical to the
-        # drop-in path below (tests/test_ns_full_gpu.py::test_train_step_equals_the_autograd_path)
+    if not args.ns_autograd:
+        # the whole step as ONE C-ABI call, pipelined (TransE: mmre_ns_step_openke_pipe -- the fused
+        # loss kernel, the row owner with SGD, the loss reduction, the next batch and the updated
+        # rows' pre-pass; DistMult / ComplEx / RotatE: mmre_ns_step_openke_gen_pipe -- forward, slot
+        # records, row owner with SGD, the loss reduction and the next batch), bit-identical to the
+        # drop-in path below (tests/test_ns_full_gpu.py::test_*train_step_equals_the_autograd_path)
         from mmre.ns import OpenKETrainStep
-        tstep = OpenKETrainStep(smp, spec, ent, rel, B, k, margin, 1.0)
+        tstep = OpenKETrainStep(smp, spec, ent, rel, B, k, margin, 1.0, ent_im=ent_im, rel_im=rel_im)
 
     def step(i, ev=None):
         if tstep is not None:
@@ -634,10 +638,13 @@ def bench_ns(args, world, rank, dev, dist):
             slot_bytes = 2 * (B * (3 + 3 * k)) * 2 * 4 * (256 if d > 128 else 128)
         kern_ms = pipe_ms if pipe_ms is not None else fused_ms
         ach = (fwd_bytes + grad_bytes) / (kern_ms * 1e-3) / 1e9
-        step_kernels = (["k_ns_transe_fused<4, false, false>", "k_ns_row_owner<4, false>"] if pipe_ms is not None else
-                        ["k_ns_prepass(", "k_ns_transe_fused<4, false, false>", "k_ns_reduce(", "k_ns_row_owner<4, false>"]
-                        if model == "transe" else
-                        ["k_ns_gen_forward<4, ", "k_ns_reduce(", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"])
+        if model == "transe":
+            step_kernels = (["k_ns_transe_fused<4, false, false>", "k_ns_row_owner<4, false>"] if pipe_ms is not None
+                            else ["k_ns_prepass(", "k_ns_transe_fused<4, false, false>", "k_ns_reduce(",
+                                  "k_ns_row_owner<4, false>"])
+        else:
+            step_kernels = (["k_ns_gen_forward<4, ", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"] if pipe_ms is not None
+                            else ["k_ns_gen_forward<4, ", "k_ns_reduce(", "k_ns_gen_slots<4, ", "k_ns_gen_owner<4>"])
         pmc_cfg = "ns" if model == "transe" else f"ns_{model}"  # profiles/pmc_<pmc_cfg>.json
         traffic, tsrc, tper = (pmc_step_traffic(pmc_cfg, step_kernels) if (world == 1 and d == 200 and k == 25)
                                else (None, None, None))
@@ -651,8 +658,10 @@ def bench_ns(args, world, rank, dev, dist):
                           f"{model} d=200 training step at the C2 training shape (margin loss)", "model": model,
                           "batch": B, "neg_ent": k, "rows_per_step": n_rows,
                           "dim": d, "margin": margin, "parallelism": f"data-parallel replicas x{world}",
-                          "step": ("mmre_ns_step_openke_pipe (fused loss kernel; row owner + SGD + loss reduction "
-                                   "+ the next batch's sampler + the updated rows' pre-pass: 2 launches)"
+                          "step": (("mmre_ns_step_openke_pipe (fused loss kernel; row owner + SGD + loss reduction "
+                                    "+ the next batch's sampler + the updated rows' pre-pass: 2 launches)" if model == "transe"
+                                    else "mmre_ns_step_openke_gen_pipe (forward; slot records; row owner + SGD + loss "
+                                    "reduction + the next batch's sampler: 3 launches)")
                                    if tstep is not None and tstep.pipeline else
                                    "mmre_ns_step_openke (sampler + pre-pass, fused loss, row owner + SGD + loss "
                                    "reduction: 3 launches)" if tstep is not None else
@@ -665,10 +674,13 @@ def bench_ns(args, world, rank, dev, dist):
                                             "2 x FETCH_SIZE + WRITE_SIZE)",
                             "traffic_source": tsrc, "traffic_per_kernel": tper,
                             "traffic_x_algorithmic": (traffic / (fwd_bytes + grad_bytes)) if traffic else None,
-                            "kernel": ("mmre_ns_step_openke_pipe = k_ns_transe_fused<4, false, false> + "
-                                       "k_ns_row_owner<4, false> (+ the loss reduction, the next batch's sampler "
-                                       "workgroups and the updated rows' pre-pass in its grid): events around "
-                                       "hipGraph replays of the step (one graph per parity)" if pipe_ms is not None else
+                            "kernel": (("mmre_ns_step_openke_pipe = k_ns_transe_fused<4, false, false> + "
+                                        "k_ns_row_owner<4, false> (+ the loss reduction, the next batch's sampler "
+                                        "workgroups and the updated rows' pre-pass in its grid)" if model == "transe" else
+                                        "mmre_ns_step_openke_gen_pipe = k_ns_gen_forward + k_ns_gen_slots + "
+                                        "k_ns_gen_owner (+ the loss reduction and the next batch's sampler workgroups "
+                                        "in its grid)") + ": events around hipGraph replays of the step (one graph per "
+                                       "parity)" if pipe_ms is not None else
                                        ("mmre_ns_forward_backward = k_ns_prepass + k_ns_transe_fused<4, false, false> + "
                                         "k_ns_reduce (the loss) + k_ns_row_owner<4, false>" if model == "transe" else
                                         "mmre_ns_forward_backward = k_ns_forward + k_ns_reduce + k_ns_gen_slots + "
@@ -1300,9 +1312,9 @@ def main():
         # the TransE sweep kernel that counted: the probe's code width (8 / 16) or the f32 fallback
         l1_bits = fst.get("bits") if fst is not None and fst["kind"] == "l1q" else None
         if model == "transe" and l1_bits == 16:
-            KERNEL_NAMES["transe"] = "k_sweep_valu<5, false, false, 0>"
+            KERNEL_NAMES["transe"] = "k_sweep_valu<5, false, false, 0,"
         elif model == "transe" and fst is not None and fst["kind"] == "l1q" and l1_bits is None:
-            KERNEL_NAMES["transe"] = "k_sweep_valu<0, false, false, 0>"
+            KERNEL_NAMES["transe"] = "k_sweep_valu<0, false, false, 0,"
         traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
         if model in ("distmult", "complex") and fst is not None and fst["kind"] == "bf3" and not fst["fallback"]:
             # the split-bf16 filter: three bf16 products of K = dim x planes per triple on the bf16

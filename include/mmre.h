@@ -455,6 +455,29 @@ int mmre_ns_step_openke_pipe(const int64_t* d_train_list, int64_t train_total, c
                              void* stream, int64_t prepared, int64_t parity, int64_t* d_next_h, int64_t* d_next_t,
                              int64_t* d_next_r, float* d_next_y);
 
+/* The one-call training step for DistMult / ComplEx / RotatE (OpenKE Trainer.train_one_step over
+ * the loader's sampling, NegativeSampling + MarginLoss, plain SGD; the models' own scoring as in
+ * mmre_ns_fused_forward: d_ent_im / d_rel_im for ComplEx, model_margin / phase_denom for RotatE):
+ * [sampler, unless prepared bit 0 says d_batch_* was drawn by the previous call] -> the forward
+ * (scores + loss partials) -> the slot records -> the row owner (gradient + SGD), whose grid also
+ * reduces the loss into d_loss and, with d_next_h, draws the next batch into d_next_*. Values
+ * bit-identical to mmre_sampler_openke_step + mmre_ns_fused_forward + mmre_ns_fused_grad_sgd;
+ * three launches a step instead of five. d_work: mmre_ns_fused_workspace. dim <= 512. */
+int mmre_ns_step_openke_gen_pipe(const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt,
+                                 const int64_t* d_tail_hrt, const int64_t* d_rel_hrt, const int64_t* d_lef_head,
+                                 const int64_t* d_rig_head, const int64_t* d_lef_tail, const int64_t* d_rig_tail,
+                                 const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+                                 const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode,
+                                 const int32_t* d_blocks, int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t,
+                                 int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket, int model,
+                                 float model_margin, int use_model_margin, float* d_ent, float* d_ent_im,
+                                 float* d_rel, float* d_rel_im, int64_t n_ent, int64_t n_rel, int dim,
+                                 float phase_denom, int64_t batch, int64_t neg, float loss_margin,
+                                 float adv_temperature, float regul_rate, float* d_score, float* d_loss,
+                                 float* d_grad_ent, float* d_grad_ent_im, float* d_grad_rel, float* d_grad_rel_im,
+                                 float* d_work, float lr, void* stream, int64_t prepared, int64_t* d_next_h,
+                                 int64_t* d_next_t, int64_t* d_next_r, float* d_next_y);
+
 /* model(data) in 'normal' mode for n_rows arbitrary rows is mmre_ns_forward with
  * batch = n_rows, neg = 0, d_loss = NULL. Its backward (OpenKE Model.forward under any loss,
  * Model.py / SoftplusLoss.py:7-31 / SigmoidLoss.py:7-30; the repo's scoring_fn / _calc,

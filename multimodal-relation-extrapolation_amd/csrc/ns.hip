@@ -1989,11 +1989,23 @@ __global__ __launch_bounds__(256) void k_ns_gen_owner(NSArgs A, int64_t n_ent, i
                                                       int dpad, const float* __restrict__ grad_loss, float* gent,
                                                       float* gent_im, float* grel, float* grel_im, float sgd_lr,
                                                       float* pent, float* pent_im, float* prel, float* prel_im,
-                                                      int64_t row_block0, int n_hub_wg, int64_t n_slots) {
+                                                      int64_t row_block0, int n_hub_wg, int64_t n_slots,
+                                                      const float* __restrict__ part, float* __restrict__ loss,
+                                                      int64_t reduce_block, NSNext nx) {
   __shared__ int64_t s_hub[4][NS_HUB];
   __shared__ uint16_t s_bits[256];
   __shared__ int32_t s_hc[2];
   (void)dpad;
+  // the one-call training step (mmre_ns_step_openke_gen_pipe): the loss reduction and the next
+  // batch's sampler workgroups ride in this grid (the forward zeroes the slot counts itself)
+  if ((int64_t)blockIdx.x == reduce_block) {
+    ns_reduce_block(A, part, loss);
+    return;
+  }
+  if ((int64_t)blockIdx.x >= nx.block0 && (int64_t)blockIdx.x < nx.block0 + nx.n_blocks) {
+    sampler_openke_block(nx.sa, (int64_t)blockIdx.x - nx.block0, nx.n_blocks);
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int d = A.dim;
   // output rows of the two halves of table row `row`
@@ -2295,7 +2307,7 @@ static int rows_backward_impl(const NSArgs& A, const float* d_coef, int64_t n_ro
     hipLaunchKernelGGL((k_ns_gen_owner<NC_>), hgrid, blk, 0, st, A, n_ent, n_rel, reg_ent, reg_rel, S.rec, S.counts, \
                        S.bucket, S.ovf, S.ovf_n, 0, d_grad_loss, d_grad_ent, d_grad_ent_im, d_grad_rel,             \
                        d_grad_rel_im, 0.0f, nullptr, nullptr, nullptr, nullptr, (int64_t)NS_HUB_WG, NS_HUB_WG,        \
-                       3 * n_rows);                                                                                 \
+                       3 * n_rows, nullptr, nullptr, (int64_t)-1, NSNext{});                                        \
   } while (0)
   if (nc == 1) MMRE_ROWS(1);
   else if (nc == 2) MMRE_ROWS(2);
@@ -2529,6 +2541,13 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     const float reg_rel = regul_rate != 0.0f ? (float)(regul_rate * 2.0 / (nterms * N * dim)) : 0.0f;
     // DistMult: a workgroup per positive; the two-half models: a wave per positive
     const dim3 sgrid((unsigned)(model == MMRE_DISTMULT ? batch : (batch + NS_WAVES - 1) / NS_WAVES));
+    // owner grid: the hub workgroups, then (the one-call step) the loss reduction's workgroup and
+    // the next batch's sampler workgroups, then one workgroup per 4 table rows
+    NSNext gnx{};
+    if (nxp) gnx = *nxp;
+    const int64_t gen_reduce = d_loss_out ? (int64_t)NS_HUB_WG : -1;
+    gnx.block0 = (int64_t)NS_HUB_WG + (d_loss_out ? 1 : 0);
+    const int64_t gen_row0 = gnx.block0 + gnx.n_blocks;
 #define MMRE_NS_GEN(NC_)                                                                                            \
   do {                                                                                                              \
     if (model == MMRE_DISTMULT)                                                                                     \
@@ -2540,10 +2559,10 @@ static int fused_grad_impl(int model, int norm_flag, float model_margin, int use
     else                                                                                                            \
       hipLaunchKernelGGL((k_ns_gen_slots<NC_, MMRE_ROTATE>), sgrid, blk, 0, st, A, d_score, S, n_ent, w.dpad,       \
                          (int)(regul_rate != 0.0f));                                                                \
-    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), dim3(ogrid.x + NS_HUB_WG), blk, 0, st, A, n_ent, n_rel, reg_ent,       \
+    hipLaunchKernelGGL((k_ns_gen_owner<NC_>), dim3(gen_row0 + ogrid.x), blk, 0, st, A, n_ent, n_rel, reg_ent,        \
                        reg_rel, S.rec, S.counts, S.bucket, S.ovf, S.ovf_n, w.dpad, d_grad_loss, d_grad_ent,          \
-                       d_grad_ent_im, d_grad_rel, d_grad_rel_im, lr, pe, pei, pr, pri, (int64_t)NS_HUB_WG, NS_HUB_WG,  \
-                       w.slots);                                                                                    \
+                       d_grad_ent_im, d_grad_rel, d_grad_rel_im, lr, pe, pei, pr, pri, gen_row0, NS_HUB_WG, w.slots,  \
+                       d_work + w.part, d_loss_out, gen_reduce, gnx);                                               \
   } while (0)
     if (nc == 1) MMRE_NS_GEN(1);
     else if (nc == 2) MMRE_NS_GEN(2);
@@ -2731,6 +2750,68 @@ static int step_openke_impl(const int64_t* d_train_list, int64_t train_total, co
                          stream, d_loss, (int)parity, pipe ? &nx : nullptr);
 }
 
+// The one-call training step for DistMult / ComplEx / RotatE (the generic fused path), pipelined
+// like the TransE one: [the sampler, when the batch was not drawn by the previous call] -> the
+// forward (scores, loss partials; it zeroes the slot counts) -> the slot records -> the row owner
+// (gradient + SGD, with the loss reduction and the NEXT batch's sampler workgroups in its grid).
+// Same kernels and values as OpenKESampler.sample + fused_ns_loss(...).backward() with the SGD
+// fused (mmre.optim.SGD), bit for bit; three launches a step instead of five.
+static int step_openke_gen_impl(const OpenKESamplerArgs& sa, int64_t n_sampler, int model, float model_margin,
+                                int use_model_margin, float* d_ent, float* d_ent_im, float* d_rel, float* d_rel_im,
+                                int64_t n_ent, int64_t n_rel, int dim, float phase_denom, int64_t batch, int64_t neg,
+                                float loss_margin, float adv_temperature, float regul_rate, float* d_score,
+                                float* d_loss, float* d_grad_ent, float* d_grad_ent_im, float* d_grad_rel,
+                                float* d_grad_rel_im, float* d_work, float lr, hipStream_t st, int64_t prepared,
+                                int64_t* d_next_h, int64_t* d_next_t, int64_t* d_next_r, float* d_next_y) {
+  NSArgs A;
+  int rc = ns_args(A, model, 0, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, dim, phase_denom,
+                   sa.bh, sa.bt, sa.br, batch, neg, loss_margin, adv_temperature, regul_rate);
+  if (rc) return rc;
+  const int gnc = gen_nc(dim);
+  if (is_transe(model) || gnc == 0 || neg > NS_MAXK) return MMRE_ERR_SHAPE;
+  FusedWs w;
+  fused_ws(model, 0, batch, neg, n_ent, n_rel, dim, w);
+  NSSlots S = ws_slots(d_work, w, n_ent, n_rel);
+  float* part = d_work + w.part;
+  if (!(prepared & 1)) {  // 1. the batch (the sampler's workgroups alone: no pre-pass for these models)
+    hipLaunchKernelGGL(k_ns_step_prep, dim3((unsigned)n_sampler), dim3(256), 0, st, sa, n_sampler, nullptr, n_ent,
+                       nullptr, n_rel, dim, nullptr, nullptr, nullptr, nullptr, S.counts, S.ovf_n);
+    MMRE_CHECK_LAUNCH();
+  }
+  // 2. the forward: scores + loss partials (zeroes the slot counts)
+  const dim3 fgrid((unsigned)(model == MMRE_DISTMULT ? batch : (batch + NS_WAVES - 1) / NS_WAVES));
+#define MMRE_NS_GF(NC_, M_)                                                                                        \
+  hipLaunchKernelGGL((k_ns_gen_forward<NC_, M_>), fgrid, dim3(256), 0, st, A, d_score, part, S.counts,             \
+                     n_ent + n_rel + 1)
+#define MMRE_NS_GF_M(NC_)                                                                                          \
+  do {                                                                                                             \
+    if (model == MMRE_DISTMULT) MMRE_NS_GF(NC_, MMRE_DISTMULT);                                                    \
+    else if (model == MMRE_COMPLEX) MMRE_NS_GF(NC_, MMRE_COMPLEX);                                                 \
+    else MMRE_NS_GF(NC_, MMRE_ROTATE);                                                                             \
+  } while (0)
+  if (gnc == 1) MMRE_NS_GF_M(1);
+  else if (gnc == 2) MMRE_NS_GF_M(2);
+  else if (gnc == 4) MMRE_NS_GF_M(4);
+  else MMRE_NS_GF_M(8);
+#undef MMRE_NS_GF_M
+#undef MMRE_NS_GF
+  MMRE_CHECK_LAUNCH();
+  // 3.-4. slots, then the row owner with SGD, the loss reduction and the next batch
+  NSNext nx{};
+  if (d_next_h) {
+    nx.sa = sa;
+    nx.sa.bh = d_next_h;
+    nx.sa.bt = d_next_t;
+    nx.sa.br = d_next_r;
+    nx.sa.by = d_next_y;
+    nx.n_blocks = n_sampler;
+  }
+  return fused_grad_impl(model, 0, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im, n_ent, n_rel, dim,
+                         phase_denom, sa.bh, sa.bt, sa.br, batch, neg, loss_margin, adv_temperature, regul_rate,
+                         d_score, nullptr, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, lr, d_ent,
+                         d_ent_im, d_rel, d_rel_im, st, d_loss, 0, d_next_h ? &nx : nullptr);
+}
+
 #define MMRE_STEP_OPENKE_PARAMS                                                                                      \
   const int64_t *d_train_list, int64_t train_total, const int64_t *d_head_hrt, const int64_t *d_tail_hrt,             \
       const int64_t *d_rel_hrt, const int64_t *d_lef_head, const int64_t *d_rig_head, const int64_t *d_lef_tail,      \
@@ -2753,4 +2834,41 @@ extern "C" int mmre_ns_step_openke(MMRE_STEP_OPENKE_PARAMS) {
 extern "C" int mmre_ns_step_openke_pipe(MMRE_STEP_OPENKE_PARAMS, int64_t prepared, int64_t parity, int64_t* d_next_h,
                                         int64_t* d_next_t, int64_t* d_next_r, float* d_next_y) {
   return step_openke_impl(MMRE_STEP_OPENKE_ARGS, prepared, parity, d_next_h, d_next_t, d_next_r, d_next_y);
+}
+
+
+// The one-call step for DistMult / ComplEx / RotatE (step_openke_gen_impl): the sampler arguments of
+// mmre_ns_step_openke, then the generic model's (ComplEx im tables, RotatE's model margin and phase),
+// then prepared (bit 0: d_batch_* already drawn) and the next batch's buffers (nullable).
+extern "C" int mmre_ns_step_openke_gen_pipe(
+    const int64_t* d_train_list, int64_t train_total, const int64_t* d_head_hrt, const int64_t* d_tail_hrt,
+    const int64_t* d_rel_hrt, const int64_t* d_lef_head, const int64_t* d_rig_head, const int64_t* d_lef_tail,
+    const int64_t* d_rig_tail, const int64_t* d_lef_rel, const int64_t* d_rig_rel, const float* d_left_mean,
+    const float* d_right_mean, uint64_t* d_seeds, int64_t work_threads, int64_t mode, const int32_t* d_blocks,
+    int64_t n_blocks, int64_t* d_batch_h, int64_t* d_batch_t, int64_t* d_batch_r, float* d_batch_y, int32_t* d_ticket,
+    int model, float model_margin, int use_model_margin, float* d_ent, float* d_ent_im, float* d_rel, float* d_rel_im,
+    int64_t n_ent, int64_t n_rel, int dim, float phase_denom, int64_t batch, int64_t neg, float loss_margin,
+    float adv_temperature, float regul_rate, float* d_score, float* d_loss, float* d_grad_ent, float* d_grad_ent_im,
+    float* d_grad_rel, float* d_grad_rel_im, float* d_work, float lr, void* stream, int64_t prepared,
+    int64_t* d_next_h, int64_t* d_next_t, int64_t* d_next_r, float* d_next_y) {
+  if (!d_train_list || !d_head_hrt || !d_tail_hrt || !d_lef_head || !d_rig_head || !d_lef_tail || !d_rig_tail ||
+      !d_seeds || !d_batch_h || !d_batch_t || !d_batch_r || !d_batch_y || !d_ticket)
+    return MMRE_ERR_ARG;
+  if ((d_left_mean == nullptr) != (d_right_mean == nullptr)) return MMRE_ERR_ARG;
+  if (train_total <= 0 || n_ent <= 1 || work_threads <= 0 || batch <= 0 || neg <= 0 || mode < -1 || mode > 1)
+    return MMRE_ERR_ARG;
+  if (n_blocks < 0 || (n_blocks > 0 && !d_blocks)) return MMRE_ERR_ARG;
+  if (!d_score || !d_loss || !d_grad_ent || !d_grad_rel || !d_work || n_rel <= 0 || !(lr != 0.0f)) return MMRE_ERR_ARG;
+  if (model == MMRE_COMPLEX && (!d_ent_im || !d_rel_im || !d_grad_ent_im || !d_grad_rel_im)) return MMRE_ERR_ARG;
+  if (prepared < 0 || prepared > 3) return MMRE_ERR_ARG;
+  if (d_next_h && (!d_next_t || !d_next_r || !d_next_y || d_next_h == d_batch_h)) return MMRE_ERR_ARG;
+  const int64_t n_sampler = (batch * (1 + neg) + 255) / 256;
+  const OpenKESamplerArgs sa{d_train_list, d_head_hrt, d_tail_hrt, d_rel_hrt, d_lef_head, d_rig_head, d_lef_tail,
+                             d_rig_tail, d_lef_rel, d_rig_rel, d_left_mean, d_right_mean, train_total, n_ent, n_rel,
+                             d_seeds, work_threads, batch, neg, 0, mode, d_blocks, n_blocks, d_batch_h, d_batch_t,
+                             d_batch_r, d_batch_y, d_ticket, mmre_sampler_draws_per_positive(neg, 0, mode), nullptr};
+  return step_openke_gen_impl(sa, n_sampler, model, model_margin, use_model_margin, d_ent, d_ent_im, d_rel, d_rel_im,
+                              n_ent, n_rel, dim, phase_denom, batch, neg, loss_margin, adv_temperature, regul_rate,
+                              d_score, d_loss, d_grad_ent, d_grad_ent_im, d_grad_rel, d_grad_rel_im, d_work, lr,
+                              (hipStream_t)stream, prepared, d_next_h, d_next_t, d_next_r, d_next_y);
 }

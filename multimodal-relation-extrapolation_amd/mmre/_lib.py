@@ -74,6 +74,9 @@ SIGNATURES = {
                                      F32, P, P, P, P, P, P, P, F32, P]),
     "mmre_ns_step_openke": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, P, P, P, P, P, I32, I32,
                                   P, P, I64, I64, I32, I64, I64, F32, F32, F32, P, P, P, P, P, F32, P]),
+    "mmre_ns_step_openke_gen_pipe": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, P, P, P, P, P,
+                                           I32, F32, I32, P, P, P, P, I64, I64, I32, F32, I64, I64, F32, F32, F32, P,
+                                           P, P, P, P, P, P, F32, P, I64, P, P, P, P]),
     "mmre_ns_step_openke_pipe": (I32, [P, I64, P, P, P, P, P, P, P, P, P, P, P, P, I64, I64, P, I64, P, P, P, P, P, I32,
                                        I32, P, P, I64, I64, I32, I64, I64, F32, F32, F32, P, P, P, P, P, F32, P, I64,
                                        I64, P, P, P, P]),

@@ -218,15 +218,27 @@ class OpenKETrainStep:
     prefetched batch is then discarded). The prefetch is used only while it is current: ent /
     rel modified in place since the previous call (torch's version counters) re-run the
     pre-pass; the sampler drawn from or reseeded elsewhere re-draws the batch.
-    pipeline=False: mmre_ns_step_openke (three launches every step)."""
+    pipeline=False: mmre_ns_step_openke (three launches every step).
+
+    DistMult / ComplEx / RotatE (mmre_ns_step_openke_gen_pipe; ent_im / rel_im for ComplEx, the
+    spec's model margin and phase for RotatE): the generic fused path's kernels -- forward,
+    slot records, row owner with SGD -- with the loss reduction and (pipeline=True) the next
+    batch's sampler in the row owner's grid: three launches a step instead of the drop-in
+    path's five (sampler, forward, loss reduction, slots, row owner), the same values."""
+
+    GENERIC = ("distmult", "complex", "rotate")
 
     def __init__(self, sampler, spec: NSSpec, ent, rel, batch: int, neg: int, loss_margin: float, lr: float,
                  adv_temperature: float | None = None, regul_rate: float = 0.0, mode: int = 0,
-                 pipeline: bool = True):
-        if spec.model not in ("transe", "transe_l2") or spec.use_model_margin:
-            raise ValueError("OpenKETrainStep: TransE without a model margin (the fused path)")
-        require_cuda(ent, rel)
+                 pipeline: bool = True, ent_im=None, rel_im=None):
+        self.generic = spec.model in self.GENERIC
+        if not self.generic and (spec.model not in ("transe", "transe_l2") or spec.use_model_margin):
+            raise ValueError("OpenKETrainStep: TransE without a model margin, DistMult, ComplEx or RotatE")
+        if (spec.model == "complex") != (ent_im is not None and rel_im is not None):
+            raise ValueError("OpenKETrainStep: ComplEx takes ent_im and rel_im (and only ComplEx)")
+        require_cuda(ent, rel, ent_im, rel_im)
         dev = ent.device
+        self.ent_im, self.rel_im = ent_im, rel_im
         self.sampler, self.spec, self.ent, self.rel = sampler, spec, ent, rel
         self.B, self.K, self.mode = int(batch), int(neg), int(mode)
         self.margin, self.lr = float(loss_margin), float(lr)
@@ -247,6 +259,8 @@ class OpenKETrainStep:
         self._parity = 0
         self._ready = None  # (sampler draws, (ent, rel) versions) right after a call that prefetched
         self.ge, self.gr = torch.empty_like(ent), torch.empty_like(rel)  # the step's gradient tables
+        self.gei = torch.empty_like(ent_im) if ent_im is not None else None
+        self.gri = torch.empty_like(rel_im) if rel_im is not None else None
 
     def invalidate(self):
         """Forget the prefetch -- after replaying captured graphs of this step, whose launches this
@@ -254,9 +268,41 @@ class OpenKETrainStep:
         self._ready = None
 
     def _state(self):
-        return (self.sampler.draws, (self.ent._version, self.rel._version))
+        return (self.sampler.draws, tuple(t._version for t in (self.ent, self.rel, self.ent_im, self.rel_im)
+                                          if t is not None))
 
-    def __call__(self):
+    def _generic_call(self, prefetch: bool):
+        s = self.spec
+        E, R = int(self.ent.shape[0]), int(self.rel.shape[0])
+        p = self._parity
+        cur = self._bufs[p]
+        nxt = self._bufs[1 - p] if (self.pipeline and prefetch) else None
+        st = self._state()
+        prepared = 1 if (self.pipeline and self._ready is not None and self._ready[0] == st[0]) else 0
+        args = self.sampler.step_args(self.B, self.K, self.mode, cur, advance=not prepared)
+        call("mmre_ns_step_openke_gen_pipe", *args, s.model_id, s.model_margin, int(s.use_model_margin), ptr(self.ent),
+             ptr(self.ent_im), ptr(self.rel), ptr(self.rel_im), E, R, s.dim, s.phase_denom, self.B, self.K,
+             self.margin, self.adv, self.regul, ptr(self.score), ptr(self.loss), ptr(self.ge), ptr(self.gei),
+             ptr(self.gr), ptr(self.gri), ptr(self.work), self.lr, stream_ptr(self.ent.device), prepared,
+             ptr(nxt["batch_h"]) if nxt else None, ptr(nxt["batch_t"]) if nxt else None,
+             ptr(nxt["batch_r"]) if nxt else None, ptr(nxt["batch_y"]) if nxt else None)
+        self.batch = cur
+        if nxt is not None:
+            self.sampler.advance(self.B, self.K, self.mode)
+            self._parity = 1 - p
+            self._ready = self._state()
+        else:
+            self._ready = None
+        self.ent.grad, self.rel.grad = self.ge, self.gr
+        if self.ent_im is not None:
+            self.ent_im.grad, self.rel_im.grad = self.gei, self.gri
+        return self.loss[0]
+
+    def __call__(self, prefetch: bool = True):
+        """One training step. prefetch=False (pipeline=True): do not draw the next batch -- the
+        last step of a run, leaving the sampler exactly where the unpipelined sequence does."""
+        if self.generic:
+            return self._generic_call(prefetch)
         s = self.spec
         E, R = int(self.ent.shape[0]), int(self.rel.shape[0])
         tail = (s.model_id, int(s.norm_flag), ptr(self.ent), ptr(self.rel), E, R, s.dim, self.B, self.K, self.margin,
@@ -266,7 +312,7 @@ class OpenKETrainStep:
             call("mmre_ns_step_openke", *self.sampler.step_args(self.B, self.K, self.mode, self.batch), *tail)
         else:
             p = self._parity
-            cur, nxt = self._bufs[p], self._bufs[1 - p]
+            cur, nxt = self._bufs[p], (self._bufs[1 - p] if prefetch else None)
             st = self._state()
             # bit 0: the current batch was drawn by the previous call's gradient launch (else this
             # call's first launch draws it); bit 1: the pre-pass that launch made is current
@@ -274,11 +320,15 @@ class OpenKETrainStep:
             if self._ready is not None:
                 prepared = (1 if self._ready[0] == st[0] else 0) | (2 if self._ready[1] == st[1] else 0)
             args = self.sampler.step_args(self.B, self.K, self.mode, cur, advance=not prepared & 1)
-            call("mmre_ns_step_openke_pipe", *args, *tail, prepared, p, ptr(nxt["batch_h"]), ptr(nxt["batch_t"]),
-                 ptr(nxt["batch_r"]), ptr(nxt["batch_y"]))
-            self.sampler.advance(self.B, self.K, self.mode)
+            nx = (ptr(nxt["batch_h"]), ptr(nxt["batch_t"]), ptr(nxt["batch_r"]), ptr(nxt["batch_y"])) if nxt \
+                else (None, None, None, None)
+            call("mmre_ns_step_openke_pipe", *args, *tail, prepared, p, *nx)
             self.batch = cur
-            self._parity = 1 - p
-            self._ready = self._state()
+            if nxt is not None:
+                self.sampler.advance(self.B, self.K, self.mode)
+                self._parity = 1 - p
+                self._ready = self._state()
+            else:
+                self._ready = None
         self.ent.grad, self.rel.grad = self.ge, self.gr  # as backward() leaves them
         return self.loss[0]

@@ -85,9 +85,12 @@ class Trainer(object):
             res = 0.0
             if fast is not None:
                 step, group = fast
-                for _ in range(len(self.data_loader)):
+                nb = len(self.data_loader)
+                for b in range(nb):
                     step.lr = float(group["lr"])
-                    res += float(step().item())
+                    # the step draws the next batch beside its gradient (a prefetching loader),
+                    # except after the run's last batch: the sampler ends where the per-batch path does
+                    res += float(step(prefetch=not (epoch == self.train_times - 1 and b == nb - 1)).item())
             else:
                 for data in self.data_loader:
                     res += self.train_one_step(data)

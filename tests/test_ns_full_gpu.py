@@ -420,3 +420,51 @@ def test_pipelined_train_step_falls_back_when_its_prefetch_is_stale(c2_training)
     assert torch.equal(plain.loss, pipe.loss)
     sa.sample(B, k)  # the pipelined sampler is one batch ahead (its prefetch)
     assert torch.equal(sa._seeds_dev, sb._seeds_dev) and np.array_equal(sa.seeds, sb.seeds)
+
+
+@pytest.mark.parametrize("model,pipeline", [("distmult", True), ("complex", True), ("rotate", True),
+                                            ("distmult", False)])
+def test_generic_train_step_equals_the_autograd_path(c2_training, model, pipeline):
+    """mmre_ns_step_openke_gen_pipe (OpenKETrainStep for DistMult / ComplEx / RotatE: the forward,
+    the slot records, the row owner with SGD + the loss reduction + (pipelined) the next batch's
+    sampler) against the drop-in path (OpenKESampler.sample + fused_ns_loss + backward +
+    mmre.optim.SGD.step, the bench's --ns-autograd) over four steps at the C2 training shape:
+    batches, losses, scores, gradients and parameters bit-identical."""
+    from mmre.link import rotate_phase_denom
+    from mmre.ns import NSSpec, OpenKETrainStep, fused_ns_loss
+    from mmre.optim import SGD
+    from mmre.sampler import OpenKESampler
+    from mmre.workloads import zs_workload
+    w0, idx = c2_training
+    w = zs_workload("FB15K-237-ZS", model, 200)
+    B, k, margin, lr, d = 2721, 25, 5.0, 1.0, 200
+    if model == "rotate":
+        spec = NSSpec("rotate", d, model_margin=6.0, phase_denom=rotate_phase_denom(6.0, 2.0, d))
+    else:
+        spec = NSSpec(model, d)
+    names = [n for n in ("ent", "rel", "ent_im", "rel_im") if n in w]
+    ta = {n: w[n].to(DEV).clone().requires_grad_(True) for n in names}
+    tb = {n: w[n].to(DEV).clone().requires_grad_(True) for n in names}
+    sa, sb = OpenKESampler(idx, DEV, bern=True), OpenKESampler(idx, DEV, bern=True)
+    opt = SGD(list(ta.values()), lr=lr)
+    step = OpenKETrainStep(sb, spec, tb["ent"], tb["rel"], B, k, margin, lr, pipeline=pipeline,
+                           ent_im=tb.get("ent_im"), rel_im=tb.get("rel_im"))
+    for i in range(4):
+        ba = sa.sample(B, k)
+        opt.zero_grad(set_to_none=True)
+        la, sc_a = fused_ns_loss(spec, ta["ent"], ta["rel"], ba["batch_h"], ba["batch_t"], ba["batch_r"], B, k, margin,
+                                 optimizer=opt, ent_im=ta.get("ent_im"), rel_im=ta.get("rel_im"))
+        la.backward()
+        opt.step()
+        lb = step()
+        torch.cuda.synchronize()
+        for key in ("batch_h", "batch_t", "batch_r", "batch_y"):
+            assert torch.equal(ba[key], step.batch[key]), (i, key)
+        assert torch.equal(la.detach().reshape(1), lb.reshape(1)), (i, float(la), float(lb))
+        assert torch.equal(sc_a, step.score), i
+        for n in names:
+            assert torch.equal(ta[n].grad, tb[n].grad), (i, n)
+            assert torch.equal(ta[n].detach(), tb[n].detach()), (i, n)
+    if pipeline:
+        sa.sample(B, k)  # the prefetch drew batch 5
+    assert torch.equal(sa._seeds_dev, sb._seeds_dev) and np.array_equal(sa.seeds, sb.seeds)
