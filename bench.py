@@ -1315,6 +1315,14 @@ def main():
             KERNEL_NAMES["transe"] = "k_sweep_valu<5, false, false, 0,"
         elif model == "transe" and fst is not None and fst["kind"] == "l1q" and l1_bits is None:
             KERNEL_NAMES["transe"] = "k_sweep_valu<0, false, false, 0,"
+        if model in ("distmult", "complex") and MFMA_FILTER:
+            # the wide split-bf16 sweep (k_sweep_bf3w) runs where the split planes exceed 64 MB (C5),
+            # as mmre_link_sweep_bf3 decides; MMRE_BF3_WIDE forces either
+            k_tot = dim * (2 if model == "complex" else 1)
+            e_pad = -(-e_local // 128) * 128
+            wide_env = os.environ.get("MMRE_BF3_WIDE")
+            wide = wide_env != "0" if wide_env is not None else e_pad * k_tot * 4 > 64 * 2 ** 20
+            KERNEL_NAMES[model] = "k_sweep_bf3w<2," if wide else "k_sweep_bf3<2>"
         traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
         if model in ("distmult", "complex") and fst is not None and fst["kind"] == "bf3" and not fst["fallback"]:
             # the split-bf16 filter: three bf16 products of K = dim x planes per triple on the bf16

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mmre_common.h"
 
@@ -257,6 +258,14 @@ __global__ __launch_bounds__(256) void k_prep_queries(int model, const float* __
 // used, not hoisted out of a loop into a register (or scratch) kept live across the loop.
 __device__ __forceinline__ int vgpr_opaque(int x) {
   __asm__ volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ float vgpr_opaque_f(float x) {
+  __asm__ volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint64_t sgpr_opaque64(uint64_t x) {
+  __asm__ volatile("" : "+s"(x));
   return x;
 }
 __device__ __forceinline__ uint32_t sgpr_opaque(uint32_t x) {
@@ -2285,8 +2294,13 @@ __global__ __launch_bounds__(256) void k_bf3_split(const float* __restrict__ km,
 // floats each; rows >= n_rows get 0 -- padding the sweep never counts): |x|_2 clamped to
 // >= 2^-30, inf / NaN kept (the bound is then inf / NaN: undecided). Any summation order
 // serves -- the bound's 2 % slack covers the norm's rounding.
+// With thr_out (the query rows of the wide sweep, k_sweep_bf3w): also the padded per-row side
+// data its DMA copies whole -- thr_out[i] = the threshold (-inf past the queries: nothing beats
+// a padded row) and qb_out[i] = cb |q|.
 __global__ __launch_bounds__(256) void k_bf3_norms(const float* __restrict__ rows, int64_t n_rows, int64_t r0,
-                                                   int64_t n_out, int ktot, float* __restrict__ norms) {
+                                                   int64_t n_out, int ktot, float* __restrict__ norms,
+                                                   const float* __restrict__ thr_in, float* __restrict__ thr_out,
+                                                   float* __restrict__ qb_out, float cb) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n_out) return;
@@ -2298,7 +2312,54 @@ __global__ __launch_bounds__(256) void k_bf3_norms(const float* __restrict__ row
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-  if (lane == 0) norms[i] = r < n_rows ? fmaxf(sqrtf(ss), 0x1p-30f) : 0.0f;
+  if (lane == 0) {
+    const float nv = r < n_rows ? fmaxf(sqrtf(ss), 0x1p-30f) : 0.0f;
+    norms[i] = nv;
+    if (thr_out) {
+      thr_out[i] = r < n_rows ? thr_in[r] : -INFINITY;
+      qb_out[i] = cb * nv;
+    }
+  }
+}
+
+// The entity norms of the wide sweep: k_bf3_norms' rows (one wave per row, 8 rows per wave) and,
+// per block of 32 consecutive columns, their largest norm (bmax[blockIdx.x]; NaN norms skipped by
+// fmaxf -- such a row's S' is NaN, undecided whatever the bound), the bound factor of
+// k_sweep_bf3w's thresholds.
+__global__ __launch_bounds__(256) void k_bf3_enorms(const float* __restrict__ rows, int64_t n_rows, int64_t r0,
+                                                    int64_t n_out, int ktot, float* __restrict__ norms,
+                                                    float* __restrict__ bmax) {
+  __shared__ float wm[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ss[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) ss[t] = 0.0f;
+  const int64_t rb = r0 + (int64_t)blockIdx.x * 32 + wave * 8;
+  for (int k = lane; k < ktot; k += 64) {
+    float x[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {  // the wave's 8 rows' loads in flight together (past the table: its last row, unused)
+      const int64_t r = rb + t < n_rows ? rb + t : n_rows - 1;
+      x[t] = rows[r * (int64_t)ktot + k];
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t) ss[t] = __builtin_fmaf(x[t], x[t], ss[t]);
+  }
+  float m = 0.0f;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int64_t i = (int64_t)blockIdx.x * 32 + wave * 8 + t;
+    const int64_t r = r0 + i;
+    float v = ss[t];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const float nv = r < n_rows ? fmaxf(sqrtf(v), 0x1p-30f) : 0.0f;
+    if (lane == 0 && i < n_out) norms[i] = nv;
+    if (i < n_out) m = fmaxf(m, nv);
+  }
+  if (lane == 0) wm[wave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) bmax[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
 }
 
 // The sweep: units, grid and staging as k_sweep_mfma's 16-row plain variant (4 workgroups per
@@ -2510,6 +2571,330 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
       if (more) swrite(buf ^ 1);
       __syncthreads();
       buf ^= 1;
+    }
+  }
+}
+
+// The wide variant (round 5). k_sweep_bf3 stages one 16-k split block per barrier through
+// registers at 128 x 128 per workgroup and decides each pair with a per-pair bound and mask
+// logic on the scalar unit (~40 scalar + ~20 vector instructions per 64 pairs): at C5 it held
+// ~0.33 of the bf16 MFMA peak, with the decision pass alone ~18 % of the time and the operand
+// traffic from L2 (134 GB per launch) the rest of the ceiling. Here:
+//  * a workgroup covers QT queries x 256 entities, waves of 64 queries x 128 entities
+//    (QT = 128: 4 waves, two workgroups per CU; QT = 256: 8 waves, one per CU, 1.5x the MFMAs
+//    per operand byte): 24 MFMAs per stage per wave for 12 ds_read_b128;
+//  * stages are copied global -> LDS by the DMA path (global_load_lds_dwordx4: no staging
+//    registers, no ds_write) into three buffers, two stages in flight across each barrier (a
+//    counted s_waitcnt vmcnt, a raw s_barrier); the per-unit side data -- the entity tile's |e|,
+//    the query tile's thresholds and bound factors cb |q| -- rides with the unit's first stage;
+//  * the MFMA's A operand is the entity rows and B the queries, so a lane's accumulator values
+//    all belong to two queries (its columns): per-lane thresholds in registers, per-lane counts
+//    (one compare + one add-with-carry per 64 pairs), and the bound is taken per 32-entity
+//    block -- B = cb |q| max|e| over the block -- folded into two thresholds per query,
+//    T_hi >= -thr + B and T_lo <= -thr - B (one ulp outward of the rounded sums): S' > T_hi
+//    beats the truth for every S within the bound, S' < T_lo for none, anything else (NaN S'
+//    included: both compares fail) is undecided and listed. No S' is +-inf unless |q| max|e|
+//    overflows, and then B and the thresholds are inf: the block's pairs are undecided
+//    (conservative; an inf-norm row costs its block's 32 x n_query pairs on the list).
+//    Per 64 pairs: two compares, one add, two scalar ORs for the per-block "any undecided"
+//    flag; blocks with a flag are re-scanned for the list (rare: truths and near ties).
+// LDS image of a stage: the query rows then the entity rows, 64 B each (hi[16] | lo[16]),
+// 16-B chunk c of row r at slot 4 r + (c ^ ((r >> 2) & 3)) as k_sweep_bf3's (conflict-free
+// operand reads); the DMA writes a wave-instruction's 1 KB lane-linearly, so the swizzle is
+// applied to the source addresses.
+constexpr int W3E = 256, W3NBUF = 3;
+template <int QT>
+struct W3Geom {
+  static constexpr int WAVES = QT / 32;                 // (QT / 64) x 2 waves
+  static constexpr int NT = WAVES * 64;
+  static constexpr int QB = QT * 64, STAGE = QB + W3E * 64;
+  static constexpr int EPW = W3E * 64 / 1024 / WAVES;   // entity DMA instructions per wave and stage
+  static constexpr int NDMA = 2 + EPW;                  // + two for the query rows
+  static constexpr int SIDE = 1024 + 8 * QT;            // block max |e| [8] (1 KB piece) | threshold [QT] | cb |q| [QT]
+  static constexpr int PIECES = SIDE / 1024;            // side DMA instructions (waves 0 .. PIECES - 1)
+  static constexpr int LDS = W3NBUF * (STAGE + SIDE);
+  static constexpr int WG_PER_CU = QT == 128 ? 2 : 1;
+};
+
+__device__ __forceinline__ void w3_glds(const void* src, char* lds_dst) {  // lds_dst wave-uniform
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+// wait until at most n of this wave's vector-memory operations are outstanding (n wave-uniform:
+// the DMA instructions issued for the next stage, 0 / NDMA / NDMA + 1)
+template <int NDMA>
+__device__ __forceinline__ void w3_wait(int n) {
+  if (n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == NDMA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA + 1) : "memory");
+}
+__device__ __forceinline__ float w3_next_up(float x) {  // the next float above x (x not NaN, inf kept)
+  if (x == INFINITY) return x;
+  if (x == 0.0f) return 0x1p-149f;
+  const uint32_t u = __float_as_uint(x);
+  return __uint_as_float(x > 0.0f ? u + 1u : u - 1u);
+}
+
+template <int PK, int QT>
+__global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep_bf3w(
+    const uint4* __restrict__ ent_b, int64_t e_pad, int64_t e_cols, int64_t n_ent, const uint4* __restrict__ q_b,
+    int64_t q_pad, int64_t n_query, int nkb, int n_et, int e_base, int n_groups, const float* __restrict__ thr_pad,
+    const float* __restrict__ qbf, const float* __restrict__ en /* block maxima */, int32_t* __restrict__ counts,
+    uint32_t* __restrict__ hdr, int2* __restrict__ pairs, int64_t cap, int emajor, int blk_qb, int blk_eb) {
+  static_assert(PK == 2, "the wide sweep folds the bound into thresholds on S (prediction = -S)");
+  using G = W3Geom<QT>;
+  __shared__ __attribute__((aligned(16))) char lds[G::LDS];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wq = wave >> 1, we = wave & 1;
+  const int lrow = lane >> 5, lcol = lane & 31;
+  const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
+  const int per_grp = gridDim.x / n_groups;
+  const bool blocked = blk_qb > 0;
+  const int n_qt = (int)(q_pad / QT);
+  const UnitMap um(grp, n_groups, n_qt, n_et, emajor != 0);
+  const BlockMap bm(grp, n_groups, gmem, per_grp, n_qt, n_et, blocked ? blk_qb : 1, blocked ? blk_eb : 1);
+  const int u0 = blocked ? 0 : (int)((int64_t)gmem * um.count / per_grp);
+  const int u1 = blocked ? bm.count : (int)((int64_t)(gmem + 1) * um.count / per_grp);
+  if (u0 >= u1) return;  // uniform over the workgroup
+  auto unit_at = [&](int i, int& qt, int& et) {
+    if (blocked) bm.at(i, qt, et);
+    else um.at(i, qt, et);
+  };
+  auto sidx = [](int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); };
+
+  // the DMA cursor: the stage (unit, k block) whose copies are issued next, and its buffers
+  int ld_unit = u0, ld_kb = 0, ld_qt, ld_et, ld_buf = 0, ld_sbuf = 0;
+  unit_at(u0, ld_qt, ld_et);
+  auto issue = [&]() -> int {  // this wave's share of the cursor's stage; returns its instruction count
+    if (ld_unit >= u1) return 0;
+    char* sb = lds + ld_buf * G::STAGE;
+    const int64_t q0 = (int64_t)ld_qt * QT, c0 = (int64_t)ld_et * W3E;
+    const uint4* qp = q_b + (int64_t)ld_kb * q_pad * 4;
+    const uint4* ep = ent_b + (int64_t)ld_kb * e_pad * 4;
+    const int sl = lane & 3;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // query rows 32 wave .. + 31: two 1-KB instructions of 16 rows
+      const int i = wave * 2 + j, row = 16 * i + (lane >> 2);
+      w3_glds(qp + (q0 + row) * 4 + (sl ^ ((row >> 2) & 3)), sb + i * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < G::EPW; ++j) {  // entity rows (past the slice's columns: its last one)
+      const int i = wave * G::EPW + j, row = 16 * i + (lane >> 2);
+      const int64_t er = c0 + row < e_cols ? c0 + row : e_cols - 1;
+      w3_glds(ep + er * 4 + (sl ^ ((row >> 2) & 3)), sb + G::QB + i * 1024);
+    }
+    int n = G::NDMA;
+    if (ld_kb == 0 && wave < G::PIECES) {  // the unit's side data, one 1-KB piece per wave
+      char* sd = lds + W3NBUF * G::STAGE + ld_sbuf * G::SIDE + wave * 1024;
+      const float* src;
+      if (wave == 0) {  // the tile's 8 block maxima (lanes 0-1; the others re-read them)
+        src = en + (c0 / 32 + 4 * (lane & 1) + 4 <= e_cols / 32 ? c0 / 32 + 4 * (lane & 1) : e_cols / 32 - 4);
+      } else {  // [threshold | cb |q|] of the tile's QT queries
+        const int f = (wave - 1) * 256 + 4 * lane;
+        src = f < QT ? thr_pad + q0 + f : qbf + q0 + (f - QT);
+      }
+      w3_glds(src, sd);
+      n = G::NDMA + 1;
+    }
+    ld_buf = ld_buf == W3NBUF - 1 ? 0 : ld_buf + 1;
+    if (++ld_kb == nkb) {
+      ld_kb = 0;
+      ld_sbuf = ld_sbuf == W3NBUF - 1 ? 0 : ld_sbuf + 1;
+      if (++ld_unit < u1) unit_at(ld_unit, ld_qt, ld_et);
+    }
+    return n;
+  };
+
+  // lane L: the count of query wq * 64 + j * 32 + (L & 31) of the current query tile over the
+  // entity rows it holds (lanes L and L ^ 32 hold the same query)
+  int cnt[2] = {0, 0};
+  auto flush_rows = [&](int qtile) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = cnt[j] + __shfl_xor(cnt[j], 32);
+      const int64_t q = (int64_t)qtile * QT + wq * 64 + j * 32 + lcol;
+      if (lrow == 0 && q < n_query && c) atomicAdd(&counts[q], c);  // raw only (k_counts_finalize)
+      cnt[j] = 0;
+    }
+  };
+
+  floatx16 acc[4][2];  // [entity block][query block]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.0f;
+
+  // the decision pass of a finished unit; FULL: every entity of the wave's 128 is in the slice
+  // (else the first nval are). Entity of (bi, r, lane): ebase + bi * 32 + (r & 3) + 8 (r >> 2) +
+  // 4 lrow -- the lanes 0-31 / 32-63 halves of a register hold two entity rows, so a row's
+  // validity is a wave-uniform half mask.
+  // Thresholds of the lane's two queries against entity block bi (32 rows of the wave's 128):
+  // B = cb |q| max |e| over the block (k_bf3_enorms: a NaN norm is skipped, and that row's S' is
+  // NaN: undecided; blocks past the slice hold no counted row), T_hi >= nt + B,
+  // T_lo <= nt - B one ulp outward of the rounded sums.
+  auto thresholds = [&](float nm, const float nt[2], const float qbv[2], float th[2], float tl[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float b = qbv[j] * nm, a = nt[j] + b, c = nt[j] - b;
+      if (nt[j] != nt[j]) {  // a NaN threshold: nothing beats it (decided)
+        th[j] = INFINITY;
+        tl[j] = INFINITY;
+      } else if (a != a || c != c) {  // a NaN / inf bound (inf - inf): every pair undecided
+        th[j] = INFINITY;
+        tl[j] = -INFINITY;
+      } else {
+        th[j] = w3_next_up(a);
+        tl[j] = -w3_next_up(-c);
+      }
+    }
+  };
+  // the decision pass of a finished unit; FULL: every entity of the wave's 128 is in the slice
+  // (else the first nval are). Entity of (bi, r, lane): ebase + bi * 32 + (r & 3) + 8 (r >> 2) +
+  // 4 lrow -- the lanes 0-31 / 32-63 halves of a register hold two entity rows, so a row's
+  // validity is a wave-uniform half mask. nt: -threshold of the lane's queries; qbv: cb |q|.
+  auto decide = [&](auto full_tag, const float* s_bm, int64_t q0, int64_t ebase, int nval, float nt0, float nt1,
+                    float qb0, float qb1) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    // (opaque copies: the two instances' compares are not merged and hoisted above the branch
+    // between them -- with all 256 masks live)
+    const float nt[2] = {vgpr_opaque_f(nt0), vgpr_opaque_f(nt1)};
+    const float qbv[2] = {vgpr_opaque_f(qb0), vgpr_opaque_f(qb1)};
+    // the wave's four block maxima: one LDS read, held in SGPRs (wave-uniform)
+    const float4 bm4 = *reinterpret_cast<const float4*>(&s_bm[we * 4]);
+    auto rfl = [](float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); };
+    const float nmb[4] = {rfl(bm4.x), rfl(bm4.y), rfl(bm4.z), rfl(bm4.w)};
+    uint64_t und[4][2];
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi) {
+      float thi[2], tlo[2];
+      thresholds(nmb[bi], nt, qbv, thi, tlo);
+#pragma unroll
+      for (int bj = 0; bj < 2; ++bj) {
+        uint64_t u = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float s = acc[bi][bj][r];
+          bool h = s > thi[bj];
+          uint64_t vm = ~0ull;
+          if constexpr (!FULL) {
+            const int row0 = bi * 32 + (r & 3) + 8 * (r >> 2);
+            vm = (row0 < nval ? 0xffffffffull : 0ull) | (row0 + 4 < nval ? 0xffffffff00000000ull : 0ull);
+            h = h && row0 + 4 * lrow < nval;
+          }
+          cnt[bj] += h ? 1 : 0;
+          u |= vm & ~(__ballot(h) | __ballot(s < tlo[bj]));
+          // consumed here, group by group: left alone the compiler hoists all 128 groups'
+          // compares and re-associates the sums, keeping 256 masks live (SGPR spills)
+          cnt[bj] = vgpr_opaque(cnt[bj]);
+          u = sgpr_opaque64(u);
+        }
+        und[bi][bj] = u;
+      }
+    }
+#pragma unroll
+    for (int bi = 0; bi < 4; ++bi) {
+      if (__builtin_expect((und[bi][0] | und[bi][1]) != 0ull, 0)) {  // rare (uniform): list the undecided pairs
+        // the thresholds recomputed from opaque copies: the compares are redone here, not the
+        // pass's masks kept live (the compiler would merge the two)
+        const float ntc[2] = {vgpr_opaque_f(nt[0]), vgpr_opaque_f(nt[1])};
+        float th[2], tl[2];
+        thresholds(nmb[bi], ntc, qbv, th, tl);
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) {
+          if (und[bi][bj] == 0ull) continue;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float s = acc[bi][bj][r];
+            const int row0 = bi * 32 + (r & 3) + 8 * (r >> 2);
+            uint64_t um = ~(__ballot(s > th[bj]) | __ballot(s < tl[bj]));
+            if constexpr (!FULL)
+              um &= (row0 < nval ? 0xffffffffull : 0ull) | (row0 + 4 < nval ? 0xffffffff00000000ull : 0ull);
+            if (um == 0ull) continue;  // uniform
+            // (the lane's query and entity from an opaque lane id: recomputed here, not 64 indices
+            // kept live across the sweep)
+            const int ol = vgpr_opaque(lane);
+            if (!((um >> ol) & 1ull)) continue;
+            const int64_t q = q0 + wq * 64 + bj * 32 + (ol & 31);
+            if (q >= n_query) continue;
+            // a 64-bit counter (header words 2-3), as k_sweep_bf3's
+            const unsigned long long i = atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 2), 1ull);
+            if (i < (unsigned long long)cap) pairs[i] = make_int2((int)q, (int)(ebase + row0 + 4 * (ol >> 5) + e_base));
+            else hdr[1] = 1u;
+          }
+        }
+      }
+    }
+  };
+
+  issue();               // stage 0
+  int nxt = issue();     // stage 1: the instructions still allowed in flight when stage 0 is read
+  int cur_qt, cur_et;
+  unit_at(u0, cur_qt, cur_et);
+  int buf = 0, sbuf = 0;
+  for (int unit = u0; unit < u1; ++unit) {
+    for (int kb = 0; kb < nkb; ++kb) {
+      w3_wait<G::NDMA>(nxt);  // this wave's copies of the stage have landed ...
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // ... and every wave's; every wave is done with the buffer refilled next
+      asm volatile("" ::: "memory");
+      nxt = issue();  // the stage after next, into the buffer read in the previous stage
+      const uint4* sq = reinterpret_cast<const uint4*>(lds + buf * G::STAGE);
+      const uint4* se = reinterpret_cast<const uint4*>(lds + buf * G::STAGE + G::QB);
+      bf16x8 eh[4], el[4], qh[2], ql[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int erow = we * 128 + i * 32 + lcol;
+        eh[i] = __builtin_bit_cast(bf16x8, se[sidx(erow, lrow)]);
+        el[i] = __builtin_bit_cast(bf16x8, se[sidx(erow, 2 + lrow)]);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int qrow = wq * 64 + j * 32 + lcol;
+        qh[j] = __builtin_bit_cast(bf16x8, sq[sidx(qrow, lrow)]);
+        ql[j] = __builtin_bit_cast(bf16x8, sq[sidx(qrow, 2 + lrow)]);
+      }
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) {
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[bi], qh[bj], acc[bi][bj], 0, 0, 0);
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[bi], qh[bj], acc[bi][bj], 0, 0, 0);
+          acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[bi], ql[bj], acc[bi][bj], 0, 0, 0);
+        }
+      buf = buf == W3NBUF - 1 ? 0 : buf + 1;
+      if (kb == nkb - 1) {  // unit finished: decide, count, list the undecided
+        const float* s_bm = reinterpret_cast<const float*>(lds + W3NBUF * G::STAGE + sbuf * G::SIDE);
+        const float* s_th = s_bm + 256;
+        const float* s_qb = s_th + QT;
+        const int64_t q0 = (int64_t)cur_qt * QT;
+        const int64_t ebase = (int64_t)cur_et * W3E + we * 128;
+        float ntv[2], qbv[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int ql_ = wq * 64 + j * 32 + lcol;
+          ntv[j] = -s_th[ql_];  // prediction -S beats the truth iff S > nt
+          qbv[j] = s_qb[ql_];
+        }
+        if (ebase + 128 <= n_ent) decide(std::true_type{}, s_bm, q0, ebase, 128, ntv[0], ntv[1], qbv[0], qbv[1]);
+        else decide(std::false_type{}, s_bm, q0, ebase, (int)(n_ent > ebase ? n_ent - ebase : 0), ntv[0], ntv[1],
+                    qbv[0], qbv[1]);
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi)
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.0f;
+        sbuf = sbuf == W3NBUF - 1 ? 0 : sbuf + 1;
+        const bool last = unit + 1 >= u1;
+        int next_qt = cur_qt, next_et = cur_et;
+        if (!last) unit_at(unit + 1, next_qt, next_et);
+        if (last || next_qt != cur_qt) flush_rows(cur_qt);  // uniform: leave this query tile
+        cur_qt = next_qt;
+        cur_et = next_et;
+      }
     }
   }
 }
@@ -3607,7 +3992,10 @@ static void bf3_window(int P, int n_qt, int m_e, int& qb, int& eb) {
 extern "C" int64_t mmre_link_bf3_workspace(int model, int dim, int64_t e_pad, int64_t q_pad) {
   if (!mfma_model(model) || dim <= 0 || e_pad <= 0 || q_pad <= 0) return 0;
   const int64_t ktot = (int64_t)n_planes(model) * plane_rows(model, dim);
-  return BF3_HDR + 8 * bf3_cap(q_pad, e_pad) + 4 * (q_pad + e_pad) + 4 * ktot * (q_pad + e_pad);
+  // ... | the wide sweep's padded thresholds and bound factors (2 x q_pad floats) | its 32-column
+  // block maxima of |e| (e_pad / 32 floats)
+  return BF3_HDR + 8 * bf3_cap(q_pad, e_pad) + 4 * (q_pad + e_pad) + 4 * ktot * (q_pad + e_pad) + 8 * q_pad +
+         4 * (e_pad / 32);
 }
 
 extern "C" int mmre_link_bf3_stats(const void* d_work, int64_t work_bytes, uint64_t* d_out, void* stream) {
@@ -3616,6 +4004,32 @@ extern "C" int mmre_link_bf3_stats(const void* d_work, int64_t work_bytes, uint6
                      (unsigned long long*)d_out);
   MMRE_CHECK_LAUNCH();
   return MMRE_OK;
+}
+
+// The wide sweep's launch (prediction -S only): a persistent grid of resident workgroups, the
+// lock-step windows where the planes overflow the caches (as k_sweep_bf3's), else contiguous
+// unit ranges.
+template <int QT>
+static void launch_bf3w(hipStream_t st, const uint4* eb, int64_t e_pad, int64_t e_cols, int64_t n_slice,
+                        const uint4* qb, int64_t q_pad, int64_t n_query, int nkb, int e_begin, const float* thr_pad,
+                        const float* qbf, const float* en, int32_t* d_counts, uint32_t* hdr, int2* pairs, int64_t cap,
+                        int emajor, bool blocked, const char* grid_env) {
+  using G = W3Geom<QT>;
+  const int n_etw = (int)((n_slice + W3E - 1) / W3E);
+  const int res = resident_groups((const void*)k_sweep_bf3w<2, QT>, G::NT);
+  const int64_t units = (q_pad / QT) * (int64_t)n_etw;
+  int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;
+  int bq = 0, be = 0;
+  if (blocked && n_etw >= 8 && res % 8 == 0) {
+    g = res;
+    bf3_window(res / 8, (int)(q_pad / QT), n_etw / 8, bq, be);
+  }
+  if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);
+  if (g < 1) g = 1;
+  const int ng = (g % 8 == 0 && n_etw >= 8) ? 8 : 1;
+  hipLaunchKernelGGL((k_sweep_bf3w<2, QT>), dim3((unsigned)g), dim3(G::NT), 0, st, eb, e_pad, e_cols, n_slice, qb,
+                     q_pad, n_query, nkb, n_etw, e_begin, ng, thr_pad, qbf, en, d_counts, hdr, pairs, cap, emajor, bq,
+                     be);
 }
 
 extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const float* d_ent_km,
@@ -3642,6 +4056,9 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   float* en = qn + q_pad;
   uint4* qb = (uint4*)(en + e_pad);
   uint4* eb = qb + (int64_t)ktot * q_pad / 4;
+  float* thr_pad = reinterpret_cast<float*>(eb + (int64_t)ktot * e_pad / 4);
+  float* qbf = thr_pad + q_pad;
+  float* ebm = qbf + q_pad;  // e_pad / 32 block maxima
   const int64_t e_cols = round_up(e_end, TE) - e_begin;  // the slice's whole tiles
   const int64_t n_slice = e_end - e_begin;
   const int n_et = (int)((n_slice + TE - 1) / TE);
@@ -3655,14 +4072,26 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
                      (int64_t)0, q_pad, nkb, qb, q_pad);
   hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((e_cols * nkb + 255) / 256)), dim3(256), 0, st, d_ent_km, e_pad,
                      e_begin, e_cols, nkb, eb, e_pad);
-  hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((q_pad + 3) / 4)), dim3(256), 0, st, d_q_rows, n_query, (int64_t)0,
-                     q_pad, ktot, qn);
-  hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((e_cols + 3) / 4)), dim3(256), 0, st, d_ent_rows, n_ent, e_begin,
-                     e_cols, ktot, en);
-  MMRE_CHECK_LAUNCH();
-  static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
   static const char* order_env = getenv("MMRE_MFMA_EMAJOR");
   const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
+  // the wide sweep (k_sweep_bf3w, prediction -S) where the planes overflow the caches (C5: 15.9
+  // -> 14.5 ms per evaluation); on cache-resident planes the 128 x 128 one is faster (C3: 0.74 vs
+  // 0.86-0.88 ms -- its per-pair bound lists fewer pairs than the wide sweep's per-tile one on
+  // trained tables, whose norms vary); MMRE_BF3_WIDE=1 / 0 forces either (tests, A/B)
+  const char* wide_env = getenv("MMRE_BF3_WIDE");  // read per call: tests switch it
+  const bool wide = pred_kind == 2 && (wide_env ? wide_env[0] != '0' : emajor != 0);
+  const char* qt_env = getenv("MMRE_BF3_QT");  // the wide sweep's query tile, 256 or 128
+  const int wide_qt = qt_env ? atoi(qt_env) : 256;
+  hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((q_pad + 3) / 4)), dim3(256), 0, st, d_q_rows, n_query, (int64_t)0,
+                     q_pad, ktot, qn, d_truth, wide ? thr_pad : nullptr, qbf, cb);
+  if (wide)
+    hipLaunchKernelGGL(k_bf3_enorms, dim3((unsigned)((e_cols + 31) / 32)), dim3(256), 0, st, d_ent_rows, n_ent,
+                       e_begin, e_cols, ktot, en, ebm);
+  else
+    hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((e_cols + 3) / 4)), dim3(256), 0, st, d_ent_rows, n_ent, e_begin,
+                       e_cols, ktot, en, nullptr, nullptr, nullptr, 0.0f);
+  MMRE_CHECK_LAUNCH();
+  static const char* grid_env = getenv("MMRE_SWEEP_GRID"); /* experiments: workgroup count */
   // the lock-step windows pay where the planes overflow the caches (C5, 1 GB: 16.45 -> 16.24 ms);
   // on planes that stay L2 / MALL resident the contiguous ranges are faster (C3, 20 MB: 0.75 vs
   // 0.85 ms, profiles/r5) -- the emajor threshold; MMRE_BF3_BLOCKED=0 / 1 forces either (A/B)
@@ -3670,6 +4099,15 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   const bool blocked = blk_env ? blk_env[0] != '0' : emajor != 0;
 #define MMRE_BF3(PKV)                                                                                           \
   do {                                                                                                          \
+    if (wide && PKV == 2) {                                                                                     \
+      if (q_pad % 256 == 0 && wide_qt == 256)                                                                  \
+        launch_bf3w<256>(st, eb, e_pad, e_cols, n_slice, qb, q_pad, n_query, ktot / 16, (int)e_begin, thr_pad,   \
+                         qbf, ebm, d_counts, hdr, pairs, cap, emajor, blocked, grid_env);                       \
+      else                                                                                                     \
+        launch_bf3w<128>(st, eb, e_pad, e_cols, n_slice, qb, q_pad, n_query, ktot / 16, (int)e_begin, thr_pad,   \
+                         qbf, ebm, d_counts, hdr, pairs, cap, emajor, blocked, grid_env);                       \
+      MMRE_CHECK_LAUNCH();                                                                                     \
+    } else {                                                                                                   \
     const int res = resident_groups((const void*)k_sweep_bf3<PKV>, NT);                                        \
     const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                        \
     int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;              \
@@ -3684,6 +4122,7 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
                        n_query, ktot / 16, n_et, (int)e_begin, ng, pred_kind, margin, d_truth, qn, en, cb,     \
                        d_counts, hdr, pairs, cap, emajor, bq, be);                                             \
     MMRE_CHECK_LAUNCH();                                                                                       \
+    }                                                                                                          \
     hipLaunchKernelGGL((k_bf3_fallback_zero), dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, hdr,  \
                        d_counts, n_query);                                                                     \
     launch_mfma(false, false, pred_kind, margin, d_ent_km + e_begin, n_slice, e_pad, n_et, (int)e_begin,       \

@@ -5,6 +5,7 @@ cd "$(dirname "$0")/.."
 f=gpurun_out/final5
 mkdir -p profiles/r5
 for j in $f/bench_*.json; do [ -s "$j" ] && cp "$j" profiles/r5/; done
+for j in $f/ab_*.json; do [ -s "$j" ] && cp "$j" profiles/r5/ab/; done
 for d in $f/prof_*/; do
   n=$(basename "$d"); n=${n#prof_}
   s=$(ls "$d"/*kernel_stats.csv 2>/dev/null | head -1)

@@ -43,6 +43,8 @@ case $1 in
       timeout -k 10 500 python bench.py --config $c > $o/bench_$c.json 2> $o/bench_$c.err || exit 1
       trace $c --config $c || exit 1
     done
+    # A/B on the same box: C5 on the 128 x 128 split-bf16 sweep
+    MMRE_BF3_WIDE=0 timeout -k 10 500 python bench.py --config c5 --no-cpu-baseline > $o/ab_c5_narrow.json 2> $o/ab_c5_narrow.err || exit 1
     ;;
   B3)
     timeout -k 10 300 python bench.py --config ns > $o/bench_ns.json 2> $o/bench_ns.err || exit 1

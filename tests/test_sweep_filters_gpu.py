@@ -255,17 +255,24 @@ def _adversarial_dot(model, E=2300, R=5, d=48, Q=300, seed=0, nonfinite=True):
     return ent, rel, ent_im, rel_im, qh, qr, qt, qm
 
 
+@pytest.mark.parametrize("wide", [None, "256", "128"])
 @pytest.mark.parametrize("model,seed,nonfinite", [("distmult", 0, True), ("distmult", 1, False),
                                                   ("complex", 0, True), ("complex", 2, False)])
-def test_mfma_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, monkeypatch, model, seed, nonfinite):
+def test_mfma_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, monkeypatch, model, seed, nonfinite, wide):
     """The split-bf16 MFMA filter (mmre_link_sweep_bf3): raw / filtered counts bit-equal to the
     score-storing exact sweep, to the exact count-only f32 MFMA sweep (MMRE_MFMA_FILTER=0) and to
     the oracle's Test.h restatement; the undecided list holds every truth and tie; entity slices
     sum to the whole table; a list too small for the undecided pairs (MMRE_BF3_CAP) takes the
-    device-side fallback to the exact sweep with the same counts."""
+    device-side fallback to the exact sweep with the same counts. wide: the wide sweep
+    (k_sweep_bf3w, the default above 64 MB of planes: C5) forced at query tile 256 (500 queries:
+    a padded last tile) or 128; every table here leaves the last entity tile partial."""
     import torch
     from mmre.link import FilterIndex, LinkSweep
-    ent, rel, ent_im, rel_im, qh, qr, qt, qm = _adversarial_dot(model, seed=seed, nonfinite=nonfinite)
+    monkeypatch.setenv("MMRE_BF3_WIDE", "1" if wide else "0")
+    if wide:
+        monkeypatch.setenv("MMRE_BF3_QT", wide)
+    ent, rel, ent_im, rel_im, qh, qr, qt, qm = _adversarial_dot(model, seed=seed, nonfinite=nonfinite,
+                                                                Q=500 if wide == "256" else 300)
     E, R, d = ent.shape[0], rel.shape[0], rel.shape[1]
     rng = np.random.default_rng(seed + 10)
     fh, fr, ft = rng.integers(0, E, 3 * E), rng.integers(0, R, 3 * E), rng.integers(0, E, 3 * E)
