@@ -2602,7 +2602,10 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
 // 16-B chunk c of row r at slot 4 r + (c ^ ((r >> 2) & 3)) as k_sweep_bf3's (conflict-free
 // operand reads); the DMA writes a wave-instruction's 1 KB lane-linearly, so the swizzle is
 // applied to the source addresses.
-constexpr int W3E = 256, W3NBUF = 3;
+constexpr int W3E = 256;
+#ifndef W3_DEEP
+#define W3_DEEP 0  // 1: four stage buffers at QT = 256 (three stages in flight; A/B)
+#endif
 template <int QT>
 struct W3Geom {
   static constexpr int WAVES = QT / 32;                 // (QT / 64) x 2 waves
@@ -2612,7 +2615,8 @@ struct W3Geom {
   static constexpr int NDMA = 2 + EPW;                  // + two for the query rows
   static constexpr int SIDE = 1024 + 8 * QT;            // block max |e| [8] (1 KB piece) | threshold [QT] | cb |q| [QT]
   static constexpr int PIECES = SIDE / 1024;            // side DMA instructions (waves 0 .. PIECES - 1)
-  static constexpr int LDS = W3NBUF * (STAGE + SIDE);
+  static constexpr int NBUF = (W3_DEEP && QT == 256) ? 4 : 3;  // stage (and side) buffers
+  static constexpr int LDS = NBUF * (STAGE + SIDE);
   static constexpr int WG_PER_CU = QT == 128 ? 2 : 1;
 };
 
@@ -2626,6 +2630,30 @@ __device__ __forceinline__ void w3_wait(int n) {
   if (n == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if (n == NDMA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA) : "memory");
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NDMA + 1) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void w3_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void w3_wait_n(int n) {  // n wave-uniform, 0 .. 15 (a larger n: wait for all)
+  switch (n) {
+    case 1: w3_vmwait<1>(); break;
+    case 2: w3_vmwait<2>(); break;
+    case 3: w3_vmwait<3>(); break;
+    case 4: w3_vmwait<4>(); break;
+    case 5: w3_vmwait<5>(); break;
+    case 6: w3_vmwait<6>(); break;
+    case 7: w3_vmwait<7>(); break;
+    case 8: w3_vmwait<8>(); break;
+    case 9: w3_vmwait<9>(); break;
+    case 10: w3_vmwait<10>(); break;
+    case 11: w3_vmwait<11>(); break;
+    case 12: w3_vmwait<12>(); break;
+    case 13: w3_vmwait<13>(); break;
+    case 14: w3_vmwait<14>(); break;
+    case 15: w3_vmwait<15>(); break;
+    default: w3_vmwait<0>(); break;
+  }
 }
 __device__ __forceinline__ float w3_next_up(float x) {  // the next float above x (x not NaN, inf kept)
   if (x == INFINITY) return x;
@@ -2686,7 +2714,7 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
     }
     int n = G::NDMA;
     if (ld_kb == 0 && wave < G::PIECES) {  // the unit's side data, one 1-KB piece per wave
-      char* sd = lds + W3NBUF * G::STAGE + ld_sbuf * G::SIDE + wave * 1024;
+      char* sd = lds + G::NBUF * G::STAGE + ld_sbuf * G::SIDE + wave * 1024;
       const float* src;
       if (wave == 0) {  // the tile's 8 block maxima (lanes 0-1; the others re-read them)
         src = en + (c0 / 32 + 4 * (lane & 1) + 4 <= e_cols / 32 ? c0 / 32 + 4 * (lane & 1) : e_cols / 32 - 4);
@@ -2697,10 +2725,10 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
       w3_glds(src, sd);
       n = G::NDMA + 1;
     }
-    ld_buf = ld_buf == W3NBUF - 1 ? 0 : ld_buf + 1;
+    ld_buf = ld_buf == G::NBUF - 1 ? 0 : ld_buf + 1;
     if (++ld_kb == nkb) {
       ld_kb = 0;
-      ld_sbuf = ld_sbuf == W3NBUF - 1 ? 0 : ld_sbuf + 1;
+      ld_sbuf = ld_sbuf == G::NBUF - 1 ? 0 : ld_sbuf + 1;
       if (++ld_unit < u1) unit_at(ld_unit, ld_qt, ld_et);
     }
     return n;
@@ -2831,16 +2859,23 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
 
   issue();               // stage 0
   int nxt = issue();     // stage 1: the instructions still allowed in flight when stage 0 is read
+  int nxt2 = G::NBUF == 4 ? issue() : 0;  // (four buffers) stage 2 as well
   int cur_qt, cur_et;
   unit_at(u0, cur_qt, cur_et);
   int buf = 0, sbuf = 0;
   for (int unit = u0; unit < u1; ++unit) {
     for (int kb = 0; kb < nkb; ++kb) {
-      w3_wait<G::NDMA>(nxt);  // this wave's copies of the stage have landed ...
+      if constexpr (G::NBUF == 4) w3_wait_n(nxt + nxt2);
+      else w3_wait<G::NDMA>(nxt);  // this wave's copies of the stage have landed ...
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // ... and every wave's; every wave is done with the buffer refilled next
       asm volatile("" ::: "memory");
-      nxt = issue();  // the stage after next, into the buffer read in the previous stage
+      if constexpr (G::NBUF == 4) {
+        nxt = nxt2;
+        nxt2 = issue();  // three stages ahead
+      } else {
+        nxt = issue();  // the stage after next, into the buffer read in the previous stage
+      }
       const uint4* sq = reinterpret_cast<const uint4*>(lds + buf * G::STAGE);
       const uint4* se = reinterpret_cast<const uint4*>(lds + buf * G::STAGE + G::QB);
       bf16x8 eh[4], el[4], qh[2], ql[2];
@@ -2864,9 +2899,9 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
           acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(el[bi], qh[bj], acc[bi][bj], 0, 0, 0);
           acc[bi][bj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(eh[bi], ql[bj], acc[bi][bj], 0, 0, 0);
         }
-      buf = buf == W3NBUF - 1 ? 0 : buf + 1;
+      buf = buf == G::NBUF - 1 ? 0 : buf + 1;
       if (kb == nkb - 1) {  // unit finished: decide, count, list the undecided
-        const float* s_bm = reinterpret_cast<const float*>(lds + W3NBUF * G::STAGE + sbuf * G::SIDE);
+        const float* s_bm = reinterpret_cast<const float*>(lds + G::NBUF * G::STAGE + sbuf * G::SIDE);
         const float* s_th = s_bm + 256;
         const float* s_qb = s_th + QT;
         const int64_t q0 = (int64_t)cur_qt * QT;
@@ -2887,7 +2922,7 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
           for (int bj = 0; bj < 2; ++bj)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[bi][bj][r] = 0.0f;
-        sbuf = sbuf == W3NBUF - 1 ? 0 : sbuf + 1;
+        sbuf = sbuf == G::NBUF - 1 ? 0 : sbuf + 1;
         const bool last = unit + 1 >= u1;
         int next_qt = cur_qt, next_et = cur_et;
         if (!last) unit_at(unit + 1, next_qt, next_et);
