@@ -211,6 +211,9 @@ int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t n_ent, con
  * with the canonical f32 chain from the row-major copies d_ent_rows (whole table) and d_q_rows.
  * If the list overflows, the device resets the raw counts and runs the exact f32 sweep instead
  * (no host round trip). e_begin / e_end as for mmre_link_sweep_range (0, n_ent: whole table).
+ * Where the split planes exceed 64 MB (and pred_kind = -score) the sweep runs its wide form
+ * (256 x 256 units, per-query thresholds per 32-entity block, a looser bound than the per-pair
+ * one, the same counts); env MMRE_BF3_WIDE=1 / 0 forces either, MMRE_BF3_QT=128 its query tile.
  * d_work: mmre_link_bf3_workspace(model, dim, e_pad, q_pad) bytes of device scratch (0 for a
  * model without the filter). */
 int64_t mmre_link_bf3_workspace(int model, int dim, int64_t e_pad, int64_t q_pad);
