@@ -2606,6 +2606,9 @@ constexpr int W3E = 256;
 #ifndef W3_DEEP
 #define W3_DEEP 0  // 1: four stage buffers at QT = 256 (three stages in flight; A/B)
 #endif
+#ifndef W3_PAIR
+#define W3_PAIR 0  // 1: four stage buffers, one barrier per two stages (A/B)
+#endif
 template <int QT>
 struct W3Geom {
   static constexpr int WAVES = QT / 32;                 // (QT / 64) x 2 waves
@@ -2615,7 +2618,7 @@ struct W3Geom {
   static constexpr int NDMA = 2 + EPW;                  // + two for the query rows
   static constexpr int SIDE = 1024 + 8 * QT;            // block max |e| [8] (1 KB piece) | threshold [QT] | cb |q| [QT]
   static constexpr int PIECES = SIDE / 1024;            // side DMA instructions (waves 0 .. PIECES - 1)
-  static constexpr int NBUF = (W3_DEEP && QT == 256) ? 4 : 3;  // stage (and side) buffers
+  static constexpr int NBUF = ((W3_DEEP && QT == 256) || W3_PAIR) ? 4 : 3;  // stage (and side) buffers
   static constexpr int LDS = NBUF * (STAGE + SIDE);
   static constexpr int WG_PER_CU = QT == 128 ? 2 : 1;
 };
@@ -2859,23 +2862,39 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
 
   issue();               // stage 0
   int nxt = issue();     // stage 1: the instructions still allowed in flight when stage 0 is read
-  int nxt2 = G::NBUF == 4 ? issue() : 0;  // (four buffers) stage 2 as well
+  int nxt2 = (G::NBUF == 4 && !W3_PAIR) ? issue() : 0;  // (four buffers) stage 2 as well
+  int g = 0;  // stages swept by this workgroup
   int cur_qt, cur_et;
   unit_at(u0, cur_qt, cur_et);
   int buf = 0, sbuf = 0;
   for (int unit = u0; unit < u1; ++unit) {
     for (int kb = 0; kb < nkb; ++kb) {
-      if constexpr (G::NBUF == 4) w3_wait_n(nxt + nxt2);
-      else w3_wait<G::NDMA>(nxt);  // this wave's copies of the stage have landed ...
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // ... and every wave's; every wave is done with the buffer refilled next
-      asm volatile("" ::: "memory");
-      if constexpr (G::NBUF == 4) {
-        nxt = nxt2;
-        nxt2 = issue();  // three stages ahead
+      if constexpr (W3_PAIR) {
+        // one barrier per two stages: at an even stage every copy of this pair has landed
+        // (nothing else is in flight), then the next pair's two stages are issued into the
+        // buffers the previous pair was read from
+        if ((g & 1) == 0) {
+          w3_vmwait<0>();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          issue();
+          issue();
+        }
       } else {
-        nxt = issue();  // the stage after next, into the buffer read in the previous stage
+        if constexpr (G::NBUF == 4) w3_wait_n(nxt + nxt2);
+        else w3_wait<G::NDMA>(nxt);  // this wave's copies of the stage have landed ...
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // ... and every wave's; every wave is done with the buffer refilled next
+        asm volatile("" ::: "memory");
+        if constexpr (G::NBUF == 4) {
+          nxt = nxt2;
+          nxt2 = issue();  // three stages ahead
+        } else {
+          nxt = issue();  // the stage after next, into the buffer read in the previous stage
+        }
       }
+      ++g;
       const uint4* sq = reinterpret_cast<const uint4*>(lds + buf * G::STAGE);
       const uint4* se = reinterpret_cast<const uint4*>(lds + buf * G::STAGE + G::QB);
       bf16x8 eh[4], el[4], qh[2], ql[2];
