@@ -166,10 +166,20 @@ def ref_tester_leg(w, n_sample: int, timeout_s: int = 600):
         return None
     n = min(int(n_sample), len(w["test_h"]))
     procs = max(1, torch.get_num_threads())
+    q = tuple(np.asarray(w[k][:n], np.int64) for k in ("test_h", "test_r", "test_t"))
     try:
         import ref_tester
-        out = ref_tester.run_parallel(w, *(np.asarray(w[k][:n], np.int64) for k in ("test_h", "test_r", "test_t")),
-                                      procs, timeout_s=timeout_s, summary=True, near_rel=REF_NEAR_REL)
+        out = ref_tester.run_parallel(w, *q, procs, timeout_s=timeout_s, summary=True, near_rel=REF_NEAR_REL)
+        # repetitions of the same statistic (whole sample / slowest chunk), so that the reported
+        # spread brackets the value: 5 in all when a repetition's loop takes <= 20 s, else 3
+        reps = [float(out["elapsed"])]
+        n_reps = 5 if reps[0] <= 20.0 else 3
+        while len(reps) < n_reps:
+            again = ref_tester.run_parallel(w, *q, procs, timeout_s=timeout_s, summary=True, near_rel=REF_NEAR_REL)
+            if not np.array_equal(again["counts"], out["counts"]):
+                raise RuntimeError("ref_tester repetition gave different counts")
+            reps.append(float(again["elapsed"]))
+        out["elapsed_reps"] = np.asarray(reps)
     except Exception as e:  # noqa: BLE001 -- the baseline is reported, never required
         print(f"cpu_baseline: ref_tester failed: {e!r}", file=sys.stderr)
         return None
@@ -179,7 +189,8 @@ def ref_tester_leg(w, n_sample: int, timeout_s: int = 600):
 
 def cpu_baseline_block(ref, w):
     E, n = int(ref["n_ent"]), int(ref["n"])
-    el = float(ref["elapsed"])
+    reps = np.asarray(ref.get("elapsed_reps", [ref["elapsed"]]), np.float64)
+    el = float(np.median(reps))  # the median repetition's slowest chunk
     P = int(ref["threads"])
     note = ""
     if w["model"] == "rotate":
@@ -190,18 +201,14 @@ def cpu_baseline_block(ref, w):
                      f"entities through the OpenKE Tester loop: reference Base.so getHeadBatch/testHead/testTail "
                      f"(oracle/_ref) + the reference {w['model']} predict op sequence on torch {torch.__version__} "
                      f"CPU (oracle/ref_tester.py), {P} processes x 1 thread side by side (contiguous chunks of "
-                     f"the sample), slowest chunk {el:.2f} s.{note}"}
-    t_idx = np.asarray(ref.get("t_idx", []), np.float64)
-    if len(t_idx) >= 5 * P:
-        # the spread: the sample's per-triple times cut into 5 consecutive blocks;
-        # each block's rate scaled to P processes (each sweep scores E entities, so the blocks
-        # repeat the same work on other triples)
-        rates = np.array([P * 2 * len(b) * E / b.sum() for b in np.array_split(t_idx, 5) if b.sum() > 0])
-        out.update({"reps": int(len(rates)), "value_min": float(rates.min()), "value_median": float(np.median(rates)),
-                    "value_max": float(rates.max()),
-                    "reps_note": f"value = whole sample / slowest chunk; min / median / max over 5 consecutive "
-                                 f"blocks of the per-triple times x {P} processes (the host share is not isolated: "
-                                 f"the spread is the box's noise)"})
+                     f"the sample), slowest chunk {el:.2f} s (median of {len(reps)} repetitions).{note}"}
+    # the spread: the same statistic (whole sample / slowest chunk) per repetition
+    rates = 2 * n * E / reps
+    out.update({"reps": int(len(rates)), "value_min": float(rates.min()), "value_median": float(np.median(rates)),
+                "value_max": float(rates.max()),
+                "reps_note": f"value = whole sample / slowest chunk of the median repetition; min / median / max of "
+                             f"that statistic over {len(rates)} repetitions of the whole leg ({P} processes each; "
+                             f"the host share is not isolated: the spread is the box's noise)"})
     return out
 
 
@@ -1017,11 +1024,12 @@ def bench_m3ae(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
-def rank_breakdown(ev, dist, dev, sweep_ms, n_local, entity_sharded, reps=20):
+def rank_breakdown(ev, dist, dev, sweep_ms, n_local, entity_sharded, reps=20, fixed_ms=None):
     """Where an N > 1 evaluation's time goes, measured on EVERY rank after the timed region and
     all-gathered: the rank's local evaluation (entity / query prep, truth + filter kernels,
     sweep; a graph replay unless --eager), its sweep kernel alone, the fixed per-rank cost
-    (local - sweep), and the collective alone (the all-gather of the count lists with its
+    (fixed_ms: the eager twins' whole-call time minus their sweep, both from the same runs; with
+    --eager, local - sweep), and the collective alone (the all-gather of the count lists with its
     scatter into query order, or the entity-sharded all-reduce), each the median of `reps`
     runs timed with events on the launch stream (barrier before every collective). Returns
     {name: [per-rank values]} and {name_min / name_max}."""
@@ -1048,7 +1056,8 @@ def rank_breakdown(ev, dist, dev, sweep_ms, n_local, entity_sharded, reps=20):
         b.record()
         torch.cuda.synchronize()
         coll.append(a.elapsed_time(b))
-    mine = torch.tensor([local_ms, sweep_ms, max(local_ms - sweep_ms, 0.0), med(coll), float(n_local)],
+    fixed = fixed_ms if fixed_ms is not None else max(local_ms - sweep_ms, 0.0)
+    mine = torch.tensor([local_ms, sweep_ms, fixed, med(coll), float(n_local)],
                         dtype=torch.float64, device=_coll_dev(dist, dev))
     allv = torch.empty(dist.get_world_size() * 5, dtype=torch.float64, device=mine.device)  # flat: gloo's rule
     dist.all_gather_into_tensor(allv, mine)
@@ -1114,15 +1123,43 @@ def _coll_dev(dist, dev):
     return dev if dist.get_backend() == "nccl" else torch.device("cpu")
 
 
+def _kfd_gpu_count() -> int:
+    """GPUs of this node from the KFD topology (/sys/class/kfd/kfd/topology/nodes/*/properties:
+    nodes with SIMDs), without any HIP call -- torch.cuda.device_count() may fall back to
+    hipGetDeviceCount, which initialises HIP in the parent before the ranks are spawned. Honours
+    HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES when set."""
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "properties")) as f:
+                    props = dict(line.split(None, 1) for line in f if line.strip() and len(line.split()) == 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        vis = os.environ.get(var)
+        if vis is not None:
+            n = min(n, len([x for x in vis.split(",") if x.strip()]))
+    return n
+
+
 def _self_launch(n: int) -> int:
     """`python bench.py --gpus N` (N > 1) without WORLD_SIZE: run this same command as N ranks of
     one torch.distributed.run job (one process per GPU, rendezvous on 127.0.0.1, a free port) and
-    return its exit code. Called before any GPU call (counting devices does not initialise the
-    GPU on this image); exits non-zero when the node has fewer than N GPUs, unless the gloo
+    return its exit code. Called before any GPU call (the GPU count comes from the KFD topology,
+    not from HIP; a HIP context already open here is refused); exits non-zero when the node has fewer than N GPUs, unless the gloo
     rehearsal (MMRE_BENCH_GLOO=1: every rank on cuda:0) was asked for."""
     import socket
     import subprocess
-    have = torch.cuda.device_count()
+    have = _kfd_gpu_count()
+    if torch.cuda.is_initialized():  # must not happen: the children would start under a live HIP context
+        print("bench.py: HIP initialised before the self-launch; not measuring", file=sys.stderr)
+        return 2
     if have < n and os.environ.get("MMRE_BENCH_GLOO") != "1":
         print(f"bench.py: --gpus {n} but this node has {have} GPU(s); not measuring", file=sys.stderr)
         return 2
@@ -1280,14 +1317,20 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    fixed_ms = None
     if graphed and n_local:  # the sweep kernel alone: events on the launch stream of eager evaluations
         from mmre.link import LinkSweep
         sw = LinkSweep(spec)
         bufs = sw.alloc_queries(len(ev.q_host[0]))
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
-        for e2 in evs:
+        # each eager twin also bracketed whole: its fixed cost (local - sweep) from the same run
+        outer = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for e2, o2 in zip(evs, outer):
+            o2[0].record()
             sw.run(*ev.q, filt=ev.filt, type_masks=ev.masks_tc, buffers=bufs, sweep_events=e2)
+            o2[1].record()
         torch.cuda.synchronize()
+        fixed_ms = float(np.median([o[0].elapsed_time(o[1]) - e[0].elapsed_time(e[1]) for o, e in zip(outer, evs)]))
         twin_fst = sw.filter_stats(bufs)
         print(f"eager twin filter record: {twin_fst}", file=sys.stderr)
         del sw, bufs
@@ -1301,7 +1344,7 @@ def main():
     print(f"evaluation filter record: {fst}", file=sys.stderr)
     breakdown = None
     if world > 1:  # every rank's local / sweep / fixed / collective time, gathered (all ranks take part)
-        breakdown = rank_breakdown(ev, dist, dev, sweep_ms, n_local, args.shard == "entity")
+        breakdown = rank_breakdown(ev, dist, dev, sweep_ms, n_local, args.shard == "entity", fixed_ms=fixed_ms)
 
     total_triples = 2 * n * E
     value = total_triples * args.steps / elapsed
@@ -1420,7 +1463,8 @@ def main():
             out["per_rank"], out["per_rank_summary"] = breakdown
             out["per_rank_note"] = ("medians of 20 runs per rank after the timed region: local_ms = the rank's local "
                                     "evaluation (prep, truth + filter, sweep), sweep_ms = its sweep kernel, fixed_ms = "
-                                    "local - sweep, collective_ms = the count exchange alone (barrier before each); "
+                                    "the eager twin's whole evaluation minus its sweep kernel (both timed in the same "
+                                    "runs), collective_ms = the count exchange alone (barrier before each); "
                                     "roofline.kernel_ms is rank 0's sweep")
         if world > 1:
             # the sharded evaluation's gathered counts vs one-GPU evaluation of every query on

@@ -2132,6 +2132,15 @@ __global__ __launch_bounds__(256) void k_l1q_quant8(L1QPlane pq, L1QPlane pe, in
 // 0.77 % / 1.18 % took 0.32 / 0.51 ms against 0.26 ms with 16-bit codes (profiles/r4).
 constexpr int L1Q_PROBE_Q = 512, L1Q_PROBE_E = 256;
 constexpr double L1Q_PROBE_FRAC = 0.006;  // undecided fraction of the sample above which 16-bit codes
+// The probe's switch point in undecided pairs for a sample of n_slice entity columns -- ONE helper
+// for both entry points (mmre_link_sweep_l1q and the fused mmre_link_evaluate_l1q), so that
+// MMRE_L1_PROBE_FRAC (experiments) moves both alike and their code widths / stats agree.
+static uint32_t l1q_probe_max(int64_t n_slice) {
+  static const char* pf_env = getenv("MMRE_L1_PROBE_FRAC");
+  const double pfrac = pf_env ? atof(pf_env) : L1Q_PROBE_FRAC;
+  const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
+  return (uint32_t)std::min(pfrac * (double)sample, 4.0e9);
+}
 
 __global__ __launch_bounds__(256) void k_l1q_probe(const uint32_t* __restrict__ uq, int64_t q_pad, int64_t n_query,
                                                    const uint32_t* __restrict__ ue, int64_t e_pad, int64_t n_slice,
@@ -3986,8 +3995,7 @@ extern "C" int mmre_link_sweep_l1q(int pred_kind, float margin, const float* d_e
   if (bits == 0) {
     hipLaunchKernelGGL(k_l1q_probe, dim3(L1Q_PROBE_Q), dim3(L1Q_PROBE_E / 4), 0, st, vq, q_pad, n_query, ve + e_begin, e_pad,
                        n_slice, k4, kt, d_truth, pred_kind, margin, hdr, tight ? q_l1c : nullptr);
-    const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
-    const uint32_t probe_max = (uint32_t)(L1Q_PROBE_FRAC * (double)sample);
+    const uint32_t probe_max = l1q_probe_max(n_slice);
     hipLaunchKernelGGL(k_l1q_quant<16>, dim3(1024, 2), dim3(256), 0, st, p16q, p16e, kp, k2, hdr, n_abs, n_elem, ratio,
                        1, probe_max);
   } else if (bits == 16) {
@@ -4319,10 +4327,7 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   MMRE_CHECK_LAUNCH();
   // K3: filter counts | the code-width probe
   const int n_cblk = (int)std::min<int64_t>((n_groups + 3) / 4, 65536);  // four groups (waves) per block
-  const int64_t sample = (int64_t)L1Q_PROBE_Q * std::min<int64_t>(L1Q_PROBE_E, n_slice);
-  static const char* pf_env = getenv("MMRE_L1_PROBE_FRAC");  /* experiments: the 16-bit switch point */
-  const double pfrac = pf_env ? atof(pf_env) : L1Q_PROBE_FRAC;
-  const uint32_t probe_max = (uint32_t)std::min(pfrac * (double)sample, 4.0e9);
+  const uint32_t probe_max = l1q_probe_max(n_slice);
   hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_cblk + L1Q_PROBE_Q / 4)), dim3(256), 0, st, d_grp_qoff, d_grp_q,
                      n_groups, n_cblk, d_filt_off, d_filt_ids, d_list_scores, d_q_true, d_truth, n_query, n_ent,
                      d_counts, vq, q_pad, ve + e_begin, e_pad, n_slice, k4, kt, tight ? q_l1c : nullptr, hdr,

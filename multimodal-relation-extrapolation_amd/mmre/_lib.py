@@ -182,6 +182,16 @@ def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def mark_written(*tensors):
+    """Bump torch's version counter of tensors a C-ABI call rewrote in place through raw pointers
+    (torch's own in-place ops do this; a raw-pointer writer must do it itself), so that version
+    checks -- autograd's saved-tensor check, OpenKETrainStep's prefetch validity -- see the write."""
+    from torch.autograd.graph import increment_version
+    for t in tensors:
+        if t is not None:
+            increment_version(t)
+
+
 def require_cuda(*tensors):
     for t in tensors:
         if t is not None and not t.is_cuda:

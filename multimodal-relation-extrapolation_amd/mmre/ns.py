@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import torch
 
-from ._lib import call, lib, ptr, require_cuda, stream_ptr
+from ._lib import call, lib, mark_written, ptr, require_cuda, stream_ptr
 
 MODEL_IDS = {"transe": 0, "transe_l2": 1, "distmult": 2, "complex": 3, "rotate": 4}
 
@@ -107,6 +107,7 @@ class _FusedNS(torch.autograd.Function):
             if ctx.sgd is not None:  # the optimizer's plain SGD step in the same pass (step() skips these tables)
                 opt, lr, tables = ctx.sgd
                 call("mmre_ns_fused_grad_sgd", *args, float(lr), stream_ptr(dev))
+                mark_written(*tables)  # the SGD update rewrote the parameters in place
                 opt._fused_applied(tables)
             else:
                 call("mmre_ns_fused_grad", *args, stream_ptr(dev))
@@ -286,6 +287,7 @@ class OpenKETrainStep:
              ptr(self.gr), ptr(self.gri), ptr(self.work), self.lr, stream_ptr(self.ent.device), prepared,
              ptr(nxt["batch_h"]) if nxt else None, ptr(nxt["batch_t"]) if nxt else None,
              ptr(nxt["batch_r"]) if nxt else None, ptr(nxt["batch_y"]) if nxt else None)
+        mark_written(self.ent, self.rel, self.ent_im, self.rel_im)
         self.batch = cur
         if nxt is not None:
             self.sampler.advance(self.B, self.K, self.mode)
@@ -310,6 +312,7 @@ class OpenKETrainStep:
                 self.lr, stream_ptr(self.ent.device))
         if not self.pipeline:
             call("mmre_ns_step_openke", *self.sampler.step_args(self.B, self.K, self.mode, self.batch), *tail)
+            mark_written(self.ent, self.rel)
         else:
             p = self._parity
             cur, nxt = self._bufs[p], (self._bufs[1 - p] if prefetch else None)
@@ -323,6 +326,7 @@ class OpenKETrainStep:
             nx = (ptr(nxt["batch_h"]), ptr(nxt["batch_t"]), ptr(nxt["batch_r"]), ptr(nxt["batch_y"])) if nxt \
                 else (None, None, None, None)
             call("mmre_ns_step_openke_pipe", *args, *tail, prepared, p, *nx)
+            mark_written(self.ent, self.rel)  # the SGD update, before the prefetch's state is recorded
             self.batch = cur
             if nxt is not None:
                 self.sampler.advance(self.B, self.K, self.mode)

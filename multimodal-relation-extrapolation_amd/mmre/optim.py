@@ -10,7 +10,7 @@ import ctypes
 
 import torch
 
-from ._lib import call, stream_ptr
+from ._lib import call, mark_written, stream_ptr
 
 _MAX_T = 8
 
@@ -139,4 +139,5 @@ class SGD(torch.optim.SGD):
                 numel = (ctypes.c_int64 * n)(*[p.numel() for p in chunk])
                 call("mmre_sgd_step", ctypes.cast(params, ctypes.c_void_p), ctypes.cast(grads, ctypes.c_void_p),
                      ctypes.cast(numel, ctypes.c_void_p), n, lr, stream_ptr(chunk[0].device))
+                mark_written(*chunk)  # as torch's in-place SGD update would
         return loss

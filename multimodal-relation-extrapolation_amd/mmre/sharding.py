@@ -92,19 +92,25 @@ def calibrate_weights(spec, qh, qr, qt, qm, index, device, group=None):
     from .link import LinkSweep
     if spec is None or index is None or spec.model != "transe":
         return None
+    if len(qh) == 0:
+        return None
     sw = LinkSweep(spec)
     if not sw._fusable((0,) * 5, None, False, True, None, True):
         return None
-    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
-    filt = tuple(to(a) for a in index.groups(qh, qr, qt, qm))
-    und = torch.zeros(len(qh), dtype=torch.int32, device=device)
-    sw.run(to(qh), to(qr), to(qt), to(qm), filt=filt, undecided_q=und)
-    w = torch.from_numpy(cost_weights(und.cpu().numpy(), sw.n_ent))
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    if not multi or dist.get_rank(group) == 0:  # the calibration runs on rank 0 only
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        filt = tuple(to(a) for a in index.groups(qh, qr, qt, qm))
+        und = torch.zeros(len(qh), dtype=torch.int32, device=device)
+        sw.run(to(qh), to(qr), to(qt), to(qm), filt=filt, undecided_q=und)
+        w = torch.from_numpy(cost_weights(und.cpu().numpy(), sw.n_ent))
+    else:
+        w = torch.empty(len(qh), dtype=torch.float64)
+    del sw
+    if multi:  # every rank packs rank 0's costs
         t = w.to(device) if dist.get_backend(group) == "nccl" else w
         dist.broadcast(t, dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         w = t.cpu()
-    del sw
     return w.numpy()
 
 
@@ -292,6 +298,7 @@ class ShardedLinkEvaluation:
         return self._counts(events, 0)
 
     def _counts(self, events=None, slot=0):
+        self._last_slot = slot
         local = self._local(events, slot)
         if self.world > 1:
             return gather_counts(local, self.plan, self.group, slot)
@@ -359,17 +366,29 @@ class ShardedLinkEvaluation:
         """(metrics, counts (4, 2n) int32) of one evaluation, synchronously."""
         return self.finish(self.launch(events), copy_counts)
 
+    def _last_sweep(self):
+        """(LinkSweep, buffers) of the slot that ran the last local evaluation, with the current
+        stream ordered after that slot's stream (its workspace is then complete and not in
+        flight when a stats kernel reads it), or (None, None)."""
+        sweeps = getattr(self, "_sweeps", None)
+        if not sweeps:
+            return None, None
+        slot = getattr(self, "_last_slot", 0)
+        if self._streams is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._streams[slot])
+        return sweeps[slot]
+
     def l1q_stats(self):
         """The TransE L1 integer filter's record of this rank's last local sweep (undecided pairs,
         fallback), or None (another model / runner)."""
-        sw = getattr(self, "sweep", None)
-        return None if sw is None else sw.l1q_stats(self.sweep_buffers)
+        sw, bufs = self._last_sweep()
+        return None if sw is None else sw.l1q_stats(bufs)
 
     def filter_stats(self):
         """The count-only filter's record of this rank's last local sweep (LinkSweep.filter_stats:
         kind l1q / bf3, undecided pairs, fallback), or None."""
-        sw = getattr(self, "sweep", None)
-        return None if sw is None else sw.filter_stats(self.sweep_buffers)
+        sw, bufs = self._last_sweep()
+        return None if sw is None else sw.filter_stats(bufs)
 
 
 def entity_slices(n_ent: int, world: int, tile: int = 128):

@@ -1,8 +1,9 @@
 """Trainer (OpenKE/openke/config/Trainer.py:16-134): same constructor, setters and run() loop.
 Batches arrive from the GPU sampler already on the device; the strategy's forward/backward is
 the fused HIP loss; plain SGD runs inside the fused backward (mmre.optim.SGD). For TransE +
-MarginLoss + SGD with 'normal' sampling, run() takes the whole step as one C-ABI call
-(mmre.ns.OpenKETrainStep: same batches, losses and parameters, bit for bit)."""
+MarginLoss + SGD with 'normal' sampling (TransE, DistMult, ComplEx, RotatE), run() takes the
+whole step as one C-ABI call (mmre.ns.OpenKETrainStep: same batches, losses and parameters, bit
+for bit)."""
 import os
 
 import numpy as np
@@ -100,8 +101,9 @@ class Trainer(object):
 
     def _one_call_step(self):
         """(mmre.ns.OpenKETrainStep, its optimizer group) when the whole step -- the loader's
-        Base.cpp sampling, NegativeSampling + MarginLoss on TransE, plain SGD -- can run as one
-        C-ABI call; else None (train_one_step)."""
+        Base.cpp sampling, NegativeSampling + MarginLoss on TransE, DistMult, ComplEx or RotatE,
+        plain SGD -- can run as one C-ABI call (mmre_ns_step_openke_pipe for TransE,
+        mmre_ns_step_openke_gen_pipe for the others); else None (train_one_step)."""
         try:
             from ..data.TrainDataLoader import TrainDataLoader
             from ..module.loss.MarginLoss import MarginLoss
@@ -118,16 +120,25 @@ class Trainer(object):
             return None
         spec = m.model.ns_spec()
         ent, rel, ent_im, rel_im = m.model._tables()
-        if spec.model not in ("transe", "transe_l2") or spec.use_model_margin or ent_im is not None:
-            return None
-        if not hasattr(self.optimizer, "fusable_lr") or self.optimizer.fusable_lr([ent, rel]) is None:
-            return None
-        if spec.dim > 512 or dl.negative_ent > 32 or dl.negative_ent < 1:  # the fused kernel's shapes
+        generic = spec.model in OpenKETrainStep.GENERIC
+        if generic:
+            # DistMult / ComplEx / RotatE: mmre_ns_step_openke_gen_pipe (the generic kernels' shapes)
+            if (spec.model == "complex") != (ent_im is not None and rel_im is not None):
+                return None
+            if spec.dim > 512 or dl.negative_ent > 512 or dl.negative_ent < 1:
+                return None
+        else:
+            if spec.model not in ("transe", "transe_l2") or spec.use_model_margin or ent_im is not None:
+                return None
+            if spec.dim > 512 or dl.negative_ent > 32 or dl.negative_ent < 1:  # the fused kernel's shapes
+                return None
+        tables = [x for x in (ent, rel, ent_im, rel_im) if x is not None]
+        if not hasattr(self.optimizer, "fusable_lr") or self.optimizer.fusable_lr(tables) is None:
             return None
         group = next(g for g in self.optimizer.param_groups if any(p is ent for p in g["params"]))
         margin, adv = m.loss.fused_args()
         step = OpenKETrainStep(dl.sampler, spec, ent, rel, dl.batch_size, dl.negative_ent, margin, float(group["lr"]),
-                               adv_temperature=adv, regul_rate=m.regul_rate)
+                               adv_temperature=adv, regul_rate=m.regul_rate, ent_im=ent_im, rel_im=rel_im)
         return step, group
 
     def set_model(self, model):

@@ -40,6 +40,9 @@ def main():
                     help="--emulate-world --graph: evaluation slots on separate streams (bench.py --eval-streams)")
     ap.add_argument("--no-order", action="store_true",
                     help="--emulate-world: keep each rank's queries ascending (default: heaviest calibrated cost first)")
+    ap.add_argument("--ranks", default="",
+                    help="--emulate-world: comma-separated ranks to measure (default: all; N = 1 always runs)")
+    ap.add_argument("--no-n1", action="store_true", help="--emulate-world: skip the N = 1 reference run")
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"],
                     help="--emulate-world: workload (c2: the bench's trained TransE tables; c3-c5: the "
                          "structured tables of the reference fixtures)")
@@ -128,8 +131,12 @@ def emulate(a):
         slices = [(0, w["n_ent"])] + list(slices)
     one = None
     from mmre.sharding import rank_order
+    only = {int(x) for x in a.ranks.split(",") if x.strip()} if a.ranks else None
     for k, m in enumerate(masks):
         er = slices[k] if a.entity else None
+        r_id = k - (1 if a.emulate_world > 1 else 0)
+        if a.emulate_world > 1 and ((k == 0 and a.no_n1) or (k > 0 and only is not None and r_id not in only)):
+            continue
         m = rank_order(m, None if a.no_order else weights)  # the rank's queries in the bench's sweep order
         q = [to(x[m]) for x in (qh, qr, qt, qm)]
         filt = tuple(to(x) for x in index.groups(qh[m], qr[m], qt[m], qm[m], entity_range=er))
@@ -228,14 +235,23 @@ def emulate(a):
             xch = timeit(exchange, 50)
         # the sweep kernel alone: events on the launch stream around it, eager twins of the
         # evaluation (the separate launches; the sweep kernel is the same one)
+        # the same eager run also bracketed whole (events before and after the call), so the
+        # rank's fixed cost = eager local evaluation - its sweep, both from the one run (>= 0)
         sw2 = LinkSweep(spec)
         b2 = sw2.alloc_queries(len(m))
-        ts = []
-        for _ in range(5):
+        ts, fx, loc = [], [], []
+        outer = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+        for _ in range(7):
+            outer[0].record()
             sw2.run(*q, filt=filt, buffers=b2, sweep_events=ev, entity_range=er)
+            outer[1].record()
             torch.cuda.synchronize()
             ts.append(ev[0].elapsed_time(ev[1]))
+            loc.append(outer[0].elapsed_time(outer[1]))
+            fx.append(loc[-1] - ts[-1])
         sweep = float(np.median(ts))
+        fixed = float(np.median(fx))
+        local_eager = float(np.median(loc))
         if a.emulate_world > 1 and k == 0:
             one = ms
             print(f"N=1: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined{' on 2 streams' if ms != ms1 else ''} "
@@ -244,11 +260,12 @@ def emulate(a):
         worst = max(worst, ms)
         worst_x = max(worst_x, xch)
         fst = sw.filter_stats(bufs)
-        print(f"rank {k - (1 if one is not None else 0)}: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined "
+        print(f"rank {r_id if a.emulate_world > 1 else k}: {len(m)} sweeps, local evaluation {ms:.3f} ms pipelined "
               f"(one stream {ms1:.3f}) "
-              f"({ms_sync:.3f} synced), sweep kernel {sweep:.3f} ms, fixed {ms - sweep:.3f} ms, exchange kernels "
+              f"({ms_sync:.3f} synced), eager local {local_eager:.3f} ms = sweep kernel {sweep:.3f} ms + fixed "
+              f"{fixed:.3f} ms (same runs), exchange kernels "
               f"{xch:.3f} ms, filter {fst}")
-    if one is not None:
+    if one is not None and worst > 0:
         est = 0.0 if a.entity else EST_ALLGATHER_MS
         tot = worst + worst_x + est
         print(f"{a.config} world {a.emulate_world}{' entity-sharded' if a.entity else ''}{' (graph)' if a.graph else ''}: "

@@ -85,34 +85,40 @@ def test_openke_training_example_runs():
     assert 0.0 <= hit1 <= hit3 <= hit10 <= 1.0 and mr >= 1.0
 
 
-@pytest.mark.parametrize("regul", [0.0, 0.25])
-def test_trainer_one_call_step_equals_per_batch_path(regul):
-    """Trainer.run() on TransE + MarginLoss + SGD takes the one-call step (mmre_ns_step_openke):
-    over 3 epochs of 10 batches its epoch losses, embedding tables and sampler states equal the
-    per-batch path's (train_one_step: loader sampling, fused loss, backward, SGD) bit for bit."""
+@pytest.mark.parametrize("model_name,regul", [("transe", 0.0), ("transe", 0.25), ("distmult", 0.0),
+                                              ("complex", 0.25), ("rotate", 0.0)])
+def test_trainer_one_call_step_equals_per_batch_path(model_name, regul):
+    """Trainer.run() on TransE / DistMult / ComplEx / RotatE + MarginLoss + SGD takes the one-call
+    step (mmre_ns_step_openke_pipe / _gen_pipe): over 3 epochs of 10 batches its epoch losses,
+    embedding tables and sampler states equal the per-batch path's (train_one_step: loader
+    sampling, fused loss, backward, SGD) bit for bit."""
     import torch
     from openke.config import Trainer
     from openke.data import TrainDataLoader
     from openke.module.loss import MarginLoss
-    from openke.module.model import TransE
+    from openke.module.model import ComplEx, DistMult, RotatE, TransE
     from openke.module.strategy import NegativeSampling
     runs = []
     for one_call in (True, False):
         torch.manual_seed(0)
         tdl = TrainDataLoader(in_path=SMALL, nbatches=10, threads=8, sampling_mode="normal", bern_flag=1,
                               filter_flag=1, neg_ent=25, neg_rel=0)
-        transe = TransE(ent_tot=tdl.get_ent_tot(), rel_tot=tdl.get_rel_tot(), dim=32, p_norm=1, norm_flag=True)
-        model = NegativeSampling(model=transe, loss=MarginLoss(margin=5.0), batch_size=tdl.get_batch_size(),
+        E, R = tdl.get_ent_tot(), tdl.get_rel_tot()
+        kg = {"transe": lambda: TransE(ent_tot=E, rel_tot=R, dim=32, p_norm=1, norm_flag=True),
+              "distmult": lambda: DistMult(ent_tot=E, rel_tot=R, dim=32),
+              "complex": lambda: ComplEx(ent_tot=E, rel_tot=R, dim=32),
+              "rotate": lambda: RotatE(ent_tot=E, rel_tot=R, dim=32, margin=6.0, epsilon=2.0)}[model_name]()
+        model = NegativeSampling(model=kg, loss=MarginLoss(margin=5.0), batch_size=tdl.get_batch_size(),
                                  regul_rate=regul)
-        trainer = Trainer(model=model, data_loader=tdl, train_times=3, alpha=1.0, use_gpu=True)
+        trainer = Trainer(model=model, data_loader=tdl, train_times=3, alpha=0.5, use_gpu=True)
         trainer.one_call_step = one_call
         trainer.run()
         assert trainer.used_one_call_step == one_call
-        runs.append((list(trainer.log), transe.ent_embeddings.weight.detach().clone(),
-                     transe.rel_embeddings.weight.detach().clone(), tdl.sampler.seeds.copy()))
-    (la, ea, ra, sa), (lb, eb, rb, sb) = runs
+        runs.append((list(trainer.log), [t.detach().clone() for t in kg._tables() if t is not None],
+                     tdl.sampler.seeds.copy()))
+    (la, ta, sa), (lb, tb, sb) = runs
     assert la == lb
-    assert torch.equal(ea, eb) and torch.equal(ra, rb)
+    assert all(torch.equal(x, y) for x, y in zip(ta, tb))
     assert np.array_equal(sa, sb)
 
 

@@ -397,6 +397,17 @@ def test_pipelined_train_step_falls_back_when_its_prefetch_is_stale(c2_training)
             t[:7].mul_(0.5)
     both("params edited")
     both("prefetched again")
+    # a C-ABI writer between steps (mmre.optim.SGD: mmre_sgd_step through raw pointers) bumps the
+    # tables' version counters like torch's in-place ops, so the pre-pass runs again
+    from mmre.optim import SGD
+    fb = SGD.fallback_steps
+    for e_, r_ in ((ea, ra), (eb, rb)):
+        v = e_._version
+        SGD([e_, r_], lr=0.25).step()
+        assert e_._version > v
+    assert SGD.fallback_steps == fb  # the HIP step ran, not torch's
+    both("mmre SGD between steps")
+    both("prefetched after SGD")
     # another consumer draws from the samplers: the pipelined step's prefetched batch is stale
     # (it drew batch i + 1 before the other consumer drew) and is discarded -- both steps then
     # train on the next batch each sampler yields from its current state
