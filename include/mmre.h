@@ -226,6 +226,19 @@ int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const float* d_e
                         const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
                         int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts, const float* d_truth,
                         void* d_work, int64_t work_bytes, void* stream);
+/* mmre_link_sweep_bf3 for a table whose row-major layout IS the plane layout -- DistMult with d a
+ * multiple of 16, whose evaluation needs no normalisation (DistMult.py:34-44, 70-72): d_ent_rows
+ * is then the raw (n_ent, d) embedding table (16-B aligned), and no prepared copy of it is made
+ * per evaluation (mmre_link_prepare_entities writes two, k-major and row-major). The split planes,
+ * norms and block maxima come from one read of the rows; d_ent_km (k_pad x e_pad floats, any
+ * contents) is written only when the list overflows, by the fallback itself, before the exact
+ * f32 sweep reads it. Same counts as mmre_link_sweep_bf3, bit for bit. MMRE_ERR_SHAPE for any
+ * other model / d. */
+int mmre_link_sweep_bf3_rows(int model, int pred_kind, float margin, const float* d_ent_rows, int64_t n_ent,
+                             int64_t e_pad, int64_t e_begin, int64_t e_end, float* d_ent_km, const float* d_q_km,
+                             const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr,
+                             const int8_t* d_qmode, int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts,
+                             const float* d_truth, void* d_work, int64_t work_bytes, void* stream);
 
 /* Test.h:232-327 test_link_prediction + getTestLink* (Test.h:356-390), host side,
  * with the reference's float accumulation order (P14). Counts: int32, column c of

@@ -84,12 +84,10 @@ __device__ __forceinline__ void write_k_major(const float* lds, int ls, int rb, 
 // Table rows -> (optional) k-major planes out_km[kt][pad] and row-major rows[n][rw]
 // (rw <= kt). TransE with norm_flag: F.normalize(x, 2, -1) = x / max(||x||_2, 1e-12)
 // (TransE.py:63-66), ||x|| from the canonical sequential sum of squares.
-__global__ __launch_bounds__(256) void k_prep_rows(int model, int norm_flag, const float* __restrict__ src,
-                                                   const float* __restrict__ src_im, int64_t n, int dim, int kp,
-                                                   int rb, float* __restrict__ out_km, int64_t pad,
-                                                   float* __restrict__ rows, int rw) {
-  extern __shared__ float lds[];
-  __shared__ float s_norm[32];
+__device__ __forceinline__ void prep_rows_body(int model, int norm_flag, const float* __restrict__ src,
+                                               const float* __restrict__ src_im, int64_t n, int dim, int kp, int rb,
+                                               float* __restrict__ out_km, int64_t pad, float* __restrict__ rows,
+                                               int rw, float* lds, float* s_norm) {
   const int kt = n_planes(model) * kp, ls = kt + 1;
   const int lane = threadIdx.x & 31, slot = threadIdx.x >> 5;
   const int64_t e0 = (int64_t)blockIdx.x * rb;
@@ -133,6 +131,25 @@ __global__ __launch_bounds__(256) void k_prep_rows(int model, int norm_flag, con
     for (int k = lane; k < rw; k += 32) rows[e * rw + k] = x[k];
   }
   if (out_km) write_k_major(lds, ls, rb, kt, out_km, pad, e0);
+}
+__global__ __launch_bounds__(256) void k_prep_rows(int model, int norm_flag, const float* __restrict__ src,
+                                                   const float* __restrict__ src_im, int64_t n, int dim, int kp,
+                                                   int rb, float* __restrict__ out_km, int64_t pad,
+                                                   float* __restrict__ rows, int rw) {
+  extern __shared__ float lds[];
+  __shared__ float s_norm[32];
+  prep_rows_body(model, norm_flag, src, src_im, n, dim, kp, rb, out_km, pad, rows, rw, lds, s_norm);
+}
+// The k-major planes of a table whose row-major copy is the raw table itself (DistMult, d a
+// multiple of 16: mmre_link_sweep_bf3_rows), gated: only when *gate != 0 -- the split-bf16
+// filter's list overflowed and the exact f32 sweep that reads these planes is about to count.
+__global__ __launch_bounds__(256) void k_prep_km_gated(const uint32_t* __restrict__ gate, int model,
+                                                       const float* __restrict__ src, int64_t n, int dim, int kp,
+                                                       int rb, float* __restrict__ out_km, int64_t pad) {
+  extern __shared__ float lds[];
+  __shared__ float s_norm[32];
+  if (__builtin_amdgcn_readfirstlane(*gate) == 0u) return;
+  prep_rows_body(model, 0, src, nullptr, n, dim, kp, rb, out_km, pad, nullptr, 0, lds, s_norm);
 }
 
 // Query vectors, one LDS block of rb queries: the anchor rows (t for head_batch, h for
@@ -2265,6 +2282,27 @@ __device__ __forceinline__ uint32_t bf16_rn_bits(float x) {  // finite x: round 
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
 
+// The split of 16 consecutive k values of one column into the 64-B block {hi[16], lo[16]}.
+__device__ __forceinline__ void bf3_split_store(const float (&x)[16], uint4* __restrict__ o) {
+  uint32_t hw[8], lw[8];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    uint32_t hb = 0u, lb = 0u;
+    if (!(fabsf(x[j]) < INFINITY)) {
+      hb = 0x7FC0u;  // inf / NaN: a NaN operand, every product NaN: the pair is undecided
+    } else if (fabsf(x[j]) >= 0x1p-60f) {
+      hb = bf16_rn_bits(x[j]);
+      lb = bf16_rn_bits(x[j] - __uint_as_float(hb << 16));  // x - hi is exact (Sterbenz)
+    }
+    if (j & 1) { hw[j >> 1] |= hb << 16; lw[j >> 1] |= lb << 16; }
+    else { hw[j >> 1] = hb; lw[j >> 1] = lb; }
+  }
+  o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  o[1] = make_uint4(hw[4], hw[5], hw[6], hw[7]);
+  o[2] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  o[3] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
+}
+
 // One thread per (column c, 16-k block kb) of a k-major plane (K rows x pad, columns col0 + c):
 // the split block out[kb][c] = {hi[16], lo[16]} (4 x 16 B). Consecutive threads take
 // consecutive columns of one block: coalesced 64-B-per-thread reads and writes.
@@ -2279,24 +2317,54 @@ __global__ __launch_bounds__(256) void k_bf3_split(const float* __restrict__ km,
   float x[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) x[j] = src[(int64_t)j * pad];  // all in flight together
-  uint32_t hw[8], lw[8];
+  bf3_split_store(x, out + ((int64_t)kb * out_pad + c) * 4);
+}
+
+// The split planes, norms and (wide sweep) 32-column norm maxima straight from a ROW-MAJOR
+// table (mmre_link_sweep_bf3_rows: DistMult, whose row-major copy is the raw table itself, so
+// no re-laid-out copy is written per evaluation): one read of the rows, one write of the split
+// blocks. 256 threads = 32 rows x 8 lanes; lane j of a row takes its 16-k blocks j, j + 8, ...
+// (8 lanes read 512 contiguous bytes of the row; for one block the 32 rows' 64-B outputs are
+// contiguous). Same split as k_bf3_split, norms as k_bf3_norms / k_bf3_enorms (any summation
+// order serves: the bound's 2 % slack covers the norm's rounding); rows past n_rows (the
+// slice's last tile) are zero with norm 0.
+__global__ __launch_bounds__(256) void k_bf3_split_rows(const float* __restrict__ rows, int64_t n_rows, int64_t r0,
+                                                        int ktot, uint4* __restrict__ out, int64_t out_pad,
+                                                        float* __restrict__ norms, float* __restrict__ bmax) {
+  __shared__ float wm[4];
+  const int i = threadIdx.x >> 3, j = threadIdx.x & 7;
+  const int64_t c = (int64_t)blockIdx.x * 32 + i;  // slice column
+  const int64_t r = r0 + c;
+  const bool valid = r < n_rows;
+  const float* src = rows + (valid ? r : 0) * (int64_t)ktot;
+  const int nkb = ktot / 16;
+  float ss = 0.0f;
+  for (int kb = j; kb < nkb; kb += 8) {
+    float x[16];
+    const float4* s4 = reinterpret_cast<const float4*>(src + kb * 16);
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    uint32_t hb = 0u, lb = 0u;
-    if (!(fabsf(x[j]) < INFINITY)) {
-      hb = 0x7FC0u;  // inf / NaN: a NaN operand, every product NaN: the pair is undecided
-    } else if (fabsf(x[j]) >= 0x1p-60f) {
-      hb = bf16_rn_bits(x[j]);
-      lb = bf16_rn_bits(x[j] - __uint_as_float(hb << 16));  // x - hi is exact (Sterbenz)
+    for (int u = 0; u < 4; ++u) {
+      const float4 v = valid ? s4[u] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      x[4 * u] = v.x; x[4 * u + 1] = v.y; x[4 * u + 2] = v.z; x[4 * u + 3] = v.w;
     }
-    if (j & 1) { hw[j >> 1] |= hb << 16; lw[j >> 1] |= lb << 16; }
-    else { hw[j >> 1] = hb; lw[j >> 1] = lb; }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) ss = __builtin_fmaf(x[u], x[u], ss);
+    bf3_split_store(x, out + ((int64_t)kb * out_pad + c) * 4);
   }
-  uint4* o = out + ((int64_t)kb * out_pad + c) * 4;
-  o[0] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-  o[1] = make_uint4(hw[4], hw[5], hw[6], hw[7]);
-  o[2] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
-  o[3] = make_uint4(lw[4], lw[5], lw[6], lw[7]);
+  ss += __shfl_xor(ss, 1);
+  ss += __shfl_xor(ss, 2);
+  ss += __shfl_xor(ss, 4);
+  const float nv = valid ? fmaxf(sqrtf(ss), 0x1p-30f) : 0.0f;
+  if (j == 0) norms[c] = nv;
+  if (bmax) {
+    float m = nv;  // the 8 rows of this wave (lanes 0, 8, .., 56 hold distinct rows)
+    m = fmaxf(m, __shfl_xor(m, 8));
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) bmax[blockIdx.x] = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+  }
 }
 
 // The bound's 2-norms, one wave per row of a row-major copy (rows r0 .. r0 + n_out - 1, K
@@ -3067,6 +3135,17 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
     const int64_t q_tiles = q_pad / TQ;
     const int64_t units = (n_et >= 8) ? 8 * q_tiles * ((n_et + 7) / 8) : q_tiles * n_et;
     if (units < g) g = (int)(units > 0 ? units : 1);
+    // Dynamic scheduling of a small share: as many workgroups per XCD group as make its units an
+    // (almost) whole number of rounds -- the same rounds as the full grid, no nearly empty last
+    // round (an 8-way C2 share: 527 units per group over 128 workgroups = 4.1 rounds, the fifth
+    // run by 15 of them; over 106 workgroups, 5 rounds). MMRE_SWEEP_BALANCE=0: the full grid (A/B).
+    static const char* bal_env = getenv("MMRE_SWEEP_BALANCE");
+    if (dyn && g % 8 == 0 && n_et >= 8 && !(bal_env && bal_env[0] == '0')) {
+      const int64_t per_group = (q_tiles * n_et + 7) / 8;  // UnitMap: every group within +-1 of this
+      const int64_t slots = g / 8;
+      const int64_t rounds = (per_group + slots - 1) / slots;
+      if (rounds <= 16) g = 8 * (int)((per_group + rounds - 1) / rounds);
+    }
   }
   // MMRE_SWEEP_GRID (experiments): "tiles" = one workgroup per (query tile, 1/8 of the
   // entity tiles); a number = that many persistent workgroups.
@@ -4094,12 +4173,14 @@ static void launch_bf3w(hipStream_t st, const uint4* eb, int64_t e_pad, int64_t 
                      be);
 }
 
-extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const float* d_ent_km,
-                                   const float* d_ent_rows, int64_t n_ent, int64_t e_pad, int64_t e_begin,
-                                   int64_t e_end, const float* d_q_km, const float* d_q_rows,
-                                   const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
-                                   int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts, const float* d_truth,
-                                   void* d_work, int64_t work_bytes, void* stream) {
+// rows_src (mmre_link_sweep_bf3_rows): the entity split planes, norms and block maxima come from
+// the row-major table d_ent_rows in one pass (k_bf3_split_rows), and d_ent_km is written only by
+// the gated overflow fallback, right before the exact f32 sweep that reads it.
+static int sweep_bf3_impl(int model, int pred_kind, float margin, float* d_ent_km, const float* d_ent_rows,
+                          int64_t n_ent, int64_t e_pad, int64_t e_begin, int64_t e_end, const float* d_q_km,
+                          const float* d_q_rows, const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
+                          int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts, const float* d_truth,
+                          void* d_work, int64_t work_bytes, void* stream, bool rows_src) {
   if (!mfma_model(model)) return MMRE_ERR_MODEL;
   int rc = check_link_args(model, pred_kind, d_ent_km, n_ent, e_pad, d_q_km, d_q_true, d_qr, d_qmode, n_query,
                            q_pad, nullptr, nullptr, d_counts, d_truth);
@@ -4132,8 +4213,9 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   const int nkb = ktot / 16;
   hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad * nkb + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad,
                      (int64_t)0, q_pad, nkb, qb, q_pad);
-  hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((e_cols * nkb + 255) / 256)), dim3(256), 0, st, d_ent_km, e_pad,
-                     e_begin, e_cols, nkb, eb, e_pad);
+  if (!rows_src)
+    hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((e_cols * nkb + 255) / 256)), dim3(256), 0, st, d_ent_km, e_pad,
+                       e_begin, e_cols, nkb, eb, e_pad);
   static const char* order_env = getenv("MMRE_MFMA_EMAJOR");
   const int emajor = order_env ? atoi(order_env) : ((double)e_pad * ktot * 4.0 > 64.0 * (1 << 20) ? 1 : 0);
   // the wide sweep (k_sweep_bf3w, prediction -S) where the planes overflow the caches (C5: 15.9
@@ -4146,7 +4228,10 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   const int wide_qt = qt_env ? atoi(qt_env) : 256;
   hipLaunchKernelGGL(k_bf3_norms, dim3((unsigned)((q_pad + 3) / 4)), dim3(256), 0, st, d_q_rows, n_query, (int64_t)0,
                      q_pad, ktot, qn, d_truth, wide ? thr_pad : nullptr, qbf, cb);
-  if (wide)
+  if (rows_src)  // split planes, norms and block maxima in one read of the rows (e_cols: whole tiles)
+    hipLaunchKernelGGL(k_bf3_split_rows, dim3((unsigned)(e_cols / 32)), dim3(256), 0, st, d_ent_rows, n_ent, e_begin,
+                       ktot, eb, e_pad, en, wide ? ebm : nullptr);
+  else if (wide)
     hipLaunchKernelGGL(k_bf3_enorms, dim3((unsigned)((e_cols + 31) / 32)), dim3(256), 0, st, d_ent_rows, n_ent,
                        e_begin, e_cols, ktot, en, ebm);
   else
@@ -4187,6 +4272,12 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
     }                                                                                                          \
     hipLaunchKernelGGL((k_bf3_fallback_zero), dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, hdr,  \
                        d_counts, n_query);                                                                     \
+    if (rows_src) { /* the fallback's k-major planes, only when it runs */                                      \
+      const int rb = stage_rows(ktot);                                                                         \
+      hipLaunchKernelGGL(k_prep_km_gated, dim3((unsigned)((e_cols + rb - 1) / rb)), dim3(256),                  \
+                         sizeof(float) * (size_t)rb * (ktot + 1), st, hdr + 1, model,                          \
+                         d_ent_rows + e_begin * (int64_t)ktot, n_slice, dim, kp, rb, d_ent_km + e_begin, e_pad); \
+    }                                                                                                          \
     launch_mfma(false, false, pred_kind, margin, d_ent_km + e_begin, n_slice, e_pad, n_et, (int)e_begin,       \
                 d_q_km, q_pad, n_query, ktot, d_truth, nullptr, nullptr, nullptr, nullptr, 0, d_counts,        \
                 nullptr, st, hdr + 1);                                                                         \
@@ -4199,6 +4290,31 @@ extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const
   else MMRE_BF3(-1);
 #undef MMRE_BF3
   return launch_finalize(st, d_counts, n_query, false);
+}
+
+extern "C" int mmre_link_sweep_bf3(int model, int pred_kind, float margin, const float* d_ent_km,
+                                   const float* d_ent_rows, int64_t n_ent, int64_t e_pad, int64_t e_begin,
+                                   int64_t e_end, const float* d_q_km, const float* d_q_rows,
+                                   const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
+                                   int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts, const float* d_truth,
+                                   void* d_work, int64_t work_bytes, void* stream) {
+  return sweep_bf3_impl(model, pred_kind, margin, const_cast<float*>(d_ent_km), d_ent_rows, n_ent, e_pad, e_begin,
+                        e_end, d_q_km, d_q_rows, d_q_true, d_qr, d_qmode, n_query, q_pad, dim, d_counts, d_truth,
+                        d_work, work_bytes, stream, false);
+}
+
+extern "C" int mmre_link_sweep_bf3_rows(int model, int pred_kind, float margin, const float* d_ent_rows,
+                                        int64_t n_ent, int64_t e_pad, int64_t e_begin, int64_t e_end,
+                                        float* d_ent_km, const float* d_q_km, const float* d_q_rows,
+                                        const int32_t* d_q_true, const int64_t* d_qr, const int8_t* d_qmode,
+                                        int64_t n_query, int64_t q_pad, int dim, int32_t* d_counts,
+                                        const float* d_truth, void* d_work, int64_t work_bytes, void* stream) {
+  // the row-major table must be the plane layout itself: DistMult with d a multiple of 16 (K = d)
+  if (model != MMRE_DISTMULT || plane_rows(model, dim) != dim) return MMRE_ERR_SHAPE;
+  if (!d_ent_rows || !d_ent_km || (reinterpret_cast<uintptr_t>(d_ent_rows) & 15)) return MMRE_ERR_ARG;
+  return sweep_bf3_impl(model, pred_kind, margin, d_ent_km, d_ent_rows, n_ent, e_pad, e_begin, e_end, d_q_km,
+                        d_q_rows, d_q_true, d_qr, d_qmode, n_query, q_pad, dim, d_counts, d_truth, d_work,
+                        work_bytes, stream, true);
 }
 
 extern "C" int mmre_link_sweep_range(int model, int pred_kind, float margin, const float* d_ent_km, int64_t n_ent,

@@ -181,6 +181,9 @@ class LinkSweep:
         # count-only TransE L1 runs with filter groups as ONE call (mmre_link_evaluate_l1q, seven
         # launches instead of thirteen); MMRE_FUSED_EVAL=0 keeps the separate entry points
         self.fused_eval = os.environ.get("MMRE_FUSED_EVAL", "1") != "0"
+        # DistMult count-only sweeps split the raw rows (mmre_link_sweep_bf3_rows); "0" keeps the
+        # prepared k-major / row-major copies (A/B; read per instance: tests switch it)
+        self.bf3_raw = os.environ.get("MMRE_BF3_RAW", "1") != "0"
 
     def prepare_entities(self):
         s = self.spec
@@ -224,12 +227,21 @@ class LinkSweep:
             return dict(counts=z, truth=torch.empty(0, dtype=torch.float32, device=self.device),
                         scores=torch.empty((0, self.n_ent), dtype=torch.float32, device=self.device)
                         if return_scores else None)
-        if prepare or not self.prepared:
+        l1q = (self.model_id == MODEL_IDS["transe"] and not return_scores and q_rows and self.l1_filter)
+        bf3 = (self.model_id in (MODEL_IDS["distmult"], MODEL_IDS["complex"]) and not return_scores and q_rows
+               and type_masks is None and self.mfma_filter)
+        # DistMult count-only with filter groups and K = d: the raw table IS the row-major copy, so no
+        # prepared copies are written (mmre_link_sweep_bf3_rows splits the raw rows; C5: 2 GB of
+        # re-laid-out writes per evaluation gone); MMRE_BF3_RAW=0 keeps the prepared path (A/B)
+        raw = (bf3 and self.model_id == MODEL_IDS["distmult"] and self.K == s.dim and filt is not None
+               and len(filt) == 5 and self._ent.data_ptr() % 16 == 0 and self.bf3_raw)
+        ent_rows = self._ent if raw else self.ent_rows
+        if not raw and (prepare or not self.prepared):
             self.prepare_entities()
         b = buffers if buffers is not None else self.alloc_queries(n)
         st = stream_ptr(self.device)
         qrow = b["q_rows"] if q_rows else None   # None: truth kernel reads the k-major plane
-        call("mmre_link_prepare_queries", self.model_id, int(bool(s.norm_flag)), ptr(self.ent_rows), ptr(self._rel),
+        call("mmre_link_prepare_queries", self.model_id, int(bool(s.norm_flag)), ptr(ent_rows), ptr(self._rel),
              ptr(self._rel_im), self.n_ent, self.n_rel, s.dim, float(s.phase_denom), ptr(qh), ptr(qr), ptr(qt),
              ptr(qmode), n, ptr(b["q_km"]), b["q_pad"], ptr(b["q_true"]), ptr(self.rel_work), ptr(qrow), st)
         scores = None
@@ -242,7 +254,7 @@ class LinkSweep:
             lv = b.get("list_scores")
             if lv is None or lv.shape[0] < n_entries:
                 lv = b["list_scores"] = torch.empty(max(n_entries, 1), dtype=torch.float32, device=self.device)
-            call("mmre_link_truth_grouped", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_rows),
+            call("mmre_link_truth_grouped", self.model_id, int(s.pred_kind), float(s.margin), ptr(ent_rows),
                  self.n_ent, ptr(qrow), ptr(b["q_true"]), ptr(qr), ptr(qmode), n, s.dim, ptr(gqo), ptr(gq),
                  int(gqo.shape[0]) - 1, ptr(off), ptr(ids), ptr(entry_q), n_entries, ptr(th), ptr(tt), ptr(lv),
                  ptr(b["counts"]), ptr(b["truth"]), st)
@@ -253,9 +265,6 @@ class LinkSweep:
             call("mmre_link_truth", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km), self.n_ent,
                  self.e_pad, ptr(self.ent_rows), ptr(b["q_km"]), ptr(b["q_true"]), ptr(qr), ptr(qmode), n,
                  b["q_pad"], s.dim, ptr(off), ptr(ids), ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), st)
-        l1q = (self.model_id == MODEL_IDS["transe"] and not return_scores and q_rows and self.l1_filter)
-        bf3 = (self.model_id in (MODEL_IDS["distmult"], MODEL_IDS["complex"]) and not return_scores and q_rows
-               and type_masks is None and self.mfma_filter)
         if l1q:
             need = int(_lib.lib().mmre_link_l1q_workspace(s.dim, self.e_pad, b["q_pad"]))
             wk = b.get("l1q_work")
@@ -274,6 +283,12 @@ class LinkSweep:
                  self.n_ent, self.e_pad, e0, e1, ptr(b["q_km"]), ptr(b["q_rows"]), ptr(b["q_true"]), ptr(qr),
                  ptr(qmode), n, b["q_pad"], s.dim, ptr(th), ptr(tt), ptr(b["counts"]), ptr(b["truth"]), ptr(wk),
                  int(wk.numel()), st)
+        elif raw:  # the same filter over the raw DistMult rows (ent_km written only by an overflow fallback)
+            e0, e1 = (0, self.n_ent) if entity_range is None else (int(entity_range[0]), int(entity_range[1]))
+            call("mmre_link_sweep_bf3_rows", self.model_id, int(s.pred_kind), float(s.margin), ptr(ent_rows),
+                 self.n_ent, self.e_pad, e0, e1, ptr(self.ent_km), ptr(b["q_km"]), ptr(b["q_rows"]),
+                 ptr(b["q_true"]), ptr(qr), ptr(qmode), n, b["q_pad"], s.dim, ptr(b["counts"]), ptr(b["truth"]),
+                 ptr(wk), int(wk.numel()), st)
         elif bf3:  # DistMult / ComplEx count-only: the split-bf16 MFMA filter (same counts, bit for bit)
             e0, e1 = (0, self.n_ent) if entity_range is None else (int(entity_range[0]), int(entity_range[1]))
             call("mmre_link_sweep_bf3", self.model_id, int(s.pred_kind), float(s.margin), ptr(self.ent_km),
@@ -294,6 +309,7 @@ class LinkSweep:
             sweep_events[1].record()
         b["l1q_used"] = l1q
         b["bf3_used"] = bf3
+        b["bf3_raw"] = raw
         return dict(counts=b["counts"], truth=b["truth"], scores=scores)
 
     def _fusable(self, filt, type_masks, return_scores, prepare, sweep_events, q_rows):

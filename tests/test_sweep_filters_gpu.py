@@ -11,6 +11,8 @@ exact copies of the truth row (exact ties: strict < must not count them), copies
 in a few coordinates (scores a few ulps from the threshold), zero rows, rows of subnormal and
 of overflowing magnitude, NaN rows, and an identity rotation (v = 0 on every k).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -292,12 +294,20 @@ def test_mfma_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, monkeypatch
             torch.from_numpy(a).to(dev) for a in index.groups(qh, qr, qt, qm, entity_range=entity_range))
         res = sw.run(*args, filt=f, buffers=bufs, entity_range=entity_range)
         torch.cuda.synchronize()
+        if model == "distmult" and os.environ.get("MMRE_MFMA_FILTER") != "0":
+            # d = 48: the raw DistMult rows are split directly (mmre_link_sweep_bf3_rows) unless MMRE_BF3_RAW=0
+            assert bufs["bf3_raw"] == (os.environ.get("MMRE_BF3_RAW") != "0")
         return res["counts"].cpu().numpy().copy(), sw.bf3_stats(bufs)
 
     fast, st = run()
     assert st is not None and not st["fallback"], st
     assert st["undecided"] >= len(qh), st               # every truth is listed (its S' is within the bound)
     assert np.array_equal(fast[:2], exact["counts"][:2])
+    if model == "distmult":  # the prepared-copy path (k-major split + separate norms): the same counts
+        monkeypatch.setenv("MMRE_BF3_RAW", "0")
+        prep, st_prep = run()
+        monkeypatch.delenv("MMRE_BF3_RAW")
+        assert np.array_equal(prep, fast), (st_prep, st)  # (undecided pairs may differ: the norms round differently)
     monkeypatch.setenv("MMRE_MFMA_FILTER", "0")
     f32, st32 = run()
     monkeypatch.delenv("MMRE_MFMA_FILTER")
