@@ -149,7 +149,7 @@ REF_SAMPLE = {"c1": 1000, "c2": 1000, "c3": 1000, "c4": 250, "c5": 250}   # test
 REF_NEAR_REL = 1e-5   # the parity block's near-tie window, x max|score| of the sweep (as the fixtures')
 
 
-def ref_tester_leg(w, n_sample: int, timeout_s: int = 600):
+def ref_tester_leg(w, n_sample: int, timeout_s: int = 600, reps: int | None = None):
     """The reference's CPU path on this host's cores, as child processes (oracle/ref_tester.py:
     the OpenKE Tester loop with the reference's own Base.so ranker -- oracle/_ref, compiled
     from /root/reference/OpenKE/openke/base/Base.cpp -- and the reference models' predict op
@@ -172,8 +172,8 @@ def ref_tester_leg(w, n_sample: int, timeout_s: int = 600):
         out = ref_tester.run_parallel(w, *q, procs, timeout_s=timeout_s, summary=True, near_rel=REF_NEAR_REL)
         # repetitions of the same statistic (whole sample / slowest chunk), so that the reported
         # spread brackets the value: 5 in all when a repetition's loop takes <= 20 s, else 3
+        n_reps = reps if reps else (5 if float(out["elapsed"]) <= 20.0 else 3)
         reps = [float(out["elapsed"])]
-        n_reps = 5 if reps[0] <= 20.0 else 3
         while len(reps) < n_reps:
             again = ref_tester.run_parallel(w, *q, procs, timeout_s=timeout_s, summary=True, near_rel=REF_NEAR_REL)
             if not np.array_equal(again["counts"], out["counts"]):
@@ -224,7 +224,7 @@ def sample_scores(spec, w, n, dev):
     return res["scores"]
 
 
-def parity_block(ref, counts, n_total, w, gpu_scores):
+def parity_block(ref, counts, n_total, w, gpu_scores, tc: bool = False):
     """GPU per-query counts vs the reference Base.so's on the cpu_baseline sample, query by
     query, as tests/test_ref_fixture_gpu.py checks the fixtures: the reference lists, per
     sweep, every entity whose reference score lies within REF_NEAR_REL x max|score| of the
@@ -234,7 +234,9 @@ def parity_block(ref, counts, n_total, w, gpu_scores):
     (filtered: unless the entity is a known triple). window_ok: the measured GPU-vs-reference
     error on those scores stays below 1/4 of the window, so no unlisted entity can flip.
     Metrics: the sample's hit@{1,3,10} / MR / MRR from the GPU's counts (the P14 reduction)
-    and the reference's (Base.so's Test.h reduction, restated over the merged chunks)."""
+    and the reference's (Base.so's Test.h reduction, restated over the merged chunks).
+    tc: the type-constrained counts (Test.h's *_constrain counters, type_constrain.txt from
+    w["type_heads"] / w["type_tails"]) instead -- a near entity moves them only when its type fits."""
     from mmre.link import link_metrics
     n = int(ref["n"])
     q = ref["q"].astype(np.int64)
@@ -244,8 +246,9 @@ def parity_block(ref, counts, n_total, w, gpu_scores):
     E, R = int(w["n_ent"]), int(w["n_rel"])
     gh = counts[:, :n].T.astype(np.int64)                  # (n, 4) raw, filt, raw_tc, filt_tc
     gt = counts[:, n_total:n_total + n].T.astype(np.int64)
-    gpu_c = np.stack([gh[:, :2], gt[:, :2]])                # (2, n, 2) [head|tail][q][raw, filt]
-    ref_c = ref["counts"].astype(np.int64)
+    cols = slice(2, 4) if tc else slice(0, 2)
+    gpu_c = np.stack([gh[:, cols], gt[:, cols]])            # (2, n, 2) [head|tail][q][raw, filt] (type-constrained: tc)
+    ref_c = ref["counts"].astype(np.int64)[:, :, cols]
     off, ids = ref["near_off"], ref["near_ids"].astype(np.int64)
     sweep_of = np.repeat(np.arange(2 * n), np.diff(off))
     dev = gpu_scores.device
@@ -267,15 +270,23 @@ def parity_block(ref, counts, n_total, w, gpu_scores):
     known_keys = np.unique(key(np.asarray(w["filter_h"], np.int64), np.asarray(w["filter_r"], np.int64),
                                np.asarray(w["filter_t"], np.int64)))
     known = np.isin(np.where(head, key(ids, r[qi], t[qi]), key(h[qi], r[qi], ids)), known_keys)
+    if tc:  # only a near entity of the relation's type moves the constrained counts
+        tkey = lambda rr, e: rr * E + e
+        types = [np.unique(np.concatenate([tkey(np.int64(rr), np.asarray(lst, np.int64)) for rr, lst in
+                                           enumerate(w[name])] + [np.zeros(0, np.int64)]))
+                 for name in ("type_heads", "type_tails")]
+        ok = np.where(head, np.isin(tkey(r[qi], ids), types[0]), np.isin(tkey(r[qi], ids), types[1]))
+        flip = flip * ok
     d_raw = np.bincount(sweep_of, weights=flip, minlength=2 * n).astype(np.int64).reshape(2, n)
     d_filt = np.bincount(sweep_of, weights=flip * (~known), minlength=2 * n).astype(np.int64).reshape(2, n)
     expect = ref_c + np.stack([d_raw, d_filt], axis=2)
     mism = gpu_c != ref_c
-    gm = link_metrics(counts[:, :n], counts[:, n_total:n_total + n])["filter"]
-    rm = ref["metrics"]  # MRR, MR, hit10, hit3, hit1 (filter, Test.h:232-327)
+    gm = link_metrics(counts[:, :n], counts[:, n_total:n_total + n])["filter_tc" if tc else "filter"]
+    rm = ref["metrics"]  # MRR, MR, hit10, hit3, hit1 (filter, or filter_tc with tc; Test.h:232-327)
     gpu_vals = np.array([gm["mrr"], gm["mr"], gm["hit10"], gm["hit3"], gm["hit1"]], np.float32)
     return {"source": f"reference Base.so Tester loop on the cpu_baseline sample (oracle/ref_tester.py, "
-                      f"{int(ref['threads'])} chunks)",
+                      f"{int(ref['threads'])} chunks)" + (", type-constrained counts (testHead/testTail with "
+                                                          "type_constrain, importTypeFiles)" if tc else ""),
             "test_triples": n, "sweeps": 2 * n, "queries_match": same_q,
             "tie_window": f"{REF_NEAR_REL} x max|s_ref| per sweep (the reference's near lists)",
             "score_err_max": float(err.max()), "window_ok": bool(np.all(err <= 0.25 * window)),
@@ -1204,6 +1215,10 @@ def main():
     ap.add_argument("--pack", default="cost", choices=["cost", "count"],
                     help="N > 1 relation-sharded: LPT by per-query cost (one calibration evaluation counts the pairs "
                          "the L1 filter leaves undecided; TransE) or by query count")
+    ap.add_argument("--type-constrain", action="store_true",
+                    help="link configs: the type-constrained evaluation (Tester.run_link_prediction(type_constrain=True), "
+                         "Test.h:70-98 / 114-126) with type_constrain.txt built from the filter set as the reference's "
+                         "n-n.py does (each relation's known heads / tails); metrics = the filter_tc group")
     ap.add_argument("--shard", default="relation", choices=["relation", "entity"],
                     help="N > 1 link configs: split the queries (relation-sharded, one all-gather; default) or "
                          "the entity table (every query against 1/N of the entities, one all-reduce)")
@@ -1268,7 +1283,13 @@ def main():
                 w[k] = t.cpu()
     E = w["n_ent"]
     n = len(w["test_h"])
-    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"])
+    tc = bool(args.type_constrain)
+    if tc:  # type_constrain.txt by n-n.py's rule: each relation's known heads / tails (train + test)
+        fh, fr, ft = (np.asarray(w[k], np.int64) for k in ("filter_h", "filter_r", "filter_t"))
+        w["type_heads"] = [np.unique(fh[fr == r]) for r in range(w["n_rel"])]
+        w["type_tails"] = [np.unique(ft[fr == r]) for r in range(w["n_rel"])]
+    index = FilterIndex(w["filter_h"], w["filter_r"], w["filter_t"], E, w["n_rel"],
+                        type_heads=w.get("type_heads"), type_tails=w.get("type_tails"))
     pk = {"transe": 0, "distmult": 2, "complex": 2, "rotate": 3}[model]
     spec = ScoreSpec(model=model, ent=w["ent"].to(dev), rel=w["rel"].to(dev), dim=dim,
                      ent_im=w.get("ent_im").to(dev) if "ent_im" in w else None,
@@ -1276,7 +1297,8 @@ def main():
                      pred_kind=pk, margin=float(w.get("margin", 0.0)),
                      phase_denom=rotate_phase_denom(w["margin"], w["epsilon"], dim) if model == "rotate" else 0.0)
     if args.shard == "entity":
-        ev = EntityShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev)
+        ev = EntityShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev,
+                                         type_constrain=tc)
         n_local = 2 * n if ev.entity_range[1] > ev.entity_range[0] else 0
         e_local = ev.entity_range[1] - ev.entity_range[0]
     else:
@@ -1284,7 +1306,7 @@ def main():
         # replayed from one hipGraph; kernel_ms comes from an eager twin after the timed region
         ev = ShardedLinkEvaluation(spec, w["test_h"], w["test_r"], w["test_t"], index=index, device=dev,
                                    graph=not args.eager, cost="undecided" if args.pack == "cost" else None,
-                                   streams=args.eval_streams)
+                                   streams=args.eval_streams, type_constrain=tc)
         n_local = int(ev.masks[rank].sum())
         e_local = E
 
@@ -1358,6 +1380,8 @@ def main():
             KERNEL_NAMES["transe"] = "k_sweep_valu<5, false, false, 0,"
         elif model == "transe" and fst is not None and fst["kind"] == "l1q" and l1_bits is None:
             KERNEL_NAMES["transe"] = "k_sweep_valu<0, false, false, 0,"
+        if tc and model == "transe":  # the type-constrained variant of the same sweep
+            KERNEL_NAMES["transe"] = KERNEL_NAMES["transe"].replace(", false, false,", ", true, false,")
         if model in ("distmult", "complex") and MFMA_FILTER:
             # the wide split-bf16 sweep (k_sweep_bf3w) runs where the split planes exceed 64 MB (C5),
             # as mmre_link_sweep_bf3 decides; MMRE_BF3_WIDE forces either
@@ -1418,7 +1442,11 @@ def main():
                      f" loss, SGD 1.0, margin 5, neg 25)" if "trained" in w else "") + \
                 f" over the real {w['dataset']} test triples; filter set = all test triples + 272,115 synthetic train"
         coll = "RCCL" if not dist or dist.get_backend() == "nccl" else "gloo rehearsal (every rank on cuda:0)"
-        out = {"metric": METRIC if args.config == "c2" else f"scored triples/sec, {cfg['workload']}",
+        metric = METRIC if args.config == "c2" else f"scored triples/sec, {cfg['workload']}"
+        if tc:
+            metric += " (type-constrained: Tester.run_link_prediction(type_constrain=True))"
+        grp = "filter_tc" if tc else "filter"
+        out = {"metric": metric,
                "value": value, "unit": "scored triples/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": data,
@@ -1432,10 +1460,12 @@ def main():
                                     (", two evaluation slots on two HIP streams (consecutive evaluations overlap)"
                                      if getattr(ev, "_streams", None) else "")},
                "roofline": roof,
-               "metrics": {"hit10": metrics["filter"]["hit10"], "hit3": metrics["filter"]["hit3"],
-                           "hit1": metrics["filter"]["hit1"], "mrr": metrics["filter"]["mrr"],
-                           "mr": metrics["filter"]["mr"]},
+               "metrics": {"group": grp, "hit10": metrics[grp]["hit10"], "hit3": metrics[grp]["hit3"],
+                           "hit1": metrics[grp]["hit1"], "mrr": metrics[grp]["mrr"], "mr": metrics[grp]["mr"]},
                "parity": None}
+        if tc:
+            out["data"] += ("; type_constrain.txt built from the filter set by the reference n-n.py's rule (each "
+                            "relation's known heads / tails)")
         if fst is not None and fst["kind"] == "l1q":
             pairs = int(n_local) * int(e_local)
             out["l1_filter"] = {"undecided_pairs": fst["undecided"],
@@ -1471,20 +1501,23 @@ def main():
             # rank 0 (itself checked against the reference Base.so at N = 1): bit-equal counts
             # mean bit-equal hit@k at this GPU count
             from mmre.link import evaluate_link_prediction
-            m1, (h1, t1) = evaluate_link_prediction(spec, w["test_h"], w["test_r"], w["test_t"], index=index)
+            m1, (h1, t1) = evaluate_link_prediction(spec, w["test_h"], w["test_r"], w["test_t"], index=index,
+                                                    type_constrain=tc)
             single = np.concatenate([h1, t1], 1)
+            rows = 4 if tc else 2
             out["parity"] = {"source": f"{args.shard}-sharded x{world} gathered counts vs a one-GPU evaluation of all "
                                        f"{2 * n} sweeps on rank 0",
                              "sweeps": 2 * n, "counts_bit_equal": bool(np.array_equal(np.asarray(counts), single)),
-                             "mismatched_sweeps": int((np.asarray(counts)[:2] != single[:2]).any(0).sum()),
-                             "metrics_bit_equal": all(metrics[g][k] == m1[g][k] for g in ("filter", "raw")
-                                                      for k in m1[g])}
+                             "mismatched_sweeps": int((np.asarray(counts)[:rows] != single[:rows]).any(0).sum()),
+                             "metrics_bit_equal": all(metrics[g][k] == m1[g][k] for g in
+                                                      (("filter", "raw", "filter_tc", "raw_tc") if tc else
+                                                       ("filter", "raw")) for k in m1[g])}
         if world == 1 and not args.no_cpu_baseline:
             ref = ref_tester_leg(w, args.cpu_sample or REF_SAMPLE[args.config])
             if ref is not None:
                 out["cpu_baseline"] = cpu_baseline_block(ref, w)
                 gs = sample_scores(spec, w, int(ref["n"]), dev)
-                out["parity"] = parity_block(ref, counts, n, w, gs)
+                out["parity"] = parity_block(ref, counts, n, w, gs, tc=tc)
                 del gs
         print(json.dumps(_with_build(out)), flush=True)
     if dist:

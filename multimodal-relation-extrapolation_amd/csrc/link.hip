@@ -969,11 +969,18 @@ struct ValuSmem {
   int32_t s_true[2][TQ];
   int32_t s_rel[2][TC ? TQ : 1];
   int8_t s_mode[2][TC ? TQ : 1];
-  int32_t s_cnt[TC ? 2 : 1][8][NT];  // per-thread counters (off the VGPR budget)
+  // per-thread counters (off the VGPR budget); 16-bit with type constraints, so that the wave
+  // lists fit beside them at four workgroups per CU (a thread adds <= 8 per unit and row; the
+  // sweep flushes every unit where a query tile could hold more than 8,190 of a workgroup's units)
+  std::conditional_t<TC, uint16_t, int32_t> s_cnt[TC ? 2 : 1][8][NT];
   uint32_t s_unc[NT / 64];           // undecided pairs per wave (the L1 filter's counter)
   uint32_t s_ts[2][TQ];              // L1 filter, prediction = score: per query row, the integer
   uint32_t s_tw[2][TQ];              // thresholds t_sure and t_out - t_sure (load_meta)
   int s_unit;                        // dynamic scheduling: the unit after the one being swept
+  // type constraints: per unit (two in flight, by unit parity), the type words of its 128 query
+  // rows over its 128 entity columns -- words 0, 2, 1, 3 of the tile, so a thread's two words
+  // (columns 4te.., 64 + 4te..) are one 8-B read -- staged with the unit's first stage
+  uint32_t s_tb[TC ? 2 : 1][TC ? TQ : 1][4];
   int2 s_pairs[LIST ? NT / 64 : 1][LIST ? 128 : 1];  // L1 filter: each wave's undecided (query, entity) pairs
 };
 
@@ -982,7 +989,7 @@ struct ValuSmem {
 // receive them in k_counts_finalize, one coalesced pass after the sweep (half the atomics).
 template <int OP, bool TC, bool STORE, int PK, int NPL, int DYNC>
 __device__ __forceinline__ void sweep_valu_body(
-    ValuSmem<NPL, TC, (OP == 5 || OP == 6) && !TC>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
+    ValuSmem<NPL, TC, (OP == 5 || OP == 6)>& sm, const float* __restrict__ ent_km, int64_t e_pad, int64_t n_ent,
     const float* __restrict__ q_km, int64_t q_pad, int64_t n_query, int kp, int n_et, int e_base, int n_groups,
     int pred_kind, float margin, const float* __restrict__ thr, const int32_t* __restrict__ qtrue,
     const int64_t* __restrict__ qr, const int8_t* __restrict__ qmode, const uint32_t* __restrict__ type_head,
@@ -1081,7 +1088,32 @@ __device__ __forceinline__ void sweep_valu_body(
   // staging position (unit, kc) of the next load, advanced incrementally (no divisions)
   int ld_unit = u0, ld_kc = 0, ld_qt, ld_et;
   um.at(u0, ld_qt, ld_et);
+  // type constraints: the staged unit's type words (row tid / 2, words (tid & 1) and 2 + (tid & 1)),
+  // whether the pending stage carries them, and the unit parity they go to (the epilogue's
+  // ep_par reads them back); the loader's parity starts at 1 so that unit u0 gets 0
+  uint32_t rt0 = 0u, rt1 = 0u;
+  bool st_new = false;
+  int ld_tpar = 1, st_par = 0, ep_par = 0;
   auto gload = [&]() {
+    if constexpr (TC) {
+      st_new = ld_kc == 0;
+      if (st_new) {  // the unit's first stage: its rows' type words ride along
+        ld_tpar ^= 1;
+        st_par = ld_tpar;
+        const int tt = vgpr_opaque(threadIdx.x);
+        const int rr = tt >> 1, jw = tt & 1;
+        const int64_t q = (int64_t)ld_qt * TQ + rr;
+        uint32_t w0 = 0u, w1 = 0u;
+        if (q < n_query) {
+          const uint32_t* tm = (qmode[q] == MMRE_HEAD_BATCH ? type_head : type_tail) + qr[q] * type_words;
+          const int64_t wb = (e_base + (int64_t)ld_et * TE) >> 5;  // e_base and tiles: whole words
+          if (wb + jw < type_words) w0 = tm[wb + jw];
+          if (wb + 2 + jw < type_words) w1 = tm[wb + 2 + jw];
+        }
+        rt0 = w0;
+        rt1 = w1;
+      }
+    }
     const int k = ld_kc * KC + srow;
     const int64_t q0 = (int64_t)ld_qt * TQ, e0 = (int64_t)ld_et * TE;
     const float* qp = q_km + (int64_t)k * q_pad + q0 + sc4 * 4;
@@ -1104,6 +1136,12 @@ __device__ __forceinline__ void sweep_valu_body(
     }
   };
   auto swrite = [&](int buf) {
+    if constexpr (TC) {
+      if (st_new) {
+        const int tt = vgpr_opaque(threadIdx.x);
+        *reinterpret_cast<uint2*>(&sm.s_tb[st_par][tt >> 1][(tt & 1) * 2]) = make_uint2(rt0, rt1);
+      }
+    }
     sq[buf][0][srow][sc4] = rq0;
     se[buf][0][srow][sc4] = re0;
     if constexpr (NPL == 2) {
@@ -1134,9 +1172,9 @@ __device__ __forceinline__ void sweep_valu_body(
   // per lane-pair with the wave waiting on its busiest lane (which made the 8-bit codes' 0.4 %
   // of undecided pairs cost 0.8 ms at C2). Rescored pairs that beat their threshold go straight
   // to the raw count columns (the query tile's counts may have been flushed already).
-  // (Type-constrained sweeps keep the per-lane loop: the list's 4 KB would push their LDS past
-  // four workgroups per CU.)
-  constexpr bool LIST = L1F && !TC;
+  // (Type-constrained sweeps too, since round 6: 16-bit LDS counters make room for the list at
+  // four workgroups per CU; their per-lane loop kept 232-240 B of scratch per lane.)
+  constexpr bool LIST = L1F;
   int list_n = 0;         // wave-uniform
   uint32_t n_listed = 0;  // the wave's undecided pairs (the filter's counter; per lane without the list)
   auto rescore = [&](int2 p) {
@@ -1272,6 +1310,13 @@ __device__ __forceinline__ void sweep_valu_body(
       if (kc == nkc - 1) {  // unit finished: rank epilogue
         const int64_t q0 = (int64_t)cur_qt * TQ;
         const int64_t ebase = (int64_t)cur_et * TE;
+        // type constraints: this thread's 8 type bits of query row ql (bit j = column j), from the
+        // unit's staged words
+        auto tbits = [&](int ql) -> uint32_t {
+          const uint2 w = *reinterpret_cast<const uint2*>(&sm.s_tb[TC ? ep_par : 0][TC ? ql : 0][(te >> 3) * 2]);
+          const int sh = (te & 7) * 4;
+          return ((w.x >> sh) & 15u) | (((w.y >> sh) & 15u) << 4);
+        };
         if constexpr (FAST) {
           if constexpr (OP == 2) {  // unpack the pair layout (register renames) and restart it
 #pragma unroll
@@ -1306,17 +1351,22 @@ __device__ __forceinline__ void sweep_valu_body(
               for (int i = 0; i < 8; ++i) {
                 const int ql = (i < 4) ? tq * 4 + i : 64 + tq * 4 + (i - 4);
                 const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
-                int c = 0;
+                // type constraints: the row's 8 type bits (a pair below t_sure is never the truth)
+                const uint32_t tb = TC ? tbits(ql) : 0u;
+                int c = 0, cc = 0;
                 uint32_t u = unc[i >> 2];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                   const uint32_t si = __float_as_uint(acc[i][j]);
                   const uint32_t d = si - t_sure;
-                  c += si < t_sure;
+                  const bool sure = si < t_sure;
+                  c += sure;
+                  if constexpr (TC) cc += sure & ((tb >> j) & 1u);
                   u = u + u + (uint32_t)(d < t_span);
                 }
                 unc[i >> 2] = u;
                 s_cnt[0][i][tid] += c;
+                if constexpr (TC) s_cnt[TC ? 1 : 0][i][tid] += cc;
               }
             }
           }
@@ -1327,9 +1377,7 @@ __device__ __forceinline__ void sweep_valu_body(
             const float th = s_thr[slot][ql];
             const int32_t tr = s_true[slot][ql];
             int c = 0, cc = 0;
-            const uint32_t tb = TC ? type_bits8(s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail, type_words,
-                                                s_rel[slot][ql], (int)(e_base + ebase) + te * 4, (int)(e_base + n_ent))
-                                   : 0u;
+            const uint32_t tb = TC ? tbits(ql) : 0u;
             if constexpr (L1F && PK == 0) {
               // prediction = the score: the integer thresholds of load_meta
               const uint32_t t_sure = sm.s_ts[slot][ql], t_span = sm.s_tw[slot][ql];
@@ -1476,9 +1524,7 @@ __device__ __forceinline__ void sweep_valu_body(
           const float th = s_thr[slot][ql];
           const int32_t tr = s_true[slot][ql];
           int c = 0, cc = 0;
-          const uint32_t tb = TC ? type_bits8(s_mode[slot][ql] == MMRE_HEAD_BATCH ? type_head : type_tail, type_words,
-                                              s_rel[slot][ql], (int)(e_base + ebase) + te * 4, (int)(e_base + n_ent))
-                                 : 0u;
+          const uint32_t tb = TC ? tbits(ql) : 0u;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             // 32-bit ids (int32 by check_link_args); bitwise &: no per-pair branch
@@ -1500,7 +1546,8 @@ __device__ __forceinline__ void sweep_valu_body(
         const bool last = unit_next >= u1;
         int next_qt = cur_qt, next_et = cur_et;
         if (!last) um.at(unit_next, next_qt, next_et);
-        if (last || next_qt != cur_qt) {  // uniform: flush this query tile's counts
+        // (TC: 16-bit counters -- flush every unit where a group's query tile could exceed them)
+        if (last || next_qt != cur_qt || (TC && n_et > 8 * 8190)) {  // uniform: flush this query tile's counts
           const int tid = vgpr_opaque(threadIdx.x);  // (see load_meta)
           const int tq = tid >> 4, te = tid & 15;
 #pragma unroll
@@ -1532,6 +1579,7 @@ __device__ __forceinline__ void sweep_valu_body(
         // here, after the accumulators were reset, where the claim costs no registers
         if (dyn && !last && ((unit_next + 1) & ch_mask) == 0 && threadIdx.x == 0)
           sm.s_unit = (per_grp + (int)atomicAdd(&l1.wq[grp * L1Q_WQ_STRIDE], 1u)) << ch_log2;
+        if constexpr (TC) ep_par ^= 1;  // the next unit's staged type words
         cur_qt = next_qt;
         cur_et = next_et;
       }
@@ -1568,7 +1616,7 @@ __global__ __launch_bounds__(NT, (OP == 2) ? 3 : 4) void k_sweep_valu(
     const uint32_t* __restrict__ type_tail, int64_t type_words, int32_t* __restrict__ counts,
     float* __restrict__ scores, L1Q l1) {
   constexpr int NPL = (OP == 2) ? 2 : 1;
-  __shared__ ValuSmem<NPL, TC, (OP == 5 || OP == 6) && !TC> sm;
+  __shared__ ValuSmem<NPL, TC, (OP == 5 || OP == 6)> sm;
   // the L1 filter's fallback (k_l1q_quant decided that the codes are too coarse for these
   // planes -- one outlier value sets the code step for everything): the filter launch does
   // nothing (sweep_valu_body tests the flag once its first stage is loaded, so the flag's load

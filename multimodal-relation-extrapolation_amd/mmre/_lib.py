@@ -41,6 +41,8 @@ SIGNATURES = {
     "mmre_link_bf3_stats": (I32, [P, I64, P, P]),
     "mmre_link_sweep_bf3": (I32, [I32, I32, F32, P, P, I64, I64, I64, I64, P, P, P, P, P, I64, I64, I32, P, P, P,
                                   I64, P]),
+    "mmre_link_sweep_bf3_rows": (I32, [I32, I32, F32, P, I64, I64, I64, I64, P, P, P, P, P, P, I64, I64, I32, P, P,
+                                       P, I64, P]),
     "mmre_link_metrics": (I32, [P, P, I64, I64, P]),
     "mmre_glibc_rand": (I32, [I64, I64, P]),
     "mmre_sampler_advance": (I32, [P, I64, I64, I64, I64, I64]),

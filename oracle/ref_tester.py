@@ -203,6 +203,16 @@ def prepare_workdir(workdir: str, w: dict, th, tr, tt, **meta_extra):
     for name, cnt in (("entity2id.txt", w["n_ent"]), ("relation2id.txt", w["n_rel"])):
         with open(os.path.join(workdir, name), "w") as f:
             f.write(f"{cnt}\n")
+    if w.get("type_heads") is not None:
+        # type_constrain.txt as importTypeFiles (Reader.h:267-317) reads it: the relation count,
+        # then per relation (every one, in order) a head line and a tail line "r n e1 .. en"
+        with open(os.path.join(workdir, "type_constrain.txt"), "w") as f:
+            f.write(f"{w['n_rel']}\n")
+            for r in range(int(w["n_rel"])):
+                for lists in (w["type_heads"], w["type_tails"]):
+                    ids = [int(x) for x in lists[r]]
+                    f.write(f"{r}\t{len(ids)}" + "".join(f"\t{e}" for e in ids) + "\n")
+        meta_extra = dict(meta_extra, type_constrain=True)
     as_np = lambda v: v.numpy() if hasattr(v, "numpy") else np.asarray(v)
     tables = {"ent": as_np(w["ent"]), "rel": as_np(w["rel"])}
     if "ent_im" in w:
@@ -237,14 +247,17 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
         getattr(lib, g).restype = ctypes.c_float
     lib.getEntityTotal.restype = I
     lib.getTestTotal.restype = I
+    tc = bool(meta.get("type_constrain", False))  # Test.h's type-constrained counters too
     with stdout_to_stderr():
         lib.setInPath((workdir.rstrip("/") + "/").encode())
         lib.importTrainFiles()
         lib.importTestFiles()
+        if tc:
+            lib.importTypeFiles()
         lib.initTest()
     E, n = int(lib.getEntityTotal()), int(lib.getTestTotal())
     ph, pt, pr = (np.zeros(E, np.int64) for _ in range(3))
-    counts = np.zeros((2, n, 2), np.int64)       # [head|tail][query][raw, filt]
+    counts = np.zeros((2, n, 4 if tc else 2), np.int64)  # [head|tail][query][raw, filt(, raw_tc, filt_tc)]
     q = np.zeros((n, 3), np.int64)               # (h, r, t) as Base.so's testList holds them
     summary = bool(meta.get("summary", False))
     near_rel = float(meta.get("near_rel", 1e-5))
@@ -266,6 +279,8 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             near_cnt[side, idx] = len(j)
 
     keys = (("l_rank", "l_filter_rank"), ("r_rank", "r_filter_rank"))
+    if tc:
+        keys = tuple(k + (f"{s}_rank_constrain", f"{s}_filter_rank_constrain") for k, s in zip(keys, ("l", "r")))
     t_keep = 0.0
     t_idx = np.zeros(n, np.float64)  # per test triple (both sweeps), the fixture bookkeeping excluded
     t0 = time.perf_counter()
@@ -276,7 +291,7 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             s = np.ascontiguousarray(predict(torch.from_numpy(ph), torch.from_numpy(pt[:1]),
                                              torch.from_numpy(pr[:1]), "head_batch"), np.float32)
             before = [_fglob(lib, k) for k in keys[0]]
-            lib.testHead(s.ctypes.data, idx, 0)
+            lib.testHead(s.ctypes.data, idx, int(tc))
             counts[0, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[0], before)]
             q[idx, 1], q[idx, 2] = pr[0], pt[0]
             head_s = s
@@ -284,7 +299,7 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             s = np.ascontiguousarray(predict(torch.from_numpy(ph[:1]), torch.from_numpy(pt),
                                              torch.from_numpy(pr[:1]), "tail_batch"), np.float32)
             before = [_fglob(lib, k) for k in keys[1]]
-            lib.testTail(s.ctypes.data, idx, 0)
+            lib.testTail(s.ctypes.data, idx, int(tc))
             counts[1, idx] = [round(_fglob(lib, k) - b) - 1 for k, b in zip(keys[1], before)]
             q[idx, 0] = ph[0]
             k0 = time.perf_counter()
@@ -292,10 +307,11 @@ def run_tester(workdir: str, base_so: str = REF_BASE_SO, tie_rel: float = 1e-4):
             keep(0, idx, head_s, int(q[idx, 0]))   # the head sweep's truth is the tail batch's anchor
             keep(1, idx, s, int(q[idx, 2]))
             t_keep += time.perf_counter() - k0
-        lib.test_link_prediction(0)
+        lib.test_link_prediction(int(tc))
         elapsed = time.perf_counter() - t0 - t_keep
-        metrics = np.array([lib.getTestLinkMRR(0), lib.getTestLinkMR(0), lib.getTestLinkHit10(0),
-                            lib.getTestLinkHit3(0), lib.getTestLinkHit1(0)], np.float32)
+        g = int(tc)  # getTestLink*(type_constrain): the type-constrained filtered metrics when tc
+        metrics = np.array([lib.getTestLinkMRR(g), lib.getTestLinkMR(g), lib.getTestLinkHit10(g),
+                            lib.getTestLinkHit3(g), lib.getTestLinkHit1(g)], np.float32)
     if not all(math.isfinite(float(m)) for m in metrics):
         raise RuntimeError("Base.so returned non-finite metrics")
     out = dict(counts=counts, q=q, metrics=metrics, elapsed=np.float64(elapsed), t_idx=t_idx,
@@ -367,18 +383,21 @@ def run_parallel(w: dict, th, tr, tt, procs: int, timeout_s: float | None = None
         for tmp in tmps:
             shutil.rmtree(tmp, ignore_errors=True)
 
-    def tc4(c):  # (2, m, 2) [raw, filt] -> the oracle's (m, 4) per side
+    def tc4(c):  # (2, m, 2) [raw, filt] (or (2, m, 4) with the type-constrained pair) -> the oracle's (m, 4)
+        if c.shape[2] == 4:
+            return [c[0], c[1]]
         z = np.zeros((c.shape[1], 4), np.int64)
         return [np.concatenate([c[s], z[:, :2]], 1) for s in (0, 1)]
 
+    grp = "filter_tc" if parts[0]["counts"].shape[2] == 4 else "filter"
     for c, p in enumerate(parts):
-        m = orc.link_metrics(*tc4(p["counts"]))["filter"]
+        m = orc.link_metrics(*tc4(p["counts"]))[grp]
         mine = np.array([m[k] for k in orc.METRIC_NAMES], np.float32)
         if not np.array_equal(mine.view(np.uint32), p["metrics"].astype(np.float32).view(np.uint32)):
             raise RuntimeError(f"chunk {c}: the oracle's metric reduction {mine} differs from Base.so's {p['metrics']}")
     cat1 = lambda k: np.concatenate([p[k] for p in parts], axis=1)
     counts = cat1("counts")
-    m = orc.link_metrics(*tc4(counts))["filter"]
+    m = orc.link_metrics(*tc4(counts))[grp]
     out = dict(counts=counts, q=np.concatenate([p["q"] for p in parts]),
                metrics=np.array([m[k] for k in orc.METRIC_NAMES], np.float32),
                chunk_metrics=np.stack([p["metrics"] for p in parts]), chunk_n=np.diff(bounds),

@@ -35,7 +35,7 @@ def _workload(model, n_ent=300, n_rel=7, n_test=60, n_train=2000, dim=24, seed=0
     return w
 
 
-def _oracle_counts(oracle_mod, w):
+def _oracle_counts(oracle_mod, w, types=False):
     kw = {}
     if w["model"] == "transe":
         kw = dict(norm_flag=True)
@@ -49,7 +49,12 @@ def _oracle_counts(oracle_mod, w):
     for mode in ("head_batch", "tail_batch"):
         p = oracle_mod.link_predict(w["model"], mode, ent, rel, w["test_h"], w["test_r"], w["test_t"], ent_im=ei,
                                     rel_im=ri, **kw)
-        out.append(oracle_mod.test_rank(mode, p, w["test_h"], w["test_r"], w["test_t"], hrt).T)
+        tk = {}
+        if types:  # CSR per relation (Test.h's head_type / tail_type ranges, sorted)
+            lists = w["type_heads" if mode == "head_batch" else "type_tails"]
+            tk = dict(type_off=np.r_[0, np.cumsum([len(x) for x in lists])],
+                      type_ids=np.concatenate([np.sort(np.asarray(x, np.int64)) for x in lists]))
+        out.append(oracle_mod.test_rank(mode, p, w["test_h"], w["test_r"], w["test_t"], hrt, **tk).T)
         scores.append(p)
     # (4, 2n) counts: head block then tail block; the oracle's scores are the GPU's bit for bit
     return np.concatenate(out, 1).astype(np.int32), scores
@@ -61,9 +66,10 @@ def test_ref_leg_and_parity_block(oracle_mod, model, n_sample):
     import bench
     w = _workload(model)
     counts, sc = _oracle_counts(oracle_mod, w)
-    ref = bench.ref_tester_leg(w, n_sample)
+    ref = bench.ref_tester_leg(w, n_sample, reps=2)
     assert ref is not None
     assert ref["counts"].shape == (2, n_sample, 2)
+    assert len(ref["elapsed_reps"]) == 2
     par = bench.parity_block(ref, counts, len(w["test_h"]), w,
                              torch.from_numpy(np.concatenate([sc[0][:n_sample], sc[1][:n_sample]])))
     assert par["window_ok"], par   # the measured error is far inside the near-tie window
@@ -75,13 +81,14 @@ def test_ref_leg_and_parity_block(oracle_mod, model, n_sample):
         assert par["metrics_bit_equal"], par   # Test.h reduction of equal counts: bit-identical metrics
     cpu = bench.cpu_baseline_block(ref, w)
     assert cpu["kind"] == "reference" and cpu["value"] > 0
+    assert cpu["value_min"] <= cpu["value"] <= cpu["value_max"] and cpu["reps"] == 2
 
 
 def test_parity_block_reports_a_planted_mismatch(oracle_mod):
     import bench
     w = _workload("distmult")
     counts, sc = _oracle_counts(oracle_mod, w)
-    ref = bench.ref_tester_leg(w, 60)
+    ref = bench.ref_tester_leg(w, 60, reps=1)
     bad = counts.copy()
     bad[1, 3] += 5     # filtered head count of query 3
     bad[0, 60 + 7] += 2  # raw tail count of query 7
@@ -89,3 +96,30 @@ def test_parity_block_reports_a_planted_mismatch(oracle_mod):
     assert par["filt_mismatches"] >= 1 and par["raw_mismatches"] >= 1
     assert par["unexplained_mismatches"] >= 1
     assert not par["metrics_bit_equal"]
+
+
+@pytest.mark.parametrize("model", ["transe", "distmult"])
+def test_ref_leg_type_constrained(oracle_mod, model):
+    """The type-constrained leg (bench.py --type-constrain): ref_tester writes type_constrain.txt
+    (Reader.h:267-317's format), runs testHead / testTail with type_constrain and reads Base.so's
+    *_constrain counters; they equal the oracle's Test.h restatement, and parity_block(tc=True)
+    compares the constrained columns."""
+    import bench
+    w = _workload(model)
+    rng = np.random.default_rng(5)
+    n_ent, n_rel = w["n_ent"], w["n_rel"]
+    # per relation: the heads / tails of its known triples (n-n.py's rule) plus random extras
+    fh, fr, ft = (np.asarray(w[k]) for k in ("filter_h", "filter_r", "filter_t"))
+    w["type_heads"] = [np.unique(np.r_[fh[fr == r], rng.integers(0, n_ent, 20)]) for r in range(n_rel)]
+    w["type_tails"] = [np.unique(np.r_[ft[fr == r], rng.integers(0, n_ent, 20)]) for r in range(n_rel)]
+    counts, sc = _oracle_counts(oracle_mod, w, types=True)
+    ref = bench.ref_tester_leg(w, 40, reps=1)
+    assert ref is not None and ref["counts"].shape == (2, 40, 4)
+    par = bench.parity_block(ref, counts, len(w["test_h"]), w,
+                             torch.from_numpy(np.concatenate([sc[0][:40], sc[1][:40]])), tc=True)
+    assert par["window_ok"] and par["unexplained_mismatches"] == 0, par
+    if par["filt_mismatches"] == 0:
+        assert par["metrics_bit_equal"], par
+    # the constrained counts are not the unconstrained ones (the types exclude entities)
+    assert (ref["counts"][:, :, 2] <= ref["counts"][:, :, 0]).all()
+    assert (ref["counts"][:, :, 2] < ref["counts"][:, :, 0]).any()
