@@ -4209,11 +4209,13 @@ static void launch_bf3w(hipStream_t st, const uint4* eb, int64_t e_pad, int64_t 
   const int64_t units = (q_pad / QT) * (int64_t)n_etw;
   int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;
   int bq = 0, be = 0;
-  if (blocked && n_etw >= 8 && res % 8 == 0) {
-    g = res;
-    bf3_window(res / 8, (int)(q_pad / QT), n_etw / 8, bq, be);
-  }
+  const bool blk = blocked && n_etw >= 8 && res % 8 == 0;
+  if (blk) g = res;
   if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);
+  if (blk) {  // the windows of the grid actually launched (an env grid: a multiple of 8)
+    g = std::max(8, g & ~7);
+    bf3_window(g / 8, (int)(q_pad / QT), n_etw / 8, bq, be);
+  }
   if (g < 1) g = 1;
   const int ng = (g % 8 == 0 && n_etw >= 8) ? 8 : 1;
   hipLaunchKernelGGL((k_sweep_bf3w<2, QT>), dim3((unsigned)g), dim3(G::NT), 0, st, eb, e_pad, e_cols, n_slice, qb,
@@ -4307,11 +4309,14 @@ static int sweep_bf3_impl(int model, int pred_kind, float margin, float* d_ent_k
     const int64_t units = (q_pad / TQ) * (int64_t)n_et;                                                        \
     int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;              \
     int bq = 0, be = 0;                                                                                        \
-    if (blocked && n_et >= 8 && res % 8 == 0) { /* the lock-step windows: one resident wave of workgroups */  \
-      g = res;                                                                                                  \
-      bf3_window(res / 8, (int)(q_pad / TQ), n_et / 8, bq, be);                                                \
-    }                                                                                                           \
+    const bool blk = blocked && n_et >= 8 && res % 8 == 0;                                                    \
+    if (blk) g = res; /* the lock-step windows: one resident wave of workgroups */                            \
     if (grid_env && grid_env[0] >= '1' && grid_env[0] <= '9') g = atoi(grid_env);                           \
+    if (blk) { /* the windows of the grid actually launched (an env grid: a multiple of 8) */                  \
+      g &= ~7;                                                                                                 \
+      if (g < 8) g = 8;                                                                                        \
+      bf3_window(g / 8, (int)(q_pad / TQ), n_et / 8, bq, be);                                                  \
+    }                                                                                                           \
     const int ng = (g % 8 == 0 && n_et >= 8) ? 8 : 1;                                                          \
     hipLaunchKernelGGL((k_sweep_bf3<PKV>), dim3((unsigned)g), dim3(NT), 0, st, eb, e_pad, n_slice, qb, q_pad,   \
                        n_query, ktot / 16, n_et, (int)e_begin, ng, pred_kind, margin, d_truth, qn, en, cb,     \
