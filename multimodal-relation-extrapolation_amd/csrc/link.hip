@@ -2312,7 +2312,18 @@ static int l1q_rows8(int dim) { return (int)round_up((plane_rows(MMRE_TRANSE_L1,
 // Workspace: header (BF3_HDR bytes: word 1 overflow flag, words 2-3 the appended pairs (uint64)) | pair list
 // (bf3_cap int2) | |q| (q_pad floats) | |e| (e_pad floats) | split query planes (K/16 blocks
 // x q_pad rows x 64 B: hi[16] | lo[16]) | split entity planes (K/16 x e_pad x 64 B).
-constexpr int BF3_HDR = 256;
+// The list: half of it cut into BF3_SEGS segments of cap / (2 BF3_SEGS) pairs, each with its own
+// counter on a 128-B line of the header (32-bit words BF3_SEG_W0 + 32 s), the other half shared
+// (its counter: segment index BF3_SEGS). A sweep workgroup b appends to segment b % BF3_SEGS and,
+// once that is full, to the shared half (bf3_list). One counter for the whole list serialised
+// every append chip-wide (~13 ns per same-address atomic): C3's 46 k listed pairs ~0.35 of a
+// 0.74-ms sweep (a build with the decision pass compiled out ran 0.39 ms); the shared half keeps
+// a burst of one workgroup (a non-finite row's pairs) from overflowing its segment. A full shared
+// half sets the overflow flag (word 1): the exact sweep then counts, as for a full list before.
+// A counter that wraps (> 4 G appends) cannot clear the flag its first overflow set.
+constexpr int BF3_SEGS = 64;
+constexpr int BF3_SEG_W0 = 64;
+constexpr int BF3_HDR = 4 * (BF3_SEG_W0 + 32 * (BF3_SEGS + 1));
 #ifndef BF3_WG_PER_CU
 #define BF3_WG_PER_CU 3  // workgroups per CU the sweep is compiled for (168 VGPRs)
 #endif
@@ -2324,6 +2335,21 @@ inline int64_t bf3_cap(int64_t q_pad, int64_t e_pad) {
   return c > (1 << 26) ? (1 << 26) : c;
 }
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+// append one undecided pair to the calling workgroup's segment of the list, or to the shared
+// half when the segment is full (see BF3_SEGS)
+__device__ __forceinline__ void bf3_list(uint32_t* __restrict__ hdr, int2* __restrict__ pairs, int64_t cap, int2 p) {
+  const int sgm = (int)(blockIdx.x & (BF3_SEGS - 1));
+  const int64_t seg_cap = cap / (2 * BF3_SEGS);
+  const uint32_t i = atomicAdd(hdr + BF3_SEG_W0 + 32 * sgm, 1u);
+  if ((int64_t)i < seg_cap) {
+    pairs[sgm * seg_cap + i] = p;
+    return;
+  }
+  const uint32_t j = atomicAdd(hdr + BF3_SEG_W0 + 32 * BF3_SEGS, 1u);
+  if ((int64_t)j < cap - BF3_SEGS * seg_cap) pairs[BF3_SEGS * seg_cap + j] = p;
+  else hdr[1] = 1u;
+}
 
 __device__ __forceinline__ uint32_t bf16_rn_bits(float x) {  // finite x: round to nearest even
   const uint32_t u = __float_as_uint(x);
@@ -2664,13 +2690,7 @@ __global__ __launch_bounds__(NT, BF3_WG_PER_CU) void k_sweep_bf3(
 #pragma unroll
                 for (int bj = 0; bj < 2; ++bj) {
                   if (!((mund[bj] >> ol) & 1ull)) continue;
-                  // a 64-bit counter (header words 2-3): a non-finite table can make every pair
-                  // undecided (1.6e10 at C5), which would wrap a 32-bit one. (A check-then-add
-                  // -- an sc1 load of the counter before each add -- made C3 3x slower: the loads
-                  // queue behind every workgroup's atomics on that one address.)
-                  const unsigned long long i = atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 2), 1ull);
-                  if (i < (unsigned long long)cap) pairs[i] = make_int2((int)q, (int)((bj ? e1 : e0) + e_base));
-                  else hdr[1] = 1u;
+                  bf3_list(hdr, pairs, cap, make_int2((int)q, (int)((bj ? e1 : e0) + e_base)));
                 }
               }
             }
@@ -2972,13 +2992,9 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
             // (the lane's query and entity from an opaque lane id: recomputed here, not 64 indices
             // kept live across the sweep)
             const int ol = vgpr_opaque(lane);
-            if (!((um >> ol) & 1ull)) continue;
             const int64_t q = q0 + wq * 64 + bj * 32 + (ol & 31);
-            if (q >= n_query) continue;
-            // a 64-bit counter (header words 2-3), as k_sweep_bf3's
-            const unsigned long long i = atomicAdd(reinterpret_cast<unsigned long long*>(hdr + 2), 1ull);
-            if (i < (unsigned long long)cap) pairs[i] = make_int2((int)q, (int)(ebase + row0 + 4 * (ol >> 5) + e_base));
-            else hdr[1] = 1u;
+            if (((um >> ol) & 1ull) && q < n_query)
+              bf3_list(hdr, pairs, cap, make_int2((int)q, (int)(ebase + row0 + 4 * (ol >> 5) + e_base)));
           }
         }
       }
@@ -3098,10 +3114,16 @@ __global__ __launch_bounds__(256) void k_bf3_rescore(const uint32_t* __restrict_
                                                      int32_t* __restrict__ counts) {
   if (hdr[1] != 0u) return;  // overflow: the exact sweep counted everything
   const PredSel<PK> pred(pred_kind, margin);
-  const unsigned long long listed = *reinterpret_cast<const unsigned long long*>(hdr + 2);
-  const int64_t n = listed < (unsigned long long)cap ? (int64_t)listed : cap;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int2 p = pairs[i];
+  // gridDim.x / (BF3_SEGS + 1) workgroups per segment; segment BF3_SEGS: the shared half
+  const int sgm = (int)(blockIdx.x % (BF3_SEGS + 1)), part = (int)(blockIdx.x / (BF3_SEGS + 1));
+  const int parts = (int)(gridDim.x / (BF3_SEGS + 1));
+  const int64_t seg_cap = cap / (2 * BF3_SEGS);
+  const int64_t scap = sgm < BF3_SEGS ? seg_cap : cap - BF3_SEGS * seg_cap;
+  const int64_t listed = hdr[BF3_SEG_W0 + 32 * sgm];
+  const int64_t n = listed < scap ? listed : scap;
+  const int2* seg = pairs + sgm * seg_cap;
+  for (int64_t i = (int64_t)part * blockDim.x + threadIdx.x; i < n; i += (int64_t)parts * blockDim.x) {
+    const int2 p = seg[i];
     const float4* a = reinterpret_cast<const float4*>(q_rows + (int64_t)p.x * ktot);
     const float4* b = reinterpret_cast<const float4*>(ent_rows + (int64_t)p.y * ktot);
     float acc = 0.0f;
@@ -3117,9 +3139,25 @@ __global__ __launch_bounds__(256) void k_bf3_rescore(const uint32_t* __restrict_
   }
 }
 
+// the list header zeroed, with word 4 = the segment capacity (read by k_bf3_stats)
+__global__ __launch_bounds__(256) void k_bf3_hdr_init(uint32_t* __restrict__ hdr, int64_t cap) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < BF3_HDR / 4; i += gridDim.x * blockDim.x)
+    hdr[i] = i == 4 ? (uint32_t)(cap / (2 * BF3_SEGS)) : 0u;
+}
+
 __global__ void k_bf3_stats(const uint32_t* __restrict__ hdr, unsigned long long* __restrict__ out) {
+  // one wave: the pairs listed = the segments' kept appends + the shared half's appends (a full
+  // segment's further appends are counted there; past the shared half's end: the fallback ran)
+  const int64_t seg_cap = hdr[4];
+  unsigned long long t = 0;
+  if (threadIdx.x < BF3_SEGS) {
+    const unsigned long long c = hdr[BF3_SEG_W0 + 32 * threadIdx.x];
+    t = c < (unsigned long long)seg_cap ? c : (unsigned long long)seg_cap;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
   if (threadIdx.x == 0) {
-    out[0] = *reinterpret_cast<const unsigned long long*>(hdr + 2);
+    out[0] = t + hdr[BF3_SEG_W0 + 32 * BF3_SEGS];
     out[1] = hdr[1];
   }
 }
@@ -3186,9 +3224,11 @@ static void launch_valu_one(hipStream_t st, const float* ent_km, int64_t e_pad, 
     // Dynamic scheduling of a small share: as many workgroups per XCD group as make its units an
     // (almost) whole number of rounds -- the same rounds as the full grid, no nearly empty last
     // round (an 8-way C2 share: 527 units per group over 128 workgroups = 4.1 rounds, the fifth
-    // run by 15 of them; over 106 workgroups, 5 rounds). MMRE_SWEEP_BALANCE=0: the full grid (A/B).
+    // run by 15 of them; over 106 workgroups, 5 rounds). Measured no faster on 8-way C2 shares
+    // (ranks 1 / 3 / 7: 0.190 / 0.203 / 0.199 against 0.185 / 0.193 / 0.196 ms, profiles/r6): off
+    // unless MMRE_SWEEP_BALANCE=1 (A/B).
     static const char* bal_env = getenv("MMRE_SWEEP_BALANCE");
-    if (dyn && g % 8 == 0 && n_et >= 8 && !(bal_env && bal_env[0] == '0')) {
+    if (dyn && g % 8 == 0 && n_et >= 8 && bal_env && bal_env[0] == '1') {
       const int64_t per_group = (q_tiles * n_et + 7) / 8;  // UnitMap: every group within +-1 of this
       const int64_t slots = g / 8;
       const int64_t rounds = (per_group + slots - 1) / slots;
@@ -4259,7 +4299,8 @@ static int sweep_bf3_impl(int model, int pred_kind, float margin, float* d_ent_k
   const double K = (double)ktot;
   const float cb = (float)(1.02 * (7.0 * K * std::ldexp(1.0, -24) * (1.0 + std::ldexp(1.0, -7)) +
                                    3.02 * std::ldexp(1.0, -16) + std::ldexp(1.0, -29) * std::sqrt(K)));
-  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(64), 0, st, hdr, 4);
+  static_assert(BF3_SEGS == 64, "k_bf3_stats sums one segment per lane of a wave");
+  hipLaunchKernelGGL(k_bf3_hdr_init, dim3((BF3_HDR / 4 + 255) / 256), dim3(256), 0, st, hdr, cap);
   const int nkb = ktot / 16;
   hipLaunchKernelGGL(k_bf3_split, dim3((unsigned)((q_pad * nkb + 255) / 256)), dim3(256), 0, st, d_q_km, q_pad,
                      (int64_t)0, q_pad, nkb, qb, q_pad);
@@ -4335,7 +4376,8 @@ static int sweep_bf3_impl(int model, int pred_kind, float margin, float* d_ent_k
                 d_q_km, q_pad, n_query, ktot, d_truth, nullptr, nullptr, nullptr, nullptr, 0, d_counts,        \
                 nullptr, st, hdr + 1);                                                                         \
     MMRE_CHECK_LAUNCH();                                                                                       \
-    hipLaunchKernelGGL((k_bf3_rescore<PKV>), dim3(1024), dim3(256), 0, st, hdr, pairs, cap, d_q_rows,          \
+    hipLaunchKernelGGL((k_bf3_rescore<PKV>), dim3(16 * (BF3_SEGS + 1)), dim3(256), 0, st, hdr, pairs, cap,     \
+                       d_q_rows,                                                                               \
                        d_ent_rows, ktot, pred_kind, margin, d_truth, d_counts);                               \
     MMRE_CHECK_LAUNCH();                                                                                       \
   } while (0)
