@@ -330,3 +330,42 @@ def test_mfma_filter_counts_equal_exact_sweep_and_oracle(oracle_mod, monkeypatch
         o_c = oracle_mod.test_rank(mode, o_pred, qh[sel], qr[sel], qt[sel], hrt)
         assert np.array_equal(fast[:2, sel].T, o_c[:, :2])
     print(f"{model}: {st['undecided']} of {len(qh) * E} pairs rescored")
+
+
+@pytest.mark.parametrize("model", ["distmult", "complex"])
+def test_wide_sweep_lockstep_windows(oracle_mod, monkeypatch, model):
+    """The wide split-bf16 sweep with its lock-step windows (MMRE_BF3_BLOCKED=1: BlockMap, the C5
+    default above 64 MB of planes, which the small tables above never reach): counts bit-equal to
+    the exact sweep, entity slices summing to the whole table."""
+    import torch
+    from mmre.link import FilterIndex, LinkSweep
+    monkeypatch.setenv("MMRE_BF3_WIDE", "1")
+    monkeypatch.setenv("MMRE_BF3_BLOCKED", "1")
+    ent, rel, ent_im, rel_im, qh, qr, qt, qm = _adversarial_dot(model, E=4700, seed=3, nonfinite=False, Q=512)
+    E, R, d = ent.shape[0], rel.shape[0], rel.shape[1]
+    rng = np.random.default_rng(13)
+    fh, fr, ft = rng.integers(0, E, 3 * E), rng.integers(0, R, 3 * E), rng.integers(0, E, 3 * E)
+    fh, fr, ft = np.concatenate([fh, qh]), np.concatenate([fr, qr]), np.concatenate([ft, qt])
+    index = FilterIndex(fh, fr, ft, E, R)
+    spec = _spec_from(model, ent, rel, ent_im, rel_im, dim=d)
+    exact = _run(spec, qh, qr, qt, qm, index=index, scores=True)
+    dev = spec.ent.device
+    tq = lambda a, dt=np.int64: torch.from_numpy(np.asarray(a, dt)).to(dev)
+    args = (tq(qh), tq(qr), tq(qt), tq(qm, np.int8))
+
+    def run(entity_range=None):
+        sw = LinkSweep(spec)
+        bufs = sw.alloc_queries(len(qh))
+        f = tuple(torch.from_numpy(a).to(dev) for a in index.groups(qh, qr, qt, qm, entity_range=entity_range))
+        res = sw.run(*args, filt=f, buffers=bufs, entity_range=entity_range)
+        torch.cuda.synchronize()
+        return res["counts"].cpu().numpy().copy(), sw.bf3_stats(bufs)
+
+    fast, st = run()
+    assert not st["fallback"] and st["undecided"] >= len(qh), st
+    assert np.array_equal(fast[:2], exact["counts"][:2])
+    total = np.zeros_like(fast)
+    for e0, e1 in ((0, 2304), (2304, E)):
+        c, _ = run((e0, e1))
+        total += c
+    assert np.array_equal(total[:2], fast[:2])
