@@ -1177,26 +1177,44 @@ __device__ __forceinline__ void sweep_valu_body(
   constexpr bool LIST = L1F;
   int list_n = 0;         // wave-uniform
   uint32_t n_listed = 0;  // the wave's undecided pairs (the filter's counter; per lane without the list)
-  auto rescore = [&](int2 p) {
+  // A batch of listed pairs, one per lane (active lanes): each rescored with the canonical chain;
+  // the beating pairs' raw counts go out as ONE atomic per distinct query of the batch (a wave's
+  // 64 pairs come from its 32 query rows, and the undecided pairs concentrate on few queries --
+  // C2: half of the 1.09 M in 103 queries of ~7,000 beating pairs each -- whose count words were
+  // a same-address chain of per-pair atomics, serialised at ~13 ns each).
+  auto rescore = [&](int2 p, bool active) {
     const int64_t q = p.x;
     const int e = p.y;
     // a guard on the list's invariant: every entry is a (query row, slice column) pair of the
     // unit just swept, with q < n_query (padding query rows open no band) and 0 <= e < n_ent.
     // A pair outside is counted in hdr[4] (mmre_link_l1q_stats, asserted 0 by the filter tests)
     // and never reaches a row gather.
-    if ((uint64_t)q >= (uint64_t)n_query || (uint32_t)e >= (uint32_t)n_ent) {
+    bool ok = active;
+    if (active && ((uint64_t)q >= (uint64_t)n_query || (uint32_t)e >= (uint32_t)n_ent)) {
       if (l1.guard) atomicAdd(l1.guard, 1u);
-      return;
+      ok = false;
     }
-    if (l1.und_q) atomicAdd(&l1.und_q[q], 1u);
-    const float th = thr[q];
-    const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
-    if (pred(sx) < th) {
-      atomicAdd(&counts[q], 1);
+    bool beat = false;
+    if (ok) {
+      if (l1.und_q) atomicAdd(&l1.und_q[q], 1u);
+      const float th = thr[q];
+      const float sx = l1_exact_rows(l1.q_rows + q * (int64_t)l1.kt, l1.ent_rows + (int64_t)(e + e_base) * l1.kt, l1.kt);
+      beat = pred(sx) < th;
       if constexpr (TC) {
         const uint32_t* tm = qmode[q] == MMRE_HEAD_BATCH ? type_head : type_tail;
-        if (type_bit(tm, type_words, qr[q], e + e_base)) atomicAdd(&counts[2 * n_query + q], 1);
+        if (beat && type_bit(tm, type_words, qr[q], e + e_base)) atomicAdd(&counts[2 * n_query + q], 1);
       }
+    }
+    const int qi = (int)q;  // (int32 ids: check_link_args)
+    uint64_t pend = __ballot(beat);
+    while (pend) {  // uniform: one query of the batch per round
+      const int leader = __builtin_ctzll(pend);
+      const int ql = __builtin_amdgcn_readlane(qi, leader);
+      const bool mine = beat && qi == ql;
+      const uint64_t same = __ballot(mine);
+      if ((int)(threadIdx.x & 63) == leader) atomicAdd(&counts[ql], (int)__builtin_popcountll(same));
+      if (mine) beat = false;
+      pend &= ~same;
     }
   };
 
@@ -1450,7 +1468,7 @@ __device__ __forceinline__ void sweep_valu_body(
               n_listed += (uint32_t)nb;
               if (list_n >= 64) {  // a full batch (the list holds < 128: < 64 before this round)
                 list_n -= 64;
-                rescore(wl[list_n + lane]);
+                rescore(wl[list_n + lane], true);
               }
             }
           }
@@ -1591,7 +1609,7 @@ __device__ __forceinline__ void sweep_valu_body(
   }
   if constexpr (L1F) {  // the filter's undecided pairs: one atomic per workgroup, 16 slots
     if constexpr (LIST) {
-      if (list_n > 0 && (tid & 63) < list_n) rescore(sm.s_pairs[tid >> 6][tid & 63]);  // the last partial batch
+      if (list_n > 0) rescore(sm.s_pairs[tid >> 6][tid & 63], (tid & 63) < list_n);  // the last partial batch
       if ((tid & 63) == 0) sm.s_unc[tid >> 6] = n_listed;
     } else {
       if (n_listed) atomicAdd(&sm.s_unc[tid >> 6], n_listed);

@@ -114,11 +114,18 @@ def calibrate_weights(spec, qh, qr, qt, qm, index, device, group=None):
     return w.numpy()
 
 
-def cost_weights(undecided_per_query, n_ent: int, pair_cost: float = 140.0):
+# swept pairs one rescored pair costs (the L1 filter's canonical-chain rescoring of an undecided
+# pair, ~200 dependent f32 operations on two gathered rows)
+PAIR_COST = 140.0
+
+
+def cost_weights(undecided_per_query, n_ent: int, pair_cost: float | None = None):
     """Per-query sweep cost for lpt_partition(weights=): the query's n_ent swept pairs plus
     pair_cost x its pairs the L1 filter left undecided (each gathered and rescored with the
     canonical chain: ~140 swept pairs' worth on MI355X), from one calibration
     evaluation (mmre_link_evaluate_l1q's per-query counters)."""
+    if pair_cost is None:  # MMRE_PAIR_COST: A/B of the calibration constant
+        pair_cost = float(os.environ.get("MMRE_PAIR_COST", PAIR_COST))
     u = np.asarray(undecided_per_query, np.float64)
     return float(n_ent) + pair_cost * u
 
