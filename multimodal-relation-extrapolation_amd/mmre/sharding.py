@@ -115,14 +115,16 @@ def calibrate_weights(spec, qh, qr, qt, qm, index, device, group=None):
 
 
 # swept pairs one rescored pair costs (the L1 filter's canonical-chain rescoring of an undecided
-# pair, ~200 dependent f32 operations on two gathered rows)
-PAIR_COST = 140.0
+# pair, ~200 dependent f32 operations on two gathered rows). 140 until the rescoring's count
+# atomics were aggregated per query (round 6); 8-way C2 emulation, slowest rank: 140 0.198 ms,
+# 90 0.187 ms (every rank 0.180-0.187), 60 0.251 ms (one rank's probe then picks 16-bit codes)
+PAIR_COST = 90.0
 
 
 def cost_weights(undecided_per_query, n_ent: int, pair_cost: float | None = None):
     """Per-query sweep cost for lpt_partition(weights=): the query's n_ent swept pairs plus
     pair_cost x its pairs the L1 filter left undecided (each gathered and rescored with the
-    canonical chain: ~140 swept pairs' worth on MI355X), from one calibration
+    canonical chain: ~90 swept pairs' worth on MI355X, PAIR_COST), from one calibration
     evaluation (mmre_link_evaluate_l1q's per-query counters)."""
     if pair_cost is None:  # MMRE_PAIR_COST: A/B of the calibration constant
         pair_cost = float(os.environ.get("MMRE_PAIR_COST", PAIR_COST))
