@@ -3353,8 +3353,6 @@ struct EvalL1 {
   uint32_t* hdr;            // the L1 filter header
   double n_elem;
   float ratio;
-  int32_t* counts;          // (4, n_query): zeroed by the query blocks (the sweep adds into column 0 before
-                            // the filter counts write column 1, which now run after it)
 };
 
 // canonical sum of squares over x[0..dim) (k ascending, LDS reads batched 16 per round) and
@@ -3441,10 +3439,6 @@ __global__ __launch_bounds__(256, 7) void k_eval_prep(EvalL1 P) {
         r = P.qr[q];
         P.q_true[q] = (int32_t)tr;
         if (P.und_q) P.und_q[q] = 0u;
-        if (P.counts) {
-#pragma unroll
-          for (int c = 0; c < 4; ++c) P.counts[c * P.n_query + q] = 0;
-        }
       }
       s_a[tid] = a;
       s_t[tid] = tr;
@@ -3788,7 +3782,12 @@ __global__ __launch_bounds__(256) void k_eval_count_probe(
             }
           }
         }
-        if (active) counts[1 * n_query + q] = -c;  // (columns 0, 2, 3: zeroed by K1; the sweep may have counted already)
+        if (active) {
+          counts[0 * n_query + q] = 0;
+          counts[1 * n_query + q] = -c;
+          counts[2 * n_query + q] = 0;
+          counts[3 * n_query + q] = 0;
+        }
       }
     }
     return;
@@ -3809,9 +3808,7 @@ __global__ __launch_bounds__(256) void k_eval_count_probe(
   const float l1c = __builtin_fmaf((float)kt * 1.03f, l1d, 0x1p-120f);
   uint32_t acc[4] = {0u, 0u, 0u, 0u};
   if (c < n_slice) {
-    // 17 rows' loads in flight per round (d = 200: 51 rows in three latency rounds, not seven --
-    // the probe is on the evaluation's critical path, between the quantization and the sweep)
-#pragma unroll 17
+#pragma unroll 8
     for (int r = 0; r < kw; ++r) {
       const uint32_t a = uq[(int64_t)r * q_pad + q];
       const uint4 e = *reinterpret_cast<const uint4*>(ue + (int64_t)r * e_pad + c);
@@ -4535,7 +4532,6 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   P.hdr = hdr;
   P.n_elem = (double)kp * (double)(q_pad + e_cols);
   P.ratio = ratio_env ? (float)atof(ratio_env) : 128.0f;
-  P.counts = d_counts;
   // K1: prep + truths + |x| statistics (the last block decides codes vs f32 and resets the header)
   hipLaunchKernelGGL(k_eval_prep, dim3((unsigned)(P.n_eblk + P.n_qblk)), dim3(256), lds1, st, P);
   MMRE_CHECK_LAUNCH();
@@ -4558,20 +4554,13 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
   hipLaunchKernelGGL(k_eval_quant_list, dim3((unsigned)(n_lblk + 2 * Q.n_blk)), dim3(256), 0, st, P, Q, d_filt_ids,
                      d_entry_q, n_entries, d_list_scores, n_lblk);
   MMRE_CHECK_LAUNCH();
-  // K3: the code-width probe alone (the filter counts of the same kernel run after the sweeps: K1
-  // zeroed the count table and only the finalize reads their column -- off the path from the
-  // quantization to the sweep, which is what a rank's share waits on)
+  // K3: filter counts | the code-width probe
   const int n_cblk = (int)std::min<int64_t>((n_groups + 3) / 4, 65536);  // four groups (waves) per block
   const uint32_t probe_max = l1q_probe_max(n_slice);
-  static const char* split_env = getenv("MMRE_EVAL_SPLIT_K3");  // 0: counts and probe in one launch (A/B)
-  const bool split_k3 = !(split_env && split_env[0] == '0');
-  auto launch_k3 = [&](int n_count_blocks, int n_probe_blocks) {
-    hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_count_blocks + n_probe_blocks)), dim3(256), 0, st, d_grp_qoff,
-                       d_grp_q, n_groups, n_count_blocks, d_filt_off, d_filt_ids, d_list_scores, d_q_true, d_truth,
-                       n_query, n_ent, d_counts, vq, q_pad, ve + e_begin, e_pad, n_slice, k4, kt,
-                       tight ? q_l1c : nullptr, hdr, ticket, probe_max, bits == 8 || bits == 16 ? bits : 0);
-  };
-  launch_k3(split_k3 ? 0 : n_cblk, L1Q_PROBE_Q / 4);
+  hipLaunchKernelGGL(k_eval_count_probe, dim3((unsigned)(n_cblk + L1Q_PROBE_Q / 4)), dim3(256), 0, st, d_grp_qoff, d_grp_q,
+                     n_groups, n_cblk, d_filt_off, d_filt_ids, d_list_scores, d_q_true, d_truth, n_query, n_ent,
+                     d_counts, vq, q_pad, ve + e_begin, e_pad, n_slice, k4, kt, tight ? q_l1c : nullptr, hdr,
+                     ticket, probe_max, bits == 8 || bits == 16 ? bits : 0);
   MMRE_CHECK_LAUNCH();
   // the sweeps: the one the code-width word names counts, the others' workgroups leave
   const int64_t tw = (n_ent + 31) / 32;
@@ -4591,10 +4580,6 @@ extern "C" int mmre_link_evaluate_l1q(int norm_flag, const float* d_ent, int64_t
                       (const float*)uq, q_pad, n_query, k2, 0, 0.0f, d_truth, d_q_true, d_qr, d_qmode, nullptr, nullptr,
                       tw, d_counts, nullptr, l16, false);
   if (rc) return rc;
-  if (split_k3) {  // the filter counts (column 1), before the finalize reads them
-    launch_k3(n_cblk, 0);
-    MMRE_CHECK_LAUNCH();
-  }
   // the f32 fallback, gated on the word; it also carries the finalize (filtered += raw)
   L1Q gate{};
   gate.gate = hdr + 1;
