@@ -1373,7 +1373,14 @@ def main():
     if rank == 0:
         bpt = bytes_per_triple(model, dim)
         triples_launch = n_local * e_local
-        tps = triples_launch / (sweep_ms * 1e-3) if sweep_ms > 0 else 0.0
+        # the sweep's time per evaluation for the roof: the eager twin's kernel time, but never more
+        # than the measured step -- with two evaluation streams consecutive sweeps overlap (one's
+        # ramp beside the other's tail), so a single sweep's latency can exceed the per-evaluation
+        # time the pipeline achieves (C1 r5: 0.091 vs 0.080 ms); the step bounds the sweep's
+        # throughput time from above, so the frac stays conservative
+        step_ms = elapsed / args.steps * 1e3
+        eff_ms = min(sweep_ms, step_ms) if sweep_ms > 0 else 0.0
+        tps = triples_launch / (eff_ms * 1e-3) if eff_ms > 0 else 0.0
         # the TransE sweep kernel that counted: the probe's code width (8 / 16) or the f32 fallback
         l1_bits = fst.get("bits") if fst is not None and fst["kind"] == "l1q" else None
         if model == "transe" and l1_bits == 16:
@@ -1417,9 +1424,13 @@ def main():
         roof.update({
             "traffic": traffic, "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE)",
             "traffic_source": tsrc, "kernel": KERNEL_NAMES[model], "kernel_ms": sweep_ms,
+            "kernel_ms_effective": eff_ms,
+            "kernel_ms_note": "achieved uses kernel_ms_effective = min(kernel_ms (eager twin, events on its launch "
+                              "stream), ms_per_step): overlapping evaluations on two streams can make one sweep's "
+                              "latency exceed the per-evaluation time the pipeline achieves",
             "triples_per_launch": triples_launch, "bytes_per_triple": bpt,
             "hbm_algorithmic_x": tps * bpt / (HBM_PEAK_GBS * 1e9),
-            "hbm_measured_GBs": (traffic / (sweep_ms * 1e-3) / 1e9) if traffic and sweep_ms else None,
+            "hbm_measured_GBs": (traffic / (eff_ms * 1e-3) / 1e9) if traffic and eff_ms else None,
             "note": "binding roof: VALU for TransE/RotatE (TransE: the integer filter's v_sad_u8, four elements per "
                     "half-rate instruction = 1/2 slot per element -- the 16-bit codes' v_sad_u16 when the probe picks them: "
                     "1 slot --, MMRE_L1_FILTER=0: sub + add-with-abs; RotatE: sub, sub, mul, "
