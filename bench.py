@@ -42,11 +42,13 @@ CONFIGS = {
     "c2": dict(dataset="FB15K-237-ZS", model="transe", dim=200, norm=True,
                workload="C2 FB15K-237-ZS TransE d=200 p=1 norm_flag, filtered link prediction"),
     "c3": dict(dataset="DB15K-ZS", model="complex", dim=200, norm=False,
-               workload="C3 DB15K-ZS ComplEx d=200, filtered link prediction (MFMA f32)"),
+               workload="C3 DB15K-ZS ComplEx d=200, filtered link prediction (split-bf16 MFMA filter, "
+                        "exact f32 ranks)"),
     "c4": dict(dataset="FB15K-237-ZS", model="rotate", dim=512, norm=False,
                workload="C4 FB15K-237-ZS RotatE d=512, filtered link prediction"),
     "c5": dict(dataset="synthetic-1M", model="distmult", dim=256, norm=False,
-               workload="C5 synthetic |E|=1M DistMult d=256, 8,192 sweeps (MFMA f32)"),
+               workload="C5 synthetic |E|=1M DistMult d=256, 8,192 sweeps (wide split-bf16 MFMA filter, "
+                        "exact f32 ranks)"),
     "zsl": dict(dataset="FB15K-237-ZS", model="extractor", dim=200, norm=False,
                 workload="ZSL eval FB15K-237-ZS: Extractor (d=200, max_neighbor=50) + mean-cosine rank of "
                          "17,596 queries x ~1,000 candidates (SURVEY 8(f) rank 1)"),
