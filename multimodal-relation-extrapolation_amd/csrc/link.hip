@@ -2821,11 +2821,10 @@ __device__ __forceinline__ void w3_wait_n(int n) {  // n wave-uniform, 0 .. 15 (
     default: w3_vmwait<0>(); break;
   }
 }
-__device__ __forceinline__ float w3_next_up(float x) {  // the next float above x (x not NaN, inf kept)
-  if (x == INFINITY) return x;
-  if (x == 0.0f) return 0x1p-149f;
+__device__ __forceinline__ float w3_next_up(float x) {  // the next float above x (x not NaN, inf kept; selects)
   const uint32_t u = __float_as_uint(x);
-  return __uint_as_float(x > 0.0f ? u + 1u : u - 1u);
+  const uint32_t r = x == 0.0f ? 1u : (x > 0.0f ? u + 1u : u - 1u);  // +-0 -> the smallest subnormal
+  return x == INFINITY ? x : __uint_as_float(r);
 }
 
 template <int PK, int QT>
@@ -2929,20 +2928,15 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
   // B = cb |q| max |e| over the block (k_bf3_enorms: a NaN norm is skipped, and that row's S' is
   // NaN: undecided; blocks past the slice hold no counted row), T_hi >= nt + B,
   // T_lo <= nt - B one ulp outward of the rounded sums.
+  // (branch-free: per-lane branches here cost exec-mask juggling on every unit)
   auto thresholds = [&](float nm, const float nt[2], const float qbv[2], float th[2], float tl[2]) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const float b = qbv[j] * nm, a = nt[j] + b, c = nt[j] - b;
-      if (nt[j] != nt[j]) {  // a NaN threshold: nothing beats it (decided)
-        th[j] = INFINITY;
-        tl[j] = INFINITY;
-      } else if (a != a || c != c) {  // a NaN / inf bound (inf - inf): every pair undecided
-        th[j] = INFINITY;
-        tl[j] = -INFINITY;
-      } else {
-        th[j] = w3_next_up(a);
-        tl[j] = -w3_next_up(-c);
-      }
+      const bool nt_nan = nt[j] != nt[j];       // a NaN threshold: nothing beats it (decided)
+      const bool bad = a != a || c != c;        // a NaN / inf bound (inf - inf): every pair undecided
+      th[j] = nt_nan || bad ? INFINITY : w3_next_up(a);
+      tl[j] = nt_nan ? INFINITY : (bad ? -INFINITY : -w3_next_up(-c));
     }
   };
   // the decision pass of a finished unit; FULL: every entity of the wave's 128 is in the slice
