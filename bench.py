@@ -726,16 +726,19 @@ def bench_ns(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
-def ref_trainer_leg(w, B, k, margin, steps=30, timeout_s=600):
+def ref_trainer_leg(w, B, k, margin, steps=30, timeout_s=600, reps=5):
     """The reference's training step on this host's cores (oracle/ref_trainer.py in a child
     process): reference Base.so sampling + the TransE / strategy / MarginLoss op sequence on
-    torch CPU + backward + SGD, `steps` steps on the same training triples."""
+    torch CPU + backward + SGD, `steps` steps on the same training triples, the whole leg
+    repeated `reps` times: value = the median repetition's rate, value_min / _max the spread of
+    that same statistic (so the reported value lies inside its own bracket)."""
     import shutil
     import subprocess
     ref_so = os.path.join(REPO, "oracle", "_ref", "Base.so")
     if not os.path.exists(ref_so):
         return None
     tmp = tempfile.mkdtemp(prefix="mmre_reftrain_")
+    runs = []
     try:
         trn = np.stack([w["filter_h"], w["filter_t"], w["filter_r"]], 1)
         with open(os.path.join(tmp, "train2id.txt"), "w") as f:
@@ -748,25 +751,34 @@ def ref_trainer_leg(w, B, k, margin, steps=30, timeout_s=600):
                     threads=torch.get_num_threads(), sampler_threads=8)
         with open(os.path.join(tmp, "meta.json"), "w") as f:
             json.dump(meta, f)
-        r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "ref_trainer.py"), tmp], cwd=REPO,
-                           capture_output=True, text=True, timeout=timeout_s)
-        if r.returncode != 0:
-            print(f"cpu_baseline: ref_trainer failed (rc {r.returncode}): {r.stderr[-800:]}", file=sys.stderr)
-            return None
-        with open(os.path.join(tmp, "result.json")) as f:
-            res = json.load(f)
+        for _ in range(reps):
+            r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "ref_trainer.py"), tmp], cwd=REPO,
+                               capture_output=True, text=True, timeout=timeout_s)
+            if r.returncode != 0:
+                print(f"cpu_baseline: ref_trainer failed (rc {r.returncode}): {r.stderr[-800:]}", file=sys.stderr)
+                return None
+            with open(os.path.join(tmp, "result.json")) as f:
+                runs.append(json.load(f))
     except subprocess.TimeoutExpired:
         return None
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+    rates = [x["rows_per_step"] * x["steps"] / x["elapsed"] for x in runs]
+    order = sorted(range(len(runs)), key=lambda i: rates[i])
+    res = runs[order[len(order) // 2]]  # the median repetition
     el = res["elapsed"]
     tm = res["times"]
-    return {"value": res["rows_per_step"] * res["steps"] / el, "unit": "training triples/s", "cores": res["threads"],
+    return {"value": rates[order[len(order) // 2]], "unit": "training triples/s", "cores": res["threads"],
             "kind": "reference",
             "sample": f"{res['steps']} training steps of B={B} x (1+{k}) rows: reference Base.so sampling (8 pthreads) "
                       f"+ TransE/NegativeSampling/MarginLoss op sequence on torch {torch.__version__} CPU + backward + "
                       f"SGD (oracle/ref_trainer.py), {el:.2f} s on {res['threads']} threads (sampling "
-                      f"{tm['sampling']:.2f} s, forward {tm['forward']:.2f} s, backward+step {tm['backward_step']:.2f} s)"}
+                      f"{tm['sampling']:.2f} s, forward {tm['forward']:.2f} s, backward+step {tm['backward_step']:.2f} s; "
+                      f"the median of {len(runs)} repetitions)",
+            "reps": len(runs), "value_min": min(rates), "value_median": rates[order[len(order) // 2]],
+            "value_max": max(rates),
+            "reps_note": f"min / median / max of the leg's rate over {len(runs)} repetitions of the whole leg (the "
+                         "host share is not isolated: the spread is the box's noise)"}
 
 
 def bench_gan(args, world, rank, dev, dist):
@@ -1399,7 +1411,9 @@ def main():
             wide_env = os.environ.get("MMRE_BF3_WIDE")
             wide = wide_env != "0" if wide_env is not None else e_pad * k_tot * 4 > 64 * 2 ** 20
             KERNEL_NAMES[model] = "k_sweep_bf3w<2," if wide else "k_sweep_bf3<2>"
-        traffic, tsrc = pmc_traffic(args.config, model) if world == 1 else (None, None)
+        # (type-constrained lines: profiles/pmc_<config>_tc.json, the TC sweep variant's counters)
+        pmc_cfg = args.config + ("_tc" if args.type_constrain else "")
+        traffic, tsrc = pmc_traffic(pmc_cfg, model) if world == 1 else (None, None)
         if model in ("distmult", "complex") and fst is not None and fst["kind"] == "bf3" and not fst["fallback"]:
             # the split-bf16 filter: three bf16 products of K = dim x planes per triple on the bf16
             # MFMA (kernel_ms brackets the whole filtered sweep: split, sweep, rescoring)

@@ -12,7 +12,7 @@ for d in $f/prof_*/; do
   [ -n "$s" ] && cp "$s" profiles/r6/${n}_kernel_stats.csv
 done
 [ -f $f/pytest_gpu.log ] && cp $f/pytest_gpu.log profiles/r6/pytest_gpu_final.log
-for c in c1 c2 c3 c4 c5 ns ns_distmult ns_complex ns_rotate; do
+for c in c1 c2 c2_tc c3 c4 c5 ns ns_distmult ns_complex ns_rotate; do
   [ -d gpurun_out/pmc_final6_$c ] && python scripts/pmc_summary.py final6_$c --json profiles/pmc_$c.json > /dev/null
 done
 ls -la profiles/r6 profiles/pmc_*.json

@@ -2,10 +2,11 @@
 # Round-6 final measurements on the GPU box, in parts (each fits one gpurun call):
 #   T: full -m gpu suite + smoke + the relation-sharded C2 emulation at 2 / 4 / 8 ways, C4 at 8
 #      ways (relation-sharded) and C5 at 8 ways (entity-sharded)
-#   P1 / P2: PMC passes (scripts/pmc.sh) of c1 c2 c4 ns / c3 c5 ns_distmult ns_complex ns_rotate
+#   P1 / P2: PMC passes (scripts/pmc.sh) of c1 c2 c4 ns / c3 c5 c2_tc ns_distmult ns_complex ns_rotate
+#   P3: the c2_tc passes alone, summarised on the box, then the c2_tc bench line again
 #   B1: C1 / C2 / C2 type-constrained / C3 lines (cpu_baseline + reference parity legs) + kernel traces
 #   B2: C4 / C5 lines + traces;  B3: NS lines (TransE k 25 / k 10, DistMult, ComplEx, RotatE) + traces
-# usage: scripts/r6_final.sh <T|P1|P2|B1|B2|B3>
+# usage: scripts/r6_final.sh <T|P1|P2|P3|B1|B2|B3|B3a>
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -33,7 +34,14 @@ case $1 in
     ;;
   P2)
     for c in c3 c5; do bash scripts/pmc.sh final6_$c --config $c || exit 1; done
+    bash scripts/pmc.sh final6_c2_tc --config c2 --type-constrain || exit 1
     for m in distmult complex rotate; do bash scripts/pmc.sh final6_ns_$m --config ns --ns-model $m || exit 1; done
+    ;;
+  P3)  # the type-constrained C2 line's counters, then its bench line again (B1's, with traffic)
+    bash scripts/pmc.sh final6_c2_tc --config c2 --type-constrain || exit 1
+    python scripts/pmc_summary.py final6_c2_tc --json profiles/pmc_c2_tc.json > /dev/null || exit 1
+    timeout -k 10 400 python bench.py --config c2 --type-constrain > $o/bench_c2_tc.json 2> $o/bench_c2_tc.err || exit 1
+    cp profiles/pmc_c2_tc.json $o/pmc_c2_tc.json
     ;;
   B1)
     for c in c1 c2 c3; do
@@ -48,6 +56,10 @@ case $1 in
       timeout -k 10 500 python bench.py --config $c > $o/bench_$c.json 2> $o/bench_$c.err || exit 1
       trace $c --config $c || exit 1
     done
+    ;;
+  B3a)  # the TransE NS lines again (their cpu_baseline now repeats the reference leg 5 times)
+    timeout -k 10 400 python bench.py --config ns > $o/bench_ns.json 2> $o/bench_ns.err || exit 1
+    timeout -k 10 300 python bench.py --config ns --ns-neg 10 > $o/bench_ns_k10.json 2> $o/bench_ns_k10.err || exit 1
     ;;
   B3)
     timeout -k 10 300 python bench.py --config ns > $o/bench_ns.json 2> $o/bench_ns.err || exit 1

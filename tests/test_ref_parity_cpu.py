@@ -123,3 +123,14 @@ def test_ref_leg_type_constrained(oracle_mod, model):
     # the constrained counts are not the unconstrained ones (the types exclude entities)
     assert (ref["counts"][:, :, 2] <= ref["counts"][:, :, 0]).all()
     assert (ref["counts"][:, :, 2] < ref["counts"][:, :, 0]).any()
+
+
+def test_ref_trainer_leg_reports_its_spread():
+    """The NS line's cpu_baseline: the reference training leg repeated; the reported value is the
+    median repetition's rate and lies inside the min / max of that same statistic."""
+    import bench
+    w = _workload("transe")
+    cpu = bench.ref_trainer_leg(w, 64, 4, 5.0, steps=2, reps=3)
+    assert cpu is not None and cpu["kind"] == "reference" and cpu["reps"] == 3
+    assert cpu["value_min"] <= cpu["value"] <= cpu["value_max"]
+    assert cpu["value"] == cpu["value_median"]
