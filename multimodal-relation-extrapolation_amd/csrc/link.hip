@@ -2827,7 +2827,9 @@ __device__ __forceinline__ float w3_next_up(float x) {  // the next float above 
   return x == INFINITY ? x : __uint_as_float(r);
 }
 
-template <int PK, int QT>
+// BLK: the lock-step XCD windows (BlockMap) or contiguous ranges (UnitMap), a template parameter
+// so that only one map's state lives in registers
+template <int PK, int QT, bool BLK>
 __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep_bf3w(
     const uint4* __restrict__ ent_b, int64_t e_pad, int64_t e_cols, int64_t n_ent, const uint4* __restrict__ q_b,
     int64_t q_pad, int64_t n_query, int nkb, int n_et, int e_base, int n_groups, const float* __restrict__ thr_pad,
@@ -2843,43 +2845,57 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
   const int lrow = lane >> 5, lcol = lane & 31;
   const int grp = blockIdx.x % n_groups, gmem = blockIdx.x / n_groups;
   const int per_grp = gridDim.x / n_groups;
-  const bool blocked = blk_qb > 0;
   const int n_qt = (int)(q_pad / QT);
-  const UnitMap um(grp, n_groups, n_qt, n_et, emajor != 0);
-  const BlockMap bm(grp, n_groups, gmem, per_grp, n_qt, n_et, blocked ? blk_qb : 1, blocked ? blk_eb : 1);
-  const int u0 = blocked ? 0 : (int)((int64_t)gmem * um.count / per_grp);
-  const int u1 = blocked ? bm.count : (int)((int64_t)(gmem + 1) * um.count / per_grp);
-  if (u0 >= u1) return;  // uniform over the workgroup
-  auto unit_at = [&](int i, int& qt, int& et) {
-    if (blocked) bm.at(i, qt, et);
-    else um.at(i, qt, et);
+  auto make_map = [&]() {
+    if constexpr (BLK) return BlockMap(grp, n_groups, gmem, per_grp, n_qt, n_et, blk_qb, blk_eb);
+    else return UnitMap(grp, n_groups, n_qt, n_et, emajor != 0);
   };
+  const auto map = make_map();
+  const int u0 = BLK ? 0 : (int)((int64_t)gmem * map.count / per_grp);
+  const int u1 = BLK ? map.count : (int)((int64_t)(gmem + 1) * map.count / per_grp);
+  if (u0 >= u1) return;  // uniform over the workgroup
+  auto unit_at = [&](int i, int& qt, int& et) { map.at(i, qt, et); };
   auto sidx = [](int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); };
 
-  // the DMA cursor: the stage (unit, k block) whose copies are issued next, and its buffers
+  // the DMA cursor: the stage (unit, k block) whose copies are issued next, and its buffers.
+  // Per lane, the source offsets (uint4 units) of its DMA rows are fixed: the query rows'
+  // relative to the query tile, the entity rows' (clamped to the slice's last column) set once
+  // per unit; a stage adds only the uniform k-block plane base (round 6: the per-stage 64-bit
+  // address arithmetic had been ~30 VALU per wave and stage, plus SGPR spill traffic).
+  const int sl = lane & 3;
+  uint32_t qoff[2], erow[G::EPW], eoff[G::EPW];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {  // query rows 32 wave .. + 31: two 1-KB instructions of 16 rows
+    const int row = 16 * (wave * 2 + j) + (lane >> 2);
+    qoff[j] = (uint32_t)(row * 4 + (sl ^ ((row >> 2) & 3)));
+  }
+#pragma unroll
+  for (int j = 0; j < G::EPW; ++j) erow[j] = (uint32_t)(16 * (wave * G::EPW + j) + (lane >> 2));
   int ld_unit = u0, ld_kb = 0, ld_qt, ld_et, ld_buf = 0, ld_sbuf = 0;
-  unit_at(u0, ld_qt, ld_et);
+  auto enter_unit = [&]() {  // the cursor's unit: its tiles and the entity rows' offsets
+    unit_at(ld_unit, ld_qt, ld_et);
+    const uint32_t c0 = (uint32_t)ld_et * W3E, last = (uint32_t)e_cols - 1u;
+#pragma unroll
+    for (int j = 0; j < G::EPW; ++j) {  // past the slice's columns: its last one
+      const uint32_t er = c0 + erow[j] <= last ? c0 + erow[j] : last;
+      eoff[j] = er * 4u + (uint32_t)(sl ^ ((erow[j] >> 2) & 3));
+    }
+  };
+  enter_unit();
   auto issue = [&]() -> int {  // this wave's share of the cursor's stage; returns its instruction count
     if (ld_unit >= u1) return 0;
     char* sb = lds + ld_buf * G::STAGE;
-    const int64_t q0 = (int64_t)ld_qt * QT, c0 = (int64_t)ld_et * W3E;
-    const uint4* qp = q_b + (int64_t)ld_kb * q_pad * 4;
+    const int64_t q0 = (int64_t)ld_qt * QT;
+    const uint4* qp = q_b + ((int64_t)ld_kb * q_pad + q0) * 4;
     const uint4* ep = ent_b + (int64_t)ld_kb * e_pad * 4;
-    const int sl = lane & 3;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {  // query rows 32 wave .. + 31: two 1-KB instructions of 16 rows
-      const int i = wave * 2 + j, row = 16 * i + (lane >> 2);
-      w3_glds(qp + (q0 + row) * 4 + (sl ^ ((row >> 2) & 3)), sb + i * 1024);
-    }
+    for (int j = 0; j < 2; ++j) w3_glds(qp + qoff[j], sb + (wave * 2 + j) * 1024);
 #pragma unroll
-    for (int j = 0; j < G::EPW; ++j) {  // entity rows (past the slice's columns: its last one)
-      const int i = wave * G::EPW + j, row = 16 * i + (lane >> 2);
-      const int64_t er = c0 + row < e_cols ? c0 + row : e_cols - 1;
-      w3_glds(ep + er * 4 + (sl ^ ((row >> 2) & 3)), sb + G::QB + i * 1024);
-    }
+    for (int j = 0; j < G::EPW; ++j) w3_glds(ep + eoff[j], sb + G::QB + (wave * G::EPW + j) * 1024);
     int n = G::NDMA;
     if (ld_kb == 0 && wave < G::PIECES) {  // the unit's side data, one 1-KB piece per wave
       char* sd = lds + G::NBUF * G::STAGE + ld_sbuf * G::SIDE + wave * 1024;
+      const int64_t c0 = (int64_t)ld_et * W3E;
       const float* src;
       if (wave == 0) {  // the tile's 8 block maxima (lanes 0-1; the others re-read them)
         src = en + (c0 / 32 + 4 * (lane & 1) + 4 <= e_cols / 32 ? c0 / 32 + 4 * (lane & 1) : e_cols / 32 - 4);
@@ -2894,7 +2910,7 @@ __global__ __launch_bounds__(W3Geom<QT>::NT, W3Geom<QT>::WG_PER_CU) void k_sweep
     if (++ld_kb == nkb) {
       ld_kb = 0;
       ld_sbuf = ld_sbuf == G::NBUF - 1 ? 0 : ld_sbuf + 1;
-      if (++ld_unit < u1) unit_at(ld_unit, ld_qt, ld_et);
+      if (++ld_unit < u1) enter_unit();
     }
     return n;
   };
@@ -4257,7 +4273,7 @@ static void launch_bf3w(hipStream_t st, const uint4* eb, int64_t e_pad, int64_t 
                         int emajor, bool blocked, const char* grid_env) {
   using G = W3Geom<QT>;
   const int n_etw = (int)((n_slice + W3E - 1) / W3E);
-  const int res = resident_groups((const void*)k_sweep_bf3w<2, QT>, G::NT);
+  const int res = resident_groups((const void*)k_sweep_bf3w<2, QT, true>, G::NT);
   const int64_t units = (q_pad / QT) * (int64_t)n_etw;
   int g = (int)std::min<int64_t>(8LL * res, std::max<int64_t>((int64_t)res, units / 16)) & ~7;
   int bq = 0, be = 0;
@@ -4270,9 +4286,14 @@ static void launch_bf3w(hipStream_t st, const uint4* eb, int64_t e_pad, int64_t 
   }
   if (g < 1) g = 1;
   const int ng = (g % 8 == 0 && n_etw >= 8) ? 8 : 1;
-  hipLaunchKernelGGL((k_sweep_bf3w<2, QT>), dim3((unsigned)g), dim3(G::NT), 0, st, eb, e_pad, e_cols, n_slice, qb,
-                     q_pad, n_query, nkb, n_etw, e_begin, ng, thr_pad, qbf, en, d_counts, hdr, pairs, cap, emajor, bq,
-                     be);
+  if (blk)
+    hipLaunchKernelGGL((k_sweep_bf3w<2, QT, true>), dim3((unsigned)g), dim3(G::NT), 0, st, eb, e_pad, e_cols, n_slice,
+                       qb, q_pad, n_query, nkb, n_etw, e_begin, ng, thr_pad, qbf, en, d_counts, hdr, pairs, cap,
+                       emajor, bq, be);
+  else
+    hipLaunchKernelGGL((k_sweep_bf3w<2, QT, false>), dim3((unsigned)g), dim3(G::NT), 0, st, eb, e_pad, e_cols, n_slice,
+                       qb, q_pad, n_query, nkb, n_etw, e_begin, ng, thr_pad, qbf, en, d_counts, hdr, pairs, cap,
+                       emajor, bq, be);
 }
 
 // rows_src (mmre_link_sweep_bf3_rows): the entity split planes, norms and block maxima come from
