@@ -2,7 +2,7 @@
 # Round-6 final measurements on the GPU box, in parts (each fits one gpurun call):
 #   T: full -m gpu suite + smoke + the relation-sharded C2 emulation at 2 / 4 / 8 ways, C4 at 8
 #      ways (relation-sharded) and C5 at 8 ways (entity-sharded)
-#   P1 / P2: PMC passes (scripts/pmc.sh) of c1 c2 c4 ns / c3 c5 c2_tc ns_distmult ns_complex ns_rotate
+#   P1 / P2: PMC passes (scripts/pmc.sh) of c1 c2 c4 ns / c3 c5 ns_distmult ns_complex ns_rotate
 #   P3: the c2_tc passes alone, summarised on the box, then the c2_tc bench line again
 #   B1: C1 / C2 / C2 type-constrained / C3 lines (cpu_baseline + reference parity legs) + kernel traces
 #   B2: C4 / C5 lines + traces;  B3: NS lines (TransE k 25 / k 10, DistMult, ComplEx, RotatE) + traces
@@ -34,7 +34,6 @@ case $1 in
     ;;
   P2)
     for c in c3 c5; do bash scripts/pmc.sh final6_$c --config $c || exit 1; done
-    bash scripts/pmc.sh final6_c2_tc --config c2 --type-constrain || exit 1
     for m in distmult complex rotate; do bash scripts/pmc.sh final6_ns_$m --config ns --ns-model $m || exit 1; done
     ;;
   P3)  # the type-constrained C2 line's counters, then its bench line again (B1's, with traffic)
