@@ -1,7 +1,7 @@
 #!/bin/bash
 # Copy the judged artefacts of scripts/r3_final.sh from gpurun_out/final (scratch) into profiles/.
 # usage: scripts/collect_final.sh   (run in the build container after the parts came back)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 f=gpurun_out/final
 mkdir -p profiles/r3
 for j in $f/bench_*.json; do [ -s "$j" ] && cp "$j" profiles/r3/; done

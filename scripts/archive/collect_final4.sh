@@ -1,7 +1,7 @@
 #!/bin/bash
 # Copy the judged artefacts of scripts/r4_final.sh from gpurun_out/final4 (scratch) into profiles/.
 # usage: scripts/collect_final4.sh   (run in the build container after the parts came back)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 f=gpurun_out/final4
 mkdir -p profiles/r4
 for j in $f/bench_*.json; do [ -s "$j" ] && cp "$j" profiles/r4/; done

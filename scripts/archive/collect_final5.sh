@@ -1,7 +1,7 @@
 #!/bin/bash
 # Copy the judged artefacts of scripts/r5_final.sh from gpurun_out/final5 (scratch) into profiles/.
 # usage: scripts/collect_final5.sh   (run in the build container after the parts came back)
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 f=gpurun_out/final5
 mkdir -p profiles/r5
 for j in $f/bench_*.json; do [ -s "$j" ] && cp "$j" profiles/r5/; done

@@ -1,6 +1,6 @@
 #!/bin/bash
 # NS step bench + kernel trace (round 3). usage: bash scripts/r3_ns_bench.sh [tag]
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 tag=${1:-ns}
 mkdir -p gpurun_out

@@ -7,7 +7,7 @@
 #   G: PMC passes of the DistMult / ComplEx / RotatE NS steps; H: their bench lines again
 # usage: scripts/r4_final.sh <A|B|C|D1|D2|E|F|G|H>
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/final4
 mkdir -p $o

@@ -3,7 +3,7 @@
 #   X: PMC passes of C2 / C1 (summaries written into profiles/ on the box and copied to
 #      gpurun_out/final5), full -m gpu suite, smoke, C2 bench line + kernel trace
 #   Y: C1 bench line + trace, per-rank C2 shard emulations
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/final5
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call A: trained C2 tables for the fixture, the changed kernels' tests, smoke
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r4a
 T="timeout -k 10"
 $T 300 python -u scripts/dump_trained_tables.py gpurun_out/trained_c2.npz > gpurun_out/r4a/dump.log 2>&1 || { echo "dump failed"; exit 1; }

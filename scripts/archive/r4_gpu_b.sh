@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4, GPU call B: the NS tests (two-launch step), bench lines of every config touched this
 # round, per-rank shard emulations
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r4b
 T="timeout -k 10"
 $T 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu -s tests/test_ns_full_gpu.py \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4, GPU call C: L1 stats diagnostic, kernel traces of the NS steps and C3, the reference
 # fixtures C2 / C4 / C5 on the production path
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4c
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call D: owner hub scan fix + parallel bf3 split: tests, L1 stats probe, traces, benches
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4d
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call E: bf3 KB=2 A/B, generic NS traces, C2 bench (l1 stats)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4e
 mkdir -p $o

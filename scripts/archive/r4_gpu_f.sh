@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call F: NS model split (DistMult only), relation-row bucket read, L1 counters
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4f
 mkdir -p $o

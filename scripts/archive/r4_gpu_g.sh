@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call G: row owner at 7 waves / SIMD, bf3 epilogue for predict = -s
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4g
 mkdir -p $o

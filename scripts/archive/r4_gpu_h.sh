@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call H: L1 filter fallback as a gated launch
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4h
 mkdir -p $o

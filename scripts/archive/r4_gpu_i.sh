@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call I: C2 kernel trace (where the 1.85 ms goes)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4i
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call J: fallback-flag latency hidden, gated launches one residency round
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4${R4TAG:-j}
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call L: C2 A/B on one box -- this build vs the round-3 tree (ab_r3, a git worktree at db688e2)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4l
 mkdir -p $o

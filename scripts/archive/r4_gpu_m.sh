@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call M: the 8-bit L1 code filter -- filter / C2 fixture / link tests, C2 bench line, kernel trace
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4m
 mkdir -p $o

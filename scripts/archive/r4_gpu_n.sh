@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call N: C2 A/B -- 8-bit codes (auto), forced 16-bit, 8-bit with the rescoring skipped (timing only)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4n
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call P: C2 A/B -- the software-pipelined L1 inner loop vs the plain one (abl/nopipe.so), L1 filter tests
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4p
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call Q: L1 filter tests, C2 bench line, kernel trace of the C2 evaluation
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4q
 mkdir -p $o

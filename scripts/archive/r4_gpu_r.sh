@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call R: NS tests, NS bench lines (TransE, DistMult), kernel trace of the C2 bench (its trainer's row owner)
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4r
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, final: per-rank shard emulations (C2 relation- and entity-sharded, C4) on the final build
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 o=gpurun_out/final4
 mkdir -p $o
 rm -f $o/c2_shard_emulation.txt $o/c4_shard_emulation.txt

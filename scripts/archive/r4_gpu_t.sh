@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call T: the widened code-width probe -- L1 tests, 8-way C2 emulation with the per-rank filter record, C2 bench
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4t
 mkdir -p $o

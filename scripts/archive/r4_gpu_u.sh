@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4, GPU call U: the tight per-pair bound of the 8-bit L1 filter -- L1 / link / sharding tests, C2 A/B
 # (MMRE_L1_TIGHT=0: the uniform bound), 2- and 8-way C2 emulations
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4u
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4, GPU call V: the quantization kernel's grid / unroll -- L1 tests, C2 kernel trace
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r4v
 mkdir -p $o

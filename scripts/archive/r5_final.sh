@@ -6,7 +6,7 @@
 #   B2: C4 / C5 lines + traces;  B3: NS lines (TransE k 25 / k 10, DistMult, ComplEx, RotatE) + traces
 # usage: scripts/r5_final.sh <T|P1|P2|B1|B2|B3>
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/final5
 mkdir -p $o

@@ -5,7 +5,7 @@
 #   targeted -m gpu tests; C2 bench lines: this build, MMRE_FUSED_EVAL=0 (separate launches),
 #   abl/kku1.so (the 8-bit loop at one LDS row per iteration); 8-way relation-sharded emulation
 #   fused and separate; a kernel trace.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5a
 mkdir -p $o

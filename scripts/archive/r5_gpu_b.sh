@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call B: the fused evaluation without fences (sc1 hand-off), the 16-bit second
 # rescoring level, cost-packed sharding.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5b
 mkdir -p $o

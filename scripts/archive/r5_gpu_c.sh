@@ -2,7 +2,7 @@
 # Round 5, GPU call C: K1 with atomic accumulators; per-kernel traces of the fused C2 evaluation
 # (default, no second rescoring level, separate launches) at N = 1 and for the heavy 8-way
 # share; the bf3 sweep's lock-step windows (C3 / C5 bench lines, blocked vs contiguous ranges).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5c
 mkdir -p $o

@@ -3,7 +3,7 @@
 # reduced in K2, K3 a wave per group / 128 probe blocks), no second rescoring level; traces at
 # N = 1 and the heavy 8-way share; the bf3 regression hunt (C3: this build, the select-based row
 # counts, the unsaturated pair counter).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5d
 mkdir -p $o

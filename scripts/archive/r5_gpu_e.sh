@@ -2,7 +2,7 @@
 # Round 5, GPU call E: finalize folded into the gated f32 launch, bf3 64-bit pair counter.
 # Fused-path tests + reference fixtures, traces (N = 1, heavy 8-way share), C2/C3/C5 bench
 # lines, the 8-way emulation.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5e
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5, GPU call F: each rank's queries swept heaviest-calibrated-cost first (and at N = 1).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5f
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5, GPU call G: heavy queries spread over the query tiles (rank_order "spread") vs Test.h order.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5g
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call H: per-rank kernel traces at 8-way (rank 7, the slowest) and N = 1 under
 # grid-size variants of the sweep (one unit per workgroup vs 2-4) and the gated launches' grid.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5h
 mkdir -p $o

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5, GPU call I: two evaluation slots on two streams (consecutive evaluations overlap).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5i
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call J: K1 two global rounds per query block, K2 rows prefetched + one atomicMax per
 # chunk; bit-identity (fused == separate), fixtures, traces (rank 7 of 8, N = 1), bench lines.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5j
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call K: K1 at 7 blocks / CU (one round for an 8-way share), K2 grid sized to one
 # round; bit-identity, two-stream sharding tests, traces, emulation in the bench's host loop.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5k
 mkdir -p $o

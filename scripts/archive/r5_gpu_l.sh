@@ -2,7 +2,7 @@
 # Round 5, GPU call L (session 2: the tree was restored from HEAD 10b1caf, earlier results lost):
 # the full -m gpu suite + smoke on the current build, C2 lines (two streams = bench default, and
 # one), a C2 kernel trace, the relation-sharded emulation at 2 / 4 / 8 ways.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5l
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call M: per-kernel traces of the fused C2 evaluation (8-way shares of ranks 0 and
 # 3, and N = 1), C3 / C5 bench lines (bf3 lock-step XCD windows) with their kernel traces.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5m
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call N: PMC passes (scripts/pmc.sh, one counter group per rocprofv3 run) of C2,
 # C3, C5 and the NS step on this build.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5n
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 5, GPU call O: the pipelined TransE training step (mmre_ns_step_openke_pipe): NS / train
 # tests + the C2 reference fixture (its tables come from the trainer), then the NS bench line
 # (two-launch step) and its kernel trace; the host-loop probe of the 8-way rank 3 share.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5o
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call P: bf3 sweep A/B (MMRE_BF3_BLOCKED=1 lock-step XCD windows vs 0 contiguous
 # unit ranges) on C3 and C5, twice each, bench lines without the CPU leg; C2 8-way emulation grids.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5p
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 5, GPU call Q: the pipelined NS step's A/B (this build; abl/ns_noprep: no pre-pass in the
 # row owner; abl/ns_smplast: the sampler workgroups after the row workgroups) -- bench lines +
 # kernel traces; the 8-way C2 emulation with pinned staging buffers (the bench's).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5q
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call R: persistent sweep grids with two evaluation streams -- C2 bench lines at
 # MMRE_SWEEP_GRID = 512 / 768 / 1024 / 1536 and the default, twice; the 8-way emulation at 512 / 768.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5r
 mkdir -p $o

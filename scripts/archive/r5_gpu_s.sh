@@ -3,7 +3,7 @@
 # per-XCD-group work counters): L1 / fused-evaluation / sharding tests + the C2 fixture, then C2
 # lines with MMRE_SWEEP_DYN=1 (default) / 0 and a 2048-workgroup dynamic grid, the 8-way
 # emulation, a C2 kernel trace.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5s
 mkdir -p $o

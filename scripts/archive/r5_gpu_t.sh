@@ -2,7 +2,7 @@
 # Round 5, GPU call T: dynamic scheduling with persistent grids below the resident count (room for
 # the other evaluation stream): C2 lines at MMRE_SWEEP_GRID = 640 / 768 / 896 and the default
 # (1,024), the 8-way emulation at 768 / 896.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5t
 mkdir -p $o

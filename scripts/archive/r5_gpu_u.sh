@@ -2,7 +2,7 @@
 # Round 5, GPU call U: dynamic scheduling by chunks of consecutive units (kDynChunk 2 = this build,
 # abl/dyn_ch4, abl/dyn_ch1): the fused-evaluation / filter tests on this build, C2 lines at the
 # default grid and 768, the 8-way emulation of the chunk-2 build.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5u
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call V: dynamic-scheduling chunk of 4 units (this build) against 8 and 16
 # (abl/dyn_ch8, abl/dyn_ch16): C2 lines twice each, the 8-way emulation of each.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5v
 mkdir -p $o

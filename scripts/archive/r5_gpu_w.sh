@@ -2,7 +2,7 @@
 # Round 5, GPU call W: dynamic scheduling with the chunk picked per launch (4 units per claim when
 # a workgroup sweeps >= 16 units, else 1): tests (fused evaluation, filters, sharding, the C2 and
 # the widened C4 reference fixtures), C2 lines, the 2 / 4 / 8-way emulation.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5w
 mkdir -p $o

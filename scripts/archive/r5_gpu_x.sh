@@ -2,7 +2,7 @@
 # Round 5, GPU call X: the bf3 sweep's mask-logic epilogue (compares as wave masks, decisions on
 # the scalar unit): the MFMA-filter tests + C3 / C5 reference fixtures, C3 / C5 lines, one PMC
 # pass of the C5 sweep's VALU instruction count.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5x
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call Y: the one-call pipelined step for DistMult / ComplEx / RotatE
 # (mmre_ns_step_openke_gen_pipe): NS tests, then the NS lines of every model and their traces.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5y
 mkdir -p $o

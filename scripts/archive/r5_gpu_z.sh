@@ -2,7 +2,7 @@
 # Round 5, GPU call Z: the wide split-bf16 sweep (k_sweep_bf3w, abl/bf3w.so = the tree with the
 # wide sweep on by default): bf3 filter tests and the C3 / C5 reference fixtures on it, then
 # C5 / C3 lines wide vs 128 x 128 (MMRE_BF3_WIDE=0, same library) and a kernel trace of C5.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5z
 mkdir -p $o

@@ -3,7 +3,7 @@
 # decision pass compiled out (abl/bf3w_noepi.so: counts wrong, timing only) against the full
 # one; (2) stall / issue counters of the wide and the 128 x 128 sweeps (abl/bf3w.so,
 # MMRE_BF3_WIDE=1 / 0), one counter group per rocprofv3 run.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5za
 mkdir -p $o

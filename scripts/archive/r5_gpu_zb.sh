@@ -3,7 +3,7 @@
 # as the MFMA's A operand, per-lane counts against per-query thresholds; abl/bf3w2.so = the tree
 # with it on by default): bf3 filter tests and the C3 / C5 reference fixtures, then C5 / C3 lines
 # for QT 256 / 128 and the 128 x 128 sweep (MMRE_BF3_WIDE=0, same library).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5zb
 mkdir -p $o

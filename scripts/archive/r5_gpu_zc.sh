@@ -2,7 +2,7 @@
 # Round 5, GPU call ZC: the in-tree build with the wide split-bf16 sweep as the C5 default:
 # the MFMA-filter tests (128 x 128 and wide at QT 256 / 128), the C3 / C5 reference fixtures,
 # smoke, and the C5 / C3 lines.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5zc
 mkdir -p $o

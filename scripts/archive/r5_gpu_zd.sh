@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5, GPU call ZD: C5 with the wide sweep's 32-column block maxima (k_bf3_enorms): the line,
 # and a kernel trace of one-stream evaluations (sweep / norms / split / rescoring times).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5zd
 mkdir -p $o

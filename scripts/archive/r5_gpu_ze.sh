@@ -2,7 +2,7 @@
 # Round 5, GPU call ZE: the wide sweep with four stage buffers at QT = 256 (three stages in
 # flight; abl/bf3deep.so = the tree built with W3_DEEP=1) against the shipped build, on one box:
 # MFMA-filter tests and the C5 fixture on the variant, C5 lines of both, a trace of the variant.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5ze
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 5, GPU call ZF: the wide sweep with one barrier per two 16-k stages (four stage buffers;
 # abl/bf3pair.so = the tree built with W3_PAIR=1) against the shipped build, on one box:
 # MFMA-filter tests and the C5 fixture on the variant, C5 lines of both, a trace of the variant.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r5zf
 mkdir -p $o

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6, call a: the review fixes' GPU tests + an 8-way C2 rank-share kernel timeline.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6a
 mkdir -p $o

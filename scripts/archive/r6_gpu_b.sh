@@ -2,7 +2,7 @@
 # Round 6, call b: 8-way C2 rank shares under sweep-grid variants (residency left for the other
 # stream's prologue) and chunk sizes; N = 1 under the same variants.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/${R6B_OUT:-r6b}
 mkdir -p $o

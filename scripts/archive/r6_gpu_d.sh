@@ -2,7 +2,7 @@
 # Round 6, call d: the DistMult raw-row split (filter tests + C5 A/B) and the balanced small-share
 # grid (8-way C2 A/B).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6d
 mkdir -p $o

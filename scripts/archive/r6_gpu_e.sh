@@ -2,7 +2,7 @@
 # Round 6, call e: the entity-rows-as-A bf3 sweep (k_sweep_bf3t) -- filter tests, C3 reference
 # fixture, C3 A/B against k_sweep_bf3 (MMRE_BF3_T=0).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6e
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 6, call f: segmented bf3 pair lists + the entity-rows-as-A sweep (k_sweep_bf3t): filter
 # tests, C3 / C5 reference fixtures, C3 / C5 timings.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6f
 mkdir -p $o

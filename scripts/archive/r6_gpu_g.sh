@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6, call g: the wide sweep's dynamic window order (tests, C5 A/B, C5 PMC traffic).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6g
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 6, call h: C5 same-box A/B -- the committed build (abl/head_a1.so) against the dynamic
 # window order (this tree; MMRE_BF3W_DYN=0 / 1).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6h
 mkdir -p $o

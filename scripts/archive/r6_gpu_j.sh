@@ -2,7 +2,7 @@
 # Round 6, call j: per-query aggregation of the L1 rescoring's count atomics -- L1 tests, C2
 # reference fixture, C2 same-box A/B against the committed build (abl/head_a1.so), 8-way shares.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6j
 mkdir -p $o

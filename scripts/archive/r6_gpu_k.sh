@@ -2,7 +2,7 @@
 # Round 6, call k: the relation-sharded packing's pair cost after the rescoring aggregation --
 # 8-way C2 emulation (all ranks) at pair costs 140 / 90 / 60.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6k
 mkdir -p $o

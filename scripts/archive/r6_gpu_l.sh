@@ -2,7 +2,7 @@
 # Round 6, call l: the fused L1 evaluation with the filter counts after the sweeps (K3 split) and
 # a deeper probe loop -- tests, then N = 1 and 8-way A/B (MMRE_EVAL_SPLIT_K3=0 / 1).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6l
 mkdir -p $o

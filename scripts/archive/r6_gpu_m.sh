@@ -2,7 +2,7 @@
 # Round 6, call m: C5 wide-sweep knobs on one box (query tile 128 = two workgroups per CU,
 # contiguous ranges instead of windows, grid sizes).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6m
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 6, call n: C3 split-bf16 sweep grid / variant A/B after the segmented pair lists
 # (one persistent round vs 2-3 rounds of equal ranges; the wide sweep; lock-step windows).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6n2
 mkdir -p $o

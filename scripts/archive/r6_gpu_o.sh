@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6, call o: the split-bf16 sweep's whole-round grid -- filter parity tests, C3 bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6o
 mkdir -p $o

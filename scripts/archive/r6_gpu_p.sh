@@ -4,7 +4,7 @@
 # + no entity-row DMA (w_noedma), + no DMA of either operand (w_nodma). Timing only: the
 # ablations' counts are wrong by construction.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6p
 mkdir -p $o

@@ -3,7 +3,7 @@
 # max screen per 16-value block, the unit's first stage from C = 0) -- filter parity tests, then
 # C5 A/B against the previous build (abl/head_82df655.so) on one box.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6q
 mkdir -p $o

@@ -2,7 +2,7 @@
 # Round 6, call r: C5 A/B of the wide sweep's decision-pass variants (scripts/variants.txt) on one
 # box: previous build, thresholds only, + screen, + C = 0 first stage, all three (in-tree).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6r
 mkdir -p $o

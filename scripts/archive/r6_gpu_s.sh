@@ -3,7 +3,7 @@
 # map as a template parameter -- filter parity tests, C5 / C3 fixtures, then C5 A/B against the
 # final-pass build (abl/head_6882e169.so) on one box.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 o=gpurun_out/r6s
 mkdir -p $o
